@@ -1,0 +1,149 @@
+"""Benchmark: PairedAttention paired-GAN training throughput (img/s) at 512x512,
+topography=all (9-ch generator input, 12-ch discriminator input), batch 8 per GPU
+(BASELINE.json configs[1]; configs[2] = the same step data-parallel over 8 GPUs).
+
+One "step" = one full iteration of models/model.py:615-651 (G forward, D step + Adam(D),
+G step against the updated D + Adam(G), the four logged losses read back) over a synthetic
+batch already resident in HBM.  Prints ONE JSON line (rank 0).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 8] [--res 512]
+  N>1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "flood-prediction-gan_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak (spec)
+STEP_GFLOP_PER_IMG_512 = 1593.5   # conv fwd 546.1 + conv bwd 1047.3 GFLOP per image
+
+
+def resblock_conv_flops(batch, res):
+    """3x3 s1 256->256 conv over (res/4)^2 pixels: 2*M*N*K per launch."""
+    m = batch * (res // 4) ** 2
+    return 2.0 * m * 256 * (256 * 9)
+
+
+def cpu_baseline(res, threads, steps=2):
+    """Time the CPU oracle (the reference algorithm restated on PyTorch-CPU, pinned to the
+    reference's own train_paired outputs) on a bounded sample: 1 warm-up + `steps` timed
+    iterations at batch 1, res x res."""
+    from oracle import paired_attention as O  # the checker / CPU baseline only
+
+    torch.set_num_threads(threads)
+    g = torch.Generator().manual_seed(4321)
+    x = torch.rand((1, 9, res, res), generator=g) * 2 - 1
+    y = torch.rand((1, 3, res, res), generator=g) * 2 - 1
+    st = O.PairedStepOracle()
+    st.step(x, y)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        st.step(x, y)
+    dt = time.perf_counter() - t0
+    return {"value": round(steps / dt, 4), "unit": "img/s", "cores": threads, "kind": "port",
+            "sample": f"{steps} timed iterations (+1 warm-up) of the CPU oracle paired step at batch 1, "
+                      f"{res}x{res}, torch-CPU fp32 with {threads} threads"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=8, help="images per GPU")
+    ap.add_argument("--res", type=int, default=512)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    from floodgan import ops
+    from floodgan.model import Model
+    from floodgan.parallel import broadcast_params
+
+    B, R = args.batch, args.res
+    m = Model(model="PairedAttention", num_epochs=2, topography="all", device=dev)
+    if world > 1:
+        broadcast_params(m.generator)
+        broadcast_params(m.discriminator)
+    step = m.step_fn
+    g = torch.Generator().manual_seed(1234 + rank)
+    x = (torch.rand((B, 9, R, R), generator=g) * 2 - 1).to(dev)
+    y = (torch.rand((B, 3, R, R), generator=g) * 2 - 1).to(dev)
+
+    for _ in range(args.warmup):
+        step(x, y).cpu()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    timer = ops.KernelTimer(["resblock_conv_fwd"])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with timer:
+        for _ in range(args.steps):
+            losses = step(x, y).cpu()       # the reference logs the four losses every iteration
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    durs = timer.durations_ms()["resblock_conv_fwd"]
+    avg_ms = sum(durs) / max(len(durs), 1)
+    flops = resblock_conv_flops(B, R)
+    achieved = flops / (avg_ms * 1e-3) / 1e12
+
+    if rank == 0:
+        img_s = world * B * args.steps / elapsed
+        out = {
+            "metric": "GAN training images/sec (512x512, PairedAttention)",
+            "value": round(img_s, 3),
+            "unit": "img/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic U[-1,1) tiles resident in HBM, seed-47 weights (models/model.py:80)",
+            "config": {"workload": f"PairedAttention paired train step, {R}x{R}, topography=all "
+                                   f"(9-ch G input, 12-ch D input), batch {B}/GPU",
+                       "global_batch": world * B, "per_gpu_batch": B, "resolution": R,
+                       "parallelism": f"dp{world}"},
+            "roofline": {"bound": "mfma", "kernel": "conv_fwd_kernel<128,128,64,64> resblock 3x3 256->256",
+                         "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                         "avg_launch_ms": round(avg_ms, 4), "launches": len(durs),
+                         "flop_per_launch": flops},
+            "step_tflops": round(STEP_GFLOP_PER_IMG_512 * (R / 512) ** 2 * world * B * args.steps / elapsed / 1e3, 2),
+            "losses_last_step": [round(float(v), 5) for v in losses],
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
+            out["cpu_baseline"] = cpu_baseline(R, threads)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

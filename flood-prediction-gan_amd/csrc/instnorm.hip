@@ -1,0 +1,390 @@
+// InstanceNorm2d (affine=False, track_running_stats=False; models/model_architectures.py
+// :313-317, :407-410, :325-332, :428-437) fused with ReLU / LeakyReLU(0.2), the residual
+// add of PairedAttentionBlock and the reflect / zero padding the next conv reads.
+//
+// Statistics: per-(n,c) plane sums over chunked pixel ranges, shifted by the plane's first
+// value (robust E[x^2]-E[x]^2), accumulated per thread in fp32, combined in fp64.
+// Backward: dL/dx = rstd * (g' - mean(g') - xhat * mean(g' xhat)), g' = g * act'(xhat).
+#include "fg_common.hpp"
+
+namespace {
+
+constexpr int NT = 256;
+constexpr int MAX_CHUNKS = 256;
+
+int choose_chunks(int n, long long hw) {
+    long long c = (1024 + n - 1) / n;
+    if (c > hw / 256) c = hw / 256;
+    if (c > MAX_CHUNKS) c = MAX_CHUNKS;
+    if (c < 1) c = 1;
+    return (int)c;
+}
+
+__device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+
+__global__ void in_stats_kernel(fg_view src, int chunks, double* __restrict__ work) {
+    const int C = src.c_alloc, L = C / 4, PG = NT / L;
+    const int n = blockIdx.y, chunk = blockIdx.x;
+    const int HW = src.h * src.w;
+    const int per = (HW + chunks - 1) / chunks;
+    const int p0 = chunk * per, p1 = min(HW, p0 + per);
+    const int g = threadIdx.x / L, c4 = threadIdx.x - (threadIdx.x / L) * L;
+    __shared__ double red[NT][8];
+    f32x4 s = {0.f, 0.f, 0.f, 0.f}, ss = {0.f, 0.f, 0.f, 0.f};
+    if (g < PG) {
+        const f32x4 K = ld4(src.ptr + fg::vidx(src, n, 0, 0) + 4 * c4);
+        for (int p = p0 + g; p < p1; p += PG) {
+            const int y = p / src.w, x = p - (p / src.w) * src.w;
+            const f32x4 v = ld4(src.ptr + fg::vidx(src, n, y, x) + 4 * c4) - K;
+            s += v;
+            ss += v * v;
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        red[threadIdx.x][e] = s[e];
+        red[threadIdx.x][4 + e] = ss[e];
+    }
+    __syncthreads();
+    if (threadIdx.x < L) {
+        double a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int gg = 0; gg < PG; ++gg)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) a[e] += red[gg * L + threadIdx.x][e];
+        double* w = work + ((size_t)(n * chunks + chunk) * C + 4 * threadIdx.x) * 2;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            w[2 * e] = a[e];
+            w[2 * e + 1] = a[4 + e];
+        }
+    }
+}
+
+__global__ void in_finalize_kernel(fg_view src, int chunks, const double* __restrict__ work, float eps,
+                                   float* __restrict__ mean, float* __restrict__ rstd) {
+    const int C = src.c_alloc;
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= src.n * C) return;
+    const int n = idx / C, c = idx - (idx / C) * C;
+    double s1 = 0, s2 = 0;
+    for (int k = 0; k < chunks; ++k) {
+        s1 += work[((size_t)(n * chunks + k) * C + c) * 2];
+        s2 += work[((size_t)(n * chunks + k) * C + c) * 2 + 1];
+    }
+    const double HW = (double)src.h * src.w;
+    const double ms = s1 / HW;
+    double var = s2 / HW - ms * ms;
+    if (var < 0) var = 0;
+    const double K = src.ptr[fg::vidx(src, n, 0, 0) + c];
+    mean[idx] = (float)(K + ms);
+    rstd[idx] = (float)(1.0 / sqrt(var + (double)eps));
+}
+
+__global__ void in_apply_kernel(fg_view src, const float* __restrict__ mean, const float* __restrict__ rstd,
+                                int act, fg_view res, fg_view dst, int pad_mode) {
+    const int C = dst.c_alloc, C4 = C / 4;
+    const int hp = dst.h + 2 * dst.pad, wp = dst.w + 2 * dst.pad;
+    const long long total = (long long)dst.n * hp * wp * C4;
+    for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const int c4 = (int)(idx % C4);
+        long long pix = idx / C4;
+        const int xp = (int)(pix % wp);
+        pix /= wp;
+        const int yp = (int)(pix % hp);
+        const int n = (int)(pix / hp);
+        int y = yp - dst.pad, x = xp - dst.pad;
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        const bool inside = y >= 0 && y < dst.h && x >= 0 && x < dst.w;
+        if (inside || pad_mode == FG_PAD_REFLECT) {
+            y = fg::reflect_idx(y, dst.h);
+            x = fg::reflect_idx(x, dst.w);
+            const f32x4 m = ld4(mean + (size_t)n * C + 4 * c4);
+            const f32x4 r = ld4(rstd + (size_t)n * C + 4 * c4);
+            v = (ld4(src.ptr + fg::vidx(src, n, y, x) + 4 * c4) - m) * r;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = fg::act_fwd(v[e], act);
+            if (res.ptr) v += ld4(res.ptr + fg::vidx(res, n, y, x) + 4 * c4);
+        }
+        *reinterpret_cast<f32x4*>(dst.ptr + ((size_t)(n * hp + yp) * wp + xp) * C + 4 * c4) = v;
+    }
+}
+
+// ---- backward ----
+
+__device__ __forceinline__ int fold_src(int y, int h, int p, int* out) {
+    int k = 0;
+    out[k++] = y + p;
+    if (y >= 1 && y <= p) out[k++] = p - y;
+    if (y >= h - 1 - p && y <= h - 2) out[k++] = p + 2 * (h - 1) - y;
+    return k;
+}
+
+__device__ __forceinline__ f32x4 load_grad(const fg_view& g, int fp, const fg_view& gadd, int n, int y, int x,
+                                           int h, int w, int c4) {
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (fp > 0) {
+        int ys[3], xs[3];
+        const int ny = fold_src(y, h, fp, ys), nx = fold_src(x, w, fp, xs);
+        for (int iy = 0; iy < ny; ++iy)
+            for (int ix = 0; ix < nx; ++ix) v += ld4(g.ptr + fg::vidx(g, n, ys[iy], xs[ix]) + 4 * c4);
+    } else {
+        v = ld4(g.ptr + fg::vidx(g, n, y, x) + 4 * c4);
+    }
+    if (gadd.ptr) v += ld4(gadd.ptr + fg::vidx(gadd, n, y, x) + 4 * c4);
+    return v;
+}
+
+__global__ void in_bwd_stats_kernel(fg_view g, int fp, fg_view gadd, fg_view src, const float* __restrict__ mean,
+                                    const float* __restrict__ rstd, int act, int chunks, double* __restrict__ work) {
+    const int C = src.c_alloc, L = C / 4, PG = NT / L;
+    const int n = blockIdx.y, chunk = blockIdx.x;
+    const int h = src.h, w = src.w, HW = h * w;
+    const int per = (HW + chunks - 1) / chunks;
+    const int p0 = chunk * per, p1 = min(HW, p0 + per);
+    const int gi = threadIdx.x / L, c4 = threadIdx.x - (threadIdx.x / L) * L;
+    __shared__ double red[NT][12];
+    f32x4 sg = {0.f, 0.f, 0.f, 0.f}, sgx = sg, sx = sg;
+    if (gi < PG) {
+        const f32x4 m = ld4(mean + (size_t)n * C + 4 * c4);
+        const f32x4 r = ld4(rstd + (size_t)n * C + 4 * c4);
+        for (int p = p0 + gi; p < p1; p += PG) {
+            const int y = p / w, x = p - (p / w) * w;
+            const f32x4 xh = (ld4(src.ptr + fg::vidx(src, n, y, x) + 4 * c4) - m) * r;
+            f32x4 gv = load_grad(g, fp, gadd, n, y, x, h, w, c4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) gv[e] *= fg::act_grad(xh[e], act);
+            sg += gv;
+            sgx += gv * xh;
+            sx += xh;
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        red[threadIdx.x][e] = sg[e];
+        red[threadIdx.x][4 + e] = sgx[e];
+        red[threadIdx.x][8 + e] = sx[e];
+    }
+    __syncthreads();
+    if (threadIdx.x < L) {
+        double a[12] = {0};
+        for (int gg = 0; gg < PG; ++gg)
+#pragma unroll
+            for (int e = 0; e < 12; ++e) a[e] += red[gg * L + threadIdx.x][e];
+        double* wk = work + ((size_t)(n * chunks + chunk) * C + 4 * threadIdx.x) * 3;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            wk[3 * e] = a[e];
+            wk[3 * e + 1] = a[4 + e];
+            wk[3 * e + 2] = a[8 + e];
+        }
+    }
+}
+
+// one thread per channel: per-(n,c) coefficients and the (cancelled) conv-bias gradient
+__global__ void in_bwd_finalize_kernel(int N, int C, int HWi, int chunks, const double* __restrict__ work,
+                                       const float* __restrict__ rstd, float* __restrict__ coef,
+                                       float* __restrict__ bias_grad) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const double HW = (double)HWi;
+    double bsum = 0;
+    for (int n = 0; n < N; ++n) {
+        double sg = 0, sgx = 0, sx = 0;
+        for (int k = 0; k < chunks; ++k) {
+            const double* wk = work + ((size_t)(n * chunks + k) * C + c) * 3;
+            sg += wk[0];
+            sgx += wk[1];
+            sx += wk[2];
+        }
+        coef[((size_t)n * C + c) * 2] = (float)(sg / HW);
+        coef[((size_t)n * C + c) * 2 + 1] = (float)(sgx / HW);
+        // sum_hw rstd*(g' - mean g' - xhat*mean(g'xhat)) = -rstd * sx * sgx / HW
+        bsum += -(double)rstd[(size_t)n * C + c] * sx * sgx / HW;
+    }
+    if (bias_grad) bias_grad[c] = (float)bsum;
+}
+
+__global__ void in_bwd_apply_kernel(fg_view g, int fp, fg_view gadd, fg_view src, const float* __restrict__ mean,
+                                    const float* __restrict__ rstd, const float* __restrict__ coef, int act,
+                                    fg_view dst) {
+    const int C = dst.c_alloc, C4 = C / 4;
+    const int h = dst.h, w = dst.w;
+    const int hp = h + 2 * dst.pad, wp = w + 2 * dst.pad;
+    const long long total = (long long)dst.n * hp * wp * C4;
+    for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const int c4 = (int)(idx % C4);
+        long long pix = idx / C4;
+        const int xp = (int)(pix % wp);
+        pix /= wp;
+        const int yp = (int)(pix % hp);
+        const int n = (int)(pix / hp);
+        const int y = yp - dst.pad, x = xp - dst.pad;
+        f32x4 out = {0.f, 0.f, 0.f, 0.f};
+        if (y >= 0 && y < h && x >= 0 && x < w) {
+            const size_t nc = (size_t)n * C + 4 * c4;
+            const f32x4 m = ld4(mean + nc), r = ld4(rstd + nc);
+            const f32x4 xh = (ld4(src.ptr + fg::vidx(src, n, y, x) + 4 * c4) - m) * r;
+            f32x4 gv = load_grad(g, fp, gadd, n, y, x, h, w, c4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float gp = gv[e] * fg::act_grad(xh[e], act);
+                out[e] = r[e] * (gp - coef[(nc + e) * 2] - xh[e] * coef[(nc + e) * 2 + 1]);
+            }
+        }
+        *reinterpret_cast<f32x4*>(dst.ptr + ((size_t)(n * hp + yp) * wp + xp) * C + 4 * c4) = out;
+    }
+}
+
+__global__ void act_bwd_kernel(fg_view g, fg_view y, int act) {
+    const int C = g.c_alloc;
+    const long long total = (long long)g.n * g.h * g.w * C;
+    for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const int c = (int)(idx % C);
+        long long pix = idx / C;
+        const int x = (int)(pix % g.w);
+        pix /= g.w;
+        const int yy = (int)(pix % g.h);
+        const int n = (int)(pix / g.h);
+        const float yv = y.ptr[fg::vidx(y, n, yy, x) + c];
+        g.ptr[fg::vidx(g, n, yy, x) + c] *= fg::act_grad(yv, act);
+    }
+}
+
+__global__ void channel_sum_kernel(fg_view src, int c_valid, int chunks, double* __restrict__ work) {
+    // block (chunk, channel-group); threads = (pixel lane g, channel cl)
+    const int cg = blockIdx.y;
+    const int cbase = cg * NT;
+    const int L = min(NT, c_valid - cbase);
+    const int PG = NT / L;
+    const int gi = threadIdx.x / L, cl = threadIdx.x - (threadIdx.x / L) * L;
+    const long long P = (long long)src.n * src.h * src.w;
+    const long long per = (P + chunks - 1) / chunks;
+    const long long p0 = blockIdx.x * per, p1 = min(P, p0 + per);
+    __shared__ double red[NT];
+    double acc = 0;
+    if (gi < PG) {
+        float s = 0.f;
+        int cnt = 0;
+        for (long long p = p0 + gi; p < p1; p += PG) {
+            const int x = (int)(p % src.w);
+            const long long t = p / src.w;
+            const int y = (int)(t % src.h);
+            const int n = (int)(t / src.h);
+            s += src.ptr[fg::vidx(src, n, y, x) + cbase + cl];
+            if (++cnt == 256) {
+                acc += s;
+                s = 0.f;
+                cnt = 0;
+            }
+        }
+        acc += s;
+    }
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    if (threadIdx.x < L) {
+        double a = 0;
+        for (int gg = 0; gg < PG; ++gg) a += red[gg * L + threadIdx.x];
+        work[(size_t)blockIdx.x * c_valid + cbase + threadIdx.x] = a;
+    }
+}
+
+__global__ void channel_sum_finalize(int c_valid, int chunks, const double* __restrict__ work, float* out,
+                                     int accumulate) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= c_valid) return;
+    double s = 0;
+    for (int k = 0; k < chunks; ++k) s += work[(size_t)k * c_valid + c];
+    float v = (float)s;
+    if (accumulate) v += out[c];
+    out[c] = v;
+}
+
+bool ok_view(const fg_view& v) { return v.ptr && v.n > 0 && v.h > 0 && v.w > 0 && v.c_alloc > 0 && v.pad >= 0; }
+
+}  // namespace
+
+FG_API long long fg_in_workspace_doubles(int n, int c) { return (long long)n * c * (MAX_CHUNKS * 3 + 2) + 64; }
+
+FG_API int fg_in_stats(fg_view src, float eps, float* mean, float* rstd, double* work, hipStream_t stream) {
+    if (!ok_view(src) || !mean || !rstd || !work || src.c_alloc % 4 || (NT % (src.c_alloc / 4)) != 0)
+        return fg::fail(FG_ERR_INVALID, "fg_in_stats: bad args (C=%d)", src.c_alloc);
+    const int chunks = choose_chunks(src.n, (long long)src.h * src.w);
+    hipLaunchKernelGGL(in_stats_kernel, dim3(chunks, src.n), dim3(NT), 0, stream, src, chunks, work);
+    int e = fg::launched("in_stats");
+    if (e) return e;
+    const int tot = src.n * src.c_alloc;
+    hipLaunchKernelGGL(in_finalize_kernel, dim3((tot + 255) / 256), dim3(256), 0, stream, src, chunks, work, eps,
+                       mean, rstd);
+    return fg::launched("in_finalize");
+}
+
+FG_API int fg_in_apply(fg_view src, const float* mean, const float* rstd, int act, fg_view residual, fg_view dst,
+                       int pad_mode, hipStream_t stream) {
+    if (!ok_view(src) || !ok_view(dst) || !mean || !rstd || src.c_alloc % 4 || dst.c_alloc != src.c_alloc ||
+        dst.h != src.h || dst.w != src.w || dst.n != src.n)
+        return fg::fail(FG_ERR_INVALID, "fg_in_apply: bad args");
+    if (residual.ptr && (residual.c_alloc != src.c_alloc || residual.h != src.h || residual.w != src.w))
+        return fg::fail(FG_ERR_INVALID, "fg_in_apply: residual shape");
+    if (pad_mode == FG_PAD_REFLECT && (dst.pad >= dst.h || dst.pad >= dst.w))
+        return fg::fail(FG_ERR_INVALID, "fg_in_apply: reflect pad too large");
+    const long long total = (long long)dst.n * (dst.h + 2 * dst.pad) * (dst.w + 2 * dst.pad) * (dst.c_alloc / 4);
+    hipLaunchKernelGGL(in_apply_kernel, dim3(fg::blocks_for(total, 256, 16384)), dim3(256), 0, stream, src, mean,
+                       rstd, act, residual, dst, pad_mode);
+    return fg::launched("in_apply");
+}
+
+FG_API int fg_in_bwd(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, const float* mean, const float* rstd,
+                     int act, fg_view dst, float* bias_grad, double* work, hipStream_t stream) {
+    if (!ok_view(gsrc) || !ok_view(src) || !ok_view(dst) || !mean || !rstd || !work || src.c_alloc % 4 ||
+        (NT % (src.c_alloc / 4)) != 0 || gsrc.c_alloc != src.c_alloc || dst.c_alloc != src.c_alloc ||
+        dst.h != src.h || dst.w != src.w || dst.n != src.n)
+        return fg::fail(FG_ERR_INVALID, "fg_in_bwd: bad args");
+    if (gsrc.h != src.h + 2 * fold_pad || gsrc.w != src.w + 2 * fold_pad || fold_pad < 0 || fold_pad >= src.h ||
+        fold_pad >= src.w)
+        return fg::fail(FG_ERR_INVALID, "fg_in_bwd: gsrc %dx%d vs src %dx%d fold %d", gsrc.h, gsrc.w, src.h, src.w,
+                        fold_pad);
+    if (gadd.ptr && (gadd.c_alloc != src.c_alloc || gadd.h != src.h || gadd.w != src.w))
+        return fg::fail(FG_ERR_INVALID, "fg_in_bwd: gadd shape");
+    const int chunks = choose_chunks(src.n, (long long)src.h * src.w);
+    const int C = src.c_alloc;
+    float* coef = reinterpret_cast<float*>(work + (size_t)src.n * C * MAX_CHUNKS * 3);
+    hipLaunchKernelGGL(in_bwd_stats_kernel, dim3(chunks, src.n), dim3(NT), 0, stream, gsrc, fold_pad, gadd, src,
+                       mean, rstd, act, chunks, work);
+    int e = fg::launched("in_bwd_stats");
+    if (e) return e;
+    hipLaunchKernelGGL(in_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, src.n, C,
+                       src.h * src.w, chunks, work, rstd, coef, bias_grad);
+    e = fg::launched("in_bwd_finalize");
+    if (e) return e;
+    const long long total = (long long)dst.n * (dst.h + 2 * dst.pad) * (dst.w + 2 * dst.pad) * (C / 4);
+    hipLaunchKernelGGL(in_bwd_apply_kernel, dim3(fg::blocks_for(total, 256, 16384)), dim3(256), 0, stream, gsrc,
+                       fold_pad, gadd, src, mean, rstd, coef, act, dst);
+    return fg::launched("in_bwd_apply");
+}
+
+FG_API int fg_act_bwd(fg_view g, fg_view y, int act, hipStream_t stream) {
+    if (!ok_view(g) || !ok_view(y) || g.c_alloc != y.c_alloc || g.h != y.h || g.w != y.w || g.n != y.n)
+        return fg::fail(FG_ERR_INVALID, "fg_act_bwd: bad args");
+    const long long total = (long long)g.n * g.h * g.w * g.c_alloc;
+    hipLaunchKernelGGL(act_bwd_kernel, dim3(fg::blocks_for(total, 256, 16384)), dim3(256), 0, stream, g, y, act);
+    return fg::launched("act_bwd");
+}
+
+FG_API int fg_channel_sum(fg_view src, int c_valid, float* out, int accumulate, double* work, hipStream_t stream) {
+    if (!ok_view(src) || !out || !work || c_valid < 1 || c_valid > src.c_alloc)
+        return fg::fail(FG_ERR_INVALID, "fg_channel_sum: bad args");
+    const long long P = (long long)src.n * src.h * src.w;
+    int chunks = (int)((P + 4095) / 4096);
+    if (chunks > MAX_CHUNKS) chunks = MAX_CHUNKS;
+    if (chunks < 1) chunks = 1;
+    const int groups = (c_valid + NT - 1) / NT;
+    hipLaunchKernelGGL(channel_sum_kernel, dim3(chunks, groups), dim3(NT), 0, stream, src, c_valid, chunks, work);
+    int e = fg::launched("channel_sum");
+    if (e) return e;
+    hipLaunchKernelGGL(channel_sum_finalize, dim3((c_valid + 255) / 256), dim3(256), 0, stream, c_valid, chunks,
+                       work, out, accumulate);
+    return fg::launched("channel_sum_finalize");
+}

@@ -1,0 +1,43 @@
+// Library plumbing: error reporting, version, device check.
+#include <string.h>
+#include <string>
+
+#include "fg_common.hpp"
+
+namespace {
+thread_local char g_err[1024] = "";
+}
+
+namespace fg {
+
+int fail(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code == 0 ? FG_ERR_INVALID : code;
+}
+
+int launched(const char* what) {
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail((int)e, "%s: launch failed: %s", what, hipGetErrorString(e));
+    return 0;
+}
+
+}  // namespace fg
+
+FG_API const char* fg_last_error(void) { return g_err; }
+
+FG_API int fg_version(void) { return 1; }
+
+FG_API int fg_device_ok(void) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return fg::fail((int)e, "hipGetDevice: %s", hipGetErrorString(e));
+    hipDeviceProp_t prop;
+    e = hipGetDeviceProperties(&prop, dev);
+    if (e != hipSuccess) return fg::fail((int)e, "hipGetDeviceProperties: %s", hipGetErrorString(e));
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fg::fail(FG_ERR_INVALID, "device %d is %s, this build targets gfx950 only", dev, prop.gcnArchName);
+    return 0;
+}

@@ -1,0 +1,133 @@
+// Generator tail (models/model_architectures.py:352-399): tanh over the 27 content logits,
+// softmax over the 10 attention logits, composite
+//     out[c] = sum_{i<9} tanh(cl[3i+c]) * att[i]  +  input[c] * att[9]
+// (summed left to right as the reference does) and last_attention_mask = att[9].
+// One thread per pixel; the backward recomputes tanh / softmax from the saved logits.
+#include "fg_common.hpp"
+
+namespace {
+
+constexpr int NCONT = 27, NATT = 10;
+
+struct PixelVals {
+    float t[NCONT];
+    float a[NATT];
+};
+
+__device__ __forceinline__ void load_pixel(const fg_view& cl, const fg_view& al, int n, int y, int x, PixelVals& v) {
+    const float* cp = cl.ptr + fg::vidx(cl, n, y, x);
+    const float* ap = al.ptr + fg::vidx(al, n, y, x);
+#pragma unroll
+    for (int i = 0; i < NCONT; ++i) v.t[i] = tanhf(cp[i]);
+    float mx = ap[0];
+#pragma unroll
+    for (int i = 1; i < NATT; ++i) mx = fmaxf(mx, ap[i]);
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NATT; ++i) {
+        v.a[i] = expf(ap[i] - mx);
+        s += v.a[i];
+    }
+#pragma unroll
+    for (int i = 0; i < NATT; ++i) v.a[i] = v.a[i] / s;
+}
+
+__global__ void tail_fwd_kernel(fg_view cl, fg_view al, fg_sview x, float* __restrict__ out,
+                                float* __restrict__ mask) {
+    const int H = cl.h, W = cl.w;
+    const long long total = (long long)cl.n * H * W;
+    for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const int xx = (int)(idx % W);
+        const long long t = idx / W;
+        const int yy = (int)(t % H);
+        const int n = (int)(t / H);
+        PixelVals v;
+        load_pixel(cl, al, n, yy, xx, v);
+        const long long HW = (long long)H * W;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            float o = v.t[c] * v.a[0];
+#pragma unroll
+            for (int i = 1; i < 9; ++i) o = o + v.t[3 * i + c] * v.a[i];
+            o = o + x.ptr[n * x.sn + c * x.sc + yy * x.sy + xx * x.sx] * v.a[9];
+            out[(n * 3 + c) * HW + yy * W + xx] = o;
+        }
+        mask[n * HW + yy * W + xx] = v.a[9];
+    }
+}
+
+__global__ void tail_bwd_kernel(fg_view cl, fg_view al, fg_sview x, fg_sview gout, fg_view gc, fg_view ga) {
+    // iterate over gc's padded extent so its zero border is written too
+    const int H = cl.h, W = cl.w;
+    const int hp = H + 2 * gc.pad, wp = W + 2 * gc.pad;
+    const long long total = (long long)cl.n * hp * wp;
+    for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const int xp = (int)(idx % wp);
+        const long long t = idx / wp;
+        const int yp = (int)(t % hp);
+        const int n = (int)(t / hp);
+        const int yy = yp - gc.pad, xx = xp - gc.pad;
+        float* gcp = gc.ptr + ((size_t)(n * hp + yp) * wp + xp) * gc.c_alloc;
+        if (yy < 0 || yy >= H || xx < 0 || xx >= W) {
+            for (int i = 0; i < gc.c_alloc; ++i) gcp[i] = 0.f;
+            continue;
+        }
+        PixelVals v;
+        load_pixel(cl, al, n, yy, xx, v);
+        float g[3], xin[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            g[c] = gout.ptr[n * gout.sn + c * gout.sc + yy * gout.sy + xx * gout.sx];
+            xin[c] = x.ptr[n * x.sn + c * x.sc + yy * x.sy + xx * x.sx];
+        }
+        float gatt[NATT];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            gatt[i] = g[0] * v.t[3 * i] + g[1] * v.t[3 * i + 1] + g[2] * v.t[3 * i + 2];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                const float tt = v.t[3 * i + c];
+                gcp[3 * i + c] = g[c] * v.a[i] * (1.f - tt * tt);
+            }
+        }
+        gatt[9] = g[0] * xin[0] + g[1] * xin[1] + g[2] * xin[2];
+        for (int i = NCONT; i < gc.c_alloc; ++i) gcp[i] = 0.f;
+        float dot = 0.f;
+#pragma unroll
+        for (int i = 0; i < NATT; ++i) dot += v.a[i] * gatt[i];
+        float* gap = ga.ptr + fg::vidx(ga, n, yy, xx);
+#pragma unroll
+        for (int i = 0; i < NATT; ++i) gap[i] = v.a[i] * (gatt[i] - dot);
+        for (int i = NATT; i < ga.c_alloc; ++i) gap[i] = 0.f;
+    }
+}
+
+}  // namespace
+
+FG_API int fg_tail_fwd(fg_view content_logits, fg_view att_logits, fg_sview x, float* out, float* mask,
+                       hipStream_t stream) {
+    if (!content_logits.ptr || !att_logits.ptr || !x.ptr || !out || !mask || content_logits.c_alloc < NCONT ||
+        att_logits.c_alloc < NATT || att_logits.h != content_logits.h || att_logits.w != content_logits.w ||
+        att_logits.n != content_logits.n)
+        return fg::fail(FG_ERR_INVALID, "fg_tail_fwd: bad args");
+    const long long total = (long long)content_logits.n * content_logits.h * content_logits.w;
+    hipLaunchKernelGGL(tail_fwd_kernel, dim3(fg::blocks_for(total, 256, 16384)), dim3(256), 0, stream,
+                       content_logits, att_logits, x, out, mask);
+    return fg::launched("tail_fwd");
+}
+
+FG_API int fg_tail_bwd(fg_view content_logits, fg_view att_logits, fg_sview x, fg_sview g_out, fg_view g_content,
+                       fg_view g_att, hipStream_t stream) {
+    if (!content_logits.ptr || !att_logits.ptr || !x.ptr || !g_out.ptr || !g_content.ptr || !g_att.ptr ||
+        g_content.c_alloc < NCONT || g_att.c_alloc < NATT || g_content.h != content_logits.h ||
+        g_content.w != content_logits.w || g_att.h != content_logits.h || g_att.w != content_logits.w ||
+        g_att.pad != 0)
+        return fg::fail(FG_ERR_INVALID, "fg_tail_bwd: bad args");
+    const long long total = (long long)content_logits.n * (content_logits.h + 2 * g_content.pad) *
+                            (content_logits.w + 2 * g_content.pad);
+    hipLaunchKernelGGL(tail_bwd_kernel, dim3(fg::blocks_for(total, 256, 16384)), dim3(256), 0, stream,
+                       content_logits, att_logits, x, g_out, g_content, g_att);
+    return fg::launched("tail_bwd");
+}

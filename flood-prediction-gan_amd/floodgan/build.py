@@ -1,0 +1,79 @@
+"""Build libfloodgan.so (HIP kernels + C-ABI) in-tree for gfx950 with hipcc.
+
+The library lands at floodgan/lib/libfloodgan.so so that it travels with the repository
+snapshot to the GPU box (it is git-ignored, not gpurun-ignored).
+"""
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(PKG)                       # flood-prediction-gan_amd/
+REPO = os.path.dirname(PKG_ROOT)
+CSRC = os.path.join(PKG_ROOT, "csrc")
+INCLUDE = os.path.join(REPO, "include")
+LIBDIR = os.path.join(PKG, "lib")
+LIB = os.path.join(LIBDIR, "libfloodgan.so")
+OBJDIR = os.path.join(PKG_ROOT, "build")
+
+ARCH = "gfx950"
+CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-fvisibility=hidden",
+          "-Wall", "-Wno-unused-variable", "-Wno-unused-but-set-variable", "-I", INCLUDE, "-I", CSRC]
+
+
+def hipcc():
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found (ROCm toolchain required to build floodgan)")
+
+
+def sources():
+    return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hip"))
+
+
+def _headers_mtime():
+    hs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hpp", ".h"))]
+    hs += [os.path.join(INCLUDE, f) for f in os.listdir(INCLUDE) if f.endswith(".h")]
+    return max(os.path.getmtime(h) for h in hs)
+
+
+def _compile(src, extra):
+    obj = os.path.join(OBJDIR, os.path.basename(src) + ".o")
+    if (os.path.exists(obj) and os.path.getmtime(obj) >= os.path.getmtime(src)
+            and os.path.getmtime(obj) >= _headers_mtime()):
+        return obj, None
+    cmd = [hipcc()] + CFLAGS + extra + ["-c", src, "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        return obj, f"$ {' '.join(cmd)}\n{r.stdout}\n{r.stderr}"
+    return obj, None
+
+
+def build(verbose=False, extra=(), jobs=None):
+    os.makedirs(OBJDIR, exist_ok=True)
+    os.makedirs(LIBDIR, exist_ok=True)
+    srcs = sources()
+    jobs = jobs or min(len(srcs), max(1, min(16, os.cpu_count() or 4)))
+    with cf.ThreadPoolExecutor(jobs) as ex:
+        results = list(ex.map(lambda s: _compile(s, list(extra)), srcs))
+    errs = [e for _, e in results if e]
+    if errs:
+        raise RuntimeError("hipcc failed:\n" + "\n".join(errs))
+    objs = [o for o, _ in results]
+    if os.path.exists(LIB) and os.path.getmtime(LIB) >= max(os.path.getmtime(o) for o in objs):
+        return LIB
+    cmd = [hipcc(), "-shared", f"--offload-arch={ARCH}", "-fPIC", "-o", LIB + ".tmp"] + objs
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n$ {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    os.replace(LIB + ".tmp", LIB)
+    if verbose:
+        print("built", LIB, file=sys.stderr)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(verbose=True))

@@ -1,0 +1,374 @@
+"""Native forward / backward executors of the PairedAttention generator and discriminator.
+
+These run the whole network as a fixed sequence of libfloodgan kernels over NHWC buffers
+(floodgan.plans.Buf), saving exactly the activations the explicit backward needs.  Both the
+autograd-facing drop-in modules (floodgan.model_architectures) and the fused training step
+(floodgan.model.paired_step) are built on them.
+
+Reference: models/model_architectures.py:339-400 (generator forward), :412-418 (resnet
+block), :424-441 (discriminator); backward = autograd of those graphs.
+"""
+import torch
+
+from . import ops
+from . import plans as PL
+from ._lib import FG_ACT_LRELU, FG_ACT_NONE, FG_ACT_RELU, FG_PAD_REFLECT, FG_PAD_ZERO, require_device
+from .plans import Buf
+
+N_BLOCKS = 9
+CONTENT_ALLOC = 32   # 27 content channels, padded for aligned NHWC rows
+ATT_ALLOC = 16       # 10 attention channels
+
+
+def _blk(i, j):
+    return f"resnet_blocks.{i}.conv{j}"
+
+
+def generator_param_names():
+    names = ["conv1", "conv2", "conv3"] + [_blk(i, j) for i in range(N_BLOCKS) for j in (1, 2)]
+    names += ["deconv1_content", "deconv2_content", "deconv3_content",
+              "deconv1_attention", "deconv2_attention", "deconv3_attention"]
+    return names
+
+
+DISC_LAYERS = ["model.0", "model.2", "model.5", "model.8", "model.11"]
+
+
+class _Grads:
+    """Destination of parameter gradients: either fresh tensors (autograd path) or
+    preallocated .grad tensors (fused step)."""
+
+    def __init__(self, params, into=None):
+        self.params, self.into = params, into
+        self.out = {}
+
+    def get(self, name):
+        if name not in self.out:
+            p = self.params[name]
+            if self.into is not None and name in self.into:
+                self.out[name] = self.into[name]
+            else:
+                self.out[name] = torch.empty_like(p)
+        return self.out[name]
+
+
+# ======================================================================================
+# generator
+# ======================================================================================
+
+def _conv_fwd(P, name, X, pad, k, stride, Y, act=FG_ACT_NONE, tag=None):
+    w = P[name + ".weight"]
+    m = PL.wmap_conv_fwd(w.shape, X.c)
+    ops.conv([PL.conv_problem(X, pad, k, stride, ops.pack_weight(w, m), m, Y, bias=P[name + ".bias"], act=act)],
+             tag=tag)
+
+
+def _convT_fwd(P, name, X, Y):
+    w = P[name + ".weight"]
+    maps = PL.phase_maps(w.shape, 3, 1, X.c)
+    wps = [ops.pack_weight(w, m) for m, _, _ in maps]
+    ops.conv(PL.phase_problems(X, w.shape, 3, 1, Y, wps, maps, bias=P[name + ".bias"]))
+
+
+def _norm(c, act, pad, mode, residual=None):
+    mean, rstd = ops.in_stats(c)
+    out = Buf.empty(c.n, c.h, c.w, c.c, pad, c.t.device)
+    ops.in_apply(c, mean, rstd, act, residual, out, mode)
+    return mean, rstd, out
+
+
+def gen_forward(P, x, save=True):
+    """x: [N, C, H, W] fp32 (any strides) on the device.  Returns (out [N,3,H,W], mask [N,H,W], saved)."""
+    require_device(x, "generator input")
+    N, Cin, H, W = x.shape
+    if H % 4 or W % 4 or H < 8 or W < 8:
+        raise RuntimeError(f"PairedAttentionGenerator needs H, W divisible by 4 and >= 8 (got {H}x{W})")
+    dev = x.device
+    S = {}
+    X0 = Buf.empty(N, H, W, Cin, 3, dev)
+    ops.pack_input(x, Cin, None, 0, X0, 0, N, FG_PAD_REFLECT)                 # F.pad(input, 3, reflect)
+    c1 = Buf.empty(N, H, W, 64, 0, dev)
+    _conv_fwd(P, "conv1", X0, 3, 7, 1, c1)
+    m1, r1, a1 = _norm(c1, FG_ACT_RELU, 1, FG_PAD_ZERO)
+    c2 = Buf.empty(N, H // 2, W // 2, 128, 0, dev)
+    _conv_fwd(P, "conv2", a1, 1, 3, 2, c2)
+    m2, r2, a2 = _norm(c2, FG_ACT_RELU, 1, FG_PAD_ZERO)
+    c3 = Buf.empty(N, H // 4, W // 4, 256, 0, dev)
+    _conv_fwd(P, "conv3", a2, 1, 3, 2, c3)
+    m3, r3, h = _norm(c3, FG_ACT_RELU, 1, FG_PAD_REFLECT)
+    S.update(x=x, X0=X0, c1=c1, m1=m1, r1=r1, a1=a1, c2=c2, m2=m2, r2=r2, a2=a2, c3=c3, m3=m3, r3=r3)
+    blocks = []
+    for i in range(N_BLOCKS):
+        # block output feeds the next block (reflect pad) or the deconv heads (zero pad)
+        mode = FG_PAD_REFLECT if i < N_BLOCKS - 1 else FG_PAD_ZERO
+        h, b = _block_fwd(P, f"resnet_blocks.{i}.", h, mode)
+        blocks.append(b)
+    S.update(blocks=blocks, h=h)
+    heads = {}
+    for tag, pad2, mode2 in (("content", 3, FG_PAD_REFLECT), ("attention", 0, FG_PAD_ZERO)):
+        d1 = Buf.empty(N, H // 2, W // 2, 128, 0, dev)
+        _convT_fwd(P, f"deconv1_{tag}", h, d1)
+        md1, rd1, ad1 = _norm(d1, FG_ACT_RELU, 1, FG_PAD_ZERO)
+        d2 = Buf.empty(N, H, W, 64, 0, dev)
+        _convT_fwd(P, f"deconv2_{tag}", ad1, d2)
+        md2, rd2, ad2 = _norm(d2, FG_ACT_RELU, pad2, mode2)
+        heads[tag] = dict(d1=d1, md1=md1, rd1=rd1, ad1=ad1, d2=d2, md2=md2, rd2=rd2, ad2=ad2)
+    cl = Buf.empty(N, H, W, CONTENT_ALLOC, 0, dev)
+    _conv_fwd(P, "deconv3_content", heads["content"]["ad2"], 3, 7, 1, cl)
+    al = Buf.empty(N, H, W, ATT_ALLOC, 0, dev)
+    _conv_fwd(P, "deconv3_attention", heads["attention"]["ad2"], 0, 1, 1, al)
+    out = torch.empty(N, 3, H, W, dtype=torch.float32, device=dev)
+    mask = torch.empty(N, H, W, dtype=torch.float32, device=dev)
+    ops.tail_fwd(cl, al, x, out, mask)
+    S.update(heads=heads, cl=cl, al=al)
+    return out, mask, (S if save else None)
+
+
+def _block_fwd(P, pre, h, out_mode):
+    """PairedAttentionBlock (models/model_architectures.py:412-418) over h (reflect border 1):
+    returns (block output with `out_mode` border 1, saved tensors)."""
+    N, Hh, Ww, Cc = h.n, h.h, h.w, h.c
+    dev = h.t.device
+    cb1 = Buf.empty(N, Hh, Ww, Cc, 0, dev)
+    _conv_fwd(P, pre + "conv1", h, 1, 3, 1, cb1, tag="resblock_conv_fwd")
+    mb1, rb1, rb = _norm(cb1, FG_ACT_RELU, 1, FG_PAD_REFLECT)
+    cb2 = Buf.empty(N, Hh, Ww, Cc, 0, dev)
+    _conv_fwd(P, pre + "conv2", rb, 1, 3, 1, cb2, tag="resblock_conv_fwd")
+    mb2, rb2, hn = _norm(cb2, FG_ACT_NONE, 1, out_mode, residual=h)
+    return hn, dict(h=h, cb1=cb1, mb1=mb1, rb1=rb1, rb=rb, cb2=cb2, mb2=mb2, rb2=rb2)
+
+
+def _block_bwd(P, pre, b, g_h, G):
+    """Backward of _block_fwd: g_h = dL/d(block output) (compact) -> dL/d(block input)."""
+    N, Hh, Ww, Cc = g_h.n, g_h.h, g_h.w, g_h.c
+    dev = g_h.t.device
+    g_cb2 = Buf.empty(N, Hh, Ww, Cc, 2, dev)          # zero border 2: full correlation of a 3x3
+    ops.in_bwd(g_h, 0, None, b["cb2"], b["mb2"], b["rb2"], FG_ACT_NONE, g_cb2, G.get(pre + "conv2.bias"))
+    _wgrad_conv(P, G, pre + "conv2", g_cb2, b["rb"], 1, 3, 1)
+    g_rbp = Buf.empty(N, Hh + 2, Ww + 2, Cc, 0, dev)  # gradient w.r.t. the reflect-padded relu output
+    _dgrad_s1(P, pre + "conv2", g_cb2, 2, 3, g_rbp)
+    g_cb1 = Buf.empty(N, Hh, Ww, Cc, 2, dev)
+    ops.in_bwd(g_rbp, 1, None, b["cb1"], b["mb1"], b["rb1"], FG_ACT_RELU, g_cb1, G.get(pre + "conv1.bias"))
+    _wgrad_conv(P, G, pre + "conv1", g_cb1, b["h"], 1, 3, 1)
+    g_hp = Buf.empty(N, Hh + 2, Ww + 2, Cc, 0, dev)
+    _dgrad_s1(P, pre + "conv1", g_cb1, 2, 3, g_hp)
+    g_new = Buf.empty(N, Hh, Ww, Cc, 0, dev)
+    ops.fold_add(g_hp, 1, g_h, g_new)                 # reflect-pad adjoint + residual path
+    return g_new
+
+
+def _to_nchw(B):
+    return B.interior().permute(0, 3, 1, 2)
+
+
+def block_forward_nchw(x, params, save=True):
+    """A lone PairedAttentionBlock on an NCHW tensor (params: w1, b1, w2, b2)."""
+    require_device(x, "block input")
+    N, Cc, Hh, Ww = x.shape
+    P = {"conv1.weight": params["w1"], "conv1.bias": params["b1"],
+         "conv2.weight": params["w2"], "conv2.bias": params["b2"]}
+    h = Buf.empty(N, Hh, Ww, Cc, 1, x.device)
+    ops.pack_input(x, Cc, None, 0, h, 0, N, FG_PAD_REFLECT)
+    hn, b = _block_fwd(P, "", h, FG_PAD_ZERO)
+    return _to_nchw(hn), (dict(P=P, b=b) if save else None)
+
+
+def block_backward_nchw(S, g, need_input=True):
+    N, Cc, Hh, Ww = g.shape
+    gb = Buf.empty(N, Hh, Ww, Cc, 0, g.device)
+    ops.pack_input(g, Cc, None, 0, gb, 0, N, FG_PAD_ZERO)
+    G = _Grads(S["P"])
+    g_new = _block_bwd(S["P"], "", S["b"], gb, G)
+    grads = {"w1": G.out["conv1.weight"], "b1": G.out["conv1.bias"],
+             "w2": G.out["conv2.weight"], "b2": G.out["conv2.bias"]}
+    return (_to_nchw(g_new) if need_input else None), grads
+
+
+def _wgrad_conv(P, G, name, gy, X, pad, k, stride):
+    w = P[name + ".weight"]
+    ops.wgrad(PL.wgrad_conv(gy, X, pad, k, stride, w.shape[0]), PL.wmap_wgrad(w.shape, True, X.c, k),
+              G.get(name + ".weight"))
+
+
+def _dgrad_s1(P, name, gyp, pad_used, k, Y):
+    w = P[name + ".weight"]
+    m = PL.wmap_conv_dgrad_s1(w.shape, gyp.c)
+    ops.conv([PL.conv_problem(gyp, pad_used, k, 1, ops.pack_weight(w, m), m, Y)])
+
+
+def _dgrad_s2(P, name, gy, k, Y=None, y_nchw=None, n_base=0, n_out=None, accumulate=0):
+    w = P[name + ".weight"]
+    maps = PL.phase_maps(w.shape, k, 1, gy.c, n_base=n_base, n_out=n_out)
+    wps = [ops.pack_weight(w, m) for m, _, _ in maps]
+    ops.conv(PL.phase_problems(gy, w.shape, k, 1, Y, wps, maps, y_nchw=y_nchw, accumulate=accumulate))
+
+
+def gen_backward(P, S, g_out, grads_into=None):
+    """Explicit backward of gen_forward.  g_out: [N,3,H,W] (any strides).  Returns
+    {param name: grad} (written into grads_into[name] when given)."""
+    G = _Grads(P, grads_into)
+    x = S["x"]
+    N, _, H, W = x.shape
+    dev = x.device
+    # ---- tail: tanh / softmax / composite backward (models/model_architectures.py:352-399)
+    cl, al = S["cl"], S["al"]
+    gcl = Buf.empty(N, H, W, CONTENT_ALLOC, 6, dev)     # zero border 6 = full correlation of a 7x7
+    gal = Buf.empty(N, H, W, ATT_ALLOC, 0, dev)
+    ops.tail_bwd(cl, al, x, g_out, gcl, gal)
+    hc, ha = S["heads"]["content"], S["heads"]["attention"]
+    # ---- deconv3_content: 7x7 over reflect-padded (3) ad2
+    _wgrad_conv(P, G, "deconv3_content", gcl, hc["ad2"], 3, 7, 1)
+    ops.channel_sum(gcl, 27, G.get("deconv3_content.bias"))
+    g_ad2c = Buf.empty(N, H + 6, W + 6, 64, 0, dev)     # gradient w.r.t. the PADDED input
+    _dgrad_s1(P, "deconv3_content", gcl, 6, 7, g_ad2c)
+    # ---- deconv3_attention: 1x1
+    _wgrad_conv(P, G, "deconv3_attention", gal, ha["ad2"], 0, 1, 1)
+    ops.channel_sum(gal, 10, G.get("deconv3_attention.bias"))
+    g_ad2a = Buf.empty(N, H, W, 64, 0, dev)
+    _dgrad_s1(P, "deconv3_attention", gal, 0, 1, g_ad2a)
+    # ---- deconv2 / deconv1 of both heads
+    g_h = Buf.empty(N, H // 4, W // 4, 256, 0, dev)
+    for idx, (tag, hd, g_ad2, fold) in enumerate((("content", hc, g_ad2c, 3), ("attention", ha, g_ad2a, 0))):
+        g_d2 = Buf.empty(N, H, W, 64, 1, dev)
+        ops.in_bwd(g_ad2, fold, None, hd["d2"], hd["md2"], hd["rd2"], FG_ACT_RELU, g_d2,
+                   G.get(f"deconv2_{tag}.bias"))
+        name = f"deconv2_{tag}"
+        w = P[name + ".weight"]
+        ops.wgrad(PL.wgrad_convT(hd["ad1"], g_d2, 3, 1, w.shape[0]), PL.wmap_wgrad(w.shape, True, g_d2.c, 3),
+                  G.get(name + ".weight"))
+        g_ad1 = Buf.empty(N, H // 2, W // 2, 128, 0, dev)
+        m = PL.wmap_convT_dgrad(w.shape, g_d2.c)
+        ops.conv([PL.conv_problem(g_d2, 1, 3, 2, ops.pack_weight(w, m), m, g_ad1)])
+        g_d1 = Buf.empty(N, H // 2, W // 2, 128, 1, dev)
+        ops.in_bwd(g_ad1, 0, None, hd["d1"], hd["md1"], hd["rd1"], FG_ACT_RELU, g_d1, G.get(f"deconv1_{tag}.bias"))
+        name = f"deconv1_{tag}"
+        w = P[name + ".weight"]
+        ops.wgrad(PL.wgrad_convT(S["h"], g_d1, 3, 1, w.shape[0]), PL.wmap_wgrad(w.shape, True, g_d1.c, 3),
+                  G.get(name + ".weight"))
+        m = PL.wmap_convT_dgrad(w.shape, g_d1.c)
+        ops.conv([PL.conv_problem(g_d1, 1, 3, 2, ops.pack_weight(w, m), m, g_h, accumulate=idx)])
+    # ---- resnet blocks in reverse: out = h + IN(conv2(pad(relu(IN(conv1(pad(h)))))))
+    for i in reversed(range(N_BLOCKS)):
+        g_h = _block_bwd(P, f"resnet_blocks.{i}.", S["blocks"][i], g_h, G)
+    # ---- encoder
+    g_c3 = Buf.empty(N, H // 4, W // 4, 256, 1, dev)
+    ops.in_bwd(g_h, 0, None, S["c3"], S["m3"], S["r3"], FG_ACT_RELU, g_c3, G.get("conv3.bias"))
+    _wgrad_conv(P, G, "conv3", g_c3, S["a2"], 1, 3, 2)
+    g_a2 = Buf.empty(N, H // 2, W // 2, 128, 0, dev)
+    _dgrad_s2(P, "conv3", g_c3, 3, Y=g_a2)
+    g_c2 = Buf.empty(N, H // 2, W // 2, 128, 1, dev)
+    ops.in_bwd(g_a2, 0, None, S["c2"], S["m2"], S["r2"], FG_ACT_RELU, g_c2, G.get("conv2.bias"))
+    _wgrad_conv(P, G, "conv2", g_c2, S["a1"], 1, 3, 2)
+    g_a1 = Buf.empty(N, H, W, 64, 0, dev)
+    _dgrad_s2(P, "conv2", g_c2, 3, Y=g_a1)
+    g_c1 = Buf.empty(N, H, W, 64, 0, dev)
+    ops.in_bwd(g_a1, 0, None, S["c1"], S["m1"], S["r1"], FG_ACT_RELU, g_c1, G.get("conv1.bias"))
+    _wgrad_conv(P, G, "conv1", g_c1, S["X0"], 3, 7, 1)
+    return G.out
+
+
+# ======================================================================================
+# discriminator
+# ======================================================================================
+
+def disc_pack(pairs, c_in_total):
+    """Stack (a [N,Ca,H,W], b [N,Cb,H,W] or None) pairs along the batch into one zero-padded
+    NHWC input buffer (torch.cat((a, b), 1) of models/model.py:616-617, fused)."""
+    a0 = pairs[0][0]
+    N = sum(a.shape[0] for a, _ in pairs)
+    H, W = a0.shape[2], a0.shape[3]
+    buf = Buf.empty(N, H, W, c_in_total, 1, a0.device)
+    img0 = 0
+    for a, b in pairs:
+        require_device(a, "discriminator input")
+        cb = 0 if b is None else b.shape[1]
+        ops.pack_input(a, a.shape[1], b, cb, buf, img0, a.shape[0], FG_PAD_ZERO)
+        img0 += a.shape[0]
+    return buf
+
+
+def disc_forward(P, inp, save=True):
+    """inp: Buf from disc_pack (zero border 1).  Returns (pred [N,1,ho,wo], saved)."""
+    N, H, W = inp.n, inp.h, inp.w
+    dev = inp.t.device
+    if H < 24 or W < 24:
+        raise RuntimeError(f"PairedAttentionDiscriminator needs H, W >= 24 (got {H}x{W})")
+    h1, w1 = PL.out_size(H, 4, 2, 1), PL.out_size(W, 4, 2, 1)
+    e0 = Buf.empty(N, h1, w1, 64, 1, dev)              # conv + bias + LeakyReLU fused, zero border
+    _conv_fwd(P, "model.0", inp, 1, 4, 2, e0, act=FG_ACT_LRELU)
+    ops.zero_border(e0)
+    h2, w2 = PL.out_size(h1, 4, 2, 1), PL.out_size(w1, 4, 2, 1)
+    e1 = Buf.empty(N, h2, w2, 128, 0, dev)
+    _conv_fwd(P, "model.2", e0, 1, 4, 2, e1)
+    m1, r1, a1 = _norm(e1, FG_ACT_LRELU, 1, FG_PAD_ZERO)
+    h3, w3 = PL.out_size(h2, 4, 2, 1), PL.out_size(w2, 4, 2, 1)
+    e2 = Buf.empty(N, h3, w3, 256, 0, dev)
+    _conv_fwd(P, "model.5", a1, 1, 4, 2, e2)
+    m2, r2, a2 = _norm(e2, FG_ACT_LRELU, 1, FG_PAD_ZERO)
+    h4, w4 = PL.out_size(h3, 4, 1, 1), PL.out_size(w3, 4, 1, 1)
+    e3 = Buf.empty(N, h4, w4, 512, 0, dev)
+    _conv_fwd(P, "model.8", a2, 1, 4, 1, e3)
+    m3, r3, a3 = _norm(e3, FG_ACT_LRELU, 1, FG_PAD_ZERO)
+    h5, w5 = PL.out_size(h4, 4, 1, 1), PL.out_size(w4, 4, 1, 1)
+    pred = torch.empty(N, 1, h5, w5, dtype=torch.float32, device=dev)
+    _conv_fwd(P, "model.11", a3, 1, 4, 1, Buf(pred.view(-1), N, h5, w5, 1, 0))
+    S = dict(inp=inp, e0=e0, e1=e1, m1=m1, r1=r1, a1=a1, e2=e2, m2=m2, r2=r2, a2=a2, e3=e3, m3=m3, r3=r3, a3=a3)
+    return pred, (S if save else None)
+
+
+def disc_backward(P, S, g_pred, param_grads=True, grads_into=None, input_grad=None, input_grad_channels=None,
+                  input_grad_accumulate=False):
+    """Explicit backward of disc_forward.
+    param_grads: compute weight / bias gradients (False in the generator step, where D is
+    frozen: models/model.py:636-637).  input_grad: NCHW tensor receiving dL/d(input
+    channels input_grad_channels=(start, count)), written or accumulated."""
+    G = _Grads(P, grads_into)
+    inp = S["inp"]
+    N = inp.n
+    dev = inp.t.device
+    a3 = S["a3"]
+    h5, w5 = g_pred.shape[2], g_pred.shape[3]
+    g11 = Buf.empty(N, h5, w5, 1, 2, dev)
+    ops.pack_input(g_pred, 1, None, 0, g11, 0, N, FG_PAD_ZERO)
+    if param_grads:
+        _wgrad_conv(P, G, "model.11", g11, a3, 1, 4, 1)
+        ops.channel_sum(g11, 1, G.get("model.11.bias"))
+    g_a3 = Buf.empty(N, a3.h, a3.w, 512, 0, dev)
+    _dgrad_s1(P, "model.11", g11, 2, 4, g_a3)
+    # model.8 (k4 s1 p1) + IN + LReLU
+    g_e3 = Buf.empty(N, a3.h, a3.w, 512, 2, dev)
+    ops.in_bwd(g_a3, 0, None, S["e3"], S["m3"], S["r3"], FG_ACT_LRELU, g_e3,
+               G.get("model.8.bias") if param_grads else None)
+    a2 = S["a2"]
+    if param_grads:
+        _wgrad_conv(P, G, "model.8", g_e3, a2, 1, 4, 1)
+    g_a2 = Buf.empty(N, a2.h, a2.w, 256, 0, dev)
+    _dgrad_s1(P, "model.8", g_e3, 2, 4, g_a2)
+    # model.5 (k4 s2 p1)
+    g_e2 = Buf.empty(N, a2.h, a2.w, 256, 1, dev)
+    ops.in_bwd(g_a2, 0, None, S["e2"], S["m2"], S["r2"], FG_ACT_LRELU, g_e2,
+               G.get("model.5.bias") if param_grads else None)
+    a1 = S["a1"]
+    if param_grads:
+        _wgrad_conv(P, G, "model.5", g_e2, a1, 1, 4, 2)
+    g_a1 = Buf.empty(N, a1.h, a1.w, 128, 0, dev)
+    _dgrad_s2(P, "model.5", g_e2, 4, Y=g_a1)
+    # model.2
+    g_e1 = Buf.empty(N, a1.h, a1.w, 128, 1, dev)
+    ops.in_bwd(g_a1, 0, None, S["e1"], S["m1"], S["r1"], FG_ACT_LRELU, g_e1,
+               G.get("model.2.bias") if param_grads else None)
+    e0 = S["e0"]
+    if param_grads:
+        _wgrad_conv(P, G, "model.2", g_e1, e0, 1, 4, 2)
+    g_e0 = Buf.empty(N, e0.h, e0.w, 64, 1, dev)
+    _dgrad_s2(P, "model.2", g_e1, 4, Y=g_e0)
+    ops.zero_border(g_e0)
+    ops.act_bwd(Buf(g_e0.t, N, e0.h, e0.w, 64, 1), e0, FG_ACT_LRELU)      # through LeakyReLU of model.1
+    if param_grads:
+        _wgrad_conv(P, G, "model.0", g_e0, inp, 1, 4, 2)
+        ops.channel_sum(g_e0, 64, G.get("model.0.bias"))
+    if input_grad is not None:
+        c0, cn = input_grad_channels
+        _dgrad_s2(P, "model.0", g_e0, 4, y_nchw=(input_grad.view(-1), cn, inp.h, inp.w), n_base=c0, n_out=cn,
+                  accumulate=int(input_grad_accumulate))
+    return G.out

@@ -1,0 +1,208 @@
+"""Training orchestration for the PairedAttention path, mirroring the reference's
+`Model` (models/model.py:26-160) and `Model.train_paired` (models/model.py:598-658).
+
+`PairedStep` is the fused device iteration: the exact sequence of models/model.py:615-646
+(G forward; D step on fake(detached)+real with LSGAN MSE x0.5 and Adam(D); G step on the
+UPDATED D with MSE(D(fake),1) + 100*L1 and Adam(G)) executed by the native executors with
+no autograd graph, one fused 2N-image discriminator pass for the D step (InstanceNorm is
+per-sample, so D(fake) and D(real) in one batch is the same computation), fused losses and
+FusedAdam.  With torch.distributed initialised it performs batch-DP over RCCL.
+"""
+import time
+
+import numpy as np
+import torch
+from torch import nn
+from torch.optim import lr_scheduler
+
+from . import executor as X
+from . import ops
+from .model_architectures import PairedAttentionDiscriminator, PairedAttentionGenerator
+from .optim import FusedAdam
+from .parallel import FlatGrads, world
+
+TOPOGRAPHY_CHANNELS = {"all": 9, "map": 6, "dem": 4, "flow": 4, "river": 4, None: 3}
+
+
+class PairedStep:
+    """One paired-GAN training iteration on device tensors x [N,C,H,W], y [N,3,H,W].
+    Returns a device tensor [D real, D synthetic, G synthetic, 100*L1] (models/model.py:648-651)."""
+
+    def __init__(self, generator, discriminator, opt_g, opt_d, group=None):
+        self.G, self.D = generator, discriminator
+        self.opt_g, self.opt_d = opt_g, opt_d
+        self.gp, self.dp = generator.param_dict(), discriminator.param_dict()
+        self.gflat, self.dflat = FlatGrads(self.gp.values()), FlatGrads(self.dp.values())
+        self.group = group
+        self.last_mask = None
+        self.last_output = None
+
+    def __call__(self, x, y):
+        ws, _ = world()
+        inv = 1.0 / ws
+        N = x.shape[0]
+        dev = x.device
+        C = x.shape[1]
+        losses = torch.empty(4, dtype=torch.float32, device=dev)
+        self.gflat.attach()
+        self.dflat.attach()
+        # generator forward                                           (models/model.py:615)
+        fake, mask, gS = X.gen_forward(self.gp, x, save=True)
+        # ---- discriminator step: fake (detached) and real in one 2N batch   (:620-633)
+        dinp = X.disc_pack([(x, fake), (x, y)], C + 3)
+        pred, dS = X.disc_forward(self.dp, dinp, save=True)
+        g_pred = torch.empty_like(pred)
+        ops.mse_const(pred[:N], 0.0, 0.5 * inv, losses[1:2], g_pred[:N])
+        ops.mse_const(pred[N:], 1.0, 0.5 * inv, losses[0:1], g_pred[N:])
+        X.disc_backward(self.dp, dS, g_pred, param_grads=True, grads_into=self._grads(self.dp))
+        del dS, dinp
+        self.dflat.allreduce_sum(self.group)
+        self.opt_d.step()
+        # ---- generator step against the updated discriminator                 (:636-646)
+        dinp = X.disc_pack([(x, fake)], C + 3)
+        pred, dS = X.disc_forward(self.dp, dinp, save=True)
+        g_pred = torch.empty_like(pred)
+        ops.mse_const(pred, 1.0, inv, losses[2:3], g_pred)
+        g_fake = torch.empty(N, 3, x.shape[2], x.shape[3], dtype=torch.float32, device=dev)
+        ops.l1(fake, y, 100.0 * inv, losses[3:4], g_fake)
+        X.disc_backward(self.dp, dS, g_pred, param_grads=False, input_grad=g_fake, input_grad_channels=(C, 3),
+                        input_grad_accumulate=True)
+        del dS, dinp
+        X.gen_backward(self.gp, gS, g_fake, grads_into=self._grads(self.gp))
+        del gS
+        self.gflat.allreduce_sum(self.group)
+        self.opt_g.step()
+        self.last_mask, self.last_output = mask, fake
+        return losses * torch.tensor([1.0, 1.0, 1.0, 100.0], device=dev)
+
+    @staticmethod
+    def _grads(params):
+        return {k: p.grad for k, p in params.items()}
+
+
+class Model:
+    """Paired-path subset of the reference's Model (models/model.py:26-160) with identical
+    construction semantics (seed, initialise_weights, Adam(2e-4, (0.5, 0.999)), LambdaLR)."""
+
+    def __init__(self, model="PairedAttention", dataset_subset="all", dataset_dem="best", data_path=None,
+                 num_epochs=1, topography="all", resize=256, crop=None, save_model_interval=0,
+                 save_images_interval=0, verbose=False, load_pretrained_model=False, pretrained_model_path=None,
+                 add_identity_loss=False, training_model=True, seed=47, device="cuda", train_loader=None):
+        self.model = model.lower()
+        if self.model != "pairedattention":
+            raise NotImplementedError("floodgan implements the PairedAttention paired training path; "
+                                      f"'{model}' is out of scope (SURVEY.md §2)")
+        saved = None
+        if load_pretrained_model:
+            saved = torch.load(pretrained_model_path, map_location="cpu", weights_only=True)
+            self.num_epochs, self.topography = saved["num_epochs"], saved["topography"]
+            self.add_identity_loss = saved["add_identity_loss"]
+        else:
+            self.num_epochs, self.topography, self.add_identity_loss = num_epochs, topography, add_identity_loss
+        self.verbose, self.save_model_interval = verbose, save_model_interval
+        self.save_images_interval = save_images_interval
+        self.load_pretrained_model, self.data_path = load_pretrained_model, data_path
+        self.dataset_subset, self.dataset_dem, self.resize, self.crop = dataset_subset, dataset_dem, resize, crop
+        self.training_model, self.seed, self.device = training_model, seed, device
+        self.model_is_cycle, self.model_is_attention = False, True
+
+        input_channels = TOPOGRAPHY_CHANNELS[self.topography]
+        torch.manual_seed(self.seed)
+        self.generator = PairedAttentionGenerator(input_channels=input_channels).apply(
+            self.initialise_weights).to(device)
+        if self.training_model:
+            self.discriminator = PairedAttentionDiscriminator(input_channels=input_channels).apply(
+                self.initialise_weights).to(device)
+            self.optimizer_discriminator = FusedAdam(self.discriminator.parameters(), lr=0.0002, betas=(0.5, 0.999))
+            self.optimizer_generator = FusedAdam(self.generator.parameters(), lr=0.0002, betas=(0.5, 0.999))
+            self.scheduler_generator = lr_scheduler.LambdaLR(self.optimizer_generator, lr_lambda=self.lambda_rule)
+            self.scheduler_discriminator = lr_scheduler.LambdaLR(self.optimizer_discriminator,
+                                                                 lr_lambda=self.lambda_rule)
+        if saved is not None:
+            self.starting_epoch, self.all_losses = saved["starting_epoch"], saved["all_losses"]
+            self.generator.load_state_dict(saved["generator"])
+            if self.training_model:
+                self.discriminator.load_state_dict(saved["discriminator"])
+                self.optimizer_discriminator.load_state_dict(saved["optimizer_discriminator"])
+                self.optimizer_generator.load_state_dict(saved["optimizer_generator"])
+                self.scheduler_discriminator.load_state_dict(saved["scheduler_discriminator"])
+                self.scheduler_generator.load_state_dict(saved["scheduler_generator"])
+        else:
+            self.starting_epoch = 1
+            self.all_losses = self.initialise_loss_storage(overall=True)
+        self.current_epoch = self.starting_epoch
+        # The tile pipeline (tifffile decode, resize, crop; models/data.py) is outside this
+        # build's scope: assign any iterable of (input [N,C,H,W], target [N,3,H,W], names).
+        self.train_loader = train_loader
+        self._step = None
+
+    @staticmethod
+    def initialise_weights(m):
+        """models/model.py:162-173"""
+        classname = m.__class__.__name__
+        if hasattr(m, "weight") and (classname.find("Conv") != -1 or classname.find("Linear") != -1):
+            nn.init.normal_(m.weight.data, 0.0, 0.02)
+            if hasattr(m, "bias") and m.bias is not None:
+                nn.init.constant_(m.bias.data, 0.0)
+        elif classname.find("BatchNorm2d") != -1:
+            nn.init.normal_(m.weight.data, 1.0, 0.02)
+            nn.init.constant_(m.bias.data, 0.0)
+
+    def lambda_rule(self, epoch):
+        """models/model.py:175-181"""
+        return 1.0 - max(0, epoch + 1 - (self.num_epochs / 2)) / float((self.num_epochs / 2) + 1)
+
+    def initialise_loss_storage(self, overall):
+        pre = "all_" if overall else ""
+        return {f"{pre}losses_discriminator_real": [], f"{pre}losses_discriminator_synthetic": [],
+                f"{pre}losses_generator_synthetic": [], f"{pre}l1_losses_generator_synthetic": []}
+
+    @property
+    def step_fn(self):
+        if self._step is None:
+            self._step = PairedStep(self.generator, self.discriminator, self.optimizer_generator,
+                                    self.optimizer_discriminator)
+        return self._step
+
+    def train_paired(self):
+        """models/model.py:598-658 on the fused device step."""
+        if self.train_loader is None:
+            raise RuntimeError("assign Model.train_loader (iterable of (input, target, names)) first")
+        keys = ["losses_discriminator_real", "losses_discriminator_synthetic", "losses_generator_synthetic",
+                "l1_losses_generator_synthetic"]
+        for epoch in range(self.starting_epoch, self.num_epochs + 1):
+            t0 = time.time()
+            losses = self.initialise_loss_storage(overall=False)
+            self.discriminator.train()
+            self.generator.train()
+            torch.manual_seed(epoch)
+            for input_stack, output_image, _ in self.train_loader:
+                input_stack = input_stack.to(self.device, non_blocking=True)
+                output_image = output_image.to(self.device, non_blocking=True)
+                vals = self.step_fn(input_stack, output_image).cpu().tolist()
+                for k, v in zip(keys, vals):
+                    losses[k].append(v)
+            self.scheduler_discriminator.step()
+            self.scheduler_generator.step()
+            self.save_results(epoch, losses, t0)
+
+    def save_results(self, epoch, losses, epoch_start_time):
+        """models/model.py:322-358 (loss bookkeeping + checkpoint; plots are out of scope)."""
+        self.current_epoch = epoch
+        for key in self.all_losses.keys():
+            self.all_losses[key].append(float(np.mean(losses[key[4:]])))
+        if self.verbose:
+            print(f"Epoch {epoch} ({time.time() - epoch_start_time:.2f} seconds) | "
+                  + " | ".join(f"{k} = {v[-1]:.2f}" for k, v in self.all_losses.items()))
+        if self.save_model_interval != 0 and epoch % self.save_model_interval == 0:
+            torch.save(self.checkpoint(epoch), f"{self.data_path}/models/PairedAttention_epoch{epoch}.pth.tar")
+
+    def checkpoint(self, epoch):
+        return {"model": self.model, "starting_epoch": epoch + 1, "num_epochs": self.num_epochs,
+                "topography": self.topography,
+                "optimizer_generator": self.optimizer_generator.state_dict(),
+                "optimizer_discriminator": self.optimizer_discriminator.state_dict(),
+                "scheduler_generator": self.scheduler_generator.state_dict(),
+                "scheduler_discriminator": self.scheduler_discriminator.state_dict(),
+                "all_losses": self.all_losses, "add_identity_loss": self.add_identity_loss,
+                "discriminator": self.discriminator.state_dict(), "generator": self.generator.state_dict()}

@@ -1,0 +1,172 @@
+"""Drop-in replacements for the PairedAttention modules of the reference
+(models/model_architectures.py:305-441), running on libfloodgan's HIP kernels.
+
+Same constructors, submodule names, parameter names / shapes / registration order (so
+`state_dict()` checkpoints interoperate), same RNG consumption at construction (the layers
+ARE nn.Conv2d / nn.ConvTranspose2d, so Model.initialise_weights, models/model.py:162-173,
+re-initialises them), same forward signatures and `last_attention_mask`.  Only the arithmetic
+differs: forward and backward of the whole network are single autograd nodes whose bodies
+are the native executors in floodgan.executor.  There is no CPU path: tensors must live on
+a HIP device (the modules raise otherwise).
+"""
+import torch
+import torch.nn as nn
+
+from . import executor as X
+
+
+def _gen_keys():
+    keys = []
+    for n in X.generator_param_names():
+        keys += [n + ".weight", n + ".bias"]
+    return keys
+
+
+def _disc_keys():
+    keys = []
+    for n in X.DISC_LAYERS:
+        keys += [n + ".weight", n + ".bias"]
+    return keys
+
+
+GEN_KEYS = _gen_keys()
+DISC_KEYS = _disc_keys()
+
+
+class _GeneratorFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, *params):
+        P = dict(zip(GEN_KEYS, params))
+        save = any(ctx.needs_input_grad)
+        out, mask, S = X.gen_forward(P, x, save=save)
+        ctx.P, ctx.S = P, S
+        ctx.mark_non_differentiable(mask)
+        return out, mask
+
+    @staticmethod
+    def backward(ctx, g_out, _g_mask):
+        if ctx.needs_input_grad[0]:
+            raise NotImplementedError("gradient w.r.t. the generator input is not part of the paired "
+                                      "training step (models/model.py:615-646)")
+        grads = X.gen_backward(ctx.P, ctx.S, g_out)
+        ctx.S = None
+        return (None,) + tuple(grads[k] if need else None
+                               for k, need in zip(GEN_KEYS, ctx.needs_input_grad[1:]))
+
+
+class _DiscriminatorFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, *params):
+        P = dict(zip(DISC_KEYS, params))
+        buf = X.disc_pack([(x, None)], x.shape[1])
+        pred, S = X.disc_forward(P, buf, save=any(ctx.needs_input_grad))
+        ctx.P, ctx.S, ctx.xshape = P, S, tuple(x.shape)
+        return pred
+
+    @staticmethod
+    def backward(ctx, g_pred):
+        need_params = any(ctx.needs_input_grad[1:])
+        gx = None
+        if ctx.needs_input_grad[0]:
+            N, C, H, W = ctx.xshape
+            gx = torch.empty(N, C, H, W, dtype=torch.float32, device=g_pred.device)
+        grads = X.disc_backward(ctx.P, ctx.S, g_pred.contiguous(), param_grads=need_params, input_grad=gx,
+                                input_grad_channels=(0, ctx.xshape[1]))
+        ctx.S = None
+        return (gx,) + tuple(grads.get(k) if need else None for k, need in zip(DISC_KEYS, ctx.needs_input_grad[1:]))
+
+
+class PairedAttentionGenerator(nn.Module):
+    """models/model_architectures.py:305-400 -- ResNet-9 encoder/decoder with a tanh content
+    head (27 ch) and a softmax attention head (10 ch) composited with input[:, :3]."""
+
+    def __init__(self, input_channels):
+        super().__init__()
+        self.input_channels = input_channels
+        self.last_attention_mask = None
+        self.conv1 = nn.Conv2d(input_channels, 64, kernel_size=7, stride=1, padding=0)
+        self.conv1_norm = nn.InstanceNorm2d(64)
+        self.conv2 = nn.Conv2d(64, 128, kernel_size=3, stride=2, padding=1)
+        self.conv2_norm = nn.InstanceNorm2d(128)
+        self.conv3 = nn.Conv2d(128, 256, kernel_size=3, stride=2, padding=1)
+        self.conv3_norm = nn.InstanceNorm2d(256)
+        self.resnet_blocks = nn.Sequential(*[PairedAttentionBlock(channel=256, kernel=3, stride=1, padding=1)
+                                             for _ in range(9)])
+        self.deconv1_content = nn.ConvTranspose2d(256, 128, kernel_size=3, stride=2, padding=1, output_padding=1)
+        self.deconv1_norm_content = nn.InstanceNorm2d(128)
+        self.deconv2_content = nn.ConvTranspose2d(128, 64, kernel_size=3, stride=2, padding=1, output_padding=1)
+        self.deconv2_norm_content = nn.InstanceNorm2d(64)
+        self.deconv3_content = nn.Conv2d(64, 27, kernel_size=7, stride=1, padding=0)
+        self.deconv1_attention = nn.ConvTranspose2d(256, 128, kernel_size=3, stride=2, padding=1, output_padding=1)
+        self.deconv1_norm_attention = nn.InstanceNorm2d(128)
+        self.deconv2_attention = nn.ConvTranspose2d(128, 64, kernel_size=3, stride=2, padding=1, output_padding=1)
+        self.deconv2_norm_attention = nn.InstanceNorm2d(64)
+        self.deconv3_attention = nn.Conv2d(64, 10, kernel_size=1, stride=1, padding=0)
+        self.tanh = nn.Tanh()
+        self.softmax = nn.Softmax(dim=1)
+
+    def param_dict(self):
+        sd = dict(self.named_parameters())
+        return {k: sd[k] for k in GEN_KEYS}
+
+    def forward(self, input):
+        params = [p for p in self.param_dict().values()]
+        out, mask = _GeneratorFn.apply(input, *params)
+        self.last_attention_mask = mask
+        return out
+
+
+class PairedAttentionBlock(nn.Module):
+    """models/model_architectures.py:402-418.  Inside the generator the blocks are executed by
+    the fused generator node; called on its own a block runs the same kernels through a
+    3-module generator-free path (forward only is needed by no caller of the reference)."""
+
+    def __init__(self, channel, kernel, stride, padding):
+        super().__init__()
+        self.padding = padding
+        self.conv1 = nn.Conv2d(channel, channel, kernel, stride, 0)
+        self.conv1_norm = nn.InstanceNorm2d(channel)
+        self.conv2 = nn.Conv2d(channel, channel, kernel, stride, 0)
+        self.conv2_norm = nn.InstanceNorm2d(channel)
+
+    def forward(self, input):
+        return _BlockFn.apply(input, self.conv1.weight, self.conv1.bias, self.conv2.weight, self.conv2.bias)
+
+
+class _BlockFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2):
+        out, S = X.block_forward_nchw(x, {"w1": w1, "b1": b1, "w2": w2, "b2": b2}, save=any(ctx.needs_input_grad))
+        ctx.S = S
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        gx, grads = X.block_backward_nchw(ctx.S, g, need_input=ctx.needs_input_grad[0])
+        ctx.S = None
+        return (gx,) + tuple(grads[k] if need else None
+                             for k, need in zip(("w1", "b1", "w2", "b2"), ctx.needs_input_grad[1:]))
+
+
+class PairedAttentionDiscriminator(nn.Module):
+    """models/model_architectures.py:420-441 -- 70x70 PatchGAN over input_channels + 3."""
+
+    def __init__(self, input_channels):
+        super().__init__()
+        sequence = [nn.Conv2d(input_channels + 3, 64, kernel_size=4, stride=2, padding=1), nn.LeakyReLU(0.2, True)]
+        nf_mult = 1
+        for n in range(1, 3):
+            nf_prev, nf_mult = nf_mult, min(2 ** n, 8)
+            sequence += [nn.Conv2d(64 * nf_prev, 64 * nf_mult, kernel_size=4, stride=2, padding=1, bias=True),
+                         nn.InstanceNorm2d(64 * nf_mult), nn.LeakyReLU(0.2, True)]
+        sequence += [nn.Conv2d(64 * nf_mult, 512, kernel_size=4, stride=1, padding=1, bias=True),
+                     nn.InstanceNorm2d(512), nn.LeakyReLU(0.2, True)]
+        sequence += [nn.Conv2d(512, 1, kernel_size=4, stride=1, padding=1)]
+        self.model = nn.Sequential(*sequence)
+
+    def param_dict(self):
+        sd = dict(self.named_parameters())
+        return {k: sd[k] for k in DISC_KEYS}
+
+    def forward(self, x):
+        return _DiscriminatorFn.apply(x, *self.param_dict().values())

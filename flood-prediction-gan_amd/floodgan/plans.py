@@ -1,0 +1,251 @@
+"""Convolution plans: how each conv of the hot path maps onto the implicit-GEMM engine.
+
+Pure host logic (no device calls), so it is unit-tested on the CPU against torch's own
+conv2d / conv_transpose2d through a numpy emulation of the engine's addressing
+(tests/test_plans_cpu.py).  A plan is a dict whose keys are the fields of
+fg_conv_problem / fg_wgrad_problem / fg_weight_map (include/floodgan.h); tensor operands
+are (Buf-or-tensor, element offset) pairs that floodgan.ops turns into device pointers.
+
+Reference geometry (models/model_architectures.py):
+  conv    k7 s1 reflect-p3   conv1 (:312), deconv3_content (:328)
+  conv    k3 s2 zero-p1      conv2, conv3 (:314-316)
+  conv    k3 s1 reflect-p1   PairedAttentionBlock.conv1/conv2 (:407-409, pads :413-415)
+  convT   k3 s2 p1 op1       deconv1_*, deconv2_* (:324-333)
+  conv    k1                 deconv3_attention (:334)
+  conv    k4 s2 zero-p1      discriminator model.0/2/5 (:424-433)
+  conv    k4 s1 zero-p1      discriminator model.8/11 (:435-437)
+"""
+import torch
+
+JQ = 16  # the engine's k-tile; packed kernel rows are padded to a multiple of it
+
+
+def rup(v, q=JQ):
+    return (v + q - 1) // q * q
+
+
+class Buf:
+    """NHWC fp32 activation buffer: interior h x w, `pad`-wide border, c channels/pixel,
+    backed by one flat tensor.  Element (n, y, x, ch) sits at
+    ((n*(h+2p) + y+p)*(w+2p) + x+p)*c + ch  (y, x may reach into the border)."""
+
+    __slots__ = ("t", "n", "h", "w", "c", "pad")
+
+    def __init__(self, t, n, h, w, c, pad=0):
+        assert t.numel() >= n * (h + 2 * pad) * (w + 2 * pad) * c
+        self.t, self.n, self.h, self.w, self.c, self.pad = t, n, h, w, c, pad
+
+    @classmethod
+    def empty(cls, n, h, w, c, pad=0, device="cuda"):
+        return cls(torch.empty(n * (h + 2 * pad) * (w + 2 * pad) * c, dtype=torch.float32, device=device),
+                   n, h, w, c, pad)
+
+    @classmethod
+    def zeros(cls, n, h, w, c, pad=0, device="cuda"):
+        return cls(torch.zeros(n * (h + 2 * pad) * (w + 2 * pad) * c, dtype=torch.float32, device=device),
+                   n, h, w, c, pad)
+
+    @property
+    def hp(self):
+        return self.h + 2 * self.pad
+
+    @property
+    def wp(self):
+        return self.w + 2 * self.pad
+
+    @property
+    def s_img(self):
+        return self.hp * self.wp * self.c
+
+    @property
+    def s_row(self):
+        return self.wp * self.c
+
+    def off(self, y, x):
+        """element offset of image 0, interior pixel (y, x)"""
+        return ((y + self.pad) * self.wp + (x + self.pad)) * self.c
+
+    def padded(self):
+        """the same storage seen as an unpadded buffer of the full padded extent"""
+        return Buf(self.t, self.n, self.hp, self.wp, self.c, 0)
+
+    def nhwc(self):
+        """4-D [n, hp, wp, c] tensor view of the storage (padded extent)"""
+        return self.t[: self.n * self.s_img].view(self.n, self.hp, self.wp, self.c)
+
+    def interior(self):
+        """[n, h, w, c] view of the interior"""
+        p = self.pad
+        return self.nhwc()[:, p:p + self.h, p:p + self.w, :]
+
+    def __repr__(self):
+        return f"Buf(n={self.n}, h={self.h}, w={self.w}, c={self.c}, pad={self.pad})"
+
+
+def out_size(h, k, s, p):
+    return (h + 2 * p - k) // s + 1
+
+
+# ------------------------------------------------------------------------------------------
+# weight maps (fg_weight_map)
+# ------------------------------------------------------------------------------------------
+
+
+def _wmap(n_out, kh, kw, c, c_valid, dim0_is_n, shape, rtab, stab, n_base=0):
+    assert len(rtab) == kh and len(stab) == kw and kh <= 8 and kw <= 8
+    return dict(n_out=n_out, kh=kh, kw=kw, c=c, c_valid=c_valid, jp=rup(kw * c), dim0_is_n=dim0_is_n,
+                d0=shape[0], d1=shape[1], KH=shape[2], KW=shape[3], n_base=n_base,
+                rtab=list(rtab), stab=list(stab))
+
+
+def wmap_conv_fwd(shape, c_alloc):
+    """forward conv, weight (O, I, k, k): packed row n = o, column (r, s, ch = i)"""
+    O, I, kh, kw = shape
+    return _wmap(O, kh, kw, c_alloc, I, 1, shape, range(kh), range(kw))
+
+
+def wmap_conv_dgrad_s1(shape, c_alloc_gy):
+    """stride-1 input gradient = correlation of gy with the flipped, transposed kernel"""
+    O, I, kh, kw = shape
+    return _wmap(I, kh, kw, c_alloc_gy, O, 0, shape, [kh - 1 - r for r in range(kh)],
+                 [kw - 1 - s for s in range(kw)])
+
+
+def phase_taps(k, p, ph):
+    """Stride-2 sub-pixel decomposition.  Output index 2a+ph of  y[o] = sum_{2i-p+r=o} x[i] w[r]
+    reads x[a + d] for taps r = ph + p - 2d, d = dmin .. dmin+len-1.  Returns (dmin, [r...])."""
+    pairs = sorted(((ph + p - r) // 2, r) for r in range(k) if (r - ph - p) % 2 == 0)
+    dmin = pairs[0][0]
+    assert [d for d, _ in pairs] == list(range(dmin, dmin + len(pairs)))
+    return dmin, [r for _, r in pairs]
+
+
+def wmap_phase(shape, gathered_is_dim0, k, p, py, px, c_alloc, n_base=0, n_out=None):
+    """Phase (py, px) of a stride-2 transposed op.  The gathered operand's channels index
+    weight dim 0 (conv-transpose weight (I, O, k, k) in its forward; conv weight (O, I, k, k)
+    in a strided conv's input gradient); packed rows index dim 1."""
+    assert gathered_is_dim0
+    dy, ry = phase_taps(k, p, py)
+    dx, rx = phase_taps(k, p, px)
+    n_out = shape[1] if n_out is None else n_out
+    return _wmap(n_out, len(ry), len(rx), c_alloc, shape[0], 0, shape, ry, rx, n_base), dy, dx
+
+
+def wmap_convT_dgrad(shape, c_alloc_gy):
+    """input gradient of a stride-2 conv-transpose (weight (I, O, k, k)) = stride-2 conv of gy"""
+    I, O, kh, kw = shape
+    return _wmap(I, kh, kw, c_alloc_gy, O, 1, shape, range(kh), range(kw))
+
+
+def wmap_wgrad(shape, a_is_dim0, c_alloc_x, k):
+    """slab [a][r, s, ch] -> PyTorch weight gradient; a indexes dim 0, ch indexes dim 1"""
+    assert a_is_dim0
+    return _wmap(shape[0], k, k, c_alloc_x, shape[1], 1, shape, range(k), range(k))
+
+
+def packed_numel(m):
+    return m["n_out"] * m["kh"] * m["jp"]
+
+
+# ------------------------------------------------------------------------------------------
+# forward-kernel problems (fg_conv_problem)
+# ------------------------------------------------------------------------------------------
+
+
+def conv_problem(X, pad_used, k, stride, wp, wmap, Y, bias=None, act=0, accumulate=0, y_nchw=None):
+    """Dense conv over X's interior with `pad_used` taken from X's (pre-filled) border.
+    Output rows (n, Ho, Wo) land in Y's interior (NHWC) or, when y_nchw=(tensor, C, H, W) is
+    given, in a contiguous NCHW tensor."""
+    assert X.pad >= pad_used
+    Ho, Wo = out_size(X.h, k, stride, pad_used), out_size(X.w, k, stride, pad_used)
+    assert wmap["kh"] == k and wmap["kw"] == k and wmap["c"] == X.c
+    prob = dict(x=(X, X.off(-pad_used, -pad_used)), w=(wp, 0), bias=bias,
+                sxn=X.s_img, sxa=stride * X.s_row, sxb=stride * X.c, sxr=X.s_row,
+                m_img=X.n, m_a=Ho, m_b=Wo, kh=k, j_valid=k * X.c, jp=wmap["jp"],
+                n_out=wmap["n_out"], ldw=k * wmap["jp"], act=act, accumulate=accumulate)
+    if y_nchw is None:
+        assert (Y.h, Y.w, Y.n) == (Ho, Wo, X.n) and Y.c >= wmap["n_out"], (Y, Ho, Wo)
+        prob.update(y=(Y, Y.off(0, 0)), syn=Y.s_img, sya=Y.s_row, syb=Y.c, syc=1)
+    else:
+        t, Cc, Hh, Ww = y_nchw
+        assert (Hh, Ww) == (Ho, Wo)
+        prob.update(y=(t, 0), syn=Cc * Hh * Ww, sya=Ww, syb=1, syc=Hh * Ww)
+    return prob
+
+
+def phase_problems(S, shape, k, p, Y, wp_list, maps, bias=None, act=0, accumulate=0, y_nchw=None, n_out=None):
+    """The four output phases of a stride-2 transposed op reading S (zero border >= 1):
+    a ConvTranspose2d(k, 2, p, output_padding) forward, or a stride-2 conv's input gradient.
+    wp_list/maps: per phase (py, px) in order (0,0), (0,1), (1,0), (1,1)."""
+    assert S.pad >= 1
+    if y_nchw is None:
+        Ho, Wo = Y.h, Y.w
+    else:
+        _, Cc, Ho, Wo = y_nchw
+    probs = []
+    for i, (py, px) in enumerate(((0, 0), (0, 1), (1, 0), (1, 1))):
+        m, dy, dx = maps[i]
+        ma, mb = (Ho - py + 1) // 2, (Wo - px + 1) // 2
+        assert ma - 1 + dy + m["kh"] - 1 <= S.h - 1 + S.pad and dy >= -S.pad
+        assert mb - 1 + dx + m["kw"] - 1 <= S.w - 1 + S.pad and dx >= -S.pad
+        prob = dict(x=(S, S.off(dy, dx)), w=(wp_list[i], 0), bias=bias,
+                    sxn=S.s_img, sxa=S.s_row, sxb=S.c, sxr=S.s_row,
+                    m_img=S.n, m_a=ma, m_b=mb, kh=m["kh"], j_valid=m["kw"] * S.c, jp=m["jp"],
+                    n_out=m["n_out"], ldw=m["kh"] * m["jp"], act=act, accumulate=accumulate)
+        if y_nchw is None:
+            prob.update(y=(Y, Y.off(py, px)), syn=Y.s_img, sya=2 * Y.s_row, syb=2 * Y.c, syc=1)
+        else:
+            t = y_nchw[0]
+            prob.update(y=(t, py * Wo + px), syn=Cc * Ho * Wo, sya=2 * Wo, syb=2, syc=Ho * Wo)
+        probs.append(prob)
+    return probs
+
+
+def phase_maps(shape, k, p, c_alloc, n_base=0, n_out=None):
+    return [wmap_phase(shape, True, k, p, py, px, c_alloc, n_base, n_out)
+            for py, px in ((0, 0), (0, 1), (1, 0), (1, 1))]
+
+
+# ------------------------------------------------------------------------------------------
+# weight-gradient problems (fg_wgrad_problem)
+# ------------------------------------------------------------------------------------------
+
+WG_BLOCKS = 2048
+
+
+def wgrad_splits(n_a, K, M):
+    ba, bk = (128, 128) if n_a > 32 else (32, 256)
+    tiles = -(-n_a // ba) * -(-K // bk)
+    splits = max(1, min(WG_BLOCKS // max(tiles, 1), -(-M // 256)))
+    chunk = rup(-(-M // splits), 16)
+    splits = -(-M // chunk)
+    return splits, chunk
+
+
+def wgrad_problem(P, n_a, X, x_off_yx, sxa, sxb, k, slab=None):
+    """out[split][a][r, s, ch] = sum over P's interior rows of P[m][a] * X-gather.
+    P: Buf whose interior rows are the reduction index; X gathered as in the forward."""
+    M = P.n * P.h * P.w
+    K = k * k * X.c
+    splits, chunk = wgrad_splits(n_a, K, M)
+    return dict(p=(P, P.off(0, 0)), x=(X, X.off(*x_off_yx)), out=slab,
+                spn=P.s_img, spa=P.s_row, spb=P.c,
+                sxn=X.s_img, sxa=sxa, sxb=sxb, sxr=X.s_row,
+                m_img=P.n, m_a=P.h, m_b=P.w, n_a=n_a, kh=k, j_valid=k * X.c,
+                splits=splits, m_chunk=chunk)
+
+
+def wgrad_conv(gy, X, pad_used, k, stride, O):
+    """conv weight gradient: P = gy (rows = output pixels), X gathered like the forward"""
+    return wgrad_problem(gy, O, X, (-pad_used, -pad_used), stride * X.s_row, stride * X.c, k)
+
+
+def wgrad_convT(x, gyp, k, p, I):
+    """ConvTranspose2d(k, s=2, p) weight gradient: P = x (rows = input pixels), gathered gy
+    (zero border >= p) at 2i - p + r."""
+    assert gyp.pad >= p
+    return wgrad_problem(x, I, gyp, (-p, -p), 2 * gyp.s_row, 2 * gyp.c, k)
+
+
+def slab_numel(prob):
+    return prob["splits"] * prob["n_a"] * prob["kh"] * prob["j_valid"]

@@ -1,0 +1,206 @@
+/*
+ * floodgan.h -- C-ABI of the MI355X-native PairedAttention GAN training-step kernels.
+ *
+ * The reference (Natasha-R/Flood-Prediction-GAN) has no native code and no FFI: its hot path
+ * is PyTorch modules (models/model_architectures.py:305-441) driven by Model.train_paired
+ * (models/model.py:598-658), whose arithmetic runs in ATen's conv / instance_norm / pad /
+ * softmax / tanh / mse / l1 / Adam kernels.  This library replaces exactly those ATen calls.
+ * Each entry point below names the reference operation it replaces.  All pointers are HIP
+ * device pointers to fp32 data (doubles where stated), sizes are in elements, every call is
+ * asynchronous on `stream` and returns 0 on success or a non-zero error code; the message of
+ * the last failure on the calling thread is returned by fg_last_error().  No torch types
+ * appear here: the Python host layer (floodgan/_lib.py) binds these with ctypes.
+ *
+ * Activation tensors are NHWC fp32 with an optional spatial border ("pad"): image n, interior
+ * pixel (y, x), channel c lives at ptr[((n*(h+2*pad) + y+pad)*(w+2*pad) + x+pad)*c_alloc + c].
+ */
+#ifndef FLOODGAN_H
+#define FLOODGAN_H
+
+#include <hip/hip_runtime.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------------------------------- */
+/* common types                                                                              */
+/* ---------------------------------------------------------------------------------------- */
+
+enum { FG_PAD_ZERO = 0, FG_PAD_REFLECT = 1 };
+enum { FG_ACT_NONE = 0, FG_ACT_RELU = 1, FG_ACT_LRELU = 2 };   /* LeakyReLU slope 0.2 */
+enum { FG_ERR_INVALID = -1 };
+
+/* An NHWC view: interior h x w, border `pad` on every side, c_alloc channels per pixel. */
+typedef struct fg_view {
+    float* ptr;
+    int n, h, w, c_alloc, pad;
+} fg_view;
+
+/* A strided 4-D view (any memory format), element (n,c,y,x) at ptr[n*sn + c*sc + y*sy + x*sx]. */
+typedef struct fg_sview {
+    const float* ptr;
+    long long sn, sc, sy, sx;
+} fg_sview;
+
+/*
+ * Implicit-GEMM convolution problem (forward conv, stride-1 dgrad, and one phase of a
+ * stride-2 transposed conv / stride-2 dgrad).  Rows m = (img, a, b) of an m_img x m_a x m_b
+ * grid; columns n < n_out; reduction k = (r, j), r < kh, j < jp (j >= j_valid reads zero):
+ *     y[row_y(m) + n*syc] (+)= act( sum_k x[row_x(m) + r*sxr + j] * w[n*ldw + r*jp + j] + bias[n] )
+ * with row_x(m) = img*sxn + a*sxa + b*sxb and row_y(m) = img*syn + a*sya + b*syb.
+ * Replaces ATen convolution / conv_transpose forward and convolution_backward's input
+ * gradient for models/model_architectures.py:312-334 (generator) and :424-438 (discriminator).
+ */
+typedef struct fg_conv_problem {
+    const float* x;
+    const float* w;
+    const float* bias;
+    float* y;
+    long long sxn, sxa, sxb, sxr;
+    long long syn, sya, syb, syc;
+    int m_img, m_a, m_b;
+    int kh, j_valid, jp;
+    int n_out, ldw;
+    int act, accumulate;
+} fg_conv_problem;
+
+/*
+ * Weight-gradient problem: out[split][a][k] = sum_{m in split} p[row_p(m) + a] * x[row_x(m) + koff(k)]
+ * with k = r*j_valid + j, koff = r*sxr + j, a < n_a.  Partial slabs are summed by
+ * fg_wgrad_reduce.  Replaces convolution_backward's weight gradient.
+ */
+typedef struct fg_wgrad_problem {
+    const float* p;
+    const float* x;
+    float* out;
+    long long spn, spa, spb;
+    long long sxn, sxa, sxb, sxr;
+    int m_img, m_a, m_b;
+    int n_a, kh, j_valid;
+    int splits, m_chunk;
+} fg_wgrad_problem;
+
+/* Maps packed-K coordinates to PyTorch weight coordinates (see fg_pack_weight). */
+typedef struct fg_weight_map {
+    int n_out;            /* packed rows                                                    */
+    int kh, kw, c;        /* packed K = kh * jp, j = s*c + ch, j_valid = kw*c                */
+    int c_valid;          /* channels ch >= c_valid are zero                                */
+    int jp;               /* padded j extent (multiple of 16) -- pack only                  */
+    int dim0_is_n;        /* 1: w[n][ch][r][s] ; 0: w[ch][n][r][s]                          */
+    int d0, d1, KH, KW;   /* PyTorch weight shape                                           */
+    int n_base;           /* packed row n reads PyTorch index n + n_base                    */
+    int rtab[8];          /* kernel-row index per packed r                                  */
+    int stab[8];          /* kernel-col index per packed s                                  */
+} fg_weight_map;
+
+/* ---------------------------------------------------------------------------------------- */
+/* library                                                                                   */
+/* ---------------------------------------------------------------------------------------- */
+const char* fg_last_error(void);
+int fg_version(void);
+int fg_device_ok(void);   /* 0 if a gfx950 device is current, else an error code */
+
+/* ---------------------------------------------------------------------------------------- */
+/* convolution engine (fp32 MFMA v_mfma_f32_32x32x2_f32)                                     */
+/* ---------------------------------------------------------------------------------------- */
+/* Up to 4 problems in one launch (the four output phases of a stride-2 transposed conv). */
+int fg_conv_fwd(const fg_conv_problem* probs, int nprob, hipStream_t stream);
+
+/* Weight gradient into partial slabs (see fg_wgrad_problem). */
+int fg_conv_wgrad(const fg_wgrad_problem* prob, hipStream_t stream);
+
+/* Sum `splits` slabs [split][n_a][kh*kw*c] and scatter into the PyTorch-layout gradient
+ * dw (shape map->d0,d1,KH,KW) through `map` (dim0 = a); accumulate != 0 adds into dw. */
+int fg_wgrad_reduce(const float* slabs, int splits, const fg_weight_map* map, float* dw,
+                    int accumulate, hipStream_t stream);
+
+/* Repack a PyTorch conv / conv-transpose weight into the engine's [n][kh*jp] layout. */
+int fg_pack_weight(const float* w, const fg_weight_map* map, float* wp, hipStream_t stream);
+
+/* ---------------------------------------------------------------------------------------- */
+/* layout / padding                                                                          */
+/* ---------------------------------------------------------------------------------------- */
+/* dst(img0+n, y, x, ch) = ch < ca ? a(n,ch,y,x) : ch < ca+cb ? b(n,ch-ca,y,x) : 0, for the full
+ * padded extent of dst (border filled by `pad_mode`).  Replaces F.pad(reflect) at
+ * models/model_architectures.py:341 and torch.cat at models/model.py:616-617. */
+int fg_pack_input(fg_sview a, int ca, fg_sview b, int cb, fg_view dst, int img0, int nimg,
+                  int pad_mode, hipStream_t stream);
+
+/* Fill the border of dst with zeros (interior untouched). */
+int fg_zero_border(fg_view dst, hipStream_t stream);
+
+/* dst = fold_reflect(gpad) (+ add): the adjoint of reflect padding (reflection_pad2d_backward)
+ * plus an optional residual-gradient add (models/model_architectures.py:418 `input + x`). */
+int fg_fold_add(fg_view gpad, int fold_pad, fg_view add, fg_view dst, hipStream_t stream);
+
+/* ---------------------------------------------------------------------------------------- */
+/* instance norm (nn.InstanceNorm2d, affine=False, eps 1e-5) fused with activation           */
+/* ---------------------------------------------------------------------------------------- */
+/* Per-(n,c) mean and 1/sqrt(var+eps) of src's interior; work >= fg_in_workspace_doubles(). */
+long long fg_in_workspace_doubles(int n, int c);
+int fg_in_stats(fg_view src, float eps, float* mean, float* rstd, double* work,
+                hipStream_t stream);
+
+/* dst = act((src - mean) * rstd) (+ residual), written over dst's full padded extent with
+ * pad_mode (reflect or zero border).  Replaces instance_norm + relu/leaky_relu + F.pad
+ * (+ the residual add of PairedAttentionBlock). */
+int fg_in_apply(fg_view src, const float* mean, const float* rstd, int act, fg_view residual,
+                fg_view dst, int pad_mode, hipStream_t stream);
+
+/* Backward of fg_in_apply.  g is read from gsrc's interior, or folded through reflect
+ * padding of width fold_pad when fold_pad > 0 (gsrc then holds the gradient of the padded
+ * tensor); optional gadd (compact) is added.  dst receives dL/dsrc (border zeroed);
+ * bias_grad (optional, [c]) receives sum over n,y,x of dst = grad of the conv bias that
+ * feeds this norm. */
+int fg_in_bwd(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, const float* mean,
+              const float* rstd, int act, fg_view dst, float* bias_grad, double* work,
+              hipStream_t stream);
+
+/* g *= act'(y) in place over the interior (y = saved activation output). */
+int fg_act_bwd(fg_view g, fg_view y, int act, hipStream_t stream);
+
+/* out[c] (+)= sum over n,y,x of src(n,y,x,c) for c < c_valid.  Bias gradients. */
+int fg_channel_sum(fg_view src, int c_valid, float* out, int accumulate, double* work,
+                   hipStream_t stream);
+
+/* ---------------------------------------------------------------------------------------- */
+/* generator tail: tanh(27) + softmax(10) + attention composite                              */
+/* (models/model_architectures.py:352-399)                                                   */
+/* ---------------------------------------------------------------------------------------- */
+int fg_tail_fwd(fg_view content_logits, fg_view att_logits, fg_sview x, float* out,
+                float* mask, hipStream_t stream);
+/* g_out: strided [N,3,H,W].  g_content: dst view (27 used of c_alloc, zero border/channels),
+ * g_att: dst view (10 used).  g_x (optional strided, may be NULL ptr) += grad wrt x[:, :3]. */
+int fg_tail_bwd(fg_view content_logits, fg_view att_logits, fg_sview x, fg_sview g_out,
+                fg_view g_content, fg_view g_att, hipStream_t stream);
+
+/* ---------------------------------------------------------------------------------------- */
+/* losses (nn.MSELoss vs a constant target, nn.L1Loss; models/model.py:626-644)             */
+/* ---------------------------------------------------------------------------------------- */
+/* loss[0] = mean((p - target)^2);  g (optional) = gscale * 2 (p - target) / n */
+int fg_mse_const(const float* p, long long n, float target, float gscale, float* loss,
+                 float* g, double* work, hipStream_t stream);
+/* loss[0] = mean(|a - b|) over [N,C,H,W] strided views; g (optional, NCHW contiguous)
+ * = gscale * sign(a - b) / n  (or += when accumulate). */
+int fg_l1(fg_sview a, fg_sview b, int N, int C, int H, int W, float gscale, float* loss,
+          float* g, int accumulate, double* work, hipStream_t stream);
+
+/* ---------------------------------------------------------------------------------------- */
+/* Adam (torch.optim.Adam, amsgrad=False, weight_decay=0; models/model.py:121-122)           */
+/* ---------------------------------------------------------------------------------------- */
+typedef struct fg_adam_tensor {
+    float* param;
+    const float* grad;
+    float* exp_avg;
+    float* exp_avg_sq;
+    long long numel;
+} fg_adam_tensor;
+/* One step for `count` tensors sharing (lr, betas, eps, step). */
+int fg_adam_step(const fg_adam_tensor* tensors, int count, double lr, double beta1,
+                 double beta2, double eps, long long step, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FLOODGAN_H */

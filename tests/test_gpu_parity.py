@@ -1,0 +1,375 @@
+"""GPU parity of the HIP path (libfloodgan via the C-ABI) against the CPU oracle / torch-CPU
+fp64 references.  Tolerance: norm-relative 1e-3 per tensor for the network and the step
+(BASELINE.json north_star "within 1e-3 relative fp32 tolerance"); kernels are held to 1e-5."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import paired_attention as O
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+KTOL = 1e-5     # single kernels vs fp64
+NTOL = 1e-3     # network / step (north-star tolerance)
+
+
+def nrel(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return float((a - b).norm() / max(float(b.norm()), 1e-30))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from floodgan import _lib as L
+    L.load()
+    L.check(L.load().fg_device_ok(), "device_ok")
+
+
+def buf_from(x_nchw, pad, mode, c_alloc=None):
+    from floodgan.plans import Buf
+    n, c, h, w = x_nchw.shape
+    c_alloc = c_alloc or c
+    xp = F.pad(x_nchw, (pad,) * 4, mode=mode) if pad else x_nchw
+    nhwc = torch.zeros(n, h + 2 * pad, w + 2 * pad, c_alloc, dtype=torch.float32)
+    nhwc[..., :c] = xp.float().permute(0, 2, 3, 1)
+    return Buf(nhwc.reshape(-1).to(DEV), n, h, w, c_alloc, pad)
+
+
+def nchw(B, c=None):
+    c = c or B.c
+    return B.interior()[..., :c].permute(0, 3, 1, 2).cpu()
+
+
+# ------------------------------------------------------------------ conv engine
+
+CONV_CASES = [(9, 64, 7, 1, 3, "reflect", 24), (64, 128, 3, 2, 1, "constant", 20), (256, 256, 3, 1, 1, "reflect", 12),
+              (64, 27, 7, 1, 3, "reflect", 16), (64, 10, 1, 1, 0, "constant", 16), (12, 64, 4, 2, 1, "constant", 32),
+              (128, 256, 4, 2, 1, "constant", 16), (256, 512, 4, 1, 1, "constant", 9), (512, 1, 4, 1, 1, "constant", 9)]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd_wgrad_dgrad(case):
+    from floodgan import ops, plans as PL
+    from floodgan.plans import Buf
+    cin, cout, k, s, p, mode, H = case
+    torch.manual_seed(1)
+    x = torch.randn(2, cin, H, H, dtype=torch.float64)
+    w = (torch.randn(cout, cin, k, k, dtype=torch.float64) * 0.05).requires_grad_(True)
+    b = torch.randn(cout, dtype=torch.float64)
+    xr = x.clone().requires_grad_(True)
+    xin = F.pad(xr, (p,) * 4, mode=mode) if p else xr
+    y = F.conv2d(xin, w, b, stride=s)
+    gy = torch.randn_like(y)
+    gx_ref, gw_ref = torch.autograd.grad(y, (xr, w), gy)
+    X = buf_from(x, p, mode)
+    wd = w.detach().float().to(DEV)
+    m = PL.wmap_conv_fwd(wd.shape, X.c)
+    Ho = PL.out_size(H, k, s, p)
+    Y = Buf.empty(2, Ho, Ho, cout, 0, DEV)
+    ops.conv([PL.conv_problem(X, p, k, s, ops.pack_weight(wd, m), m, Y, bias=b.float().to(DEV))])
+    assert nrel(nchw(Y), y) < KTOL
+    # weight gradient
+    GY = buf_from(gy, 0, "constant")
+    dw = torch.empty_like(wd)
+    ops.wgrad(PL.wgrad_conv(GY, X, p, k, s, cout), PL.wmap_wgrad(wd.shape, True, X.c, k), dw)
+    assert nrel(dw, gw_ref) < KTOL
+    # input gradient
+    if s == 1:
+        if mode == "reflect":
+            GYP = buf_from(gy, k - 1, "constant")
+            gxp = Buf.empty(2, H + 2 * p, H + 2 * p, cin, 0, DEV)
+            md = PL.wmap_conv_dgrad_s1(wd.shape, GYP.c)
+            ops.conv([PL.conv_problem(GYP, k - 1, k, 1, ops.pack_weight(wd, md), md, gxp)])
+            gx = Buf.empty(2, H, H, cin, 0, DEV)
+            ops.fold_add(gxp, p, None, gx)
+        else:
+            GYP = buf_from(gy, k - 1 - p, "constant")
+            gx = Buf.empty(2, H, H, cin, 0, DEV)
+            md = PL.wmap_conv_dgrad_s1(wd.shape, GYP.c)
+            ops.conv([PL.conv_problem(GYP, k - 1 - p, k, 1, ops.pack_weight(wd, md), md, gx)])
+    else:
+        GYP = buf_from(gy, 1, "constant")
+        gx = Buf.empty(2, H, H, cin, 0, DEV)
+        maps = PL.phase_maps(wd.shape, k, p, GYP.c)
+        ops.conv(PL.phase_problems(GYP, wd.shape, k, p, gx, [ops.pack_weight(wd, mm) for mm, _, _ in maps], maps))
+    torch.cuda.synchronize()
+    assert nrel(nchw(gx), gx_ref) < KTOL
+
+
+@pytest.mark.parametrize("cin,cout,H", [(256, 128, 12), (128, 64, 20)])
+def test_convT(cin, cout, H):
+    from floodgan import ops, plans as PL
+    from floodgan.plans import Buf
+    torch.manual_seed(2)
+    x = torch.randn(2, cin, H, H, dtype=torch.float64, requires_grad=True)
+    w = (torch.randn(cin, cout, 3, 3, dtype=torch.float64) * 0.05).requires_grad_(True)
+    b = torch.randn(cout, dtype=torch.float64)
+    y = F.conv_transpose2d(x, w, b, stride=2, padding=1, output_padding=1)
+    gy = torch.randn_like(y)
+    gx_ref, gw_ref = torch.autograd.grad(y, (x, w), gy)
+    X = buf_from(x.detach(), 1, "constant")
+    wd = w.detach().float().to(DEV)
+    Y = Buf.empty(2, 2 * H, 2 * H, cout, 0, DEV)
+    maps = PL.phase_maps(wd.shape, 3, 1, X.c)
+    ops.conv(PL.phase_problems(X, wd.shape, 3, 1, Y, [ops.pack_weight(wd, m) for m, _, _ in maps], maps,
+                               bias=b.float().to(DEV)))
+    assert nrel(nchw(Y), y) < KTOL
+    GY = buf_from(gy, 1, "constant")
+    dw = torch.empty_like(wd)
+    ops.wgrad(PL.wgrad_convT(X, GY, 3, 1, cin), PL.wmap_wgrad(wd.shape, True, GY.c, 3), dw)
+    assert nrel(dw, gw_ref) < KTOL
+    gx = Buf.empty(2, H, H, cin, 0, DEV)
+    m = PL.wmap_convT_dgrad(wd.shape, GY.c)
+    ops.conv([PL.conv_problem(GY, 1, 3, 2, ops.pack_weight(wd, m), m, gx)])
+    assert nrel(nchw(gx), gx_ref) < KTOL
+
+
+# ------------------------------------------------------------------ instance norm
+
+@pytest.mark.parametrize("act,fold,residual", [(1, 0, False), (2, 0, False), (0, 0, True), (1, 1, False),
+                                               (1, 3, False)])
+def test_instnorm_fwd_bwd(act, fold, residual):
+    from floodgan import ops
+    from floodgan.plans import Buf
+    torch.manual_seed(3)
+    C, H = 64, 20
+    c = (torch.randn(2, C, H, H, dtype=torch.float64) * 2 + 0.7).requires_grad_(True)
+    r = torch.randn(2, C, H, H, dtype=torch.float64)
+    y = F.instance_norm(c, eps=1e-5)
+    y = F.relu(y) if act == 1 else (F.leaky_relu(y, 0.2) if act == 2 else y)
+    if residual:
+        y = y + r
+    pad_mode = "reflect" if fold else "constant"
+    yp = F.pad(y, (max(fold, 1),) * 4, mode=pad_mode if fold else "constant")
+    gy = torch.randn_like(yp)
+    (gc_ref,) = torch.autograd.grad(yp, c, gy)
+    cb = buf_from(c.detach(), 0, "constant")
+    rb = buf_from(r, 0, "constant") if residual else None
+    mean, rstd = ops.in_stats(cb)
+    pad = max(fold, 1)
+    out = Buf.empty(2, H, H, C, pad, DEV)
+    ops.in_apply(cb, mean, rstd, act, rb, out, 1 if fold else 0)
+    assert nrel(out.nhwc().permute(0, 3, 1, 2).cpu(), yp) < KTOL
+    # backward: gradient of the padded output -> fold when reflect, else interior only
+    gdst = Buf.empty(2, H, H, C, 2, DEV)
+    bias_g = torch.empty(C, device=DEV)
+    if fold:
+        gsrc = buf_from(gy, 0, "constant")
+        gsrc = Buf(gsrc.t, 2, H + 2 * fold, H + 2 * fold, C, 0)
+        ops.in_bwd(gsrc, fold, None, cb, mean, rstd, act, gdst, bias_g)
+    else:
+        gsrc = buf_from(gy[:, :, pad:-pad, pad:-pad], 0, "constant")
+        ops.in_bwd(gsrc, 0, None, cb, mean, rstd, act, gdst, bias_g)
+    torch.cuda.synchronize()
+    assert nrel(nchw(gdst), gc_ref) < 1e-5
+    assert float(gdst.nhwc()[:, 0].abs().max()) == 0.0       # zero border
+    assert abs(float(bias_g.sum())) < 1e-3
+
+
+# ------------------------------------------------------------------ tail, losses, adam
+
+def test_tail():
+    from floodgan import ops
+    from floodgan.plans import Buf
+    torch.manual_seed(4)
+    N, H = 2, 16
+    cl = torch.randn(N, 27, H, H, dtype=torch.float64, requires_grad=True)
+    al = torch.randn(N, 10, H, H, dtype=torch.float64, requires_grad=True)
+    x = torch.randn(N, 9, H, H, dtype=torch.float64)
+    t = torch.tanh(cl)
+    a = torch.softmax(al, 1)
+    out = sum(t[:, 3 * i:3 * i + 3] * a[:, i:i + 1] for i in range(9)) + x[:, :3] * a[:, 9:10]
+    g = torch.randn_like(out)
+    gcl_ref, gal_ref = torch.autograd.grad(out, (cl, al), g)
+    CL = buf_from(cl.detach(), 0, "constant", 32)
+    AL = buf_from(al.detach(), 0, "constant", 16)
+    xd = x.float().to(DEV)
+    o = torch.empty(N, 3, H, H, device=DEV)
+    mk = torch.empty(N, H, H, device=DEV)
+    ops.tail_fwd(CL, AL, xd, o, mk)
+    assert nrel(o, out) < KTOL and nrel(mk, a[:, 9]) < KTOL
+    GC = Buf.empty(N, H, H, 32, 6, DEV)
+    GA = Buf.empty(N, H, H, 16, 0, DEV)
+    ops.tail_bwd(CL, AL, xd, g.float().to(DEV), GC, GA)
+    torch.cuda.synchronize()
+    assert nrel(nchw(GC, 27), gcl_ref) < KTOL and nrel(nchw(GA, 10), gal_ref) < KTOL
+    assert float(GC.nhwc()[..., 27:].abs().max()) == 0.0 and float(GC.nhwc()[:, :6].abs().max()) == 0.0
+
+
+def test_losses_and_adam():
+    from floodgan import ops
+    torch.manual_seed(5)
+    p = torch.randn(2, 1, 62, 62)
+    loss = torch.empty(1, device=DEV)
+    g = torch.empty(2, 1, 62, 62, device=DEV)
+    ops.mse_const(p.to(DEV), 1.0, 0.5, loss, g)
+    pr = p.double().requires_grad_(True)
+    ref = F.mse_loss(pr, torch.ones_like(pr))
+    (gr,) = torch.autograd.grad(ref * 0.5, pr)
+    assert abs(float(loss) - float(ref)) < 1e-6 * float(ref) + 1e-7 and nrel(g, gr) < 1e-6
+    a = torch.randn(2, 3, 16, 16)
+    b = torch.randn(2, 3, 16, 16)
+    gl = torch.empty(2, 3, 16, 16, device=DEV)
+    ops.l1(a.to(DEV), b.to(DEV), 100.0, loss, gl)
+    ar = a.double().requires_grad_(True)
+    ref = F.l1_loss(ar, b.double())
+    (gr,) = torch.autograd.grad(ref * 100, ar)
+    assert abs(float(loss) - float(ref)) < 1e-6 and nrel(gl, gr) < 1e-6
+    # Adam against torch.optim.Adam on the CPU (the oracle's optimiser), 3 steps
+    from floodgan.optim import FusedAdam
+    w0 = torch.randn(1000) * 0.02
+    pc = torch.nn.Parameter(w0.clone())
+    pd = torch.nn.Parameter(w0.clone().to(DEV))
+    oc = torch.optim.Adam([pc], lr=2e-4, betas=(0.5, 0.999))
+    od = FusedAdam([pd], lr=2e-4, betas=(0.5, 0.999))
+    for _ in range(3):
+        gg = torch.randn(1000)
+        pc.grad = gg.clone()
+        pd.grad = gg.clone().to(DEV)
+        oc.step()
+        od.step()
+    torch.cuda.synchronize()
+    assert float((pd.detach().cpu() - pc.detach()).abs().max()) < 1e-9 + 1e-6 * float(pc.detach().abs().max())
+    sd_c, sd_d = oc.state_dict(), od.state_dict()
+    assert sd_c["param_groups"][0].keys() == sd_d["param_groups"][0].keys()
+    assert float(sd_d["state"][0]["step"]) == 3.0
+
+
+# ------------------------------------------------------------------ modules / step
+
+def _make_models(c_in=9):
+    from floodgan.model import Model
+    m = Model(model="PairedAttention", num_epochs=2, topography="all")
+    return m
+
+
+def _load_oracle_into(module, P):
+    sd = module.state_dict()
+    for k in sd:
+        sd[k].copy_(P[k])
+
+
+@pytest.mark.parametrize("R", [32, 64])
+def test_modules_forward_vs_golden(golden, R):
+    g = golden(R)
+    m = _make_models()
+    x0 = torch.from_numpy(g["x0"]).to(DEV)
+    y0 = torch.from_numpy(g["y0"]).to(DEV)
+    with torch.no_grad():
+        out = m.generator(x0)
+        mask = m.generator.last_attention_mask
+        d = m.discriminator(torch.cat((x0, y0), 1))
+    assert nrel(out, torch.from_numpy(g["init_g_out"])) < 1e-5
+    assert nrel(mask, torch.from_numpy(g["init_mask"])) < 1e-5
+    assert nrel(d, torch.from_numpy(g["init_d_out"])) < 1e-5
+
+
+@pytest.mark.parametrize("R", [32, 64])
+def test_module_autograd_vs_oracle(R):
+    """Gradients of G and D through the drop-in modules vs the oracle's CPU autograd."""
+    torch.manual_seed(11)
+    x = torch.rand(2, 9, R, R) * 2 - 1
+    y = torch.rand(2, 3, R, R) * 2 - 1
+    m = _make_models()
+    Gp, Dp = O.init_params()
+    Gd = {k: v.double().requires_grad_(True) for k, v in Gp.items()}
+    Dd = {k: v.double().requires_grad_(True) for k, v in Dp.items()}
+    fake_r, _ = O.generator_forward(Gd, x.double())
+    pr = O.discriminator_forward(Dd, torch.cat((x.double(), fake_r), 1))
+    loss_r = F.mse_loss(pr, torch.ones_like(pr)) + 100 * F.l1_loss(fake_r, y.double())
+    loss_r.backward()
+    xd, yd = x.to(DEV), y.to(DEV)
+    fake = m.generator(xd)
+    pred = m.discriminator(torch.cat((xd, fake), 1))
+    loss = F.mse_loss(pred, torch.ones_like(pred)) + 100 * F.l1_loss(fake, yd)
+    loss.backward()
+    skip_g, skip_d = O.cancelled_biases()
+    for k, p in m.generator.named_parameters():
+        if k not in skip_g:
+            assert nrel(p.grad, Gd[k].grad) < NTOL, k
+    for k, p in m.discriminator.named_parameters():
+        if k not in skip_d:
+            assert nrel(p.grad, Dd[k].grad) < NTOL, k
+
+
+@pytest.mark.parametrize("R", [32, 64])
+def test_paired_step_vs_golden(golden, R):
+    """Two iterations of the fused step vs the REFERENCE's own train_paired outputs."""
+    g = golden(R)
+    m = _make_models()
+    x0 = torch.from_numpy(g["x0"]).to(DEV)
+    y0 = torch.from_numpy(g["y0"]).to(DEV)
+    skip_g, skip_d = O.cancelled_biases()
+    for it in range(2):
+        for opt in (m.optimizer_generator, m.optimizer_discriminator):
+            for grp in opt.param_groups:
+                grp["lr"] = float(g[f"it{it}_lr"][0])
+        x = torch.from_numpy(g[f"x{it}"]).to(DEV)
+        y = torch.from_numpy(g[f"y{it}"]).to(DEV)
+        losses = m.step_fn(x, y).cpu().numpy()
+        ref = g[f"it{it}_losses"].copy()
+        ref[3] *= 100
+        assert np.allclose(losses, ref, rtol=1e-4, atol=1e-5), (it, losses, ref)
+        with torch.no_grad():
+            out = m.generator(x0)
+            d = m.discriminator(torch.cat((x0, y0), 1))
+        assert nrel(out, torch.from_numpy(g[f"it{it}_g_out"])) < NTOL
+        assert nrel(d, torch.from_numpy(g[f"it{it}_d_out"])) < NTOL
+        for prefix, mod, skip in (("G", m.generator, skip_g), ("D", m.discriminator, skip_d)):
+            for name, p in mod.state_dict().items():
+                if name in skip:
+                    continue
+                t = p.detach().double().flatten().cpu()
+                refc = g[f"it{it}_{prefix}/{name}"]
+                assert abs(t.abs().sum().item() - refc[1]) <= 1e-3 * refc[1] + 1e-6, (it, name)
+
+
+def test_paired_step_256_vs_oracle():
+    """Fused step at 256x256, batch 2, vs the CPU oracle (both from seed-47 weights)."""
+    torch.manual_seed(7)
+    R = 256
+    x = torch.rand(2, 9, R, R) * 2 - 1
+    y = torch.rand(2, 3, R, R) * 2 - 1
+    st = O.PairedStepOracle()
+    rec = {}
+    ref_losses = st.step(x, y, record=rec)
+    m = _make_models()
+    losses = m.step_fn(x.to(DEV), y.to(DEV)).cpu().numpy()
+    ref_losses[3] *= 100
+    assert np.allclose(losses, ref_losses, rtol=1e-3, atol=1e-5), (losses, ref_losses)
+    skip_g, skip_d = O.cancelled_biases()
+    for k, p in m.generator.named_parameters():
+        if k not in skip_g:
+            assert nrel(p, st.G[k]) < NTOL, k
+            assert nrel(p.grad, rec["g_grads"][k]) < NTOL, k
+    for k, p in m.discriminator.named_parameters():
+        if k not in skip_d:
+            assert nrel(p, st.D[k]) < NTOL, k
+    assert nrel(m.step_fn.last_output, rec["fake"]) < NTOL
+
+
+def test_block_module():
+    from floodgan.model_architectures import PairedAttentionBlock
+    torch.manual_seed(8)
+    blk = PairedAttentionBlock(256, 3, 1, 1)
+    x = torch.randn(2, 256, 12, 12)
+    P = {"resnet_blocks.0.conv1.weight": blk.conv1.weight.detach().double().requires_grad_(True),
+         "resnet_blocks.0.conv1.bias": blk.conv1.bias.detach().double().requires_grad_(True),
+         "resnet_blocks.0.conv2.weight": blk.conv2.weight.detach().double().requires_grad_(True),
+         "resnet_blocks.0.conv2.bias": blk.conv2.bias.detach().double().requires_grad_(True)}
+    xr = x.double().requires_grad_(True)
+    yr = O.resnet_block(P, 0, xr)
+    g = torch.randn_like(yr)
+    yr.backward(g)
+    blk = blk.to(DEV)
+    xd = x.to(DEV).requires_grad_(True)
+    yd = blk(xd)
+    yd.backward(g.float().to(DEV))
+    assert nrel(yd, yr) < 1e-5
+    assert nrel(xd.grad, xr.grad) < 1e-5
+    assert nrel(blk.conv1.weight.grad, P["resnet_blocks.0.conv1.weight"].grad) < 1e-5
