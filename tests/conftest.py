@@ -25,3 +25,18 @@ def golden():
         return {k.replace("__", "."): z[k] for k in z.files}
 
     return load
+
+
+@pytest.fixture(scope="session")
+def report():
+    """Append measured parity numbers to gpurun_out/parity_report.jsonl (evidence for DESIGN.md)."""
+    import json
+
+    path = os.path.join(ROOT, "gpurun_out", "parity_report.jsonl")
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+
+    def rec(name, **vals):
+        with open(path, "a") as f:
+            f.write(json.dumps({"test": name, **vals}) + "\n")
+
+    return rec

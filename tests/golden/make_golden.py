@@ -13,7 +13,9 @@ Recorded per resolution R (batch N=2, input_channels=9, seed 47):
   * inputs x0, y0, x1, y1 (two iterations) ~ U[-1, 1) from torch.Generator().manual_seed(1234)
   * G(x0), last_attention_mask, D(cat(x0, y0)) at initialisation
   * per-parameter init checksums (float64 sum, abs-sum, first 8 values, 16 strided samples)
-  * the four per-iteration losses of two training iterations (epochs 1 and 2)
+  * the four per-iteration losses of two training iterations (epochs 1 and 2 of one
+    train_paired() call, one batch per epoch, lr 2e-4 then 1e-4 from the reference's LambdaLR);
+    the L1 entry is the raw mean |fake - y| (the reference multiplies it by 100)
   * G(x0), D(cat(x0,y0)) and parameter checksums after each iteration
 
 Usage:  python tests/golden/make_golden.py   (takes ~1 minute on 8 vCPU)
@@ -117,15 +119,29 @@ def run(R, N=2):
     m.loss_func = _Recorder(m.loss_func, mse_log)
     m.l1_loss = _Recorder(m.l1_loss, l1_log)
 
-    for it, (x, y) in enumerate(((x0, y0), (x1, y1))):
-        m.train_loader = [(x, y, ["synthetic"] * N)]
-        m.starting_epoch = it + 1
-        m.num_epochs = it + 1          # lr schedule was fixed at construction from num_epochs=2
-        lr_g = m.optimizer_generator.param_groups[0]["lr"]
-        m.train_paired()
+    class _PerEpochLoader:
+        """epoch e (1-based) sees the single batch (x_{e-1}, y_{e-1})"""
+
+        def __init__(self, batches):
+            self.batches, self.calls = batches, 0
+
+        def __iter__(self):
+            b = self.batches[self.calls]
+            self.calls += 1
+            return iter([b])
+
+        def __len__(self):
+            return 1
+
+    m.train_loader = _PerEpochLoader([(x0, y0, ["synthetic"] * N), (x1, y1, ["synthetic"] * N)])
+    lrs = []
+    orig_save = m.save_results
+
+    def _record(epoch, losses, epoch_start_time):
+        it = epoch - 1
         # call order inside one iteration: D(fake) vs 0, D(real) vs 1, D(fake) vs 1 (+ l1)
         d_syn, d_real, g_syn = mse_log[-3:]
-        rec[f"it{it}_lr"] = np.array([lr_g])
+        rec[f"it{it}_lr"] = np.array([lrs[it]])
         rec[f"it{it}_losses"] = np.array([d_real, d_syn, g_syn, l1_log[-1]])
         with torch.no_grad():
             rec[f"it{it}_g_out"] = G(x0).numpy()
@@ -135,6 +151,13 @@ def run(R, N=2):
             rec[f"it{it}_G/" + k] = v
         for k, v in checksums(D).items():
             rec[f"it{it}_D/" + k] = v
+        orig_save(epoch=epoch, losses=losses, epoch_start_time=epoch_start_time)
+        lrs.append(m.optimizer_generator.param_groups[0]["lr"])
+
+    m.save_results = _record
+    lrs.append(m.optimizer_generator.param_groups[0]["lr"])
+    # epochs 1 and 2 of the unmodified loop; LambdaLR (num_epochs=2): lr 2e-4 then 1e-4
+    m.train_paired()
     rec["meta"] = np.array([R, N, 47, 2, 1234], dtype=np.int64)
     return rec
 
