@@ -204,6 +204,224 @@ conv_fwd_kernel(const ConvBatch batch) {
 }
 
 // ------------------------------------------------------------------------------------------
+// Split-bf16 forward kernel ("bf16x6"): fp32-equivalent products on bf16 MFMA.
+//
+// Every fp32 operand v is split at staging time into three bf16 pieces v = h + m + l
+// (h = bf16(v), m = bf16(v - h), l = bf16(v - h - m): 3 x 8 significant bits = the 24 of fp32).
+// A*B is accumulated in fp32 from the six bf16 products whose order is <= 2^-16:
+//     hh + hm + mh + hl + lh + mm            (dropped: ml, lm ~2^-24, ll ~2^-32)
+// bf16 x bf16 products are exact in fp32, so the result carries fp32-level error
+// (|dropped| <= 3*2^-24 relative, the same order as fp32 rounding) while the MFMA rate is
+// 6 x v_mfma_f32_32x32x16_bf16 (192 cycles) per 32x32x16 block instead of 8 x
+// v_mfma_f32_32x32x2_f32 (512 cycles): 2.67x the fp32 matrix peak.
+// Operand layout in LDS: [buf][piece][row][k] bf16, 16 k per stage, row pitch 24 bf16 (48 B:
+// conflict-free ds_read_b128 fragment reads).  Lane l feeds rows l&31, k = 8(l>>5)..+7.
+// ------------------------------------------------------------------------------------------
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void split3(const float (&v)[8], bf16x8& h, bf16x8& m, bf16x8& l) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const __bf16 hh = (__bf16)v[e];
+        const float r = v[e] - (float)hh;
+        const __bf16 mm = (__bf16)r;
+        const float r2 = r - (float)mm;
+        h[e] = hh;
+        m[e] = mm;
+        l[e] = (__bf16)r2;
+    }
+}
+
+template <int BM, int BN, int WM, int WN, bool VEC>
+__global__ void __launch_bounds__((BM / WM) * (BN / WN) * 64, 2)
+conv_fwd_x6_kernel(const ConvBatch batch) {
+    constexpr int NWN = BN / WN;
+    constexpr int NT = (BM / WM) * (BN / WN) * 64;
+    constexpr int TM = WM / 32, TN = WN / 32;
+    constexpr int LDP = 24;                       // bf16 per LDS row (16 + 8 pad)
+    constexpr int A_SLOTS = BM * 2, B_SLOTS = BN * 2;   // slot = 8 consecutive k of one row
+    constexpr int A_IT = (A_SLOTS + NT - 1) / NT, B_IT = (B_SLOTS + NT - 1) / NT;
+
+    __shared__ __attribute__((aligned(16))) __bf16 As[2][3][BM][LDP];
+    __shared__ __attribute__((aligned(16))) __bf16 Bs[2][3][BN][LDP];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / NWN, wn = wave - (wave / NWN) * NWN;
+
+    const int wid = fg::xcd_remap(blockIdx.x, gridDim.x);
+    int pi = 0;
+    while (pi + 1 < batch.count && wid >= batch.blk_start[pi + 1]) ++pi;
+    const fg_conv_problem& P = batch.p[pi];
+    const int local = wid - batch.blk_start[pi];
+    const int ntn = batch.ntiles_n[pi];
+    const int mt = local / ntn, nt = local - (local / ntn) * ntn;
+    const int m0 = mt * BM, n0 = nt * BN;
+    const int mab = P.m_a * P.m_b;
+    const int M = P.m_img * mab;
+    const int jtr = P.jp / 16;
+    const int nkt = P.kh * jtr;
+    const int jv = P.j_valid;
+    const long long sxr = P.sxr;
+
+    const float* arow[A_IT];
+    int a_r[A_IT], a_g[A_IT];
+    bool aok[A_IT], aslot[A_IT];
+#pragma unroll
+    for (int i = 0; i < A_IT; ++i) {
+        const int s = tid + i * NT;
+        a_r[i] = s >> 1;
+        a_g[i] = s & 1;
+        aslot[i] = s < A_SLOTS;
+        const int m = m0 + (s >> 1);
+        aok[i] = aslot[i] && (m < M);
+        arow[i] = P.x;
+        if (aok[i]) {
+            int img, a, b;
+            decomp(m, P.m_b, mab, img, a, b);
+            arow[i] = P.x + img * P.sxn + a * P.sxa + b * P.sxb;
+        }
+    }
+    const float* brow[B_IT];
+    int b_r[B_IT], b_g[B_IT];
+    bool bok[B_IT], bslot[B_IT];
+#pragma unroll
+    for (int i = 0; i < B_IT; ++i) {
+        const int s = tid + i * NT;
+        b_r[i] = s >> 1;
+        b_g[i] = s & 1;
+        bslot[i] = s < B_SLOTS;
+        bok[i] = bslot[i] && (n0 + (s >> 1) < P.n_out);
+        brow[i] = P.w + (size_t)(bok[i] ? n0 + (s >> 1) : 0) * P.ldw;
+    }
+
+    float ra[A_IT][8], rb[B_IT][8];
+    auto load = [&](int kt) {
+        const int r = kt / jtr;
+        const int jb = (kt - r * jtr) * 16;
+#pragma unroll
+        for (int i = 0; i < A_IT; ++i) {
+            const int j = jb + a_g[i] * 8;
+            const float* src = arow[i] + r * sxr + j;
+            if constexpr (VEC) {
+                f32x4 v0 = {0.f, 0.f, 0.f, 0.f}, v1 = v0;
+                if (aok[i] && j < jv) v0 = *reinterpret_cast<const f32x4*>(src);
+                if (aok[i] && j + 4 < jv) v1 = *reinterpret_cast<const f32x4*>(src + 4);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    ra[i][e] = v0[e];
+                    ra[i][4 + e] = v1[e];
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) ra[i][e] = (aok[i] && j + e < jv) ? src[e] : 0.f;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < B_IT; ++i) {
+            f32x4 v0 = {0.f, 0.f, 0.f, 0.f}, v1 = v0;
+            if (bok[i]) {
+                const float* src = brow[i] + kt * 16 + b_g[i] * 8;
+                v0 = *reinterpret_cast<const f32x4*>(src);
+                v1 = *reinterpret_cast<const f32x4*>(src + 4);
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                rb[i][e] = v0[e];
+                rb[i][4 + e] = v1[e];
+            }
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < A_IT; ++i)
+            if (aslot[i]) {
+                bf16x8 h, m, l;
+                split3(ra[i], h, m, l);
+                *reinterpret_cast<bf16x8*>(&As[buf][0][a_r[i]][a_g[i] * 8]) = h;
+                *reinterpret_cast<bf16x8*>(&As[buf][1][a_r[i]][a_g[i] * 8]) = m;
+                *reinterpret_cast<bf16x8*>(&As[buf][2][a_r[i]][a_g[i] * 8]) = l;
+            }
+#pragma unroll
+        for (int i = 0; i < B_IT; ++i)
+            if (bslot[i]) {
+                bf16x8 h, m, l;
+                split3(rb[i], h, m, l);
+                *reinterpret_cast<bf16x8*>(&Bs[buf][0][b_r[i]][b_g[i] * 8]) = h;
+                *reinterpret_cast<bf16x8*>(&Bs[buf][1][b_r[i]][b_g[i] * 8]) = m;
+                *reinterpret_cast<bf16x8*>(&Bs[buf][2][b_r[i]][b_g[i] * 8]) = l;
+            }
+    };
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[tm][tn][e] = 0.f;
+
+    const int lrow = lane & 31, lk = (lane >> 5) * 8;
+    if (nkt > 0) {
+        load(0);
+        store(0);
+    }
+    __syncthreads();
+    for (int kt = 0; kt < nkt; ++kt) {
+        const int cur = kt & 1;
+        if (kt + 1 < nkt) load(kt + 1);
+        bf16x8 af[TM][3], bfr[TN][3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+                af[tm][p] = *reinterpret_cast<const bf16x8*>(&As[cur][p][wm * WM + tm * 32 + lrow][lk]);
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn)
+                bfr[tn][p] = *reinterpret_cast<const bf16x8*>(&Bs[cur][p][wn * WN + tn * 32 + lrow][lk]);
+        }
+        // six fp32-relevant piece products; each pair's (tm, tn) blocks interleaved
+        constexpr int PA[6] = {1, 0, 2, 0, 1, 0};
+        constexpr int PB[6] = {1, 2, 0, 1, 0, 0};
+#pragma unroll
+        for (int c = 0; c < 6; ++c)
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                for (int tn = 0; tn < TN; ++tn)
+                    acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[tm][PA[c]], bfr[tn][PB[c]], acc[tm][tn],
+                                                                          0, 0, 0);
+        if (kt + 1 < nkt) store(cur ^ 1);
+        __syncthreads();
+    }
+
+    const int act = P.act;
+    const bool accum = P.accumulate != 0;
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) {
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+            const int row = wm * WM + tm * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
+            const int m = m0 + row;
+            if (m >= M) continue;
+            int img, a, b;
+            decomp(m, P.m_b, mab, img, a, b);
+            float* yrow = P.y + img * P.syn + a * P.sya + b * P.syb;
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) {
+                const int n = n0 + wn * WN + tn * 32 + lrow;
+                if (n >= P.n_out) continue;
+                float v = acc[tm][tn][reg];
+                if (P.bias) v += P.bias[n];
+                v = fg::act_fwd(v, act);
+                float* dst = yrow + n * P.syc;
+                if (accum) v += *dst;
+                *dst = v;
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // weight gradient: out[split][a][k] = sum_m p[row_p(m)+a] * x[row_x(m)+koff(k)]
 // ------------------------------------------------------------------------------------------
 template <int BA, int BKC, int WA, int WK, bool VX, bool VP>
@@ -383,8 +601,16 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ slabs, int splits,
         const int kr = k / J, j = k - (k / J) * J;
         const int ks = j / map.c, ch = j - (j / map.c) * map.c;
         if (ch >= map.c_valid) continue;
-        double s = 0.0;
-        for (int sp = 0; sp < splits; ++sp) s += slabs[(size_t)sp * total + idx];
+        double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+        int sp = 0;
+        for (; sp + 4 <= splits; sp += 4) {
+            s0 += slabs[(size_t)sp * total + idx];
+            s1 += slabs[(size_t)(sp + 1) * total + idx];
+            s2 += slabs[(size_t)(sp + 2) * total + idx];
+            s3 += slabs[(size_t)(sp + 3) * total + idx];
+        }
+        for (; sp < splits; ++sp) s0 += slabs[(size_t)sp * total + idx];
+        const double s = (s0 + s1) + (s2 + s3);
         const int r = map.rtab[kr], c2 = map.stab[ks];
         const int n = a + map.n_base;
         const size_t dst = map.dim0_is_n ? (((size_t)n * map.d1 + ch) * map.KH + r) * map.KW + c2
@@ -416,6 +642,18 @@ __global__ void pack_weight_kernel(const float* __restrict__ w, fg_weight_map ma
         }
         wp[idx] = v;
     }
+}
+
+int g_conv_math = FG_MATH_FP32;
+
+template <int BM, int BN, int WM, int WN>
+int launch_fwd_x6(const ConvBatch& b, int total, bool vec, hipStream_t stream) {
+    constexpr int NT = (BM / WM) * (BN / WN) * 64;
+    if (vec)
+        hipLaunchKernelGGL((conv_fwd_x6_kernel<BM, BN, WM, WN, true>), dim3(total), dim3(NT), 0, stream, b);
+    else
+        hipLaunchKernelGGL((conv_fwd_x6_kernel<BM, BN, WM, WN, false>), dim3(total), dim3(NT), 0, stream, b);
+    return fg::launched("conv_fwd_x6");
 }
 
 template <int BM, int BN, int WM, int WN>
@@ -485,6 +723,7 @@ FG_API int fg_conv_fwd(const fg_conv_problem* probs, int nprob, hipStream_t stre
     b.blk_start[nprob] = total;
     b.blk_start[4] = total;
     if (total == 0) return 0;
+    if (BN == 128 && g_conv_math == FG_MATH_BF16X6) return launch_fwd_x6<128, 128, 64, 64>(b, total, vec, stream);
     if (BN == 128) return launch_fwd<128, 128, 64, 64>(b, total, vec, stream);
     if (BN == 64) return launch_fwd<256, 64, 64, 64>(b, total, vec, stream);
     return launch_fwd<256, 32, 64, 32>(b, total, vec, stream);
@@ -502,7 +741,8 @@ FG_API int fg_conv_wgrad(const fg_wgrad_problem* prob, hipStream_t stream) {
         return fg::fail(FG_ERR_INVALID, "fg_conv_wgrad: splits*m_chunk < M");
     const bool vx = aligned16(p.x) && (p.sxn | p.sxa | p.sxb | p.sxr) % 4 == 0 && p.j_valid % 4 == 0;
     const bool vp = aligned16(p.p) && (p.spn | p.spa | p.spb) % 4 == 0;
-    if (p.n_a > 32) return launch_wgrad<128, 128, 64, 64>(p, vx, vp, stream);
+    if (p.n_a > 64) return launch_wgrad<128, 128, 64, 64>(p, vx, vp, stream);
+    if (p.n_a > 32) return launch_wgrad<64, 256, 64, 64>(p, vx, vp, stream);
     return launch_wgrad<32, 256, 32, 64>(p, vx, vp, stream);
 }
 
@@ -527,3 +767,11 @@ FG_API int fg_pack_weight(const float* w, const fg_weight_map* map, float* wp, h
                        wp);
     return fg::launched("pack_weight");
 }
+
+FG_API int fg_set_conv_math(int mode) {
+    if (mode != FG_MATH_FP32 && mode != FG_MATH_BF16X6) return fg::fail(FG_ERR_INVALID, "fg_set_conv_math: %d", mode);
+    g_conv_math = mode;
+    return 0;
+}
+
+FG_API int fg_get_conv_math(void) { return g_conv_math; }

@@ -181,28 +181,34 @@ __global__ void in_bwd_stats_kernel(fg_view g, int fp, fg_view gadd, fg_view src
     }
 }
 
-// one thread per channel: per-(n,c) coefficients and the (cancelled) conv-bias gradient
+// one thread per (n,c): coefficients of the apply pass and the per-plane part of the
+// (mathematically cancelled) conv-bias gradient
 __global__ void in_bwd_finalize_kernel(int N, int C, int HWi, int chunks, const double* __restrict__ work,
                                        const float* __restrict__ rstd, float* __restrict__ coef,
-                                       float* __restrict__ bias_grad) {
+                                       double* __restrict__ bpart) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= N * C) return;
+    const int n = idx / C, c = idx - (idx / C) * C;
+    const double HW = (double)HWi;
+    double sg = 0, sgx = 0, sx = 0;
+    for (int k = 0; k < chunks; ++k) {
+        const double* wk = work + ((size_t)(n * chunks + k) * C + c) * 3;
+        sg += wk[0];
+        sgx += wk[1];
+        sx += wk[2];
+    }
+    coef[(size_t)idx * 2] = (float)(sg / HW);
+    coef[(size_t)idx * 2 + 1] = (float)(sgx / HW);
+    // sum_hw rstd*(g' - mean g' - xhat*mean(g'xhat)) = -rstd * sx * sgx / HW
+    bpart[idx] = -(double)rstd[idx] * sx * sgx / HW;
+}
+
+__global__ void in_bwd_bias_kernel(int N, int C, const double* __restrict__ bpart, float* __restrict__ bias_grad) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= C) return;
-    const double HW = (double)HWi;
-    double bsum = 0;
-    for (int n = 0; n < N; ++n) {
-        double sg = 0, sgx = 0, sx = 0;
-        for (int k = 0; k < chunks; ++k) {
-            const double* wk = work + ((size_t)(n * chunks + k) * C + c) * 3;
-            sg += wk[0];
-            sgx += wk[1];
-            sx += wk[2];
-        }
-        coef[((size_t)n * C + c) * 2] = (float)(sg / HW);
-        coef[((size_t)n * C + c) * 2 + 1] = (float)(sgx / HW);
-        // sum_hw rstd*(g' - mean g' - xhat*mean(g'xhat)) = -rstd * sx * sgx / HW
-        bsum += -(double)rstd[(size_t)n * C + c] * sx * sgx / HW;
-    }
-    if (bias_grad) bias_grad[c] = (float)bsum;
+    double s = 0;
+    for (int n = 0; n < N; ++n) s += bpart[(size_t)n * C + c];
+    bias_grad[c] = (float)s;
 }
 
 __global__ void in_bwd_apply_kernel(fg_view g, int fp, fg_view gadd, fg_view src, const float* __restrict__ mean,
@@ -291,6 +297,53 @@ __global__ void channel_sum_kernel(fg_view src, int c_valid, int chunks, double*
     }
 }
 
+__global__ void channel_sum4_kernel(fg_view src, int chunks, double* __restrict__ work) {
+    // c_alloc % 4 == 0: threads = (pixel lane g, float4 channel group c4)
+    const int C = src.c_alloc, L = C / 4, PG = NT / L;
+    const int gi = threadIdx.x / L, c4 = threadIdx.x - (threadIdx.x / L) * L;
+    const long long P = (long long)src.n * src.h * src.w;
+    const long long per = (P + chunks - 1) / chunks;
+    const long long p0 = blockIdx.x * per, p1 = min(P, p0 + per);
+    __shared__ double red[NT][4];
+    double acc[4] = {0, 0, 0, 0};
+    if (gi < PG) {
+        f32x4 s = {0.f, 0.f, 0.f, 0.f};
+        int cnt = 0;
+        for (long long p = p0 + gi; p < p1; p += PG) {
+            const int x = (int)(p % src.w);
+            const long long t = p / src.w;
+            const int y = (int)(t % src.h);
+            const int n = (int)(t / src.h);
+            s += ld4(src.ptr + fg::vidx(src, n, y, x) + 4 * c4);
+            if (++cnt == 64) {
+                for (int e = 0; e < 4; ++e) acc[e] += s[e];
+                s = f32x4{0.f, 0.f, 0.f, 0.f};
+                cnt = 0;
+            }
+        }
+        for (int e = 0; e < 4; ++e) acc[e] += s[e];
+    }
+    for (int e = 0; e < 4; ++e) red[threadIdx.x][e] = acc[e];
+    __syncthreads();
+    if (threadIdx.x < L) {
+        double a[4] = {0, 0, 0, 0};
+        for (int gg = 0; gg < PG; ++gg)
+            for (int e = 0; e < 4; ++e) a[e] += red[gg * L + threadIdx.x][e];
+        for (int e = 0; e < 4; ++e) work[(size_t)blockIdx.x * C + 4 * threadIdx.x + e] = a[e];
+    }
+}
+
+__global__ void channel_sum4_finalize(int C, int c_valid, int chunks, const double* __restrict__ work, float* out,
+                                      int accumulate) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= c_valid) return;
+    double s = 0;
+    for (int k = 0; k < chunks; ++k) s += work[(size_t)k * C + c];
+    float v = (float)s;
+    if (accumulate) v += out[c];
+    out[c] = v;
+}
+
 __global__ void channel_sum_finalize(int c_valid, int chunks, const double* __restrict__ work, float* out,
                                      int accumulate) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -307,6 +360,7 @@ bool ok_view(const fg_view& v) { return v.ptr && v.n > 0 && v.h > 0 && v.w > 0 &
 }  // namespace
 
 FG_API long long fg_in_workspace_doubles(int n, int c) { return (long long)n * c * (MAX_CHUNKS * 3 + 2) + 64; }
+// layout: [stats n*c*MAX_CHUNKS*3][coef n*c*2 floats = n*c doubles][bias partials n*c]
 
 FG_API int fg_in_stats(fg_view src, float eps, float* mean, float* rstd, double* work, hipStream_t stream) {
     if (!ok_view(src) || !mean || !rstd || !work || src.c_alloc % 4 || (NT % (src.c_alloc / 4)) != 0)
@@ -355,10 +409,18 @@ FG_API int fg_in_bwd(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, cons
                        mean, rstd, act, chunks, work);
     int e = fg::launched("in_bwd_stats");
     if (e) return e;
-    hipLaunchKernelGGL(in_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, src.n, C,
-                       src.h * src.w, chunks, work, rstd, coef, bias_grad);
+    double* bpart = work + (size_t)src.n * C * MAX_CHUNKS * 3 + (size_t)src.n * C;
+    const int nc = src.n * C;
+    hipLaunchKernelGGL(in_bwd_finalize_kernel, dim3((nc + 255) / 256), dim3(256), 0, stream, src.n, C,
+                       src.h * src.w, chunks, work, rstd, coef, bpart);
     e = fg::launched("in_bwd_finalize");
     if (e) return e;
+    if (bias_grad) {
+        hipLaunchKernelGGL(in_bwd_bias_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, src.n, C, bpart,
+                           bias_grad);
+        e = fg::launched("in_bwd_bias");
+        if (e) return e;
+    }
     const long long total = (long long)dst.n * (dst.h + 2 * dst.pad) * (dst.w + 2 * dst.pad) * (C / 4);
     hipLaunchKernelGGL(in_bwd_apply_kernel, dim3(fg::blocks_for(total, 256, 16384)), dim3(256), 0, stream, gsrc,
                        fold_pad, gadd, src, mean, rstd, coef, act, dst);
@@ -380,6 +442,14 @@ FG_API int fg_channel_sum(fg_view src, int c_valid, float* out, int accumulate, 
     int chunks = (int)((P + 4095) / 4096);
     if (chunks > MAX_CHUNKS) chunks = MAX_CHUNKS;
     if (chunks < 1) chunks = 1;
+    if (src.c_alloc % 4 == 0 && NT % (src.c_alloc / 4) == 0) {
+        hipLaunchKernelGGL(channel_sum4_kernel, dim3(chunks), dim3(NT), 0, stream, src, chunks, work);
+        int e = fg::launched("channel_sum4");
+        if (e) return e;
+        hipLaunchKernelGGL(channel_sum4_finalize, dim3((c_valid + 255) / 256), dim3(256), 0, stream, src.c_alloc,
+                           c_valid, chunks, work, out, accumulate);
+        return fg::launched("channel_sum4_finalize");
+    }
     const int groups = (c_valid + NT - 1) / NT;
     hipLaunchKernelGGL(channel_sum_kernel, dim3(chunks, groups), dim3(NT), 0, stream, src, c_valid, chunks, work);
     int e = fg::launched("channel_sum");

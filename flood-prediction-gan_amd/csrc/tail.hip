@@ -15,10 +15,22 @@ struct PixelVals {
 };
 
 __device__ __forceinline__ void load_pixel(const fg_view& cl, const fg_view& al, int n, int y, int x, PixelVals& v) {
-    const float* cp = cl.ptr + fg::vidx(cl, n, y, x);
-    const float* ap = al.ptr + fg::vidx(al, n, y, x);
+    // c_alloc >= 28 / >= 12 and 16-byte aligned rows (checked by the launchers): vector loads
+    const f32x4* cp = reinterpret_cast<const f32x4*>(cl.ptr + fg::vidx(cl, n, y, x));
+    const f32x4* ap4 = reinterpret_cast<const f32x4*>(al.ptr + fg::vidx(al, n, y, x));
+    float cv[28], ap[12];
 #pragma unroll
-    for (int i = 0; i < NCONT; ++i) v.t[i] = tanhf(cp[i]);
+    for (int q = 0; q < 7; ++q) {
+        const f32x4 t = cp[q];
+        cv[4 * q] = t[0]; cv[4 * q + 1] = t[1]; cv[4 * q + 2] = t[2]; cv[4 * q + 3] = t[3];
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        const f32x4 t = ap4[q];
+        ap[4 * q] = t[0]; ap[4 * q + 1] = t[1]; ap[4 * q + 2] = t[2]; ap[4 * q + 3] = t[3];
+    }
+#pragma unroll
+    for (int i = 0; i < NCONT; ++i) v.t[i] = tanhf(cv[i]);
     float mx = ap[0];
 #pragma unroll
     for (int i = 1; i < NATT; ++i) mx = fmaxf(mx, ap[i]);
@@ -71,7 +83,7 @@ __global__ void tail_bwd_kernel(fg_view cl, fg_view al, fg_sview x, fg_sview gou
         const int yy = yp - gc.pad, xx = xp - gc.pad;
         float* gcp = gc.ptr + ((size_t)(n * hp + yp) * wp + xp) * gc.c_alloc;
         if (yy < 0 || yy >= H || xx < 0 || xx >= W) {
-            for (int i = 0; i < gc.c_alloc; ++i) gcp[i] = 0.f;
+            for (int i = 0; i < gc.c_alloc; i += 4) *reinterpret_cast<f32x4*>(gcp + i) = f32x4{0.f, 0.f, 0.f, 0.f};
             continue;
         }
         PixelVals v;
@@ -83,24 +95,36 @@ __global__ void tail_bwd_kernel(fg_view cl, fg_view al, fg_sview x, fg_sview gou
             xin[c] = x.ptr[n * x.sn + c * x.sc + yy * x.sy + xx * x.sx];
         }
         float gatt[NATT];
+        float go[32];
 #pragma unroll
         for (int i = 0; i < 9; ++i) {
             gatt[i] = g[0] * v.t[3 * i] + g[1] * v.t[3 * i + 1] + g[2] * v.t[3 * i + 2];
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
                 const float tt = v.t[3 * i + c];
-                gcp[3 * i + c] = g[c] * v.a[i] * (1.f - tt * tt);
+                go[3 * i + c] = g[c] * v.a[i] * (1.f - tt * tt);
             }
         }
+#pragma unroll
+        for (int i = NCONT; i < 32; ++i) go[i] = 0.f;
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            *reinterpret_cast<f32x4*>(gcp + 4 * q) = f32x4{go[4 * q], go[4 * q + 1], go[4 * q + 2], go[4 * q + 3]};
+        for (int i = 32; i < gc.c_alloc; i += 4) *reinterpret_cast<f32x4*>(gcp + i) = f32x4{0.f, 0.f, 0.f, 0.f};
         gatt[9] = g[0] * xin[0] + g[1] * xin[1] + g[2] * xin[2];
-        for (int i = NCONT; i < gc.c_alloc; ++i) gcp[i] = 0.f;
         float dot = 0.f;
 #pragma unroll
         for (int i = 0; i < NATT; ++i) dot += v.a[i] * gatt[i];
         float* gap = ga.ptr + fg::vidx(ga, n, yy, xx);
+        float ao[16];
 #pragma unroll
-        for (int i = 0; i < NATT; ++i) gap[i] = v.a[i] * (gatt[i] - dot);
-        for (int i = NATT; i < ga.c_alloc; ++i) gap[i] = 0.f;
+        for (int i = 0; i < NATT; ++i) ao[i] = v.a[i] * (gatt[i] - dot);
+#pragma unroll
+        for (int i = NATT; i < 16; ++i) ao[i] = 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            *reinterpret_cast<f32x4*>(gap + 4 * q) = f32x4{ao[4 * q], ao[4 * q + 1], ao[4 * q + 2], ao[4 * q + 3]};
+        for (int i = 16; i < ga.c_alloc; i += 4) *reinterpret_cast<f32x4*>(gap + i) = f32x4{0.f, 0.f, 0.f, 0.f};
     }
 }
 
@@ -108,8 +132,8 @@ __global__ void tail_bwd_kernel(fg_view cl, fg_view al, fg_sview x, fg_sview gou
 
 FG_API int fg_tail_fwd(fg_view content_logits, fg_view att_logits, fg_sview x, float* out, float* mask,
                        hipStream_t stream) {
-    if (!content_logits.ptr || !att_logits.ptr || !x.ptr || !out || !mask || content_logits.c_alloc < NCONT ||
-        att_logits.c_alloc < NATT || att_logits.h != content_logits.h || att_logits.w != content_logits.w ||
+    if (!content_logits.ptr || !att_logits.ptr || !x.ptr || !out || !mask || content_logits.c_alloc < 28 ||
+        content_logits.c_alloc % 4 || att_logits.c_alloc < 12 || att_logits.c_alloc % 4 || att_logits.h != content_logits.h || att_logits.w != content_logits.w ||
         att_logits.n != content_logits.n)
         return fg::fail(FG_ERR_INVALID, "fg_tail_fwd: bad args");
     const long long total = (long long)content_logits.n * content_logits.h * content_logits.w;
@@ -121,7 +145,9 @@ FG_API int fg_tail_fwd(fg_view content_logits, fg_view att_logits, fg_sview x, f
 FG_API int fg_tail_bwd(fg_view content_logits, fg_view att_logits, fg_sview x, fg_sview g_out, fg_view g_content,
                        fg_view g_att, hipStream_t stream) {
     if (!content_logits.ptr || !att_logits.ptr || !x.ptr || !g_out.ptr || !g_content.ptr || !g_att.ptr ||
-        g_content.c_alloc < NCONT || g_att.c_alloc < NATT || g_content.h != content_logits.h ||
+        content_logits.c_alloc < 28 || content_logits.c_alloc % 4 || att_logits.c_alloc < 12 ||
+        att_logits.c_alloc % 4 || g_content.c_alloc < 32 || g_content.c_alloc % 4 || g_att.c_alloc < 16 ||
+        g_att.c_alloc % 4 || g_content.h != content_logits.h ||
         g_content.w != content_logits.w || g_att.h != content_logits.h || g_att.w != content_logits.w ||
         g_att.pad != 0)
         return fg::fail(FG_ERR_INVALID, "fg_tail_bwd: bad args");

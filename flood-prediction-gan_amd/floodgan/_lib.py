@@ -14,6 +14,8 @@ LIB_PATH = os.environ.get("FLOODGAN_LIB", os.path.join(_HERE, "lib", "libfloodga
 
 FG_PAD_ZERO, FG_PAD_REFLECT = 0, 1
 FG_ACT_NONE, FG_ACT_RELU, FG_ACT_LRELU = 0, 1, 2
+FG_MATH_FP32, FG_MATH_BF16X6 = 0, 1
+CONV_MATH = {"fp32": FG_MATH_FP32, "bf16x6": FG_MATH_BF16X6}
 
 
 class fg_view(C.Structure):
@@ -62,6 +64,8 @@ SIGNATURES = {
     "fg_version": [],
     "fg_device_ok": [],
     "fg_conv_fwd": [C.POINTER(fg_conv_problem), C.c_int, C.c_void_p],
+    "fg_set_conv_math": [C.c_int],
+    "fg_get_conv_math": [],
     "fg_conv_wgrad": [C.POINTER(fg_wgrad_problem), C.c_void_p],
     "fg_wgrad_reduce": [C.c_void_p, C.c_int, C.POINTER(fg_weight_map), C.c_void_p, C.c_int, C.c_void_p],
     "fg_pack_weight": [C.c_void_p, C.POINTER(fg_weight_map), C.c_void_p, C.c_void_p],
@@ -105,7 +109,20 @@ def load(path=LIB_PATH):
         fn.argtypes = argt
         fn.restype = RESTYPES.get(name, C.c_int)
     _lib = lib
+    mode = os.environ.get("FLOODGAN_CONV_MATH")
+    if mode:
+        set_conv_math(mode)
     return lib
+
+
+def set_conv_math(mode):
+    """'fp32' (v_mfma_f32_32x32x2_f32) or 'bf16x6' (fp32-equivalent split-bf16 MFMA)."""
+    check(load().fg_set_conv_math(CONV_MATH[mode]), "set_conv_math")
+
+
+def get_conv_math():
+    inv = {v: k for k, v in CONV_MATH.items()}
+    return inv[load().fg_get_conv_math()]
 
 
 def check(rc, what):

@@ -210,11 +210,16 @@ def phase_maps(shape, k, p, c_alloc, n_base=0, n_out=None):
 # weight-gradient problems (fg_wgrad_problem)
 # ------------------------------------------------------------------------------------------
 
-WG_BLOCKS = 2048
+WG_BLOCKS = 1024   # ~ one full wave of resident workgroups (256 CUs x 4)
+
+
+def wgrad_tile(n_a):
+    """(rows, cols) of the weight-gradient tile the engine picks for n_a result rows"""
+    return (128, 128) if n_a > 64 else ((64, 256) if n_a > 32 else (32, 256))
 
 
 def wgrad_splits(n_a, K, M):
-    ba, bk = (128, 128) if n_a > 32 else (32, 256)
+    ba, bk = wgrad_tile(n_a)
     tiles = -(-n_a // ba) * -(-K // bk)
     splits = max(1, min(WG_BLOCKS // max(tiles, 1), -(-M // 256)))
     chunk = rup(-(-M // splits), 16)

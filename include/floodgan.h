@@ -30,6 +30,9 @@ extern "C" {
 enum { FG_PAD_ZERO = 0, FG_PAD_REFLECT = 1 };
 enum { FG_ACT_NONE = 0, FG_ACT_RELU = 1, FG_ACT_LRELU = 2 };   /* LeakyReLU slope 0.2 */
 enum { FG_ERR_INVALID = -1 };
+/* Convolution arithmetic: fp32 MFMA (v_mfma_f32_32x32x2_f32), or fp32-equivalent split-bf16
+ * (each fp32 operand = 3 bf16 pieces, 6 exact bf16 products accumulated in fp32). */
+enum { FG_MATH_FP32 = 0, FG_MATH_BF16X6 = 1 };
 
 /* An NHWC view: interior h x w, border `pad` on every side, c_alloc channels per pixel. */
 typedef struct fg_view {
@@ -106,6 +109,10 @@ int fg_device_ok(void);   /* 0 if a gfx950 device is current, else an error code
 /* ---------------------------------------------------------------------------------------- */
 /* Up to 4 problems in one launch (the four output phases of a stride-2 transposed conv). */
 int fg_conv_fwd(const fg_conv_problem* probs, int nprob, hipStream_t stream);
+
+/* Select the convolution arithmetic (FG_MATH_*) for subsequent launches (process-wide). */
+int fg_set_conv_math(int mode);
+int fg_get_conv_math(void);
 
 /* Weight gradient into partial slabs (see fg_wgrad_problem). */
 int fg_conv_wgrad(const fg_wgrad_problem* prob, hipStream_t stream);

@@ -1,0 +1,90 @@
+"""Micro-benchmark (GPU): conv engine kernels at the real bs-8 512^2 geometries, both conv
+maths, interleaved in one process, plus an accuracy check vs fp64 on a smaller problem."""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "flood-prediction-gan_amd"))
+import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+from floodgan import _lib as L, ops, plans as PL  # noqa: E402
+from floodgan.plans import Buf  # noqa: E402
+
+
+def nrel(a, b):
+    a = a.detach().double().cpu(); b = b.detach().double().cpu()
+    return float((a - b).norm() / max(float(b.norm()), 1e-30))
+
+
+def make(N, H, Cin, Cout, k, s, p, dev="cuda"):
+    X = Buf.empty(N, H, H, Cin, p, dev)
+    X.t.uniform_(-1, 1)
+    w = torch.randn(Cout, Cin, k, k, device=dev) * 0.02
+    m = PL.wmap_conv_fwd(w.shape, Cin)
+    wp = ops.pack_weight(w, m)
+    Ho = PL.out_size(H, k, s, p)
+    Y = Buf.empty(N, Ho, Ho, Cout, 0, dev)
+    prob = PL.conv_problem(X, p, k, s, wp, m, Y, bias=torch.zeros(Cout, device=dev))
+    flops = 2.0 * N * Ho * Ho * Cout * Cin * k * k
+    return prob, flops, (X, w, Y)
+
+
+def time_it(fn, reps=10):
+    for _ in range(2):
+        fn()
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record()
+    for _ in range(reps):
+        fn()
+    ev[1].record()
+    torch.cuda.synchronize()
+    return ev[0].elapsed_time(ev[1]) / reps
+
+
+def accuracy(mode):
+    L.set_conv_math(mode)
+    torch.manual_seed(0)
+    x = torch.randn(2, 256, 24, 24, dtype=torch.float64)
+    w = torch.randn(256, 256, 3, 3, dtype=torch.float64) * 0.02
+    ref = F.conv2d(F.pad(x, (1,) * 4, mode="reflect"), w)
+    X = Buf(torch.zeros(2, 26, 26, 256).reshape(-1), 2, 24, 24, 256, 1)
+    X.nhwc().copy_(F.pad(x, (1,) * 4, mode="reflect").float().permute(0, 2, 3, 1))
+    X = Buf(X.t.cuda(), 2, 24, 24, 256, 1)
+    wd = w.float().cuda()
+    m = PL.wmap_conv_fwd(wd.shape, 256)
+    Y = Buf.empty(2, 24, 24, 256, 0, "cuda")
+    ops.conv([PL.conv_problem(X, 1, 3, 1, ops.pack_weight(wd, m), m, Y)])
+    torch.cuda.synchronize()
+    out = Y.interior().permute(0, 3, 1, 2).cpu()
+    # fp32 CPU reference of the same conv for scale
+    ref32 = F.conv2d(F.pad(x.float(), (1,) * 4, mode="reflect"), w.float())
+    return nrel(out, ref), nrel(ref32, ref)
+
+
+def main():
+    L.load()
+    for mode in ("fp32", "bf16x6"):
+        e, e32 = accuracy(mode)
+        print(f"accuracy {mode}: rel err vs fp64 {e:.3e}  (torch CPU fp32: {e32:.3e})")
+    cases = {"resblock 3x3 256->256 @128": (8, 128, 256, 256, 3, 1, 1),
+             "conv2 3x3s2 64->128 @512": (8, 512, 64, 128, 3, 2, 1),
+             "D model.8 4x4 256->512 @64 (2N)": (16, 64, 256, 512, 4, 1, 1)}
+    for name, c in cases.items():
+        prob, flops, keep = make(*c)
+        res = {}
+        for rep in range(3):
+            for mode in ("fp32", "bf16x6"):
+                L.set_conv_math(mode)
+                ms = time_it(lambda: ops.conv([prob]))
+                res.setdefault(mode, []).append(ms)
+        for mode, v in res.items():
+            ms = min(v)
+            print(f"{name:36s} {mode:7s} {ms:8.3f} ms  {flops / ms / 1e9:7.1f} TFLOP/s")
+
+
+if __name__ == "__main__":
+    main()
