@@ -23,6 +23,7 @@ namespace {
 
 constexpr int BK = 16;
 constexpr int LDK = BK + 4;
+int g_conv_math = FG_MATH_FP32;
 
 struct ConvBatch {
     fg_conv_problem p[4];
@@ -589,6 +590,175 @@ conv_wgrad_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
         }
 }
 
+// ------------------------------------------------------------------------------------------
+// Split-bf16 weight gradient.  Operands are staged reduction-contiguous ([piece][a or k][m],
+// 16 pixels m per stage): each thread gathers ONE column (a of P, or k of X) over 8
+// consecutive pixels -- lanes of a wave take consecutive columns, so every global load is a
+// coalesced 256-byte row segment -- splits the 8 values into h/m/l and writes one
+// ds_write_b128 per piece.  The MFMA loop is the forward kernel's.
+// ------------------------------------------------------------------------------------------
+template <int BA, int BKC, int WA, int WK>
+__global__ void __launch_bounds__((BA / WA) * (BKC / WK) * 64, 2)
+conv_wgrad_x6_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
+    constexpr int NWK = BKC / WK;
+    constexpr int NT = (BA / WA) * (BKC / WK) * 64;
+    constexpr int TM = WA / 32, TN = WK / 32;
+    constexpr int LDP = 24;
+    constexpr int P_SLOTS = BA * 2, X_SLOTS = BKC * 2;    // slot = one column x 8 pixels
+    constexpr int P_IT = (P_SLOTS + NT - 1) / NT, X_IT = (X_SLOTS + NT - 1) / NT;
+
+    __shared__ __attribute__((aligned(16))) __bf16 Ps[2][3][BA][LDP];
+    __shared__ __attribute__((aligned(16))) __bf16 Xs[2][3][BKC][LDP];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wa = wave / NWK, wk = wave - (wave / NWK) * NWK;
+    const int wid = fg::xcd_remap(blockIdx.x, gridDim.x);
+    const int ntile = tiles_a * tiles_k;
+    const int split = wid / ntile;
+    const int tile = wid - split * ntile;
+    const int ta = tile / tiles_k, tk = tile - (tile / tiles_k) * tiles_k;
+    const int a0 = ta * BA, k0 = tk * BKC;
+    const int mab = P.m_a * P.m_b;
+    const int M = P.m_img * mab;
+    const int mbeg = split * P.m_chunk;
+    const int mend = min(M, mbeg + P.m_chunk);
+    const int K = P.kh * P.j_valid;
+    const int nit = mend > mbeg ? (mend - mbeg + 15) / 16 : 0;
+
+    // column slots: s -> (column c = s % BCOLS, pixel half h = s / BCOLS)
+    int p_col[P_IT], p_h[P_IT];
+    bool p_ok[P_IT], p_slot[P_IT];
+#pragma unroll
+    for (int i = 0; i < P_IT; ++i) {
+        const int s = tid + i * NT;
+        p_slot[i] = s < P_SLOTS;
+        p_col[i] = s % BA;
+        p_h[i] = s / BA;
+        p_ok[i] = p_slot[i] && (a0 + p_col[i] < P.n_a);
+    }
+    int x_col[X_IT], x_h[X_IT];
+    bool x_ok[X_IT], x_slot[X_IT];
+    long long x_off[X_IT];
+#pragma unroll
+    for (int i = 0; i < X_IT; ++i) {
+        const int s = tid + i * NT;
+        x_slot[i] = s < X_SLOTS;
+        x_col[i] = s % BKC;
+        x_h[i] = s / BKC;
+        const int k = k0 + x_col[i];
+        x_ok[i] = x_slot[i] && k < K;
+        const int kk = k < K ? k : 0;
+        const int r = kk / P.j_valid;
+        x_off[i] = r * P.sxr + (kk - r * P.j_valid);
+    }
+
+    float rp[P_IT][8], rx[X_IT][8];
+    auto load = [&](int it) {
+        const int mb = mbeg + it * 16;
+        // pixel coordinates of the 8 rows of each half (same for P and X slots of that half)
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+            int m = mb + 8 * hh;
+            int img = 0, a = 0, b = 0;
+            if (m < mend) decomp(m, P.m_b, mab, img, a, b);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const bool valid = m + e < mend;
+                const float* pb = P.p + img * P.spn + a * P.spa + b * P.spb;
+                const float* xb = P.x + img * P.sxn + a * P.sxa + b * P.sxb;
+#pragma unroll
+                for (int i = 0; i < P_IT; ++i)
+                    if (p_h[i] == hh) rp[i][e] = (valid && p_ok[i]) ? pb[a0 + p_col[i]] : 0.f;
+#pragma unroll
+                for (int i = 0; i < X_IT; ++i)
+                    if (x_h[i] == hh) rx[i][e] = (valid && x_ok[i]) ? xb[x_off[i]] : 0.f;
+                if (++b == P.m_b) {
+                    b = 0;
+                    if (++a == P.m_a) {
+                        a = 0;
+                        ++img;
+                    }
+                }
+            }
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < P_IT; ++i)
+            if (p_slot[i]) {
+                bf16x8 h, m, l;
+                split3(rp[i], h, m, l);
+                *reinterpret_cast<bf16x8*>(&Ps[buf][0][p_col[i]][p_h[i] * 8]) = h;
+                *reinterpret_cast<bf16x8*>(&Ps[buf][1][p_col[i]][p_h[i] * 8]) = m;
+                *reinterpret_cast<bf16x8*>(&Ps[buf][2][p_col[i]][p_h[i] * 8]) = l;
+            }
+#pragma unroll
+        for (int i = 0; i < X_IT; ++i)
+            if (x_slot[i]) {
+                bf16x8 h, m, l;
+                split3(rx[i], h, m, l);
+                *reinterpret_cast<bf16x8*>(&Xs[buf][0][x_col[i]][x_h[i] * 8]) = h;
+                *reinterpret_cast<bf16x8*>(&Xs[buf][1][x_col[i]][x_h[i] * 8]) = m;
+                *reinterpret_cast<bf16x8*>(&Xs[buf][2][x_col[i]][x_h[i] * 8]) = l;
+            }
+    };
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[tm][tn][e] = 0.f;
+
+    const int lrow = lane & 31, lk = (lane >> 5) * 8;
+    if (nit > 0) {
+        load(0);
+        store(0);
+    }
+    __syncthreads();
+    for (int it = 0; it < nit; ++it) {
+        const int cur = it & 1;
+        if (it + 1 < nit) load(it + 1);
+        bf16x8 af[TM][3], bfr[TN][3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+                af[tm][p] = *reinterpret_cast<const bf16x8*>(&Ps[cur][p][wa * WA + tm * 32 + lrow][lk]);
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn)
+                bfr[tn][p] = *reinterpret_cast<const bf16x8*>(&Xs[cur][p][wk * WK + tn * 32 + lrow][lk]);
+        }
+        constexpr int PA[6] = {1, 0, 2, 0, 1, 0};
+        constexpr int PB[6] = {1, 2, 0, 1, 0, 0};
+#pragma unroll
+        for (int c = 0; c < 6; ++c)
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                for (int tn = 0; tn < TN; ++tn)
+                    acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[tm][PA[c]], bfr[tn][PB[c]], acc[tm][tn],
+                                                                          0, 0, 0);
+        if (it + 1 < nit) store(cur ^ 1);
+        __syncthreads();
+    }
+
+    float* out = P.out + (size_t)split * P.n_a * K;
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+            const int a = a0 + wa * WA + tm * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
+            if (a >= P.n_a) continue;
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) {
+                const int k = k0 + wk * WK + tn * 32 + lrow;
+                if (k < K) out[(size_t)a * K + k] = acc[tm][tn][reg];
+            }
+        }
+}
+
 __global__ void wgrad_reduce_kernel(const float* __restrict__ slabs, int splits, fg_weight_map map,
                                     float* __restrict__ dw, int accumulate) {
     const int J = map.kw * map.c;
@@ -644,8 +814,6 @@ __global__ void pack_weight_kernel(const float* __restrict__ w, fg_weight_map ma
     }
 }
 
-int g_conv_math = FG_MATH_FP32;
-
 template <int BM, int BN, int WM, int WN>
 int launch_fwd_x6(const ConvBatch& b, int total, bool vec, hipStream_t stream) {
     constexpr int NT = (BM / WM) * (BN / WN) * 64;
@@ -667,6 +835,16 @@ int launch_fwd(const ConvBatch& b, int total, bool vec, hipStream_t stream) {
 }
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+template <int BA, int BKC, int WA, int WK>
+int launch_wgrad_x6(const fg_wgrad_problem& p, hipStream_t stream) {
+    constexpr int NT = (BA / WA) * (BKC / WK) * 64;
+    const int K = p.kh * p.j_valid;
+    const int ta = (p.n_a + BA - 1) / BA, tk = (K + BKC - 1) / BKC;
+    hipLaunchKernelGGL((conv_wgrad_x6_kernel<BA, BKC, WA, WK>), dim3(ta * tk * p.splits), dim3(NT), 0, stream, p,
+                       ta, tk);
+    return fg::launched("conv_wgrad_x6");
+}
 
 template <int BA, int BKC, int WA, int WK>
 int launch_wgrad(const fg_wgrad_problem& p, bool vx, bool vp, hipStream_t stream) {
@@ -741,6 +919,11 @@ FG_API int fg_conv_wgrad(const fg_wgrad_problem* prob, hipStream_t stream) {
         return fg::fail(FG_ERR_INVALID, "fg_conv_wgrad: splits*m_chunk < M");
     const bool vx = aligned16(p.x) && (p.sxn | p.sxa | p.sxb | p.sxr) % 4 == 0 && p.j_valid % 4 == 0;
     const bool vp = aligned16(p.p) && (p.spn | p.spa | p.spb) % 4 == 0;
+    if (g_conv_math == FG_MATH_BF16X6) {
+        if (p.n_a > 64) return launch_wgrad_x6<128, 128, 64, 64>(p, stream);
+        if (p.n_a > 32) return launch_wgrad_x6<64, 256, 64, 64>(p, stream);
+        return launch_wgrad_x6<32, 256, 32, 64>(p, stream);
+    }
     if (p.n_a > 64) return launch_wgrad<128, 128, 64, 64>(p, vx, vp, stream);
     if (p.n_a > 32) return launch_wgrad<64, 256, 64, 64>(p, vx, vp, stream);
     return launch_wgrad<32, 256, 32, 64>(p, vx, vp, stream);

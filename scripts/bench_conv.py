@@ -84,6 +84,21 @@ def main():
         for mode, v in res.items():
             ms = min(v)
             print(f"{name:36s} {mode:7s} {ms:8.3f} ms  {flops / ms / 1e9:7.1f} TFLOP/s")
+        # weight gradient of the same conv
+        X, w, Y = keep
+        Y.t.uniform_(-1, 1)
+        N, H, Cin, Cout, k, s_, p_ = c
+        wprob = PL.wgrad_conv(Y, X, p_, k, s_, Cout)
+        dw = torch.empty_like(w)
+        wm = PL.wmap_wgrad(w.shape, True, X.c, k)
+        res = {}
+        for rep in range(3):
+            for mode in ("fp32", "bf16x6"):
+                L.set_conv_math(mode)
+                res.setdefault(mode, []).append(time_it(lambda: ops.wgrad(wprob, wm, dw)))
+        for mode, v in res.items():
+            ms = min(v)
+            print(f"{name + ' wgrad':36s} {mode:7s} {ms:8.3f} ms  {flops / ms / 1e9:7.1f} TFLOP/s")
 
 
 if __name__ == "__main__":
