@@ -602,10 +602,10 @@ __global__ void __launch_bounds__((BA / WA) * (BKC / WK) * 64, 2)
 conv_wgrad_x6_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
     constexpr int NWK = BKC / WK;
     constexpr int NT = (BA / WA) * (BKC / WK) * 64;
+    constexpr int HALF = NT / 2;                          // threads per pixel half
     constexpr int TM = WA / 32, TN = WK / 32;
     constexpr int LDP = 24;
-    constexpr int P_SLOTS = BA * 2, X_SLOTS = BKC * 2;    // slot = one column x 8 pixels
-    constexpr int P_IT = (P_SLOTS + NT - 1) / NT, X_IT = (X_SLOTS + NT - 1) / NT;
+    constexpr int P_IT = (BA + HALF - 1) / HALF, X_IT = (BKC + HALF - 1) / HALF;
 
     __shared__ __attribute__((aligned(16))) __bf16 Ps[2][3][BA][LDP];
     __shared__ __attribute__((aligned(16))) __bf16 Xs[2][3][BKC][LDP];
@@ -625,59 +625,62 @@ conv_wgrad_x6_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
     const int K = P.kh * P.j_valid;
     const int nit = mend > mbeg ? (mend - mbeg + 15) / 16 : 0;
 
-    // column slots: s -> (column c = s % BCOLS, pixel half h = s / BCOLS)
-    int p_col[P_IT], p_h[P_IT];
-    bool p_ok[P_IT], p_slot[P_IT];
+    // this thread gathers 8 consecutive pixels (half hh of each 16-pixel stage) of the
+    // columns c0 + i*HALF of P (i < P_IT) and of X (i < X_IT)
+    const int hh = tid / HALF, c0 = tid - (tid / HALF) * HALF;
+    bool p_slot[P_IT], p_ok[P_IT];
+    long long p_off[P_IT];
 #pragma unroll
     for (int i = 0; i < P_IT; ++i) {
-        const int s = tid + i * NT;
-        p_slot[i] = s < P_SLOTS;
-        p_col[i] = s % BA;
-        p_h[i] = s / BA;
-        p_ok[i] = p_slot[i] && (a0 + p_col[i] < P.n_a);
+        const int c = c0 + i * HALF;
+        p_slot[i] = c < BA;
+        p_ok[i] = p_slot[i] && a0 + c < P.n_a;
+        p_off[i] = p_ok[i] ? a0 + c : 0;
     }
-    int x_col[X_IT], x_h[X_IT];
-    bool x_ok[X_IT], x_slot[X_IT];
+    bool x_slot[X_IT], x_ok[X_IT];
     long long x_off[X_IT];
 #pragma unroll
     for (int i = 0; i < X_IT; ++i) {
-        const int s = tid + i * NT;
-        x_slot[i] = s < X_SLOTS;
-        x_col[i] = s % BKC;
-        x_h[i] = s / BKC;
-        const int k = k0 + x_col[i];
+        const int c = c0 + i * HALF;
+        x_slot[i] = c < BKC;
+        const int k = k0 + c;
         x_ok[i] = x_slot[i] && k < K;
-        const int kk = k < K ? k : 0;
+        const int kk = x_ok[i] ? k : 0;
         const int r = kk / P.j_valid;
         x_off[i] = r * P.sxr + (kk - r * P.j_valid);
     }
 
     float rp[P_IT][8], rx[X_IT][8];
     auto load = [&](int it) {
-        const int mb = mbeg + it * 16;
-        // pixel coordinates of the 8 rows of each half (same for P and X slots of that half)
+        const int m = mbeg + it * 16 + 8 * hh;
+        int img = 0, a = 0, b = 0;
+        if (m < mend) decomp(m, P.m_b, mab, img, a, b);
+        long long po = img * P.spn + a * P.spa + b * P.spb;
+        long long xo = img * P.sxn + a * P.sxa + b * P.sxb;
 #pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-            int m = mb + 8 * hh;
-            int img = 0, a = 0, b = 0;
-            if (m < mend) decomp(m, P.m_b, mab, img, a, b);
+        for (int e = 0; e < 8; ++e) {
+            const bool valid = m + e < mend;
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const bool valid = m + e < mend;
-                const float* pb = P.p + img * P.spn + a * P.spa + b * P.spb;
-                const float* xb = P.x + img * P.sxn + a * P.sxa + b * P.sxb;
+            for (int i = 0; i < P_IT; ++i) {
+                const float v = P.p[valid && p_ok[i] ? po + p_off[i] : 0];
+                rp[i][e] = (valid && p_ok[i]) ? v : 0.f;
+            }
 #pragma unroll
-                for (int i = 0; i < P_IT; ++i)
-                    if (p_h[i] == hh) rp[i][e] = (valid && p_ok[i]) ? pb[a0 + p_col[i]] : 0.f;
-#pragma unroll
-                for (int i = 0; i < X_IT; ++i)
-                    if (x_h[i] == hh) rx[i][e] = (valid && x_ok[i]) ? xb[x_off[i]] : 0.f;
-                if (++b == P.m_b) {
-                    b = 0;
-                    if (++a == P.m_a) {
-                        a = 0;
-                        ++img;
-                    }
+            for (int i = 0; i < X_IT; ++i) {
+                const float v = P.x[valid && x_ok[i] ? xo + x_off[i] : 0];
+                rx[i][e] = (valid && x_ok[i]) ? v : 0.f;
+            }
+            po += P.spb;
+            xo += P.sxb;
+            if (++b == P.m_b) {           // next pixel row (rare: once per image row)
+                b = 0;
+                po += P.spa - P.m_b * P.spb;
+                xo += P.sxa - P.m_b * P.sxb;
+                if (++a == P.m_a) {
+                    a = 0;
+                    ++img;
+                    po += P.spn - P.m_a * P.spa;
+                    xo += P.sxn - P.m_a * P.sxa;
                 }
             }
         }
@@ -686,20 +689,22 @@ conv_wgrad_x6_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
 #pragma unroll
         for (int i = 0; i < P_IT; ++i)
             if (p_slot[i]) {
-                bf16x8 h, m, l;
-                split3(rp[i], h, m, l);
-                *reinterpret_cast<bf16x8*>(&Ps[buf][0][p_col[i]][p_h[i] * 8]) = h;
-                *reinterpret_cast<bf16x8*>(&Ps[buf][1][p_col[i]][p_h[i] * 8]) = m;
-                *reinterpret_cast<bf16x8*>(&Ps[buf][2][p_col[i]][p_h[i] * 8]) = l;
+                bf16x8 h, mm, l;
+                split3(rp[i], h, mm, l);
+                const int c = c0 + i * HALF;
+                *reinterpret_cast<bf16x8*>(&Ps[buf][0][c][hh * 8]) = h;
+                *reinterpret_cast<bf16x8*>(&Ps[buf][1][c][hh * 8]) = mm;
+                *reinterpret_cast<bf16x8*>(&Ps[buf][2][c][hh * 8]) = l;
             }
 #pragma unroll
         for (int i = 0; i < X_IT; ++i)
             if (x_slot[i]) {
-                bf16x8 h, m, l;
-                split3(rx[i], h, m, l);
-                *reinterpret_cast<bf16x8*>(&Xs[buf][0][x_col[i]][x_h[i] * 8]) = h;
-                *reinterpret_cast<bf16x8*>(&Xs[buf][1][x_col[i]][x_h[i] * 8]) = m;
-                *reinterpret_cast<bf16x8*>(&Xs[buf][2][x_col[i]][x_h[i] * 8]) = l;
+                bf16x8 h, mm, l;
+                split3(rx[i], h, mm, l);
+                const int c = c0 + i * HALF;
+                *reinterpret_cast<bf16x8*>(&Xs[buf][0][c][hh * 8]) = h;
+                *reinterpret_cast<bf16x8*>(&Xs[buf][1][c][hh * 8]) = mm;
+                *reinterpret_cast<bf16x8*>(&Xs[buf][2][c][hh * 8]) = l;
             }
     };
 
@@ -901,7 +906,7 @@ FG_API int fg_conv_fwd(const fg_conv_problem* probs, int nprob, hipStream_t stre
     b.blk_start[nprob] = total;
     b.blk_start[4] = total;
     if (total == 0) return 0;
-    if (BN == 128 && g_conv_math == FG_MATH_BF16X6) return launch_fwd_x6<128, 128, 64, 64>(b, total, vec, stream);
+    if (BN == 128 && (g_conv_math & FG_MATH_FWD_X6)) return launch_fwd_x6<128, 128, 64, 64>(b, total, vec, stream);
     if (BN == 128) return launch_fwd<128, 128, 64, 64>(b, total, vec, stream);
     if (BN == 64) return launch_fwd<256, 64, 64, 64>(b, total, vec, stream);
     return launch_fwd<256, 32, 64, 32>(b, total, vec, stream);
@@ -919,7 +924,7 @@ FG_API int fg_conv_wgrad(const fg_wgrad_problem* prob, hipStream_t stream) {
         return fg::fail(FG_ERR_INVALID, "fg_conv_wgrad: splits*m_chunk < M");
     const bool vx = aligned16(p.x) && (p.sxn | p.sxa | p.sxb | p.sxr) % 4 == 0 && p.j_valid % 4 == 0;
     const bool vp = aligned16(p.p) && (p.spn | p.spa | p.spb) % 4 == 0;
-    if (g_conv_math == FG_MATH_BF16X6) {
+    if (g_conv_math & FG_MATH_WGRAD_X6) {
         if (p.n_a > 64) return launch_wgrad_x6<128, 128, 64, 64>(p, stream);
         if (p.n_a > 32) return launch_wgrad_x6<64, 256, 64, 64>(p, stream);
         return launch_wgrad_x6<32, 256, 32, 64>(p, stream);
@@ -952,7 +957,8 @@ FG_API int fg_pack_weight(const float* w, const fg_weight_map* map, float* wp, h
 }
 
 FG_API int fg_set_conv_math(int mode) {
-    if (mode != FG_MATH_FP32 && mode != FG_MATH_BF16X6) return fg::fail(FG_ERR_INVALID, "fg_set_conv_math: %d", mode);
+    if (mode < 0 || mode > (FG_MATH_FWD_X6 | FG_MATH_WGRAD_X6))
+        return fg::fail(FG_ERR_INVALID, "fg_set_conv_math: %d", mode);
     g_conv_math = mode;
     return 0;
 }

@@ -14,8 +14,8 @@ LIB_PATH = os.environ.get("FLOODGAN_LIB", os.path.join(_HERE, "lib", "libfloodga
 
 FG_PAD_ZERO, FG_PAD_REFLECT = 0, 1
 FG_ACT_NONE, FG_ACT_RELU, FG_ACT_LRELU = 0, 1, 2
-FG_MATH_FP32, FG_MATH_BF16X6 = 0, 1
-CONV_MATH = {"fp32": FG_MATH_FP32, "bf16x6": FG_MATH_BF16X6}
+FG_MATH_FP32, FG_MATH_FWD_X6, FG_MATH_WGRAD_X6, FG_MATH_BF16X6 = 0, 1, 2, 3
+CONV_MATH = {"fp32": FG_MATH_FP32, "fwd_x6": FG_MATH_FWD_X6, "wgrad_x6": FG_MATH_WGRAD_X6, "bf16x6": FG_MATH_BF16X6}
 
 
 class fg_view(C.Structure):

@@ -30,9 +30,11 @@ extern "C" {
 enum { FG_PAD_ZERO = 0, FG_PAD_REFLECT = 1 };
 enum { FG_ACT_NONE = 0, FG_ACT_RELU = 1, FG_ACT_LRELU = 2 };   /* LeakyReLU slope 0.2 */
 enum { FG_ERR_INVALID = -1 };
-/* Convolution arithmetic: fp32 MFMA (v_mfma_f32_32x32x2_f32), or fp32-equivalent split-bf16
- * (each fp32 operand = 3 bf16 pieces, 6 exact bf16 products accumulated in fp32). */
-enum { FG_MATH_FP32 = 0, FG_MATH_BF16X6 = 1 };
+/* Convolution arithmetic, per kernel family (bit mask): fp32 MFMA (v_mfma_f32_32x32x2_f32), or
+ * fp32-equivalent split-bf16 (each fp32 operand = 3 bf16 pieces, the 6 exact bf16 products of
+ * order >= 2^-16 accumulated in fp32) for the forward/input-gradient kernel and/or the
+ * weight-gradient kernel. */
+enum { FG_MATH_FP32 = 0, FG_MATH_FWD_X6 = 1, FG_MATH_WGRAD_X6 = 2, FG_MATH_BF16X6 = 3 };
 
 /* An NHWC view: interior h x w, border `pad` on every side, c_alloc channels per pixel. */
 typedef struct fg_view {

@@ -96,6 +96,13 @@ def main():
             for mode in ("fp32", "bf16x6"):
                 L.set_conv_math(mode)
                 res.setdefault(mode, []).append(time_it(lambda: ops.wgrad(wprob, wm, dw)))
+        L.set_conv_math("fp32")
+        ops.wgrad(wprob, wm, dw)
+        ref = dw.clone()
+        L.set_conv_math("bf16x6")
+        ops.wgrad(wprob, wm, dw)
+        torch.cuda.synchronize()
+        print(f"{name + ' wgrad':36s} x6 vs fp32 rel diff {nrel(dw, ref):.2e}")
         for mode, v in res.items():
             ms = min(v)
             print(f"{name + ' wgrad':36s} {mode:7s} {ms:8.3f} ms  {flops / ms / 1e9:7.1f} TFLOP/s")
