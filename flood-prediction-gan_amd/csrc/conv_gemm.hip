@@ -591,24 +591,51 @@ conv_wgrad_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
 }
 
 // ------------------------------------------------------------------------------------------
-// Split-bf16 weight gradient.  Operands are staged reduction-contiguous ([piece][a or k][m],
-// 16 pixels m per stage): each thread gathers ONE column (a of P, or k of X) over 8
-// consecutive pixels -- lanes of a wave take consecutive columns, so every global load is a
-// coalesced 256-byte row segment -- splits the 8 values into h/m/l and writes one
-// ds_write_b128 per piece.  The MFMA loop is the forward kernel's.
+// Split-bf16 weight gradient.  Both operands are staged in their natural pixel-major layout
+// ([piece][m][column] bf16, 16 pixels per stage) from coalesced float4 loads, split into
+// h/m/l pieces on the way (ds_write_b64 per piece), and the MFMA fragments -- which need 8
+// consecutive pixels per lane -- are read with the gfx950 transposing LDS read
+// ds_read_b64_tr_b16 (2 per fragment: pixels 0-3 and 4-7 of the lane's k-half).  Row pitch
+// = columns + 32 bf16, so the four rows a 32-lane half reads land on disjoint banks.
 // ------------------------------------------------------------------------------------------
-template <int BA, int BKC, int WA, int WK>
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+__device__ __forceinline__ bf16x8 tr_frag(const __bf16* r0, const __bf16* r4) {
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(r0));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(r4));
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+}
+
+__device__ __forceinline__ void split3x4(const f32x4& v, bf16x4& h, bf16x4& m, bf16x4& l) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const __bf16 hh = (__bf16)v[e];
+        const float r = v[e] - (float)hh;
+        const __bf16 mm = (__bf16)r;
+        const float r2 = r - (float)mm;
+        h[e] = hh;
+        m[e] = mm;
+        l[e] = (__bf16)r2;
+    }
+}
+
+template <int BA, int BKC, int WA, int WK, bool VX, bool VP>
 __global__ void __launch_bounds__((BA / WA) * (BKC / WK) * 64, 2)
 conv_wgrad_x6_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
     constexpr int NWK = BKC / WK;
     constexpr int NT = (BA / WA) * (BKC / WK) * 64;
-    constexpr int HALF = NT / 2;                          // threads per pixel half
     constexpr int TM = WA / 32, TN = WK / 32;
-    constexpr int LDP = 24;
-    constexpr int P_IT = (BA + HALF - 1) / HALF, X_IT = (BKC + HALF - 1) / HALF;
+    constexpr int BR = 16;
+    constexpr int PA_ = BA + 32, PX_ = BKC + 32;     // bf16 row pitches
+    constexpr int P_SLOTS = BR * BA / 4, X_SLOTS = BR * BKC / 4;
+    constexpr int P_IT = (P_SLOTS + NT - 1) / NT, X_IT = (X_SLOTS + NT - 1) / NT;
 
-    __shared__ __attribute__((aligned(16))) __bf16 Ps[2][3][BA][LDP];
-    __shared__ __attribute__((aligned(16))) __bf16 Xs[2][3][BKC][LDP];
+    __shared__ __attribute__((aligned(16))) __bf16 Ps[2][3][BR][PA_];
+    __shared__ __attribute__((aligned(16))) __bf16 Xs[2][3][BR][PX_];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wa = wave / NWK, wk = wave - (wave / NWK) * NWK;
@@ -623,88 +650,101 @@ conv_wgrad_x6_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
     const int mbeg = split * P.m_chunk;
     const int mend = min(M, mbeg + P.m_chunk);
     const int K = P.kh * P.j_valid;
-    const int nit = mend > mbeg ? (mend - mbeg + 15) / 16 : 0;
+    const int nit = mend > mbeg ? (mend - mbeg + BR - 1) / BR : 0;
 
-    // this thread gathers 8 consecutive pixels (half hh of each 16-pixel stage) of the
-    // columns c0 + i*HALF of P (i < P_IT) and of X (i < X_IT)
-    const int hh = tid / HALF, c0 = tid - (tid / HALF) * HALF;
-    bool p_slot[P_IT], p_ok[P_IT];
-    long long p_off[P_IT];
+    int p_row[P_IT], p_col[P_IT];
+    bool p_slot[P_IT];
 #pragma unroll
     for (int i = 0; i < P_IT; ++i) {
-        const int c = c0 + i * HALF;
-        p_slot[i] = c < BA;
-        p_ok[i] = p_slot[i] && a0 + c < P.n_a;
-        p_off[i] = p_ok[i] ? a0 + c : 0;
+        const int s = tid + i * NT;
+        p_slot[i] = s < P_SLOTS;
+        p_row[i] = s / (BA / 4);
+        p_col[i] = (s - (s / (BA / 4)) * (BA / 4)) * 4;
     }
-    bool x_slot[X_IT], x_ok[X_IT];
-    long long x_off[X_IT];
+    int x_row[X_IT], x_col[X_IT];
+    bool x_slot[X_IT];
+    long long x_off[X_IT][VX ? 1 : 4];
+    bool x_kok[X_IT][VX ? 1 : 4];
 #pragma unroll
     for (int i = 0; i < X_IT; ++i) {
-        const int c = c0 + i * HALF;
-        x_slot[i] = c < BKC;
-        const int k = k0 + c;
-        x_ok[i] = x_slot[i] && k < K;
-        const int kk = x_ok[i] ? k : 0;
-        const int r = kk / P.j_valid;
-        x_off[i] = r * P.sxr + (kk - r * P.j_valid);
+        const int s = tid + i * NT;
+        x_slot[i] = s < X_SLOTS;
+        x_row[i] = s / (BKC / 4);
+        x_col[i] = (s - (s / (BKC / 4)) * (BKC / 4)) * 4;
+#pragma unroll
+        for (int e = 0; e < (VX ? 1 : 4); ++e) {
+            const int k = k0 + x_col[i] + e;
+            x_kok[i][e] = k < K;
+            const int kk = k < K ? k : 0;
+            const int r = kk / P.j_valid;
+            x_off[i][e] = r * P.sxr + (kk - r * P.j_valid);
+        }
     }
 
-    float rp[P_IT][8], rx[X_IT][8];
+    f32x4 rp[P_IT], rx[X_IT];
     auto load = [&](int it) {
-        const int m = mbeg + it * 16 + 8 * hh;
-        int img = 0, a = 0, b = 0;
-        if (m < mend) decomp(m, P.m_b, mab, img, a, b);
-        long long po = img * P.spn + a * P.spa + b * P.spb;
-        long long xo = img * P.sxn + a * P.sxa + b * P.sxb;
+        const int mb = mbeg + it * BR;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            const bool valid = m + e < mend;
+        for (int i = 0; i < P_IT; ++i) {
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            const int m = mb + p_row[i];
+            if (p_slot[i] && m < mend) {
+                int img, a, b;
+                decomp(m, P.m_b, mab, img, a, b);
+                const float* src = P.p + img * P.spn + a * P.spa + b * P.spb + a0 + p_col[i];
+                const int na = P.n_a - (a0 + p_col[i]);
+                if constexpr (VP) {
+                    if (na > 0) {
+                        v = *reinterpret_cast<const f32x4*>(src);
 #pragma unroll
-            for (int i = 0; i < P_IT; ++i) {
-                const float v = P.p[valid && p_ok[i] ? po + p_off[i] : 0];
-                rp[i][e] = (valid && p_ok[i]) ? v : 0.f;
-            }
+                        for (int e = 0; e < 4; ++e)
+                            if (e >= na) v[e] = 0.f;
+                    }
+                } else {
 #pragma unroll
-            for (int i = 0; i < X_IT; ++i) {
-                const float v = P.x[valid && x_ok[i] ? xo + x_off[i] : 0];
-                rx[i][e] = (valid && x_ok[i]) ? v : 0.f;
-            }
-            po += P.spb;
-            xo += P.sxb;
-            if (++b == P.m_b) {           // next pixel row (rare: once per image row)
-                b = 0;
-                po += P.spa - P.m_b * P.spb;
-                xo += P.sxa - P.m_b * P.sxb;
-                if (++a == P.m_a) {
-                    a = 0;
-                    ++img;
-                    po += P.spn - P.m_a * P.spa;
-                    xo += P.sxn - P.m_a * P.sxa;
+                    for (int e = 0; e < 4; ++e)
+                        if (e < na) v[e] = src[e];
                 }
             }
+            rp[i] = v;
+        }
+#pragma unroll
+        for (int i = 0; i < X_IT; ++i) {
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            const int m = mb + x_row[i];
+            if (x_slot[i] && m < mend) {
+                int img, a, b;
+                decomp(m, P.m_b, mab, img, a, b);
+                const float* base = P.x + img * P.sxn + a * P.sxa + b * P.sxb;
+                if constexpr (VX) {
+                    if (x_kok[i][0]) v = *reinterpret_cast<const f32x4*>(base + x_off[i][0]);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if (x_kok[i][e]) v[e] = base[x_off[i][e]];
+                }
+            }
+            rx[i] = v;
         }
     };
     auto store = [&](int buf) {
 #pragma unroll
         for (int i = 0; i < P_IT; ++i)
             if (p_slot[i]) {
-                bf16x8 h, mm, l;
-                split3(rp[i], h, mm, l);
-                const int c = c0 + i * HALF;
-                *reinterpret_cast<bf16x8*>(&Ps[buf][0][c][hh * 8]) = h;
-                *reinterpret_cast<bf16x8*>(&Ps[buf][1][c][hh * 8]) = mm;
-                *reinterpret_cast<bf16x8*>(&Ps[buf][2][c][hh * 8]) = l;
+                bf16x4 h, m, l;
+                split3x4(rp[i], h, m, l);
+                *reinterpret_cast<bf16x4*>(&Ps[buf][0][p_row[i]][p_col[i]]) = h;
+                *reinterpret_cast<bf16x4*>(&Ps[buf][1][p_row[i]][p_col[i]]) = m;
+                *reinterpret_cast<bf16x4*>(&Ps[buf][2][p_row[i]][p_col[i]]) = l;
             }
 #pragma unroll
         for (int i = 0; i < X_IT; ++i)
             if (x_slot[i]) {
-                bf16x8 h, mm, l;
-                split3(rx[i], h, mm, l);
-                const int c = c0 + i * HALF;
-                *reinterpret_cast<bf16x8*>(&Xs[buf][0][c][hh * 8]) = h;
-                *reinterpret_cast<bf16x8*>(&Xs[buf][1][c][hh * 8]) = mm;
-                *reinterpret_cast<bf16x8*>(&Xs[buf][2][c][hh * 8]) = l;
+                bf16x4 h, m, l;
+                split3x4(rx[i], h, m, l);
+                *reinterpret_cast<bf16x4*>(&Xs[buf][0][x_row[i]][x_col[i]]) = h;
+                *reinterpret_cast<bf16x4*>(&Xs[buf][1][x_row[i]][x_col[i]]) = m;
+                *reinterpret_cast<bf16x4*>(&Xs[buf][2][x_row[i]][x_col[i]]) = l;
             }
     };
 
@@ -716,7 +756,11 @@ conv_wgrad_x6_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[tm][tn][e] = 0.f;
 
-    const int lrow = lane & 31, lk = (lane >> 5) * 8;
+    // transposed-read lane roles: group g = lane>>4 reads columns 16(g&1).. of pixel rows
+    // 8(g>>1) + {0..3} and + {4..7}; lane 4q+p of the group addresses row q, columns 4p..4p+3
+    const int g = lane >> 4, gi = lane & 15;
+    const int tr_row = 8 * (g >> 1) + (gi >> 2);
+    const int tr_col = 16 * (g & 1) + 4 * (gi & 3);
     if (nit > 0) {
         load(0);
         store(0);
@@ -729,11 +773,15 @@ conv_wgrad_x6_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
 #pragma unroll
-            for (int tm = 0; tm < TM; ++tm)
-                af[tm][p] = *reinterpret_cast<const bf16x8*>(&Ps[cur][p][wa * WA + tm * 32 + lrow][lk]);
+            for (int tm = 0; tm < TM; ++tm) {
+                const int c = wa * WA + tm * 32 + tr_col;
+                af[tm][p] = tr_frag(&Ps[cur][p][tr_row][c], &Ps[cur][p][tr_row + 4][c]);
+            }
 #pragma unroll
-            for (int tn = 0; tn < TN; ++tn)
-                bfr[tn][p] = *reinterpret_cast<const bf16x8*>(&Xs[cur][p][wk * WK + tn * 32 + lrow][lk]);
+            for (int tn = 0; tn < TN; ++tn) {
+                const int c = wk * WK + tn * 32 + tr_col;
+                bfr[tn][p] = tr_frag(&Xs[cur][p][tr_row][c], &Xs[cur][p][tr_row + 4][c]);
+            }
         }
         constexpr int PA[6] = {1, 0, 2, 0, 1, 0};
         constexpr int PB[6] = {1, 2, 0, 1, 0, 0};
@@ -758,7 +806,7 @@ conv_wgrad_x6_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
             if (a >= P.n_a) continue;
 #pragma unroll
             for (int tn = 0; tn < TN; ++tn) {
-                const int k = k0 + wk * WK + tn * 32 + lrow;
+                const int k = k0 + wk * WK + tn * 32 + (lane & 31);
                 if (k < K) out[(size_t)a * K + k] = acc[tm][tn][reg];
             }
         }
@@ -842,12 +890,19 @@ int launch_fwd(const ConvBatch& b, int total, bool vec, hipStream_t stream) {
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 template <int BA, int BKC, int WA, int WK>
-int launch_wgrad_x6(const fg_wgrad_problem& p, hipStream_t stream) {
+int launch_wgrad_x6(const fg_wgrad_problem& p, bool vx, bool vp, hipStream_t stream) {
     constexpr int NT = (BA / WA) * (BKC / WK) * 64;
     const int K = p.kh * p.j_valid;
     const int ta = (p.n_a + BA - 1) / BA, tk = (K + BKC - 1) / BKC;
-    hipLaunchKernelGGL((conv_wgrad_x6_kernel<BA, BKC, WA, WK>), dim3(ta * tk * p.splits), dim3(NT), 0, stream, p,
-                       ta, tk);
+    dim3 g(ta * tk * p.splits), blk(NT);
+    if (vx && vp)
+        hipLaunchKernelGGL((conv_wgrad_x6_kernel<BA, BKC, WA, WK, true, true>), g, blk, 0, stream, p, ta, tk);
+    else if (vx)
+        hipLaunchKernelGGL((conv_wgrad_x6_kernel<BA, BKC, WA, WK, true, false>), g, blk, 0, stream, p, ta, tk);
+    else if (vp)
+        hipLaunchKernelGGL((conv_wgrad_x6_kernel<BA, BKC, WA, WK, false, true>), g, blk, 0, stream, p, ta, tk);
+    else
+        hipLaunchKernelGGL((conv_wgrad_x6_kernel<BA, BKC, WA, WK, false, false>), g, blk, 0, stream, p, ta, tk);
     return fg::launched("conv_wgrad_x6");
 }
 
@@ -925,9 +980,9 @@ FG_API int fg_conv_wgrad(const fg_wgrad_problem* prob, hipStream_t stream) {
     const bool vx = aligned16(p.x) && (p.sxn | p.sxa | p.sxb | p.sxr) % 4 == 0 && p.j_valid % 4 == 0;
     const bool vp = aligned16(p.p) && (p.spn | p.spa | p.spb) % 4 == 0;
     if (g_conv_math & FG_MATH_WGRAD_X6) {
-        if (p.n_a > 64) return launch_wgrad_x6<128, 128, 64, 64>(p, stream);
-        if (p.n_a > 32) return launch_wgrad_x6<64, 256, 64, 64>(p, stream);
-        return launch_wgrad_x6<32, 256, 32, 64>(p, stream);
+        if (p.n_a > 64) return launch_wgrad_x6<128, 128, 64, 64>(p, vx, vp, stream);
+        if (p.n_a > 32) return launch_wgrad_x6<64, 256, 64, 64>(p, vx, vp, stream);
+        return launch_wgrad_x6<32, 256, 32, 64>(p, vx, vp, stream);
     }
     if (p.n_a > 64) return launch_wgrad<128, 128, 64, 64>(p, vx, vp, stream);
     if (p.n_a > 32) return launch_wgrad<64, 256, 64, 64>(p, vx, vp, stream);
