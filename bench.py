@@ -23,6 +23,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak (spec)
+BF16_MFMA_PEAK_TFLOPS = 2500.0    # MI355X_MICROARCH.md: bf16 dense MFMA peak (spec)
 STEP_GFLOP_PER_IMG_512 = 1593.5   # conv fwd 546.1 + conv bwd 1047.3 GFLOP per image
 
 
@@ -72,7 +73,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
 
-    from floodgan import ops
+    from floodgan import _lib, ops
     from floodgan.model import Model
     from floodgan.parallel import broadcast_params
 
@@ -105,6 +106,11 @@ def main():
         t = torch.tensor([elapsed], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
+    math = _lib.get_conv_math()
+    fwd_x6 = math in ("bf16x6", "fwd_x6")
+    # fp32-equivalent split-bf16 executes 6 bf16 MFMA products per fp32 multiply-add: its
+    # roof for fp32 work is the bf16 dense peak / 6 (the fp32 MFMA path's roof is 157.3)
+    peak = BF16_MFMA_PEAK_TFLOPS / 6 if fwd_x6 else FP32_MFMA_PEAK_TFLOPS
     durs = timer.durations_ms()["resblock_conv_fwd"]
     avg_ms = sum(durs) / max(len(durs), 1)
     flops = resblock_conv_flops(B, R)
@@ -129,9 +135,14 @@ def main():
                                    f"(9-ch G input, 12-ch D input), batch {B}/GPU",
                        "global_batch": world * B, "per_gpu_batch": B, "resolution": R,
                        "parallelism": f"dp{world}"},
-            "roofline": {"bound": "mfma", "kernel": "conv_fwd_kernel<128,128,64,64> resblock 3x3 256->256",
-                         "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+            "conv_math": math,
+            "roofline": {"bound": "mfma",
+                         "kernel": ("conv_fwd_x6_kernel<128,128,64,64>" if fwd_x6 else
+                                    "conv_fwd_kernel<128,128,64,64>") + " resblock 3x3 256->256 @128x128",
+                         "achieved": round(achieved, 2), "peak": round(peak, 2), "unit": "TFLOP/s",
+                         "peak_basis": ("bf16 dense MFMA 2500 TFLOP/s / 6 bf16 products per fp32 MAC" if fwd_x6
+                                        else "fp32 MFMA dense peak"),
+                         "frac": round(achieved / peak, 4), "traffic": None,
                          "avg_launch_ms": round(avg_ms, 4), "launches": len(durs),
                          "flop_per_launch": flops},
             "step_tflops": round(STEP_GFLOP_PER_IMG_512 * (R / 512) ** 2 * world * B * args.steps / elapsed / 1e3, 2),

@@ -23,7 +23,7 @@ namespace {
 
 constexpr int BK = 16;
 constexpr int LDK = BK + 4;
-int g_conv_math = FG_MATH_FP32;
+int g_conv_math = FG_MATH_BF16X6;   // default: fp32-equivalent split-bf16 (tests: tests/test_gpu_parity.py)
 
 struct ConvBatch {
     fg_conv_problem p[4];
