@@ -137,7 +137,7 @@ def main():
                        "parallelism": f"dp{world}"},
             "conv_math": math,
             "roofline": {"bound": "mfma",
-                         "kernel": ("conv_fwd_x6_kernel<128,128,64,64>" if fwd_x6 else
+                         "kernel": ("conv_fwd_x6_kernel<128,256,64,64> (8 waves, pre-split weights)" if fwd_x6 else
                                     "conv_fwd_kernel<128,128,64,64>") + " resblock 3x3 256->256 @128x128",
                          "achieved": round(achieved, 2), "peak": round(peak, 2), "unit": "TFLOP/s",
                          "peak_basis": ("bf16 dense MFMA 2500 TFLOP/s / 6 bf16 products per fp32 MAC" if fwd_x6

@@ -17,6 +17,8 @@
 //
 // The weight-gradient kernel reduces over the M (pixel) dimension instead: both operands
 // stay row(pixel)-major in LDS, split-M partial slabs are summed by wgrad_reduce.
+#include <algorithm>
+
 #include "fg_common.hpp"
 
 namespace {
@@ -219,27 +221,42 @@ conv_fwd_kernel(const ConvBatch batch) {
 // conflict-free ds_read_b128 fragment reads).  Lane l feeds rows l&31, k = 8(l>>5)..+7.
 // ------------------------------------------------------------------------------------------
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// Split of two fp32 values at once: v_cvt_pk_bf16_f32 (RNE) + v_pk_add_f32 (exact residuals).
+__device__ __forceinline__ void split3x2(float a, float b, bf16x2& h, bf16x2& m, bf16x2& l) {
+    const f32x2 x = {a, b};
+    h = __builtin_convertvector(x, bf16x2);
+    const f32x2 r = x - __builtin_convertvector(h, f32x2);
+    m = __builtin_convertvector(r, bf16x2);
+    const f32x2 r2 = r - __builtin_convertvector(m, f32x2);
+    l = __builtin_convertvector(r2, bf16x2);
+}
 
 __device__ __forceinline__ void split3(const float (&v)[8], bf16x8& h, bf16x8& m, bf16x8& l) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        const __bf16 hh = (__bf16)v[e];
-        const float r = v[e] - (float)hh;
-        const __bf16 mm = (__bf16)r;
-        const float r2 = r - (float)mm;
-        h[e] = hh;
-        m[e] = mm;
-        l[e] = (__bf16)r2;
+    for (int e = 0; e < 4; ++e) {
+        bf16x2 hh, mm, ll;
+        split3x2(v[2 * e], v[2 * e + 1], hh, mm, ll);
+        h[2 * e] = hh[0];
+        h[2 * e + 1] = hh[1];
+        m[2 * e] = mm[0];
+        m[2 * e + 1] = mm[1];
+        l[2 * e] = ll[0];
+        l[2 * e + 1] = ll[1];
     }
 }
 
-template <int BM, int BN, int WM, int WN, bool VEC>
-__global__ void __launch_bounds__((BM / WM) * (BN / WN) * 64, 2)
+template <int BM, int BN, int WM, int WN, bool VEC, bool WS, int MINW, int PF, bool SWZ>
+__global__ void __launch_bounds__((BM / WM) * (BN / WN) * 64, MINW)
 conv_fwd_x6_kernel(const ConvBatch batch) {
     constexpr int NWN = BN / WN;
     constexpr int NT = (BM / WM) * (BN / WN) * 64;
     constexpr int TM = WM / 32, TN = WN / 32;
-    constexpr int LDP = 24;                       // bf16 per LDS row (16 + 8 pad)
+    // bf16 per LDS row: 16 + 8 pad, or (SWZ) 16 with the two 8-k halves of a row swapped when
+    // bit 3 of the row is set -- both conflict-free for the ds_read_b128 fragment reads
+    constexpr int LDP = SWZ ? 16 : 24;
     constexpr int A_SLOTS = BM * 2, B_SLOTS = BN * 2;   // slot = 8 consecutive k of one row
     constexpr int A_IT = (A_SLOTS + NT - 1) / NT, B_IT = (B_SLOTS + NT - 1) / NT;
 
@@ -264,92 +281,121 @@ conv_fwd_x6_kernel(const ConvBatch batch) {
     const int jv = P.j_valid;
     const long long sxr = P.sxr;
 
-    const float* arow[A_IT];
-    int a_r[A_IT], a_g[A_IT];
-    bool aok[A_IT], aslot[A_IT];
+    // Branch-free staging loads: buffer loads whose out-of-range offset (kOOB) returns zeros,
+    // so the compiler can count vmcnt exactly across the pipelined loop.  fg_conv_fwd keeps
+    // every byte offset below 2^31 (it splits the image range otherwise).
+    constexpr bool A_FULL = A_SLOTS % NT == 0, B_FULL = B_SLOTS % NT == 0;
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)P.x, 0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)P.w, 0, 0x7fffffff, 0x00020000);
+    int a_off[A_IT], a_r[A_IT], a_g[A_IT];
+    bool aslot[A_IT];
 #pragma unroll
     for (int i = 0; i < A_IT; ++i) {
         const int s = tid + i * NT;
         a_r[i] = s >> 1;
         a_g[i] = s & 1;
-        aslot[i] = s < A_SLOTS;
+        aslot[i] = A_FULL || s < A_SLOTS;
         const int m = m0 + (s >> 1);
-        aok[i] = aslot[i] && (m < M);
-        arow[i] = P.x;
-        if (aok[i]) {
+        a_off[i] = -1;                                   // row outside the problem: loads read zeros
+        if (aslot[i] && m < M) {
             int img, a, b;
             decomp(m, P.m_b, mab, img, a, b);
-            arow[i] = P.x + img * P.sxn + a * P.sxa + b * P.sxb;
+            a_off[i] = (int)(img * P.sxn + a * P.sxa + b * P.sxb) + a_g[i] * 8;
         }
     }
-    const float* brow[B_IT];
-    int b_r[B_IT], b_g[B_IT];
-    bool bok[B_IT], bslot[B_IT];
+    // B: fp32 rows split at staging time, or (WS) pre-split rows of [slot][piece][8] bf16
+    int b_off[B_IT], b_r[B_IT], b_g[B_IT];
+    bool bslot[B_IT];
 #pragma unroll
     for (int i = 0; i < B_IT; ++i) {
         const int s = tid + i * NT;
         b_r[i] = s >> 1;
         b_g[i] = s & 1;
-        bslot[i] = s < B_SLOTS;
-        bok[i] = bslot[i] && (n0 + (s >> 1) < P.n_out);
-        brow[i] = P.w + (size_t)(bok[i] ? n0 + (s >> 1) : 0) * P.ldw;
+        bslot[i] = B_FULL || s < B_SLOTS;
+        const int n = n0 + (s >> 1);
+        // byte offset of this slot's first k-slot (WS: 48 B per 8-k slot, else 32 B of fp32)
+        b_off[i] = (bslot[i] && n < P.n_out) ? (WS ? (n * (P.ldw / 8) + b_g[i]) * 48 : (n * P.ldw + b_g[i] * 8) * 4)
+                                             : -1;
     }
+    constexpr int kOOB = 0x7fffffff;   // >= num_records: the load returns zeros
 
-    float ra[A_IT][8], rb[B_IT][8];
-    auto load = [&](int kt) {
+    struct Stage {
+        float ra[A_IT][8], rb[WS ? 1 : B_IT][8];
+        bf16x8 rbs[WS ? B_IT : 1][3];
+    };
+    auto load = [&](int kt, Stage& S) {
         const int r = kt / jtr;
         const int jb = (kt - r * jtr) * 16;
+        const int koff = r * (int)sxr + jb;              // element offset of this stage's k-run
 #pragma unroll
         for (int i = 0; i < A_IT; ++i) {
             const int j = jb + a_g[i] * 8;
-            const float* src = arow[i] + r * sxr + j;
+            const int base = (a_off[i] + koff) * 4;
             if constexpr (VEC) {
-                f32x4 v0 = {0.f, 0.f, 0.f, 0.f}, v1 = v0;
-                if (aok[i] && j < jv) v0 = *reinterpret_cast<const f32x4*>(src);
-                if (aok[i] && j + 4 < jv) v1 = *reinterpret_cast<const f32x4*>(src + 4);
+                const int o0 = (a_off[i] >= 0 && j < jv) ? base : kOOB;
+                const int o1 = (a_off[i] >= 0 && j + 4 < jv) ? base + 16 : kOOB;
+                const f32x4 v0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, o0, 0, 0));
+                const f32x4 v1 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, o1, 0, 0));
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    ra[i][e] = v0[e];
-                    ra[i][4 + e] = v1[e];
+                    S.ra[i][e] = v0[e];
+                    S.ra[i][4 + e] = v1[e];
                 }
             } else {
 #pragma unroll
-                for (int e = 0; e < 8; ++e) ra[i][e] = (aok[i] && j + e < jv) ? src[e] : 0.f;
+                for (int e = 0; e < 8; ++e) {
+                    const int o = (a_off[i] >= 0 && j + e < jv) ? base + 4 * e : kOOB;
+                    S.ra[i][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, o, 0, 0));
+                }
             }
         }
 #pragma unroll
         for (int i = 0; i < B_IT; ++i) {
-            f32x4 v0 = {0.f, 0.f, 0.f, 0.f}, v1 = v0;
-            if (bok[i]) {
-                const float* src = brow[i] + kt * 16 + b_g[i] * 8;
-                v0 = *reinterpret_cast<const f32x4*>(src);
-                v1 = *reinterpret_cast<const f32x4*>(src + 4);
-            }
+            if constexpr (WS) {
+                const int o = b_off[i] >= 0 ? b_off[i] + kt * 96 : kOOB;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                rb[i][e] = v0[e];
-                rb[i][4 + e] = v1[e];
+                for (int p = 0; p < 3; ++p)
+                    S.rbs[i][p] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                                                                 wr, o == kOOB ? kOOB : o + 16 * p, 0, 0));
+            } else {
+                const int o = b_off[i] >= 0 ? b_off[i] + kt * 64 : kOOB;
+                const f32x4 v0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(wr, o, 0, 0));
+                const f32x4 v1 = __builtin_bit_cast(f32x4,
+                                                    __builtin_amdgcn_raw_buffer_load_b128(wr, o == kOOB ? kOOB : o + 16, 0, 0));
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    S.rb[i][e] = v0[e];
+                    S.rb[i][4 + e] = v1[e];
+                }
             }
         }
     };
-    auto store = [&](int buf) {
+    auto store = [&](int buf, const Stage& S) {
 #pragma unroll
         for (int i = 0; i < A_IT; ++i)
             if (aslot[i]) {
                 bf16x8 h, m, l;
-                split3(ra[i], h, m, l);
-                *reinterpret_cast<bf16x8*>(&As[buf][0][a_r[i]][a_g[i] * 8]) = h;
-                *reinterpret_cast<bf16x8*>(&As[buf][1][a_r[i]][a_g[i] * 8]) = m;
-                *reinterpret_cast<bf16x8*>(&As[buf][2][a_r[i]][a_g[i] * 8]) = l;
+                split3(S.ra[i], h, m, l);
+                const int c = (SWZ ? a_g[i] ^ ((a_r[i] >> 3) & 1) : a_g[i]) * 8;
+                *reinterpret_cast<bf16x8*>(&As[buf][0][a_r[i]][c]) = h;
+                *reinterpret_cast<bf16x8*>(&As[buf][1][a_r[i]][c]) = m;
+                *reinterpret_cast<bf16x8*>(&As[buf][2][a_r[i]][c]) = l;
             }
 #pragma unroll
         for (int i = 0; i < B_IT; ++i)
             if (bslot[i]) {
                 bf16x8 h, m, l;
-                split3(rb[i], h, m, l);
-                *reinterpret_cast<bf16x8*>(&Bs[buf][0][b_r[i]][b_g[i] * 8]) = h;
-                *reinterpret_cast<bf16x8*>(&Bs[buf][1][b_r[i]][b_g[i] * 8]) = m;
-                *reinterpret_cast<bf16x8*>(&Bs[buf][2][b_r[i]][b_g[i] * 8]) = l;
+                if constexpr (WS) {
+                    h = S.rbs[i][0];
+                    m = S.rbs[i][1];
+                    l = S.rbs[i][2];
+                } else {
+                    split3(S.rb[i], h, m, l);
+                }
+                const int c = (SWZ ? b_g[i] ^ ((b_r[i] >> 3) & 1) : b_g[i]) * 8;
+                *reinterpret_cast<bf16x8*>(&Bs[buf][0][b_r[i]][c]) = h;
+                *reinterpret_cast<bf16x8*>(&Bs[buf][1][b_r[i]][c]) = m;
+                *reinterpret_cast<bf16x8*>(&Bs[buf][2][b_r[i]][c]) = l;
             }
     };
 
@@ -361,15 +407,8 @@ conv_fwd_x6_kernel(const ConvBatch batch) {
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[tm][tn][e] = 0.f;
 
-    const int lrow = lane & 31, lk = (lane >> 5) * 8;
-    if (nkt > 0) {
-        load(0);
-        store(0);
-    }
-    __syncthreads();
-    for (int kt = 0; kt < nkt; ++kt) {
-        const int cur = kt & 1;
-        if (kt + 1 < nkt) load(kt + 1);
+    const int lrow = lane & 31, lk = (SWZ ? (lane >> 5) ^ ((lane >> 3) & 1) : (lane >> 5)) * 8;
+    auto compute = [&](int cur) {
         bf16x8 af[TM][3], bfr[TN][3];
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
@@ -391,8 +430,39 @@ conv_fwd_x6_kernel(const ConvBatch batch) {
                 for (int tn = 0; tn < TN; ++tn)
                     acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[tm][PA[c]], bfr[tn][PB[c]], acc[tm][tn],
                                                                           0, 0, 0);
-        if (kt + 1 < nkt) store(cur ^ 1);
+    };
+    Stage R0, R1;
+    if constexpr (PF == 1) {
+        load(0, R0);
+        store(0, R0);
         __syncthreads();
+        for (int kt = 0; kt < nkt; ++kt) {
+            const int cur = kt & 1;
+            load(min(kt + 1, nkt - 1), R0);
+            compute(cur);
+            if (kt + 1 < nkt) store(cur ^ 1, R0);
+            __syncthreads();
+        }
+    } else {
+        // prefetch distance 2: the global loads of stage kt+2 are issued before stage kt's
+        // MFMAs and land in LDS only at the end of stage kt+1 (two register sets, loop x2)
+        load(0, R0);
+        load(min(1, nkt - 1), R1);
+        store(0, R0);
+        __syncthreads();
+        // loads past the last stage are clamped (re-read the last stage, never stored): keeping
+        // them unconditional lets the compiler count vmcnt exactly across iterations
+        for (int kt = 0; kt < nkt; kt += 2) {
+            load(min(kt + 2, nkt - 1), R0);
+            compute(0);
+            if (kt + 1 < nkt) store(1, R1);
+            __syncthreads();
+            if (kt + 1 >= nkt) break;
+            load(min(kt + 3, nkt - 1), R1);
+            compute(1);
+            if (kt + 2 < nkt) store(0, R0);
+            __syncthreads();
+        }
     }
 
     const int act = P.act;
@@ -612,30 +682,42 @@ __device__ __forceinline__ bf16x8 tr_frag(const __bf16* r0, const __bf16* r4) {
 
 __device__ __forceinline__ void split3x4(const f32x4& v, bf16x4& h, bf16x4& m, bf16x4& l) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        const __bf16 hh = (__bf16)v[e];
-        const float r = v[e] - (float)hh;
-        const __bf16 mm = (__bf16)r;
-        const float r2 = r - (float)mm;
-        h[e] = hh;
-        m[e] = mm;
-        l[e] = (__bf16)r2;
+    for (int e = 0; e < 2; ++e) {
+        bf16x2 hh, mm, ll;
+        split3x2(v[2 * e], v[2 * e + 1], hh, mm, ll);
+        h[2 * e] = hh[0];
+        h[2 * e + 1] = hh[1];
+        m[2 * e] = mm[0];
+        m[2 * e + 1] = mm[1];
+        l[2 * e] = ll[0];
+        l[2 * e + 1] = ll[1];
     }
 }
 
-template <int BA, int BKC, int WA, int WK, bool VX, bool VP>
-__global__ void __launch_bounds__((BA / WA) * (BKC / WK) * 64, 2)
+// LDS column swizzle of the weight-gradient staging tiles (pitch PITCH bf16, no padding): the
+// transposed fragment reads touch 4 consecutive rows x 32 columns per 32-lane group; XOR-ing
+// 32-column chunks by the row puts those 4 rows in 4 distinct 16-bank quarters.
+template <int PITCH>
+__device__ __forceinline__ int wg_swz(int row) {
+    if constexpr (PITCH >= 128) return (row & 3) << 5;
+    else if constexpr (PITCH == 64) return ((row >> 1) & 1) << 5;
+    else return 0;
+}
+
+template <int BA, int BKC, int WA, int WK, bool VX, bool VP, int MINW>
+__global__ void __launch_bounds__((BA / WA) * (BKC / WK) * 64, MINW)
 conv_wgrad_x6_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
     constexpr int NWK = BKC / WK;
     constexpr int NT = (BA / WA) * (BKC / WK) * 64;
     constexpr int TM = WA / 32, TN = WK / 32;
-    constexpr int BR = 16;
-    constexpr int PA_ = BA + 32, PX_ = BKC + 32;     // bf16 row pitches
+    constexpr int BR = 16;                              // pixel rows per stage
     constexpr int P_SLOTS = BR * BA / 4, X_SLOTS = BR * BKC / 4;
     constexpr int P_IT = (P_SLOTS + NT - 1) / NT, X_IT = (X_SLOTS + NT - 1) / NT;
+    constexpr bool P_FULL = P_SLOTS % NT == 0, X_FULL = X_SLOTS % NT == 0;
+    constexpr int kOOB = 0x7fffffff;
 
-    __shared__ __attribute__((aligned(16))) __bf16 Ps[2][3][BR][PA_];
-    __shared__ __attribute__((aligned(16))) __bf16 Xs[2][3][BR][PX_];
+    __shared__ __attribute__((aligned(16))) __bf16 Ps[2][3][BR][BA];
+    __shared__ __attribute__((aligned(16))) __bf16 Xs[2][3][BR][BKC];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wa = wave / NWK, wk = wave - (wave / NWK) * NWK;
@@ -651,80 +733,104 @@ conv_wgrad_x6_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
     const int mend = min(M, mbeg + P.m_chunk);
     const int K = P.kh * P.j_valid;
     const int nit = mend > mbeg ? (mend - mbeg + BR - 1) / BR : 0;
+    // advancing a pixel row index by BR = (i16 images, a16 rows, b16 columns)
+    const int i16 = BR / mab, a16 = (BR - i16 * mab) / P.m_b, b16 = BR - i16 * mab - a16 * P.m_b;
+    const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc((void*)P.p, 0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)P.x, 0, 0x7fffffff, 0x00020000);
 
-    int p_row[P_IT], p_col[P_IT];
+    // per-slot pixel walk: slot rows are fixed within the stage, the pixel advances by BR
+    struct Walk {
+        int m, img, a, b;
+    };
+    auto walk_init = [&](int row) {
+        Walk w;
+        w.m = mbeg + row;
+        decomp(min(w.m, M - 1), P.m_b, mab, w.img, w.a, w.b);
+        return w;
+    };
+    auto walk_next = [&](Walk& w) {
+        w.m += BR;
+        w.b += b16;
+        const int cb = w.b >= P.m_b;
+        w.b -= cb ? P.m_b : 0;
+        w.a += a16 + cb;
+        const int ca = w.a >= P.m_a;
+        w.a -= ca ? P.m_a : 0;
+        w.img += i16 + ca;
+    };
+
+    int p_row[P_IT], p_col[P_IT], p_na[P_IT];
     bool p_slot[P_IT];
+    Walk p_w[P_IT];
 #pragma unroll
     for (int i = 0; i < P_IT; ++i) {
         const int s = tid + i * NT;
-        p_slot[i] = s < P_SLOTS;
+        p_slot[i] = P_FULL || s < P_SLOTS;
         p_row[i] = s / (BA / 4);
         p_col[i] = (s - (s / (BA / 4)) * (BA / 4)) * 4;
+        p_na[i] = P.n_a - (a0 + p_col[i]);            // valid columns in this slot (<= 0: none)
+        p_w[i] = walk_init(p_row[i]);
     }
     int x_row[X_IT], x_col[X_IT];
     bool x_slot[X_IT];
-    long long x_off[X_IT][VX ? 1 : 4];
-    bool x_kok[X_IT][VX ? 1 : 4];
+    int x_off[X_IT][VX ? 1 : 4];
+    Walk x_w[X_IT];
 #pragma unroll
     for (int i = 0; i < X_IT; ++i) {
         const int s = tid + i * NT;
-        x_slot[i] = s < X_SLOTS;
+        x_slot[i] = X_FULL || s < X_SLOTS;
         x_row[i] = s / (BKC / 4);
         x_col[i] = (s - (s / (BKC / 4)) * (BKC / 4)) * 4;
 #pragma unroll
         for (int e = 0; e < (VX ? 1 : 4); ++e) {
             const int k = k0 + x_col[i] + e;
-            x_kok[i][e] = k < K;
-            const int kk = k < K ? k : 0;
-            const int r = kk / P.j_valid;
-            x_off[i][e] = r * P.sxr + (kk - r * P.j_valid);
+            const int r = k / P.j_valid;
+            x_off[i][e] = k < K ? (int)(r * P.sxr) + (k - r * P.j_valid) : -1;
         }
+        x_w[i] = walk_init(x_row[i]);
     }
 
     f32x4 rp[P_IT], rx[X_IT];
-    auto load = [&](int it) {
-        const int mb = mbeg + it * BR;
+    // branch-free staging loads (out-of-range offsets read zeros), then advance the walks
+    auto load = [&]() {
 #pragma unroll
         for (int i = 0; i < P_IT; ++i) {
-            f32x4 v = {0.f, 0.f, 0.f, 0.f};
-            const int m = mb + p_row[i];
-            if (p_slot[i] && m < mend) {
-                int img, a, b;
-                decomp(m, P.m_b, mab, img, a, b);
-                const float* src = P.p + img * P.spn + a * P.spa + b * P.spb + a0 + p_col[i];
-                const int na = P.n_a - (a0 + p_col[i]);
-                if constexpr (VP) {
-                    if (na > 0) {
-                        v = *reinterpret_cast<const f32x4*>(src);
+            const Walk& w = p_w[i];
+            const int base = (w.img * (int)P.spn + w.a * (int)P.spa + w.b * (int)P.spb + a0 + p_col[i]) * 4;
+            const bool ok = p_slot[i] && w.m < mend && p_na[i] > 0;
+            f32x4 v;
+            if constexpr (VP) {
+                v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(pr, ok ? base : kOOB, 0, 0));
+            } else {
 #pragma unroll
-                        for (int e = 0; e < 4; ++e)
-                            if (e >= na) v[e] = 0.f;
-                    }
-                } else {
-#pragma unroll
-                    for (int e = 0; e < 4; ++e)
-                        if (e < na) v[e] = src[e];
-                }
+                for (int e = 0; e < 4; ++e)
+                    v[e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                         pr, ok && e < p_na[i] ? base + 4 * e : kOOB, 0, 0));
             }
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (e >= p_na[i]) v[e] = 0.f;
             rp[i] = v;
+            walk_next(p_w[i]);
         }
 #pragma unroll
         for (int i = 0; i < X_IT; ++i) {
-            f32x4 v = {0.f, 0.f, 0.f, 0.f};
-            const int m = mb + x_row[i];
-            if (x_slot[i] && m < mend) {
-                int img, a, b;
-                decomp(m, P.m_b, mab, img, a, b);
-                const float* base = P.x + img * P.sxn + a * P.sxa + b * P.sxb;
-                if constexpr (VX) {
-                    if (x_kok[i][0]) v = *reinterpret_cast<const f32x4*>(base + x_off[i][0]);
-                } else {
+            const Walk& w = x_w[i];
+            const int base = w.img * (int)P.sxn + w.a * (int)P.sxa + w.b * (int)P.sxb;
+            const bool ok = x_slot[i] && w.m < mend;
+            f32x4 v;
+            if constexpr (VX) {
+                v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                  xr, ok && x_off[i][0] >= 0 ? (base + x_off[i][0]) * 4 : kOOB, 0, 0));
+            } else {
 #pragma unroll
-                    for (int e = 0; e < 4; ++e)
-                        if (x_kok[i][e]) v[e] = base[x_off[i][e]];
-                }
+                for (int e = 0; e < 4; ++e)
+                    v[e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                         xr, ok && x_off[i][e] >= 0 ? (base + x_off[i][e]) * 4 : kOOB,
+                                                         0, 0));
             }
             rx[i] = v;
+            walk_next(x_w[i]);
         }
     };
     auto store = [&](int buf) {
@@ -733,18 +839,20 @@ conv_wgrad_x6_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
             if (p_slot[i]) {
                 bf16x4 h, m, l;
                 split3x4(rp[i], h, m, l);
-                *reinterpret_cast<bf16x4*>(&Ps[buf][0][p_row[i]][p_col[i]]) = h;
-                *reinterpret_cast<bf16x4*>(&Ps[buf][1][p_row[i]][p_col[i]]) = m;
-                *reinterpret_cast<bf16x4*>(&Ps[buf][2][p_row[i]][p_col[i]]) = l;
+                const int c = p_col[i] ^ wg_swz<BA>(p_row[i]);
+                *reinterpret_cast<bf16x4*>(&Ps[buf][0][p_row[i]][c]) = h;
+                *reinterpret_cast<bf16x4*>(&Ps[buf][1][p_row[i]][c]) = m;
+                *reinterpret_cast<bf16x4*>(&Ps[buf][2][p_row[i]][c]) = l;
             }
 #pragma unroll
         for (int i = 0; i < X_IT; ++i)
             if (x_slot[i]) {
                 bf16x4 h, m, l;
                 split3x4(rx[i], h, m, l);
-                *reinterpret_cast<bf16x4*>(&Xs[buf][0][x_row[i]][x_col[i]]) = h;
-                *reinterpret_cast<bf16x4*>(&Xs[buf][1][x_row[i]][x_col[i]]) = m;
-                *reinterpret_cast<bf16x4*>(&Xs[buf][2][x_row[i]][x_col[i]]) = l;
+                const int c = x_col[i] ^ wg_swz<BKC>(x_row[i]);
+                *reinterpret_cast<bf16x4*>(&Xs[buf][0][x_row[i]][c]) = h;
+                *reinterpret_cast<bf16x4*>(&Xs[buf][1][x_row[i]][c]) = m;
+                *reinterpret_cast<bf16x4*>(&Xs[buf][2][x_row[i]][c]) = l;
             }
     };
 
@@ -761,25 +869,24 @@ conv_wgrad_x6_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
     const int g = lane >> 4, gi = lane & 15;
     const int tr_row = 8 * (g >> 1) + (gi >> 2);
     const int tr_col = 16 * (g & 1) + 4 * (gi & 3);
-    if (nit > 0) {
-        load(0);
-        store(0);
-    }
+    const int swp = wg_swz<BA>(tr_row), swx = wg_swz<BKC>(tr_row);   // rows tr_row and tr_row+4 alike
+    load();
+    store(0);
     __syncthreads();
     for (int it = 0; it < nit; ++it) {
         const int cur = it & 1;
-        if (it + 1 < nit) load(it + 1);
+        load();                         // past the last stage: reads zeros (m >= mend), never stored
         bf16x8 af[TM][3], bfr[TN][3];
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
 #pragma unroll
             for (int tm = 0; tm < TM; ++tm) {
-                const int c = wa * WA + tm * 32 + tr_col;
+                const int c = (wa * WA + tm * 32 + tr_col) ^ swp;
                 af[tm][p] = tr_frag(&Ps[cur][p][tr_row][c], &Ps[cur][p][tr_row + 4][c]);
             }
 #pragma unroll
             for (int tn = 0; tn < TN; ++tn) {
-                const int c = wk * WK + tn * 32 + tr_col;
+                const int c = (wk * WK + tn * 32 + tr_col) ^ swx;
                 bfr[tn][p] = tr_frag(&Xs[cur][p][tr_row][c], &Xs[cur][p][tr_row + 4][c]);
             }
         }
@@ -844,36 +951,59 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ slabs, int splits,
     }
 }
 
+__device__ __forceinline__ float packed_w(const float* __restrict__ w, const fg_weight_map& map, int n, int kr, int j) {
+    if (j >= map.kw * map.c) return 0.f;
+    const int ks = j / map.c, ch = j - (j / map.c) * map.c;
+    if (ch >= map.c_valid) return 0.f;
+    const int r = map.rtab[kr], s = map.stab[ks], nn = n + map.n_base;
+    const size_t src = map.dim0_is_n ? (((size_t)nn * map.d1 + ch) * map.KH + r) * map.KW + s
+                                     : (((size_t)ch * map.d1 + nn) * map.KH + r) * map.KW + s;
+    return w[src];
+}
+
 __global__ void pack_weight_kernel(const float* __restrict__ w, fg_weight_map map, float* __restrict__ wp) {
     const int K = map.kh * map.jp;
     const long long total = (long long)map.n_out * K;
-    const int J = map.kw * map.c;
     for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
          idx += (long long)gridDim.x * blockDim.x) {
         const int n = (int)(idx / K);
         const int rem = (int)(idx - (long long)n * K);
         const int kr = rem / map.jp, j = rem - (rem / map.jp) * map.jp;
-        float v = 0.f;
-        if (j < J) {
-            const int ks = j / map.c, ch = j - (j / map.c) * map.c;
-            if (ch < map.c_valid) {
-                const int r = map.rtab[kr], s = map.stab[ks], nn = n + map.n_base;
-                const size_t src = map.dim0_is_n ? (((size_t)nn * map.d1 + ch) * map.KH + r) * map.KW + s
-                                                 : (((size_t)ch * map.d1 + nn) * map.KH + r) * map.KW + s;
-                v = w[src];
-            }
-        }
-        wp[idx] = v;
+        wp[idx] = packed_w(w, map, n, kr, j);
     }
 }
 
-template <int BM, int BN, int WM, int WN>
-int launch_fwd_x6(const ConvBatch& b, int total, bool vec, hipStream_t stream) {
+// one thread per (row, 8-k slot): 8 weights -> h, m, l pieces, 48 contiguous bytes
+__global__ void pack_weight_split_kernel(const float* __restrict__ w, fg_weight_map map, bf16x8* __restrict__ wps) {
+    const int QS = map.kh * map.jp / 8;
+    const long long total = (long long)map.n_out * QS;
+    for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const int n = (int)(idx / QS);
+        const int k0 = (int)(idx - (long long)n * QS) * 8;
+        const int kr = k0 / map.jp, j0 = k0 - (k0 / map.jp) * map.jp;   // jp % 16 == 0: one kernel row
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = packed_w(w, map, n, kr, j0 + e);
+        bf16x8 h, m, l;
+        split3(v, h, m, l);
+        wps[idx * 3] = h;
+        wps[idx * 3 + 1] = m;
+        wps[idx * 3 + 2] = l;
+    }
+}
+
+template <int BM, int BN, int WM, int WN, int MINW, int PF, bool SWZ = false>
+int launch_fwd_x6(const ConvBatch& b, int total, bool vec, bool ws, hipStream_t stream) {
     constexpr int NT = (BM / WM) * (BN / WN) * 64;
-    if (vec)
-        hipLaunchKernelGGL((conv_fwd_x6_kernel<BM, BN, WM, WN, true>), dim3(total), dim3(NT), 0, stream, b);
+    if (vec && ws)
+        hipLaunchKernelGGL((conv_fwd_x6_kernel<BM, BN, WM, WN, true, true, MINW, PF, SWZ>), dim3(total), dim3(NT), 0, stream, b);
+    else if (vec)
+        hipLaunchKernelGGL((conv_fwd_x6_kernel<BM, BN, WM, WN, true, false, MINW, PF, SWZ>), dim3(total), dim3(NT), 0, stream, b);
+    else if (ws)
+        hipLaunchKernelGGL((conv_fwd_x6_kernel<BM, BN, WM, WN, false, true, MINW, PF, SWZ>), dim3(total), dim3(NT), 0, stream, b);
     else
-        hipLaunchKernelGGL((conv_fwd_x6_kernel<BM, BN, WM, WN, false>), dim3(total), dim3(NT), 0, stream, b);
+        hipLaunchKernelGGL((conv_fwd_x6_kernel<BM, BN, WM, WN, false, false, MINW, PF, SWZ>), dim3(total), dim3(NT), 0, stream, b);
     return fg::launched("conv_fwd_x6");
 }
 
@@ -889,22 +1019,36 @@ int launch_fwd(const ConvBatch& b, int total, bool vec, hipStream_t stream) {
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
-template <int BA, int BKC, int WA, int WK>
+template <int BA, int BKC, int WA, int WK, int MINW>
 int launch_wgrad_x6(const fg_wgrad_problem& p, bool vx, bool vp, hipStream_t stream) {
     constexpr int NT = (BA / WA) * (BKC / WK) * 64;
     const int K = p.kh * p.j_valid;
     const int ta = (p.n_a + BA - 1) / BA, tk = (K + BKC - 1) / BKC;
     dim3 g(ta * tk * p.splits), blk(NT);
     if (vx && vp)
-        hipLaunchKernelGGL((conv_wgrad_x6_kernel<BA, BKC, WA, WK, true, true>), g, blk, 0, stream, p, ta, tk);
+        hipLaunchKernelGGL((conv_wgrad_x6_kernel<BA, BKC, WA, WK, true, true, MINW>), g, blk, 0, stream, p, ta, tk);
     else if (vx)
-        hipLaunchKernelGGL((conv_wgrad_x6_kernel<BA, BKC, WA, WK, true, false>), g, blk, 0, stream, p, ta, tk);
+        hipLaunchKernelGGL((conv_wgrad_x6_kernel<BA, BKC, WA, WK, true, false, MINW>), g, blk, 0, stream, p, ta, tk);
     else if (vp)
-        hipLaunchKernelGGL((conv_wgrad_x6_kernel<BA, BKC, WA, WK, false, true>), g, blk, 0, stream, p, ta, tk);
+        hipLaunchKernelGGL((conv_wgrad_x6_kernel<BA, BKC, WA, WK, false, true, MINW>), g, blk, 0, stream, p, ta, tk);
     else
-        hipLaunchKernelGGL((conv_wgrad_x6_kernel<BA, BKC, WA, WK, false, false>), g, blk, 0, stream, p, ta, tk);
+        hipLaunchKernelGGL((conv_wgrad_x6_kernel<BA, BKC, WA, WK, false, false, MINW>), g, blk, 0, stream, p, ta, tk);
     return fg::launched("conv_wgrad_x6");
 }
+
+int g_wgrad_tile = -1;   // tuning hook (fg_set_wgrad_tile)
+
+int launch_wgrad_x6_cfg(int cfg, const fg_wgrad_problem& p, bool vx, bool vp, hipStream_t stream) {
+    switch (cfg) {
+        case 0: return launch_wgrad_x6<128, 128, 64, 64, 3>(p, vx, vp, stream);
+        case 1: return launch_wgrad_x6<256, 128, 64, 64, 4>(p, vx, vp, stream);
+        case 2: return launch_wgrad_x6<128, 256, 64, 64, 4>(p, vx, vp, stream);
+        case 3: return launch_wgrad_x6<64, 256, 64, 64, 3>(p, vx, vp, stream);
+        case 4: return launch_wgrad_x6<32, 256, 32, 64, 3>(p, vx, vp, stream);
+        default: return launch_wgrad_x6<32, 512, 32, 64, 2>(p, vx, vp, stream);
+    }
+}
+constexpr int kWgradTiles = 6;
 
 template <int BA, int BKC, int WA, int WK>
 int launch_wgrad(const fg_wgrad_problem& p, bool vx, bool vp, hipStream_t stream) {
@@ -924,6 +1068,31 @@ int launch_wgrad(const fg_wgrad_problem& p, bool vx, bool vp, hipStream_t stream
     return fg::launched("conv_wgrad");
 }
 
+int g_fwd_tile = -1;   // tuning hook (fg_set_fwd_tile): force one bf16x6 forward tile config
+
+// bf16x6 forward tile configs {BM, BN, wave tile, prefetch distance}: index = g_fwd_tile
+int launch_fwd_x6_cfg(int cfg, const ConvBatch& b, int total, bool vec, bool ws, hipStream_t stream) {
+    switch (cfg) {
+        case 0: return launch_fwd_x6<128, 128, 64, 64, 2, 1>(b, total, vec, ws, stream);
+        case 1: return launch_fwd_x6<128, 128, 64, 64, 2, 2>(b, total, vec, ws, stream);
+        case 2: return launch_fwd_x6<256, 128, 64, 64, 2, 2>(b, total, vec, ws, stream);
+        case 3: return launch_fwd_x6<128, 64, 32, 64, 2, 1>(b, total, vec, ws, stream);
+        case 4: return launch_fwd_x6<128, 64, 32, 64, 2, 2>(b, total, vec, ws, stream);
+        case 5: return launch_fwd_x6<128, 32, 32, 32, 2, 1>(b, total, vec, ws, stream);
+        case 6: return launch_fwd_x6<128, 32, 32, 32, 2, 2>(b, total, vec, ws, stream);
+        case 7: return launch_fwd_x6<256, 64, 32, 64, 2, 2>(b, total, vec, ws, stream);
+        case 8: return launch_fwd_x6<128, 128, 64, 64, 3, 1, true>(b, total, vec, ws, stream);
+        case 9: return launch_fwd_x6<256, 128, 64, 64, 2, 1, true>(b, total, vec, ws, stream);
+        case 10: return launch_fwd_x6<128, 64, 32, 64, 3, 1, true>(b, total, vec, ws, stream);
+        case 11: return launch_fwd_x6<128, 32, 32, 32, 4, 1, true>(b, total, vec, ws, stream);
+        case 12: return launch_fwd_x6<256, 256, 128, 64, 2, 1, true>(b, total, vec, ws, stream);
+        default: return launch_fwd_x6<128, 256, 64, 64, 2, 1, true>(b, total, vec, ws, stream);
+    }
+}
+constexpr int kFwdTiles = 14;
+constexpr int kFwdTileBM[kFwdTiles] = {128, 128, 256, 128, 128, 128, 128, 256, 128, 256, 128, 128, 256, 128};
+constexpr int kFwdTileBN[kFwdTiles] = {128, 128, 128, 64, 64, 32, 32, 64, 128, 128, 64, 32, 256, 256};
+
 }  // namespace
 
 FG_API int fg_conv_fwd(const fg_conv_problem* probs, int nprob, hipStream_t stream) {
@@ -932,22 +1101,64 @@ FG_API int fg_conv_fwd(const fg_conv_problem* probs, int nprob, hipStream_t stre
     b.count = nprob;
     int max_n = 0;
     bool vec = true;
+    const int ws = probs[0].w_split;
     for (int i = 0; i < nprob; ++i) {
         const fg_conv_problem& p = probs[i];
         if (!p.x || !p.w || !p.y) return fg::fail(FG_ERR_INVALID, "fg_conv_fwd: null pointer (problem %d)", i);
         if (p.m_img < 0 || p.m_a < 0 || p.m_b < 0 || p.kh < 1 || p.jp < BK || p.jp % BK || p.j_valid < 1 ||
-            p.j_valid > p.jp || p.n_out < 1 || p.ldw < p.kh * p.jp || p.ldw % 4 || !aligned16(p.w))
+            p.j_valid > p.jp || p.n_out < 1 || p.ldw < p.kh * p.jp || p.ldw % 8 || !aligned16(p.w))
             return fg::fail(FG_ERR_INVALID,
                             "fg_conv_fwd: bad geometry (problem %d: m=%dx%dx%d kh=%d j=%d/%d n=%d ldw=%d)", i,
                             p.m_img, p.m_a, p.m_b, p.kh, p.j_valid, p.jp, p.n_out, p.ldw);
         if ((long long)p.m_img * p.m_a * p.m_b >= (1LL << 31))
             return fg::fail(FG_ERR_INVALID, "fg_conv_fwd: too many rows");
+        if (p.w_split != ws || (ws != 0 && ws != 1))
+            return fg::fail(FG_ERR_INVALID, "fg_conv_fwd: w_split must be 0 or 1 and equal across problems");
         if (!aligned16(p.x) || (p.sxn | p.sxa | p.sxb | p.sxr) % 4 || p.j_valid % 4) vec = false;
         if (p.n_out > max_n) max_n = p.n_out;
         b.p[i] = p;
     }
-    int BM, BN;
-    if (max_n > 64) { BM = 128; BN = 128; }
+    const bool x6 = (g_conv_math & FG_MATH_FWD_X6) != 0;
+    if (ws && !x6)
+        return fg::fail(FG_ERR_INVALID, "fg_conv_fwd: pre-split weights need the bf16x6 forward math");
+    if (x6) {
+        // the bf16x6 kernels address operands with 31-bit buffer offsets: split oversized
+        // problems over images (each chunk launched on its own)
+        constexpr long long kLim = (1LL << 31) - 256;
+        bool fits = true;
+        for (int i = 0; i < nprob; ++i) {
+            const fg_conv_problem& p = probs[i];
+            const long long tail = (long long)(p.m_a - 1) * p.sxa + (long long)(p.m_b - 1) * p.sxb +
+                                   (long long)(p.kh - 1) * p.sxr + p.jp;
+            const long long ext = 4 * ((long long)(p.m_img - 1) * p.sxn + tail);
+            const long long wext = (long long)p.n_out * p.ldw * (ws ? 6 : 4);
+            if (wext > kLim || 4 * tail > kLim || p.sxn < 0 || p.sxa < 0 || p.sxb < 0 || p.sxr < 0)
+                return fg::fail(FG_ERR_INVALID, "fg_conv_fwd: operand extent beyond 2 GiB per image (problem %d)", i);
+            if (ext > kLim) fits = false;
+        }
+        if (!fits) {
+            for (int i = 0; i < nprob; ++i) {
+                fg_conv_problem q = probs[i];
+                const long long tail = (long long)(q.m_a - 1) * q.sxa + (long long)(q.m_b - 1) * q.sxb +
+                                       (long long)(q.kh - 1) * q.sxr + q.jp;
+                const int per = (int)std::max(1LL, (kLim / 4 - tail) / std::max(1LL, q.sxn) + 1);
+                for (int i0 = 0; i0 < probs[i].m_img; i0 += per) {
+                    q.x = probs[i].x + (long long)i0 * probs[i].sxn;
+                    q.y = probs[i].y + (long long)i0 * probs[i].syn;
+                    q.m_img = std::min(per, probs[i].m_img - i0);
+                    const int rc = fg_conv_fwd(&q, 1, stream);
+                    if (rc) return rc;
+                }
+            }
+            return 0;
+        }
+    }
+    int cfg = -1, BM, BN;
+    if (x6) {
+        cfg = g_fwd_tile >= 0 ? g_fwd_tile : (max_n > 128 ? 13 : max_n > 64 ? 9 : max_n > 32 ? 10 : 6);
+        BM = kFwdTileBM[cfg];
+        BN = kFwdTileBN[cfg];
+    } else if (max_n > 64) { BM = 128; BN = 128; }
     else if (max_n > 32) { BM = 256; BN = 64; }
     else { BM = 256; BN = 32; }
     int total = 0;
@@ -961,10 +1172,22 @@ FG_API int fg_conv_fwd(const fg_conv_problem* probs, int nprob, hipStream_t stre
     b.blk_start[nprob] = total;
     b.blk_start[4] = total;
     if (total == 0) return 0;
-    if (BN == 128 && (g_conv_math & FG_MATH_FWD_X6)) return launch_fwd_x6<128, 128, 64, 64>(b, total, vec, stream);
+    if (x6) return launch_fwd_x6_cfg(cfg, b, total, vec, ws != 0, stream);
     if (BN == 128) return launch_fwd<128, 128, 64, 64>(b, total, vec, stream);
     if (BN == 64) return launch_fwd<256, 64, 64, 64>(b, total, vec, stream);
     return launch_fwd<256, 32, 64, 32>(b, total, vec, stream);
+}
+
+FG_API int fg_set_wgrad_tile(int cfg) {
+    if (cfg < -1 || cfg >= kWgradTiles) return fg::fail(FG_ERR_INVALID, "fg_set_wgrad_tile: %d", cfg);
+    g_wgrad_tile = cfg;
+    return 0;
+}
+
+FG_API int fg_set_fwd_tile(int cfg) {
+    if (cfg < -1 || cfg >= kFwdTiles) return fg::fail(FG_ERR_INVALID, "fg_set_fwd_tile: %d", cfg);
+    g_fwd_tile = cfg;
+    return 0;
 }
 
 FG_API int fg_conv_wgrad(const fg_wgrad_problem* prob, hipStream_t stream) {
@@ -980,9 +1203,15 @@ FG_API int fg_conv_wgrad(const fg_wgrad_problem* prob, hipStream_t stream) {
     const bool vx = aligned16(p.x) && (p.sxn | p.sxa | p.sxb | p.sxr) % 4 == 0 && p.j_valid % 4 == 0;
     const bool vp = aligned16(p.p) && (p.spn | p.spa | p.spb) % 4 == 0;
     if (g_conv_math & FG_MATH_WGRAD_X6) {
-        if (p.n_a > 64) return launch_wgrad_x6<128, 128, 64, 64>(p, vx, vp, stream);
-        if (p.n_a > 32) return launch_wgrad_x6<64, 256, 64, 64>(p, vx, vp, stream);
-        return launch_wgrad_x6<32, 256, 32, 64>(p, vx, vp, stream);
+        // 31-bit buffer offsets: the extent of either operand must stay below 2 GiB
+        const long long pext = 4 * ((long long)(p.m_img - 1) * p.spn + (long long)(p.m_a - 1) * p.spa +
+                                    (long long)(p.m_b - 1) * p.spb + p.n_a + 4);
+        const long long xext = 4 * ((long long)(p.m_img - 1) * p.sxn + (long long)(p.m_a - 1) * p.sxa +
+                                    (long long)(p.m_b - 1) * p.sxb + (long long)(p.kh - 1) * p.sxr + p.j_valid + 4);
+        if (pext >= (1LL << 31) - 256 || xext >= (1LL << 31) - 256 || p.spn < 0 || p.sxn < 0)
+            return fg::fail(FG_ERR_INVALID, "fg_conv_wgrad: operand extent beyond 2 GiB; split the batch");
+        const int cfg = g_wgrad_tile >= 0 ? g_wgrad_tile : (p.n_a > 128 ? 1 : p.n_a > 64 ? 0 : p.n_a > 32 ? 3 : 4);
+        return launch_wgrad_x6_cfg(cfg, p, vx, vp, stream);
     }
     if (p.n_a > 64) return launch_wgrad<128, 128, 64, 64>(p, vx, vp, stream);
     if (p.n_a > 32) return launch_wgrad<64, 256, 64, 64>(p, vx, vp, stream);
@@ -1009,6 +1238,17 @@ FG_API int fg_pack_weight(const float* w, const fg_weight_map* map, float* wp, h
     hipLaunchKernelGGL(pack_weight_kernel, dim3(fg::blocks_for(total, 256, 8192)), dim3(256), 0, stream, w, *map,
                        wp);
     return fg::launched("pack_weight");
+}
+
+FG_API int fg_pack_weight_split(const float* w, const fg_weight_map* map, void* wps, hipStream_t stream) {
+    if (!w || !map || !wps || !aligned16(wps)) return fg::fail(FG_ERR_INVALID, "fg_pack_weight_split: null/unaligned");
+    if (map->kh > 8 || map->kw > 8 || map->jp % BK || map->jp < map->kw * map->c || map->c < 1)
+        return fg::fail(FG_ERR_INVALID, "fg_pack_weight_split: bad map kh=%d kw=%d c=%d jp=%d", map->kh, map->kw,
+                        map->c, map->jp);
+    const long long total = (long long)map->n_out * map->kh * map->jp / 8;
+    hipLaunchKernelGGL(pack_weight_split_kernel, dim3(fg::blocks_for(total, 256, 8192)), dim3(256), 0, stream, w,
+                       *map, reinterpret_cast<bf16x8*>(wps));
+    return fg::launched("pack_weight_split");
 }
 
 FG_API int fg_set_conv_math(int mode) {

@@ -34,7 +34,8 @@ class fg_conv_problem(C.Structure):
                 ("syn", C.c_longlong), ("sya", C.c_longlong), ("syb", C.c_longlong), ("syc", C.c_longlong),
                 ("m_img", C.c_int), ("m_a", C.c_int), ("m_b", C.c_int),
                 ("kh", C.c_int), ("j_valid", C.c_int), ("jp", C.c_int),
-                ("n_out", C.c_int), ("ldw", C.c_int), ("act", C.c_int), ("accumulate", C.c_int)]
+                ("n_out", C.c_int), ("ldw", C.c_int), ("act", C.c_int), ("accumulate", C.c_int),
+                ("w_split", C.c_int)]
 
 
 class fg_wgrad_problem(C.Structure):
@@ -66,9 +67,12 @@ SIGNATURES = {
     "fg_conv_fwd": [C.POINTER(fg_conv_problem), C.c_int, C.c_void_p],
     "fg_set_conv_math": [C.c_int],
     "fg_get_conv_math": [],
+    "fg_set_fwd_tile": [C.c_int],
+    "fg_set_wgrad_tile": [C.c_int],
     "fg_conv_wgrad": [C.POINTER(fg_wgrad_problem), C.c_void_p],
     "fg_wgrad_reduce": [C.c_void_p, C.c_int, C.POINTER(fg_weight_map), C.c_void_p, C.c_int, C.c_void_p],
     "fg_pack_weight": [C.c_void_p, C.POINTER(fg_weight_map), C.c_void_p, C.c_void_p],
+    "fg_pack_weight_split": [C.c_void_p, C.POINTER(fg_weight_map), C.c_void_p, C.c_void_p],
     "fg_pack_input": [fg_sview, C.c_int, fg_sview, C.c_int, fg_view, C.c_int, C.c_int, C.c_int, C.c_void_p],
     "fg_zero_border": [fg_view, C.c_void_p],
     "fg_fold_add": [fg_view, C.c_int, fg_view, fg_view, C.c_void_p],
@@ -118,6 +122,21 @@ def load(path=LIB_PATH):
 def set_conv_math(mode):
     """'fp32' (v_mfma_f32_32x32x2_f32) or 'bf16x6' (fp32-equivalent split-bf16 MFMA)."""
     check(load().fg_set_conv_math(CONV_MATH[mode]), "set_conv_math")
+
+
+def fwd_x6():
+    """True when the forward / input-gradient convs run the bf16x6 kernels (pre-split weights)."""
+    return bool(load().fg_get_conv_math() & FG_MATH_FWD_X6)
+
+
+def set_fwd_tile(cfg):
+    """Tuning hook: force a bf16x6 forward tile config (-1 = automatic)."""
+    check(load().fg_set_fwd_tile(int(cfg)), "set_fwd_tile")
+
+
+def set_wgrad_tile(cfg):
+    """Tuning hook: force a bf16x6 weight-gradient tile config (-1 = automatic)."""
+    check(load().fg_set_wgrad_tile(int(cfg)), "set_wgrad_tile")
 
 
 def get_conv_math():

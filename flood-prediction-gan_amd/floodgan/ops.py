@@ -53,11 +53,20 @@ def wmap_struct(m):
 
 # ------------------------------------------------------------------ conv engine
 
-def pack_weight(w, m):
+def pack_weight(w, m, split=None):
+    """Packed weight for the conv engine: fp32 [n][kh*jp], or (split, the default under the
+    bf16x6 forward math) the pre-split bf16 h/m/l layout of fg_pack_weight_split, returned as a
+    bfloat16 tensor (conv problems built on it carry w_split = 1)."""
     L.require_device(w, "weight")
     w = w.contiguous()
-    wp = torch.empty(packed_numel(m), dtype=torch.float32, device=w.device)
     s = wmap_struct(m)
+    if split is None:
+        split = L.fwd_x6()
+    if split:
+        wp = torch.empty(3 * packed_numel(m), dtype=torch.bfloat16, device=w.device)
+        L.check(_lib().fg_pack_weight_split(L.ptr(w), C.byref(s), L.ptr(wp), L.stream_handle()), "pack_weight_split")
+        return wp
+    wp = torch.empty(packed_numel(m), dtype=torch.float32, device=w.device)
     L.check(_lib().fg_pack_weight(L.ptr(w), C.byref(s), L.ptr(wp), L.stream_handle()), "pack_weight")
     return wp
 
@@ -108,6 +117,7 @@ def _conv(probs):
     for i, p in enumerate(probs):
         s = arr[i]
         s.x, s.w, s.y = _addr(p["x"]), _addr(p["w"]), _addr(p["y"])
+        s.w_split = int(p["w"][0].dtype == torch.bfloat16)
         s.bias = p["bias"].data_ptr() if p["bias"] is not None else None
         for k in _CONV_FIELDS:
             setattr(s, k, int(p[k]))

@@ -215,6 +215,8 @@ WG_BLOCKS = 1024   # ~ one full wave of resident workgroups (256 CUs x 4)
 
 def wgrad_tile(n_a):
     """(rows, cols) of the weight-gradient tile the engine picks for n_a result rows"""
+    if n_a > 128:
+        return (256, 128)
     return (128, 128) if n_a > 64 else ((64, 256) if n_a > 32 else (32, 256))
 
 

@@ -68,6 +68,8 @@ typedef struct fg_conv_problem {
     int kh, j_valid, jp;
     int n_out, ldw;
     int act, accumulate;
+    int w_split;          /* 0: w is fp32 [n][ldw] (fg_pack_weight); 1: w is the pre-split bf16 layout
+                             of fg_pack_weight_split (bf16x6 forward kernels only)                   */
 } fg_conv_problem;
 
 /*
@@ -116,6 +118,12 @@ int fg_conv_fwd(const fg_conv_problem* probs, int nprob, hipStream_t stream);
 int fg_set_conv_math(int mode);
 int fg_get_conv_math(void);
 
+/* Tuning hook: force one bf16x6 forward tile configuration (0..7, see conv_gemm.hip), or -1 for
+ * the automatic choice by output-channel count (the default). */
+int fg_set_fwd_tile(int cfg);
+/* Same for the bf16x6 weight-gradient kernel (0..5). */
+int fg_set_wgrad_tile(int cfg);
+
 /* Weight gradient into partial slabs (see fg_wgrad_problem). */
 int fg_conv_wgrad(const fg_wgrad_problem* prob, hipStream_t stream);
 
@@ -126,6 +134,12 @@ int fg_wgrad_reduce(const float* slabs, int splits, const fg_weight_map* map, fl
 
 /* Repack a PyTorch conv / conv-transpose weight into the engine's [n][kh*jp] layout. */
 int fg_pack_weight(const float* w, const fg_weight_map* map, float* wp, hipStream_t stream);
+
+/* Same repack, pre-split for the bf16x6 forward kernels: for packed row n and k-slot q (8
+ * consecutive k of [0, kh*jp)), wps[(n*(kh*jp/8) + q)*24 + piece*8 + e] (piece 0,1,2 = h,m,l,
+ * bf16 bit patterns) with w = h + m + l exactly.  Size n_out*kh*jp*3 bf16.  Conv problems that
+ * read it set w_split = 1. */
+int fg_pack_weight_split(const float* w, const fg_weight_map* map, void* wps, hipStream_t stream);
 
 /* ---------------------------------------------------------------------------------------- */
 /* layout / padding                                                                          */

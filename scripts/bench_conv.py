@@ -24,13 +24,14 @@ def make(N, H, Cin, Cout, k, s, p, dev="cuda"):
     X.t.uniform_(-1, 1)
     w = torch.randn(Cout, Cin, k, k, device=dev) * 0.02
     m = PL.wmap_conv_fwd(w.shape, Cin)
-    wp = ops.pack_weight(w, m)
     Ho = PL.out_size(H, k, s, p)
     Y = Buf.empty(N, Ho, Ho, Cout, 0, dev)
-    prob = PL.conv_problem(X, p, k, s, wp, m, Y, bias=torch.zeros(Cout, device=dev))
     flops = 2.0 * N * Ho * Ho * Cout * Cin * k * k
-    return prob, flops, (X, w, Y)
 
+    def prob(split):
+        wp = ops.pack_weight(w, m, split=split)
+        return PL.conv_problem(X, p, k, s, wp, m, Y, bias=torch.zeros(Cout, device=dev))
+    return prob, flops, (X, w, Y)
 
 def time_it(fn, reps=10):
     for _ in range(2):
@@ -67,23 +68,31 @@ def accuracy(mode):
 
 def main():
     L.load()
-    for mode in ("fp32", "bf16x6"):
+    for mode in (("fp32", "bf16x6") if os.environ.get("ACCURACY", "1") == "1" else ()):
         e, e32 = accuracy(mode)
-        print(f"accuracy {mode}: rel err vs fp64 {e:.3e}  (torch CPU fp32: {e32:.3e})")
+        print(f"accuracy {mode}: rel err vs fp64 {e:.3e}  (torch CPU fp32: {e32:.3e})", flush=True)
     cases = {"resblock 3x3 256->256 @128": (8, 128, 256, 256, 3, 1, 1),
              "conv2 3x3s2 64->128 @512": (8, 512, 64, 128, 3, 2, 1),
-             "D model.8 4x4 256->512 @64 (2N)": (16, 64, 256, 512, 4, 1, 1)}
+             "D model.8 4x4 256->512 @64 (2N)": (16, 64, 256, 512, 4, 1, 1),
+             "3x3 128->64 @256 (N=64 class)": (8, 256, 128, 64, 3, 1, 1),
+             "deconv3_content 7x7 64->27 @512": (8, 512, 64, 27, 7, 1, 3)}
+    tiles = [int(t) for t in os.environ.get("TILES", "0,1,2,3,4,5,6,7,8").split(",")]
     for name, c in cases.items():
-        prob, flops, keep = make(*c)
+        mk, flops, keep = make(*c)
+        variants = [("fp32", -1, False)] + [("bf16x6", t, True) for t in tiles] + [("bf16x6", -1, False)]
         res = {}
-        for rep in range(3):
-            for mode in ("fp32", "bf16x6"):
+        for rep in range(2):
+            for mode, tile, split in variants:
                 L.set_conv_math(mode)
+                L.set_fwd_tile(tile)
+                prob = mk(split)
                 ms = time_it(lambda: ops.conv([prob]))
-                res.setdefault(mode, []).append(ms)
-        for mode, v in res.items():
+                res.setdefault((mode, tile, split), []).append(ms)
+        L.set_fwd_tile(-1)
+        for (mode, tile, split), v in res.items():
             ms = min(v)
-            print(f"{name:36s} {mode:7s} {ms:8.3f} ms  {flops / ms / 1e9:7.1f} TFLOP/s")
+            tag = f"{mode} tile {tile:2d} {'presplit' if split else 'onfly'}" if mode != "fp32" else "fp32"
+            print(f"{name:36s} {tag:26s} {ms:8.3f} ms  {flops / ms / 1e9:7.1f} TFLOP/s", flush=True)
         # weight gradient of the same conv
         X, w, Y = keep
         Y.t.uniform_(-1, 1)
@@ -91,21 +100,28 @@ def main():
         wprob = PL.wgrad_conv(Y, X, p_, k, s_, Cout)
         dw = torch.empty_like(w)
         wm = PL.wmap_wgrad(w.shape, True, X.c, k)
+        wtiles = [int(t) for t in os.environ.get("WTILES", "-1").split(",")]
+        wvariants = [("fp32", -1)] + [("bf16x6", t) for t in wtiles]
         res = {}
-        for rep in range(3):
-            for mode in ("fp32", "bf16x6"):
+        for rep in range(2):
+            for mode, t in wvariants:
                 L.set_conv_math(mode)
-                res.setdefault(mode, []).append(time_it(lambda: ops.wgrad(wprob, wm, dw)))
+                L.set_wgrad_tile(t)
+                res.setdefault((mode, t), []).append(time_it(lambda: ops.wgrad(wprob, wm, dw)))
         L.set_conv_math("fp32")
+        L.set_wgrad_tile(-1)
         ops.wgrad(wprob, wm, dw)
         ref = dw.clone()
         L.set_conv_math("bf16x6")
-        ops.wgrad(wprob, wm, dw)
-        torch.cuda.synchronize()
-        print(f"{name + ' wgrad':36s} x6 vs fp32 rel diff {nrel(dw, ref):.2e}")
-        for mode, v in res.items():
+        for t in wtiles:
+            L.set_wgrad_tile(t)
+            ops.wgrad(wprob, wm, dw)
+            torch.cuda.synchronize()
+            print(f"{name + ' wgrad':36s} x6 tile {t} vs fp32 rel diff {nrel(dw, ref):.2e}")
+        L.set_wgrad_tile(-1)
+        for (mode, t), v in res.items():
             ms = min(v)
-            print(f"{name + ' wgrad':36s} {mode:7s} {ms:8.3f} ms  {flops / ms / 1e9:7.1f} TFLOP/s")
+            print(f"{name + ' wgrad':36s} {mode:7s} tile {t:2d} {ms:8.3f} ms  {flops / ms / 1e9:7.1f} TFLOP/s", flush=True)
 
 
 if __name__ == "__main__":
