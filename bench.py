@@ -23,7 +23,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak (spec)
-BF16_MFMA_PEAK_TFLOPS = 2500.0    # MI355X_MICROARCH.md: bf16 dense MFMA peak (spec)
+BF16_MFMA_PEAK_TFLOPS = 2500.0    # MI355X_MICROARCH.md: bf16 / fp16 dense MFMA peak (spec)
 STEP_GFLOP_PER_IMG_512 = 1593.5   # conv fwd 546.1 + conv bwd 1047.3 GFLOP per image
 
 
@@ -107,10 +107,11 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
     math = _lib.get_conv_math()
-    fwd_x6 = math in ("bf16x6", "fwd_x6")
-    # fp32-equivalent split-bf16 executes 6 bf16 MFMA products per fp32 multiply-add: its
-    # roof for fp32 work is the bf16 dense peak / 6 (the fp32 MFMA path's roof is 157.3)
-    peak = BF16_MFMA_PEAK_TFLOPS / 6 if fwd_x6 else FP32_MFMA_PEAK_TFLOPS
+    # split maths execute several 16-bit MFMA products per fp32 multiply-add: the roof for fp32
+    # work is the 16-bit dense MFMA peak / products (the fp32 MFMA path's roof is 157.3)
+    nprod = {"f16x3": 3, "fwd_f16x3": 3, "bf16x6": 6, "fwd_x6": 6}.get(math)
+    peak = BF16_MFMA_PEAK_TFLOPS / nprod if nprod else FP32_MFMA_PEAK_TFLOPS
+    fwd_x6 = nprod is not None
     durs = timer.durations_ms()["resblock_conv_fwd"]
     avg_ms = sum(durs) / max(len(durs), 1)
     flops = resblock_conv_flops(B, R)
@@ -137,11 +138,12 @@ def main():
                        "parallelism": f"dp{world}"},
             "conv_math": math,
             "roofline": {"bound": "mfma",
-                         "kernel": ("conv_fwd_x6_kernel<128,256,64,64> (8 waves, pre-split weights)" if fwd_x6 else
+                         "kernel": (f"conv_fwd_x6_kernel<{'MathF16x3' if nprod == 3 else 'MathBF16x6'},128,256,64,64> "
+                                    "(8 waves, pre-split weights)" if fwd_x6 else
                                     "conv_fwd_kernel<128,128,64,64>") + " resblock 3x3 256->256 @128x128",
                          "achieved": round(achieved, 2), "peak": round(peak, 2), "unit": "TFLOP/s",
-                         "peak_basis": ("bf16 dense MFMA 2500 TFLOP/s / 6 bf16 products per fp32 MAC" if fwd_x6
-                                        else "fp32 MFMA dense peak"),
+                         "peak_basis": (f"16-bit dense MFMA 2500 TFLOP/s / {nprod} split products per fp32 MAC"
+                                        if fwd_x6 else "fp32 MFMA dense peak"),
                          "frac": round(achieved / peak, 4), "traffic": None,
                          "avg_launch_ms": round(avg_ms, 4), "launches": len(durs),
                          "flop_per_launch": flops},

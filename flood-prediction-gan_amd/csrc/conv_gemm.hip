@@ -25,7 +25,7 @@ namespace {
 
 constexpr int BK = 16;
 constexpr int LDK = BK + 4;
-int g_conv_math = FG_MATH_BF16X6;   // default: fp32-equivalent split-bf16 (tests: tests/test_gpu_parity.py)
+int g_conv_math = FG_MATH_F16X3;    // default: scaled split-fp16 (accuracy: scripts/bench_conv.py, tests/)
 
 struct ConvBatch {
     fg_conv_problem p[4];
@@ -248,9 +248,102 @@ __device__ __forceinline__ void split3(const float (&v)[8], bf16x8& h, bf16x8& m
     }
 }
 
-template <int BM, int BN, int WM, int WN, bool VEC, bool WS, int MINW, int PF, bool SWZ>
+// ------------------------------------------------------------------------------------------
+// Split-fp16 variant ("f16x3"): every operand is scaled by an exact power of two s (so that
+// |v*s| < 2^14, from the operand's absolute maximum) and split into two fp16 pieces
+// v*s = h + l (h = fp16(v*s), l = fp16(v*s - h): 11 + 11 significant bits, representation
+// error <= 2^-22 |v|).  Three exact fp16 products hh + hl + lh (dropped: ll ~2^-22) are
+// accumulated in fp32 by v_mfma_f32_32x32x16_f16 and the result is multiplied back by
+// 1/(s_a s_b).  Half the MFMAs and 2/3 of the staging of bf16x6, at ~4x its per-product error
+// (still far below the fp32 accumulation error of the convolution sums).
+// ------------------------------------------------------------------------------------------
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+
+// power-of-two operand scale from an absmax slot (max over its FG_AMAX_SHARDS shards, one per
+// lane, reduced across the wave): |v * s| < 2^14
+__device__ __forceinline__ float pow2_scale(const float* amax) {
+    unsigned b = amax ? __float_as_uint(amax[threadIdx.x & (FG_AMAX_SHARDS - 1)]) & 0x7fffffffu : 0u;
+#pragma unroll
+    for (int off = 1; off < FG_AMAX_SHARDS; off <<= 1) b = max(b, (unsigned)__shfl_xor((int)b, off));
+    const float m = __uint_as_float(b);
+    if (!(m > 0.f) || !(m < 3.0e38f)) return 1.f;
+    int e;
+    frexpf(m, &e);                                        // m < 2^e
+    return ldexpf(1.f, 14 - e);
+}
+
+// split math traits: piece type, piece count, the products kept (PA[c] x PB[c], small first)
+struct MathBF16x6 {
+    using T = __bf16;
+    using V8 = bf16x8;
+    static constexpr int NP = 3, NPROD = 6;
+    static constexpr int PA[6] = {1, 0, 2, 0, 1, 0};
+    static constexpr int PB[6] = {1, 2, 0, 1, 0, 0};
+    using V4 = __bf16 __attribute__((ext_vector_type(4)));
+    static constexpr bool SCALED = false;
+    __device__ static void split(const float (&v)[8], float, V8 (&o)[3]) { split3(v, o[0], o[1], o[2]); }
+    __device__ static void split4(const f32x4& v, float, V4 (&o)[3]) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            bf16x2 h, m, l;
+            split3x2(v[2 * e], v[2 * e + 1], h, m, l);
+            o[0][2 * e] = h[0];
+            o[0][2 * e + 1] = h[1];
+            o[1][2 * e] = m[0];
+            o[1][2 * e + 1] = m[1];
+            o[2][2 * e] = l[0];
+            o[2][2 * e + 1] = l[1];
+        }
+    }
+    __device__ static f32x16 mfma(const V8& a, const V8& b, const f32x16& c) {
+        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+    }
+};
+struct MathF16x3 {
+    using T = _Float16;
+    using V8 = f16x8;
+    static constexpr int NP = 2, NPROD = 3;
+    static constexpr int PA[3] = {1, 0, 0};
+    static constexpr int PB[3] = {0, 1, 0};
+    using V4 = f16x4;
+    static constexpr bool SCALED = true;
+    __device__ static void split4(const f32x4& v, float s, V4 (&o)[2]) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const f32x2 x = f32x2{v[2 * e], v[2 * e + 1]} * s;
+            const f16x2 h = __builtin_convertvector(x, f16x2);
+            const f16x2 l = __builtin_convertvector(x - __builtin_convertvector(h, f32x2), f16x2);
+            o[0][2 * e] = h[0];
+            o[0][2 * e + 1] = h[1];
+            o[1][2 * e] = l[0];
+            o[1][2 * e + 1] = l[1];
+        }
+    }
+    __device__ static void split(const float (&v)[8], float s, V8 (&o)[2]) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const f32x2 x = f32x2{v[2 * e], v[2 * e + 1]} * s;
+            const f16x2 h = __builtin_convertvector(x, f16x2);
+            const f16x2 l = __builtin_convertvector(x - __builtin_convertvector(h, f32x2), f16x2);
+            o[0][2 * e] = h[0];
+            o[0][2 * e + 1] = h[1];
+            o[1][2 * e] = l[0];
+            o[1][2 * e + 1] = l[1];
+        }
+    }
+    __device__ static f32x16 mfma(const V8& a, const V8& b, const f32x16& c) {
+        return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+    }
+};
+
+template <class SM, int BM, int BN, int WM, int WN, bool VEC, bool WS, int MINW, int PF, bool SWZ>
 __global__ void __launch_bounds__((BM / WM) * (BN / WN) * 64, MINW)
 conv_fwd_x6_kernel(const ConvBatch batch) {
+    using T = typename SM::T;
+    using V8 = typename SM::V8;
+    constexpr int NP = SM::NP;
     constexpr int NWN = BN / WN;
     constexpr int NT = (BM / WM) * (BN / WN) * 64;
     constexpr int TM = WM / 32, TN = WN / 32;
@@ -260,8 +353,8 @@ conv_fwd_x6_kernel(const ConvBatch batch) {
     constexpr int A_SLOTS = BM * 2, B_SLOTS = BN * 2;   // slot = 8 consecutive k of one row
     constexpr int A_IT = (A_SLOTS + NT - 1) / NT, B_IT = (B_SLOTS + NT - 1) / NT;
 
-    __shared__ __attribute__((aligned(16))) __bf16 As[2][3][BM][LDP];
-    __shared__ __attribute__((aligned(16))) __bf16 Bs[2][3][BN][LDP];
+    __shared__ __attribute__((aligned(16))) T As[2][NP][BM][LDP];
+    __shared__ __attribute__((aligned(16))) T Bs[2][NP][BN][LDP];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave / NWN, wn = wave - (wave / NWN) * NWN;
@@ -313,15 +406,20 @@ conv_fwd_x6_kernel(const ConvBatch batch) {
         b_g[i] = s & 1;
         bslot[i] = B_FULL || s < B_SLOTS;
         const int n = n0 + (s >> 1);
-        // byte offset of this slot's first k-slot (WS: 48 B per 8-k slot, else 32 B of fp32)
-        b_off[i] = (bslot[i] && n < P.n_out) ? (WS ? (n * (P.ldw / 8) + b_g[i]) * 48 : (n * P.ldw + b_g[i] * 8) * 4)
-                                             : -1;
+        // byte offset of this slot's first k-slot (WS: NP x 16 B per 8-k slot, else 32 B of fp32)
+        b_off[i] = (bslot[i] && n < P.n_out)
+                       ? (WS ? (n * (P.ldw / 8) + b_g[i]) * NP * 16 : (n * P.ldw + b_g[i] * 8) * 4)
+                       : -1;
     }
     constexpr int kOOB = 0x7fffffff;   // >= num_records: the load returns zeros
+    // f16x3: operand scales (exact powers of two) and the epilogue's inverse
+    const float sa = SM::SCALED ? pow2_scale(P.x_absmax) : 1.f;
+    const float sb = SM::SCALED ? pow2_scale(P.w_absmax) : 1.f;
+    const float out_scale = 1.f / (sa * sb);
 
     struct Stage {
         float ra[A_IT][8], rb[WS ? 1 : B_IT][8];
-        bf16x8 rbs[WS ? B_IT : 1][3];
+        V8 rbs[WS ? B_IT : 1][NP];
     };
     auto load = [&](int kt, Stage& S) {
         const int r = kt / jtr;
@@ -352,11 +450,11 @@ conv_fwd_x6_kernel(const ConvBatch batch) {
 #pragma unroll
         for (int i = 0; i < B_IT; ++i) {
             if constexpr (WS) {
-                const int o = b_off[i] >= 0 ? b_off[i] + kt * 96 : kOOB;
+                const int o = b_off[i] >= 0 ? b_off[i] + kt * 32 * NP : kOOB;
 #pragma unroll
-                for (int p = 0; p < 3; ++p)
-                    S.rbs[i][p] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
-                                                                 wr, o == kOOB ? kOOB : o + 16 * p, 0, 0));
+                for (int p = 0; p < NP; ++p)
+                    S.rbs[i][p] = __builtin_bit_cast(V8, __builtin_amdgcn_raw_buffer_load_b128(
+                                                             wr, o == kOOB ? kOOB : o + 16 * p, 0, 0));
             } else {
                 const int o = b_off[i] >= 0 ? b_off[i] + kt * 64 : kOOB;
                 const f32x4 v0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(wr, o, 0, 0));
@@ -374,28 +472,25 @@ conv_fwd_x6_kernel(const ConvBatch batch) {
 #pragma unroll
         for (int i = 0; i < A_IT; ++i)
             if (aslot[i]) {
-                bf16x8 h, m, l;
-                split3(S.ra[i], h, m, l);
+                V8 pc[NP];
+                SM::split(S.ra[i], sa, pc);
                 const int c = (SWZ ? a_g[i] ^ ((a_r[i] >> 3) & 1) : a_g[i]) * 8;
-                *reinterpret_cast<bf16x8*>(&As[buf][0][a_r[i]][c]) = h;
-                *reinterpret_cast<bf16x8*>(&As[buf][1][a_r[i]][c]) = m;
-                *reinterpret_cast<bf16x8*>(&As[buf][2][a_r[i]][c]) = l;
+#pragma unroll
+                for (int p = 0; p < NP; ++p) *reinterpret_cast<V8*>(&As[buf][p][a_r[i]][c]) = pc[p];
             }
 #pragma unroll
         for (int i = 0; i < B_IT; ++i)
             if (bslot[i]) {
-                bf16x8 h, m, l;
+                V8 pc[NP];
                 if constexpr (WS) {
-                    h = S.rbs[i][0];
-                    m = S.rbs[i][1];
-                    l = S.rbs[i][2];
+#pragma unroll
+                    for (int p = 0; p < NP; ++p) pc[p] = S.rbs[i][p];
                 } else {
-                    split3(S.rb[i], h, m, l);
+                    SM::split(S.rb[i], sb, pc);
                 }
                 const int c = (SWZ ? b_g[i] ^ ((b_r[i] >> 3) & 1) : b_g[i]) * 8;
-                *reinterpret_cast<bf16x8*>(&Bs[buf][0][b_r[i]][c]) = h;
-                *reinterpret_cast<bf16x8*>(&Bs[buf][1][b_r[i]][c]) = m;
-                *reinterpret_cast<bf16x8*>(&Bs[buf][2][b_r[i]][c]) = l;
+#pragma unroll
+                for (int p = 0; p < NP; ++p) *reinterpret_cast<V8*>(&Bs[buf][p][b_r[i]][c]) = pc[p];
             }
     };
 
@@ -409,27 +504,24 @@ conv_fwd_x6_kernel(const ConvBatch batch) {
 
     const int lrow = lane & 31, lk = (SWZ ? (lane >> 5) ^ ((lane >> 3) & 1) : (lane >> 5)) * 8;
     auto compute = [&](int cur) {
-        bf16x8 af[TM][3], bfr[TN][3];
+        V8 af[TM][NP], bfr[TN][NP];
 #pragma unroll
-        for (int p = 0; p < 3; ++p) {
+        for (int p = 0; p < NP; ++p) {
 #pragma unroll
             for (int tm = 0; tm < TM; ++tm)
-                af[tm][p] = *reinterpret_cast<const bf16x8*>(&As[cur][p][wm * WM + tm * 32 + lrow][lk]);
+                af[tm][p] = *reinterpret_cast<const V8*>(&As[cur][p][wm * WM + tm * 32 + lrow][lk]);
 #pragma unroll
             for (int tn = 0; tn < TN; ++tn)
-                bfr[tn][p] = *reinterpret_cast<const bf16x8*>(&Bs[cur][p][wn * WN + tn * 32 + lrow][lk]);
+                bfr[tn][p] = *reinterpret_cast<const V8*>(&Bs[cur][p][wn * WN + tn * 32 + lrow][lk]);
         }
-        // six fp32-relevant piece products; each pair's (tm, tn) blocks interleaved
-        constexpr int PA[6] = {1, 0, 2, 0, 1, 0};
-        constexpr int PB[6] = {1, 2, 0, 1, 0, 0};
+        // the kept piece products, smallest first; each product's (tm, tn) blocks interleaved
 #pragma unroll
-        for (int c = 0; c < 6; ++c)
+        for (int c = 0; c < SM::NPROD; ++c)
 #pragma unroll
             for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
                 for (int tn = 0; tn < TN; ++tn)
-                    acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[tm][PA[c]], bfr[tn][PB[c]], acc[tm][tn],
-                                                                          0, 0, 0);
+                    acc[tm][tn] = SM::mfma(af[tm][SM::PA[c]], bfr[tn][SM::PB[c]], acc[tm][tn]);
     };
     Stage R0, R1;
     if constexpr (PF == 1) {
@@ -481,7 +573,7 @@ conv_fwd_x6_kernel(const ConvBatch batch) {
             for (int tn = 0; tn < TN; ++tn) {
                 const int n = n0 + wn * WN + tn * 32 + lrow;
                 if (n >= P.n_out) continue;
-                float v = acc[tm][tn][reg];
+                float v = SM::SCALED ? acc[tm][tn][reg] * out_scale : acc[tm][tn][reg];
                 if (P.bias) v += P.bias[n];
                 v = fg::act_fwd(v, act);
                 float* dst = yrow + n * P.syc;
@@ -672,12 +764,13 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
-__device__ __forceinline__ bf16x8 tr_frag(const __bf16* r0, const __bf16* r4) {
+template <class V8, class T>
+__device__ __forceinline__ V8 tr_frag(const T* r0, const T* r4) {
     const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(r0));
     const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(r4));
     typedef short s16x8 __attribute__((ext_vector_type(8)));
     const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    return __builtin_bit_cast(bf16x8, v);
+    return __builtin_bit_cast(V8, v);
 }
 
 __device__ __forceinline__ void split3x4(const f32x4& v, bf16x4& h, bf16x4& m, bf16x4& l) {
@@ -704,9 +797,13 @@ __device__ __forceinline__ int wg_swz(int row) {
     else return 0;
 }
 
-template <int BA, int BKC, int WA, int WK, bool VX, bool VP, int MINW>
+template <class SM, int BA, int BKC, int WA, int WK, bool VX, bool VP, int MINW>
 __global__ void __launch_bounds__((BA / WA) * (BKC / WK) * 64, MINW)
 conv_wgrad_x6_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
+    using T = typename SM::T;
+    using V8 = typename SM::V8;
+    using V4 = typename SM::V4;
+    constexpr int NP = SM::NP;
     constexpr int NWK = BKC / WK;
     constexpr int NT = (BA / WA) * (BKC / WK) * 64;
     constexpr int TM = WA / 32, TN = WK / 32;
@@ -716,8 +813,8 @@ conv_wgrad_x6_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
     constexpr bool P_FULL = P_SLOTS % NT == 0, X_FULL = X_SLOTS % NT == 0;
     constexpr int kOOB = 0x7fffffff;
 
-    __shared__ __attribute__((aligned(16))) __bf16 Ps[2][3][BR][BA];
-    __shared__ __attribute__((aligned(16))) __bf16 Xs[2][3][BR][BKC];
+    __shared__ __attribute__((aligned(16))) T Ps[2][NP][BR][BA];
+    __shared__ __attribute__((aligned(16))) T Xs[2][NP][BR][BKC];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wa = wave / NWK, wk = wave - (wave / NWK) * NWK;
@@ -737,6 +834,8 @@ conv_wgrad_x6_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
     const int i16 = BR / mab, a16 = (BR - i16 * mab) / P.m_b, b16 = BR - i16 * mab - a16 * P.m_b;
     const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc((void*)P.p, 0, 0x7fffffff, 0x00020000);
     const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)P.x, 0, 0x7fffffff, 0x00020000);
+    const float sp = SM::SCALED ? pow2_scale(P.p_absmax) : 1.f;
+    const float sx = SM::SCALED ? pow2_scale(P.x_absmax) : 1.f;
 
     // per-slot pixel walk: slot rows are fixed within the stage, the pixel advances by BR
     struct Walk {
@@ -837,22 +936,20 @@ conv_wgrad_x6_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
 #pragma unroll
         for (int i = 0; i < P_IT; ++i)
             if (p_slot[i]) {
-                bf16x4 h, m, l;
-                split3x4(rp[i], h, m, l);
+                V4 pc[NP];
+                SM::split4(rp[i], sp, pc);
                 const int c = p_col[i] ^ wg_swz<BA>(p_row[i]);
-                *reinterpret_cast<bf16x4*>(&Ps[buf][0][p_row[i]][c]) = h;
-                *reinterpret_cast<bf16x4*>(&Ps[buf][1][p_row[i]][c]) = m;
-                *reinterpret_cast<bf16x4*>(&Ps[buf][2][p_row[i]][c]) = l;
+#pragma unroll
+                for (int q = 0; q < NP; ++q) *reinterpret_cast<V4*>(&Ps[buf][q][p_row[i]][c]) = pc[q];
             }
 #pragma unroll
         for (int i = 0; i < X_IT; ++i)
             if (x_slot[i]) {
-                bf16x4 h, m, l;
-                split3x4(rx[i], h, m, l);
+                V4 pc[NP];
+                SM::split4(rx[i], sx, pc);
                 const int c = x_col[i] ^ wg_swz<BKC>(x_row[i]);
-                *reinterpret_cast<bf16x4*>(&Xs[buf][0][x_row[i]][c]) = h;
-                *reinterpret_cast<bf16x4*>(&Xs[buf][1][x_row[i]][c]) = m;
-                *reinterpret_cast<bf16x4*>(&Xs[buf][2][x_row[i]][c]) = l;
+#pragma unroll
+                for (int q = 0; q < NP; ++q) *reinterpret_cast<V4*>(&Xs[buf][q][x_row[i]][c]) = pc[q];
             }
     };
 
@@ -876,35 +973,33 @@ conv_wgrad_x6_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
     for (int it = 0; it < nit; ++it) {
         const int cur = it & 1;
         load();                         // past the last stage: reads zeros (m >= mend), never stored
-        bf16x8 af[TM][3], bfr[TN][3];
+        V8 af[TM][NP], bfr[TN][NP];
 #pragma unroll
-        for (int p = 0; p < 3; ++p) {
+        for (int p = 0; p < NP; ++p) {
 #pragma unroll
             for (int tm = 0; tm < TM; ++tm) {
                 const int c = (wa * WA + tm * 32 + tr_col) ^ swp;
-                af[tm][p] = tr_frag(&Ps[cur][p][tr_row][c], &Ps[cur][p][tr_row + 4][c]);
+                af[tm][p] = tr_frag<V8>(&Ps[cur][p][tr_row][c], &Ps[cur][p][tr_row + 4][c]);
             }
 #pragma unroll
             for (int tn = 0; tn < TN; ++tn) {
                 const int c = (wk * WK + tn * 32 + tr_col) ^ swx;
-                bfr[tn][p] = tr_frag(&Xs[cur][p][tr_row][c], &Xs[cur][p][tr_row + 4][c]);
+                bfr[tn][p] = tr_frag<V8>(&Xs[cur][p][tr_row][c], &Xs[cur][p][tr_row + 4][c]);
             }
         }
-        constexpr int PA[6] = {1, 0, 2, 0, 1, 0};
-        constexpr int PB[6] = {1, 2, 0, 1, 0, 0};
 #pragma unroll
-        for (int c = 0; c < 6; ++c)
+        for (int c = 0; c < SM::NPROD; ++c)
 #pragma unroll
             for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
                 for (int tn = 0; tn < TN; ++tn)
-                    acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[tm][PA[c]], bfr[tn][PB[c]], acc[tm][tn],
-                                                                          0, 0, 0);
+                    acc[tm][tn] = SM::mfma(af[tm][SM::PA[c]], bfr[tn][SM::PB[c]], acc[tm][tn]);
         if (it + 1 < nit) store(cur ^ 1);
         __syncthreads();
     }
 
     float* out = P.out + (size_t)split * P.n_a * K;
+    const float out_scale = 1.f / (sp * sx);
 #pragma unroll
     for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
@@ -914,7 +1009,7 @@ conv_wgrad_x6_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
 #pragma unroll
             for (int tn = 0; tn < TN; ++tn) {
                 const int k = k0 + wk * WK + tn * 32 + (lane & 31);
-                if (k < K) out[(size_t)a * K + k] = acc[tm][tn][reg];
+                if (k < K) out[(size_t)a * K + k] = SM::SCALED ? acc[tm][tn][reg] * out_scale : acc[tm][tn][reg];
             }
         }
 }
@@ -993,17 +1088,61 @@ __global__ void pack_weight_split_kernel(const float* __restrict__ w, fg_weight_
     }
 }
 
-template <int BM, int BN, int WM, int WN, int MINW, int PF, bool SWZ = false>
+// f16x3 weights: one thread per (row, 8-k slot): 8 scaled weights -> h, l fp16 pieces (32 B)
+__global__ void pack_weight_f16_kernel(const float* __restrict__ w, fg_weight_map map, const float* __restrict__ amax,
+                                       f16x8* __restrict__ wps) {
+    const int QS = map.kh * map.jp / 8;
+    const long long total = (long long)map.n_out * QS;
+    const float sc = pow2_scale(amax);
+    for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const int n = (int)(idx / QS);
+        const int k0 = (int)(idx - (long long)n * QS) * 8;
+        const int kr = k0 / map.jp, j0 = k0 - (k0 / map.jp) * map.jp;
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = packed_w(w, map, n, kr, j0 + e);
+        f16x8 pc[2];
+        MathF16x3::split(v, sc, pc);
+        wps[idx * 2] = pc[0];
+        wps[idx * 2 + 1] = pc[1];
+    }
+}
+
+// max |x| as the bit pattern of a non-negative float (uint order = float order; NaN sorts high)
+__global__ void absmax_kernel(const float* __restrict__ x, long long n, unsigned* __restrict__ out) {
+    unsigned m = 0;
+    const long long n4 = (((uintptr_t)x & 15) == 0) ? n / 4 : 0;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+        const f32x4 v = reinterpret_cast<const f32x4*>(x)[i];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) m = max(m, __float_as_uint(v[e]) & 0x7fffffffu);
+    }
+    for (long long i = n4 * 4 + blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x)
+        m = max(m, __float_as_uint(x[i]) & 0x7fffffffu);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, off));
+    __shared__ unsigned red[16];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int i = 1; i < (int)(blockDim.x >> 6); ++i) m = max(m, red[i]);
+        atomicMax(out + (blockIdx.x & (FG_AMAX_SHARDS - 1)), m);
+    }
+}
+
+template <class SM, int BM, int BN, int WM, int WN, int MINW, int PF, bool SWZ = false>
 int launch_fwd_x6(const ConvBatch& b, int total, bool vec, bool ws, hipStream_t stream) {
     constexpr int NT = (BM / WM) * (BN / WN) * 64;
     if (vec && ws)
-        hipLaunchKernelGGL((conv_fwd_x6_kernel<BM, BN, WM, WN, true, true, MINW, PF, SWZ>), dim3(total), dim3(NT), 0, stream, b);
+        hipLaunchKernelGGL((conv_fwd_x6_kernel<SM, BM, BN, WM, WN, true, true, MINW, PF, SWZ>), dim3(total), dim3(NT), 0, stream, b);
     else if (vec)
-        hipLaunchKernelGGL((conv_fwd_x6_kernel<BM, BN, WM, WN, true, false, MINW, PF, SWZ>), dim3(total), dim3(NT), 0, stream, b);
+        hipLaunchKernelGGL((conv_fwd_x6_kernel<SM, BM, BN, WM, WN, true, false, MINW, PF, SWZ>), dim3(total), dim3(NT), 0, stream, b);
     else if (ws)
-        hipLaunchKernelGGL((conv_fwd_x6_kernel<BM, BN, WM, WN, false, true, MINW, PF, SWZ>), dim3(total), dim3(NT), 0, stream, b);
+        hipLaunchKernelGGL((conv_fwd_x6_kernel<SM, BM, BN, WM, WN, false, true, MINW, PF, SWZ>), dim3(total), dim3(NT), 0, stream, b);
     else
-        hipLaunchKernelGGL((conv_fwd_x6_kernel<BM, BN, WM, WN, false, false, MINW, PF, SWZ>), dim3(total), dim3(NT), 0, stream, b);
+        hipLaunchKernelGGL((conv_fwd_x6_kernel<SM, BM, BN, WM, WN, false, false, MINW, PF, SWZ>), dim3(total), dim3(NT), 0, stream, b);
     return fg::launched("conv_fwd_x6");
 }
 
@@ -1019,36 +1158,35 @@ int launch_fwd(const ConvBatch& b, int total, bool vec, hipStream_t stream) {
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
-template <int BA, int BKC, int WA, int WK, int MINW>
+template <class SM, int BA, int BKC, int WA, int WK, int MINW>
 int launch_wgrad_x6(const fg_wgrad_problem& p, bool vx, bool vp, hipStream_t stream) {
     constexpr int NT = (BA / WA) * (BKC / WK) * 64;
     const int K = p.kh * p.j_valid;
     const int ta = (p.n_a + BA - 1) / BA, tk = (K + BKC - 1) / BKC;
     dim3 g(ta * tk * p.splits), blk(NT);
     if (vx && vp)
-        hipLaunchKernelGGL((conv_wgrad_x6_kernel<BA, BKC, WA, WK, true, true, MINW>), g, blk, 0, stream, p, ta, tk);
+        hipLaunchKernelGGL((conv_wgrad_x6_kernel<SM, BA, BKC, WA, WK, true, true, MINW>), g, blk, 0, stream, p, ta, tk);
     else if (vx)
-        hipLaunchKernelGGL((conv_wgrad_x6_kernel<BA, BKC, WA, WK, true, false, MINW>), g, blk, 0, stream, p, ta, tk);
+        hipLaunchKernelGGL((conv_wgrad_x6_kernel<SM, BA, BKC, WA, WK, true, false, MINW>), g, blk, 0, stream, p, ta, tk);
     else if (vp)
-        hipLaunchKernelGGL((conv_wgrad_x6_kernel<BA, BKC, WA, WK, false, true, MINW>), g, blk, 0, stream, p, ta, tk);
+        hipLaunchKernelGGL((conv_wgrad_x6_kernel<SM, BA, BKC, WA, WK, false, true, MINW>), g, blk, 0, stream, p, ta, tk);
     else
-        hipLaunchKernelGGL((conv_wgrad_x6_kernel<BA, BKC, WA, WK, false, false, MINW>), g, blk, 0, stream, p, ta, tk);
+        hipLaunchKernelGGL((conv_wgrad_x6_kernel<SM, BA, BKC, WA, WK, false, false, MINW>), g, blk, 0, stream, p, ta, tk);
     return fg::launched("conv_wgrad_x6");
 }
 
 int g_wgrad_tile = -1;   // tuning hook (fg_set_wgrad_tile)
 
-int launch_wgrad_x6_cfg(int cfg, const fg_wgrad_problem& p, bool vx, bool vp, hipStream_t stream) {
+template <class SM>
+int launch_wgrad_split_cfg(int cfg, const fg_wgrad_problem& p, bool vx, bool vp, hipStream_t stream) {
     switch (cfg) {
-        case 0: return launch_wgrad_x6<128, 128, 64, 64, 3>(p, vx, vp, stream);
-        case 1: return launch_wgrad_x6<256, 128, 64, 64, 4>(p, vx, vp, stream);
-        case 2: return launch_wgrad_x6<128, 256, 64, 64, 4>(p, vx, vp, stream);
-        case 3: return launch_wgrad_x6<64, 256, 64, 64, 3>(p, vx, vp, stream);
-        case 4: return launch_wgrad_x6<32, 256, 32, 64, 3>(p, vx, vp, stream);
-        default: return launch_wgrad_x6<32, 512, 32, 64, 2>(p, vx, vp, stream);
+        case 0: return launch_wgrad_x6<SM, 128, 128, 64, 64, 3>(p, vx, vp, stream);
+        case 1: return launch_wgrad_x6<SM, 256, 128, 64, 64, 4>(p, vx, vp, stream);
+        case 2: return launch_wgrad_x6<SM, 64, 256, 64, 64, 3>(p, vx, vp, stream);
+        default: return launch_wgrad_x6<SM, 32, 256, 32, 64, 3>(p, vx, vp, stream);
     }
 }
-constexpr int kWgradTiles = 6;
+constexpr int kWgradTiles = 4;
 
 template <int BA, int BKC, int WA, int WK>
 int launch_wgrad(const fg_wgrad_problem& p, bool vx, bool vp, hipStream_t stream) {
@@ -1070,28 +1208,21 @@ int launch_wgrad(const fg_wgrad_problem& p, bool vx, bool vp, hipStream_t stream
 
 int g_fwd_tile = -1;   // tuning hook (fg_set_fwd_tile): force one bf16x6 forward tile config
 
-// bf16x6 forward tile configs {BM, BN, wave tile, prefetch distance}: index = g_fwd_tile
-int launch_fwd_x6_cfg(int cfg, const ConvBatch& b, int total, bool vec, bool ws, hipStream_t stream) {
+// split-math forward tile configs {BM, BN, wave tile, waves/SIMD, prefetch distance, LDS swizzle}
+template <class SM>
+int launch_fwd_split_cfg(int cfg, const ConvBatch& b, int total, bool vec, bool ws, hipStream_t stream) {
     switch (cfg) {
-        case 0: return launch_fwd_x6<128, 128, 64, 64, 2, 1>(b, total, vec, ws, stream);
-        case 1: return launch_fwd_x6<128, 128, 64, 64, 2, 2>(b, total, vec, ws, stream);
-        case 2: return launch_fwd_x6<256, 128, 64, 64, 2, 2>(b, total, vec, ws, stream);
-        case 3: return launch_fwd_x6<128, 64, 32, 64, 2, 1>(b, total, vec, ws, stream);
-        case 4: return launch_fwd_x6<128, 64, 32, 64, 2, 2>(b, total, vec, ws, stream);
-        case 5: return launch_fwd_x6<128, 32, 32, 32, 2, 1>(b, total, vec, ws, stream);
-        case 6: return launch_fwd_x6<128, 32, 32, 32, 2, 2>(b, total, vec, ws, stream);
-        case 7: return launch_fwd_x6<256, 64, 32, 64, 2, 2>(b, total, vec, ws, stream);
-        case 8: return launch_fwd_x6<128, 128, 64, 64, 3, 1, true>(b, total, vec, ws, stream);
-        case 9: return launch_fwd_x6<256, 128, 64, 64, 2, 1, true>(b, total, vec, ws, stream);
-        case 10: return launch_fwd_x6<128, 64, 32, 64, 3, 1, true>(b, total, vec, ws, stream);
-        case 11: return launch_fwd_x6<128, 32, 32, 32, 4, 1, true>(b, total, vec, ws, stream);
-        case 12: return launch_fwd_x6<256, 256, 128, 64, 2, 1, true>(b, total, vec, ws, stream);
-        default: return launch_fwd_x6<128, 256, 64, 64, 2, 1, true>(b, total, vec, ws, stream);
+        case 0: return launch_fwd_x6<SM, 128, 256, 64, 64, 2, 1, true>(b, total, vec, ws, stream);
+        case 1: return launch_fwd_x6<SM, 256, 128, 64, 64, 2, 1, true>(b, total, vec, ws, stream);
+        case 2: return launch_fwd_x6<SM, 128, 64, 32, 64, 3, 1, true>(b, total, vec, ws, stream);
+        case 3: return launch_fwd_x6<SM, 128, 32, 32, 32, 2, 2, false>(b, total, vec, ws, stream);
+        case 4: return launch_fwd_x6<SM, 128, 128, 64, 64, 3, 1, true>(b, total, vec, ws, stream);
+        default: return launch_fwd_x6<SM, 128, 32, 32, 32, 4, 1, true>(b, total, vec, ws, stream);
     }
 }
-constexpr int kFwdTiles = 14;
-constexpr int kFwdTileBM[kFwdTiles] = {128, 128, 256, 128, 128, 128, 128, 256, 128, 256, 128, 128, 256, 128};
-constexpr int kFwdTileBN[kFwdTiles] = {128, 128, 128, 64, 64, 32, 32, 64, 128, 128, 64, 32, 256, 256};
+constexpr int kFwdTiles = 6;
+constexpr int kFwdTileBM[kFwdTiles] = {128, 256, 128, 128, 128, 128};
+constexpr int kFwdTileBN[kFwdTiles] = {256, 128, 64, 32, 128, 32};
 
 }  // namespace
 
@@ -1112,17 +1243,21 @@ FG_API int fg_conv_fwd(const fg_conv_problem* probs, int nprob, hipStream_t stre
                             p.m_img, p.m_a, p.m_b, p.kh, p.j_valid, p.jp, p.n_out, p.ldw);
         if ((long long)p.m_img * p.m_a * p.m_b >= (1LL << 31))
             return fg::fail(FG_ERR_INVALID, "fg_conv_fwd: too many rows");
-        if (p.w_split != ws || (ws != 0 && ws != 1))
-            return fg::fail(FG_ERR_INVALID, "fg_conv_fwd: w_split must be 0 or 1 and equal across problems");
+        if (p.w_split != ws || ws < 0 || ws > 2)
+            return fg::fail(FG_ERR_INVALID, "fg_conv_fwd: w_split must be 0, 1 or 2 and equal across problems");
+        if ((g_conv_math & FG_MATH_FWD_F16X3) && (!p.x_absmax || !p.w_absmax))
+            return fg::fail(FG_ERR_INVALID, "fg_conv_fwd: the f16x3 math needs x_absmax and w_absmax (problem %d)", i);
         if (!aligned16(p.x) || (p.sxn | p.sxa | p.sxb | p.sxr) % 4 || p.j_valid % 4) vec = false;
         if (p.n_out > max_n) max_n = p.n_out;
         b.p[i] = p;
     }
-    const bool x6 = (g_conv_math & FG_MATH_FWD_X6) != 0;
-    if (ws && !x6)
-        return fg::fail(FG_ERR_INVALID, "fg_conv_fwd: pre-split weights need the bf16x6 forward math");
+    const bool f16 = (g_conv_math & FG_MATH_FWD_F16X3) != 0;
+    const bool x6 = f16 || (g_conv_math & FG_MATH_FWD_X6) != 0;   // a split-math kernel
+    if ((ws == 1 && (!x6 || f16)) || (ws == 2 && !f16))
+        return fg::fail(FG_ERR_INVALID, "fg_conv_fwd: pre-split weights (w_split=%d) do not match the conv math %d",
+                        ws, g_conv_math);
     if (x6) {
-        // the bf16x6 kernels address operands with 31-bit buffer offsets: split oversized
+        // the split-math kernels address operands with 31-bit buffer offsets: split oversized
         // problems over images (each chunk launched on its own)
         constexpr long long kLim = (1LL << 31) - 256;
         bool fits = true;
@@ -1131,7 +1266,7 @@ FG_API int fg_conv_fwd(const fg_conv_problem* probs, int nprob, hipStream_t stre
             const long long tail = (long long)(p.m_a - 1) * p.sxa + (long long)(p.m_b - 1) * p.sxb +
                                    (long long)(p.kh - 1) * p.sxr + p.jp;
             const long long ext = 4 * ((long long)(p.m_img - 1) * p.sxn + tail);
-            const long long wext = (long long)p.n_out * p.ldw * (ws ? 6 : 4);
+            const long long wext = (long long)p.n_out * p.ldw * (ws == 1 ? 6 : 4);
             if (wext > kLim || 4 * tail > kLim || p.sxn < 0 || p.sxa < 0 || p.sxb < 0 || p.sxr < 0)
                 return fg::fail(FG_ERR_INVALID, "fg_conv_fwd: operand extent beyond 2 GiB per image (problem %d)", i);
             if (ext > kLim) fits = false;
@@ -1155,7 +1290,7 @@ FG_API int fg_conv_fwd(const fg_conv_problem* probs, int nprob, hipStream_t stre
     }
     int cfg = -1, BM, BN;
     if (x6) {
-        cfg = g_fwd_tile >= 0 ? g_fwd_tile : (max_n > 128 ? 13 : max_n > 64 ? 9 : max_n > 32 ? 10 : 6);
+        cfg = g_fwd_tile >= 0 ? g_fwd_tile : (max_n > 128 ? 0 : max_n > 64 ? 1 : max_n > 32 ? 2 : 3);
         BM = kFwdTileBM[cfg];
         BN = kFwdTileBN[cfg];
     } else if (max_n > 64) { BM = 128; BN = 128; }
@@ -1172,7 +1307,8 @@ FG_API int fg_conv_fwd(const fg_conv_problem* probs, int nprob, hipStream_t stre
     b.blk_start[nprob] = total;
     b.blk_start[4] = total;
     if (total == 0) return 0;
-    if (x6) return launch_fwd_x6_cfg(cfg, b, total, vec, ws != 0, stream);
+    if (f16) return launch_fwd_split_cfg<MathF16x3>(cfg, b, total, vec, ws != 0, stream);
+    if (x6) return launch_fwd_split_cfg<MathBF16x6>(cfg, b, total, vec, ws != 0, stream);
     if (BN == 128) return launch_fwd<128, 128, 64, 64>(b, total, vec, stream);
     if (BN == 64) return launch_fwd<256, 64, 64, 64>(b, total, vec, stream);
     return launch_fwd<256, 32, 64, 32>(b, total, vec, stream);
@@ -1202,7 +1338,7 @@ FG_API int fg_conv_wgrad(const fg_wgrad_problem* prob, hipStream_t stream) {
         return fg::fail(FG_ERR_INVALID, "fg_conv_wgrad: splits*m_chunk < M");
     const bool vx = aligned16(p.x) && (p.sxn | p.sxa | p.sxb | p.sxr) % 4 == 0 && p.j_valid % 4 == 0;
     const bool vp = aligned16(p.p) && (p.spn | p.spa | p.spb) % 4 == 0;
-    if (g_conv_math & FG_MATH_WGRAD_X6) {
+    if (g_conv_math & (FG_MATH_WGRAD_X6 | FG_MATH_WGRAD_F16X3)) {
         // 31-bit buffer offsets: the extent of either operand must stay below 2 GiB
         const long long pext = 4 * ((long long)(p.m_img - 1) * p.spn + (long long)(p.m_a - 1) * p.spa +
                                     (long long)(p.m_b - 1) * p.spb + p.n_a + 4);
@@ -1210,8 +1346,13 @@ FG_API int fg_conv_wgrad(const fg_wgrad_problem* prob, hipStream_t stream) {
                                     (long long)(p.m_b - 1) * p.sxb + (long long)(p.kh - 1) * p.sxr + p.j_valid + 4);
         if (pext >= (1LL << 31) - 256 || xext >= (1LL << 31) - 256 || p.spn < 0 || p.sxn < 0)
             return fg::fail(FG_ERR_INVALID, "fg_conv_wgrad: operand extent beyond 2 GiB; split the batch");
-        const int cfg = g_wgrad_tile >= 0 ? g_wgrad_tile : (p.n_a > 128 ? 1 : p.n_a > 64 ? 0 : p.n_a > 32 ? 3 : 4);
-        return launch_wgrad_x6_cfg(cfg, p, vx, vp, stream);
+        const int cfg = g_wgrad_tile >= 0 ? g_wgrad_tile : (p.n_a > 128 ? 1 : p.n_a > 64 ? 0 : p.n_a > 32 ? 2 : 3);
+        if (g_conv_math & FG_MATH_WGRAD_F16X3) {
+            if (!p.p_absmax || !p.x_absmax)
+                return fg::fail(FG_ERR_INVALID, "fg_conv_wgrad: the f16x3 math needs p_absmax and x_absmax");
+            return launch_wgrad_split_cfg<MathF16x3>(cfg, p, vx, vp, stream);
+        }
+        return launch_wgrad_split_cfg<MathBF16x6>(cfg, p, vx, vp, stream);
     }
     if (p.n_a > 64) return launch_wgrad<128, 128, 64, 64>(p, vx, vp, stream);
     if (p.n_a > 32) return launch_wgrad<64, 256, 64, 64>(p, vx, vp, stream);
@@ -1251,8 +1392,31 @@ FG_API int fg_pack_weight_split(const float* w, const fg_weight_map* map, void* 
     return fg::launched("pack_weight_split");
 }
 
+FG_API int fg_pack_weight_f16(const float* w, const fg_weight_map* map, const float* w_absmax, void* wps,
+                              hipStream_t stream) {
+    if (!w || !map || !wps || !w_absmax || !aligned16(wps))
+        return fg::fail(FG_ERR_INVALID, "fg_pack_weight_f16: null/unaligned");
+    if (map->kh > 8 || map->kw > 8 || map->jp % BK || map->jp < map->kw * map->c || map->c < 1)
+        return fg::fail(FG_ERR_INVALID, "fg_pack_weight_f16: bad map kh=%d kw=%d c=%d jp=%d", map->kh, map->kw,
+                        map->c, map->jp);
+    const long long total = (long long)map->n_out * map->kh * map->jp / 8;
+    hipLaunchKernelGGL(pack_weight_f16_kernel, dim3(fg::blocks_for(total, 256, 8192)), dim3(256), 0, stream, w, *map,
+                       w_absmax, reinterpret_cast<f16x8*>(wps));
+    return fg::launched("pack_weight_f16");
+}
+
+FG_API int fg_absmax(const float* x, long long n, float* out, hipStream_t stream) {
+    if (!x || !out || n < 0) return fg::fail(FG_ERR_INVALID, "fg_absmax: bad args");
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(absmax_kernel, dim3(fg::blocks_for((n + 3) / 4, 256, 2048)), dim3(256), 0, stream, x, n,
+                       reinterpret_cast<unsigned*>(out));
+    return fg::launched("absmax");
+}
+
 FG_API int fg_set_conv_math(int mode) {
-    if (mode < 0 || mode > (FG_MATH_FWD_X6 | FG_MATH_WGRAD_X6))
+    const int fwd = mode & (FG_MATH_FWD_X6 | FG_MATH_FWD_F16X3), wg = mode & (FG_MATH_WGRAD_X6 | FG_MATH_WGRAD_F16X3);
+    if (mode < 0 || mode > FG_MATH_F16X3 || fwd == (FG_MATH_FWD_X6 | FG_MATH_FWD_F16X3) ||
+        wg == (FG_MATH_WGRAD_X6 | FG_MATH_WGRAD_F16X3))
         return fg::fail(FG_ERR_INVALID, "fg_set_conv_math: %d", mode);
     g_conv_math = mode;
     return 0;

@@ -9,6 +9,22 @@
 
 namespace {
 
+// fold this thread's max |v| (as uint bits) into the absmax slot: block max, then one atomic
+// per block into shard blockIdx % FG_AMAX_SHARDS (256-thread blocks)
+__device__ __forceinline__ void absmax_flush(unsigned m, unsigned* out) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, off));
+    __shared__ unsigned red[4];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0)
+        atomicMax(out + (blockIdx.x & (FG_AMAX_SHARDS - 1)), max(max(red[0], red[1]), max(red[2], red[3])));
+}
+__device__ __forceinline__ unsigned absbits4(const f32x4& v) {
+    return max(max(__float_as_uint(v[0]) & 0x7fffffffu, __float_as_uint(v[1]) & 0x7fffffffu),
+               max(__float_as_uint(v[2]) & 0x7fffffffu, __float_as_uint(v[3]) & 0x7fffffffu));
+}
+
 constexpr int NT = 256;
 constexpr int MAX_CHUNKS = 256;
 
@@ -81,7 +97,8 @@ __global__ void in_finalize_kernel(fg_view src, int chunks, const double* __rest
 }
 
 __global__ void in_apply_kernel(fg_view src, const float* __restrict__ mean, const float* __restrict__ rstd,
-                                int act, fg_view res, fg_view dst, int pad_mode) {
+                                int act, fg_view res, fg_view dst, int pad_mode, unsigned* __restrict__ amax) {
+    unsigned am = 0;
     const int C = dst.c_alloc, C4 = C / 4;
     const int hp = dst.h + 2 * dst.pad, wp = dst.w + 2 * dst.pad;
     const long long total = (long long)dst.n * hp * wp * C4;
@@ -106,8 +123,10 @@ __global__ void in_apply_kernel(fg_view src, const float* __restrict__ mean, con
             for (int e = 0; e < 4; ++e) v[e] = fg::act_fwd(v[e], act);
             if (res.ptr) v += ld4(res.ptr + fg::vidx(res, n, y, x) + 4 * c4);
         }
+        am = max(am, absbits4(v));
         *reinterpret_cast<f32x4*>(dst.ptr + ((size_t)(n * hp + yp) * wp + xp) * C + 4 * c4) = v;
     }
+    if (amax) absmax_flush(am, amax);
 }
 
 // ---- backward ----
@@ -213,7 +232,8 @@ __global__ void in_bwd_bias_kernel(int N, int C, const double* __restrict__ bpar
 
 __global__ void in_bwd_apply_kernel(fg_view g, int fp, fg_view gadd, fg_view src, const float* __restrict__ mean,
                                     const float* __restrict__ rstd, const float* __restrict__ coef, int act,
-                                    fg_view dst) {
+                                    fg_view dst, unsigned* __restrict__ amax) {
+    unsigned am = 0;
     const int C = dst.c_alloc, C4 = C / 4;
     const int h = dst.h, w = dst.w;
     const int hp = h + 2 * dst.pad, wp = w + 2 * dst.pad;
@@ -239,8 +259,10 @@ __global__ void in_bwd_apply_kernel(fg_view g, int fp, fg_view gadd, fg_view src
                 out[e] = r[e] * (gp - coef[(nc + e) * 2] - xh[e] * coef[(nc + e) * 2 + 1]);
             }
         }
+        am = max(am, absbits4(out));
         *reinterpret_cast<f32x4*>(dst.ptr + ((size_t)(n * hp + yp) * wp + xp) * C + 4 * c4) = out;
     }
+    if (amax) absmax_flush(am, amax);
 }
 
 __global__ void act_bwd_kernel(fg_view g, fg_view y, int act) {
@@ -376,7 +398,7 @@ FG_API int fg_in_stats(fg_view src, float eps, float* mean, float* rstd, double*
 }
 
 FG_API int fg_in_apply(fg_view src, const float* mean, const float* rstd, int act, fg_view residual, fg_view dst,
-                       int pad_mode, hipStream_t stream) {
+                       int pad_mode, float* absmax, hipStream_t stream) {
     if (!ok_view(src) || !ok_view(dst) || !mean || !rstd || src.c_alloc % 4 || dst.c_alloc != src.c_alloc ||
         dst.h != src.h || dst.w != src.w || dst.n != src.n)
         return fg::fail(FG_ERR_INVALID, "fg_in_apply: bad args");
@@ -385,13 +407,13 @@ FG_API int fg_in_apply(fg_view src, const float* mean, const float* rstd, int ac
     if (pad_mode == FG_PAD_REFLECT && (dst.pad >= dst.h || dst.pad >= dst.w))
         return fg::fail(FG_ERR_INVALID, "fg_in_apply: reflect pad too large");
     const long long total = (long long)dst.n * (dst.h + 2 * dst.pad) * (dst.w + 2 * dst.pad) * (dst.c_alloc / 4);
-    hipLaunchKernelGGL(in_apply_kernel, dim3(fg::blocks_for(total, 256, 16384)), dim3(256), 0, stream, src, mean,
-                       rstd, act, residual, dst, pad_mode);
+    hipLaunchKernelGGL(in_apply_kernel, dim3(fg::blocks_for(total, 256, 4096)), dim3(256), 0, stream, src, mean,
+                       rstd, act, residual, dst, pad_mode, reinterpret_cast<unsigned*>(absmax));
     return fg::launched("in_apply");
 }
 
 FG_API int fg_in_bwd(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, const float* mean, const float* rstd,
-                     int act, fg_view dst, float* bias_grad, double* work, hipStream_t stream) {
+                     int act, fg_view dst, float* bias_grad, double* work, float* absmax, hipStream_t stream) {
     if (!ok_view(gsrc) || !ok_view(src) || !ok_view(dst) || !mean || !rstd || !work || src.c_alloc % 4 ||
         (NT % (src.c_alloc / 4)) != 0 || gsrc.c_alloc != src.c_alloc || dst.c_alloc != src.c_alloc ||
         dst.h != src.h || dst.w != src.w || dst.n != src.n)
@@ -422,8 +444,8 @@ FG_API int fg_in_bwd(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, cons
         if (e) return e;
     }
     const long long total = (long long)dst.n * (dst.h + 2 * dst.pad) * (dst.w + 2 * dst.pad) * (C / 4);
-    hipLaunchKernelGGL(in_bwd_apply_kernel, dim3(fg::blocks_for(total, 256, 16384)), dim3(256), 0, stream, gsrc,
-                       fold_pad, gadd, src, mean, rstd, coef, act, dst);
+    hipLaunchKernelGGL(in_bwd_apply_kernel, dim3(fg::blocks_for(total, 256, 4096)), dim3(256), 0, stream, gsrc,
+                       fold_pad, gadd, src, mean, rstd, coef, act, dst, reinterpret_cast<unsigned*>(absmax));
     return fg::launched("in_bwd_apply");
 }
 

@@ -15,7 +15,9 @@ LIB_PATH = os.environ.get("FLOODGAN_LIB", os.path.join(_HERE, "lib", "libfloodga
 FG_PAD_ZERO, FG_PAD_REFLECT = 0, 1
 FG_ACT_NONE, FG_ACT_RELU, FG_ACT_LRELU = 0, 1, 2
 FG_MATH_FP32, FG_MATH_FWD_X6, FG_MATH_WGRAD_X6, FG_MATH_BF16X6 = 0, 1, 2, 3
-CONV_MATH = {"fp32": FG_MATH_FP32, "fwd_x6": FG_MATH_FWD_X6, "wgrad_x6": FG_MATH_WGRAD_X6, "bf16x6": FG_MATH_BF16X6}
+FG_MATH_FWD_F16X3, FG_MATH_WGRAD_F16X3, FG_MATH_F16X3 = 4, 8, 12
+CONV_MATH = {"fp32": FG_MATH_FP32, "fwd_x6": FG_MATH_FWD_X6, "wgrad_x6": FG_MATH_WGRAD_X6, "bf16x6": FG_MATH_BF16X6,
+             "fwd_f16x3": FG_MATH_FWD_F16X3, "wgrad_f16x3": FG_MATH_WGRAD_F16X3, "f16x3": FG_MATH_F16X3}
 
 
 class fg_view(C.Structure):
@@ -35,7 +37,7 @@ class fg_conv_problem(C.Structure):
                 ("m_img", C.c_int), ("m_a", C.c_int), ("m_b", C.c_int),
                 ("kh", C.c_int), ("j_valid", C.c_int), ("jp", C.c_int),
                 ("n_out", C.c_int), ("ldw", C.c_int), ("act", C.c_int), ("accumulate", C.c_int),
-                ("w_split", C.c_int)]
+                ("w_split", C.c_int), ("x_absmax", C.c_void_p), ("w_absmax", C.c_void_p)]
 
 
 class fg_wgrad_problem(C.Structure):
@@ -44,7 +46,7 @@ class fg_wgrad_problem(C.Structure):
                 ("sxn", C.c_longlong), ("sxa", C.c_longlong), ("sxb", C.c_longlong), ("sxr", C.c_longlong),
                 ("m_img", C.c_int), ("m_a", C.c_int), ("m_b", C.c_int),
                 ("n_a", C.c_int), ("kh", C.c_int), ("j_valid", C.c_int),
-                ("splits", C.c_int), ("m_chunk", C.c_int)]
+                ("splits", C.c_int), ("m_chunk", C.c_int), ("p_absmax", C.c_void_p), ("x_absmax", C.c_void_p)]
 
 
 class fg_weight_map(C.Structure):
@@ -73,14 +75,16 @@ SIGNATURES = {
     "fg_wgrad_reduce": [C.c_void_p, C.c_int, C.POINTER(fg_weight_map), C.c_void_p, C.c_int, C.c_void_p],
     "fg_pack_weight": [C.c_void_p, C.POINTER(fg_weight_map), C.c_void_p, C.c_void_p],
     "fg_pack_weight_split": [C.c_void_p, C.POINTER(fg_weight_map), C.c_void_p, C.c_void_p],
+    "fg_pack_weight_f16": [C.c_void_p, C.POINTER(fg_weight_map), C.c_void_p, C.c_void_p, C.c_void_p],
+    "fg_absmax": [C.c_void_p, C.c_longlong, C.c_void_p, C.c_void_p],
     "fg_pack_input": [fg_sview, C.c_int, fg_sview, C.c_int, fg_view, C.c_int, C.c_int, C.c_int, C.c_void_p],
     "fg_zero_border": [fg_view, C.c_void_p],
     "fg_fold_add": [fg_view, C.c_int, fg_view, fg_view, C.c_void_p],
     "fg_in_workspace_doubles": [C.c_int, C.c_int],
     "fg_in_stats": [fg_view, C.c_float, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p],
-    "fg_in_apply": [fg_view, C.c_void_p, C.c_void_p, C.c_int, fg_view, fg_view, C.c_int, C.c_void_p],
+    "fg_in_apply": [fg_view, C.c_void_p, C.c_void_p, C.c_int, fg_view, fg_view, C.c_int, C.c_void_p, C.c_void_p],
     "fg_in_bwd": [fg_view, C.c_int, fg_view, fg_view, C.c_void_p, C.c_void_p, C.c_int, fg_view, C.c_void_p,
-                  C.c_void_p, C.c_void_p],
+                  C.c_void_p, C.c_void_p, C.c_void_p],
     "fg_act_bwd": [fg_view, fg_view, C.c_int, C.c_void_p],
     "fg_channel_sum": [fg_view, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p],
     "fg_tail_fwd": [fg_view, fg_view, fg_sview, C.c_void_p, C.c_void_p, C.c_void_p],
@@ -127,6 +131,15 @@ def set_conv_math(mode):
 def fwd_x6():
     """True when the forward / input-gradient convs run the bf16x6 kernels (pre-split weights)."""
     return bool(load().fg_get_conv_math() & FG_MATH_FWD_X6)
+
+
+def fwd_f16x3():
+    """True when the forward / input-gradient convs run the f16x3 kernels."""
+    return bool(load().fg_get_conv_math() & FG_MATH_FWD_F16X3)
+
+
+def wgrad_f16x3():
+    return bool(load().fg_get_conv_math() & FG_MATH_WGRAD_F16X3)
 
 
 def set_fwd_tile(cfg):

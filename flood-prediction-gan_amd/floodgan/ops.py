@@ -53,16 +53,93 @@ def wmap_struct(m):
 
 # ------------------------------------------------------------------ conv engine
 
+# ------------------------------------------------------------------ f16x3 operand scales
+#
+# The f16x3 conv math scales each operand by a power of two derived from a device scalar >=
+# max |operand|.  Those scalars live in slots of a zero-initialised pool (one fill per 4096
+# slots).  Producers that already touch every element (IN apply / backward) raise their
+# output's slot for free; otherwise the conv computes one with fg_absmax.  The slot is cached
+# on the tensor object and dropped by every op that writes that tensor (a stale slot is only
+# safe while it still bounds the contents).
+
+
+SHARDS = 64     # FG_AMAX_SHARDS: floats per absmax slot
+
+
+class _SlotPool:
+    SIZE = 4096     # slots per zero-filled pool
+
+    def __init__(self):
+        self.t, self.i = None, 0
+
+    def take(self, device):
+        if self.t is None or self.i >= self.SIZE or self.t.device != torch.device(device):
+            self.t, self.i = torch.zeros(self.SIZE * SHARDS, dtype=torch.float32, device=device), 0
+        self.i += 1
+        return self.t[(self.i - 1) * SHARDS:self.i * SHARDS]
+
+
+_SLOTS = _SlotPool()
+
+
+def _tensor(obj):
+    return obj.t if isinstance(obj, Buf) else obj
+
+
+def _wrote(*objs):
+    """an op wrote these buffers: forget their cached absmax slots"""
+    for o in objs:
+        if o is not None:
+            t = _tensor(o)
+            if getattr(t, "_fg_amax", None) is not None:
+                t._fg_amax = None
+
+
+def absmax(t):
+    """Device scalar >= max |t| (the f16x3 operand-scale source), over the whole storage of a
+    tensor or of a Buf (border and padding channels included: everything a gather can read);
+    cached on the tensor until an op writes it."""
+    t = _tensor(t)
+    cached = getattr(t, "_fg_amax", None)
+    if cached is not None:
+        return cached
+    out = _SLOTS.take(t.device)
+    L.check(_lib().fg_absmax(L.ptr(t), t.numel(), L.ptr(out), L.stream_handle()), "absmax")
+    t._fg_amax = out
+    return out
+
+
+def _amax_out(dst):
+    """slot for a producer to raise to max |dst| (f16x3 only), recorded on dst"""
+    if not L.fwd_f16x3() and not L.wgrad_f16x3():
+        _wrote(dst)
+        return None
+    slot = _SLOTS.take(_dev(dst))
+    _tensor(dst)._fg_amax = slot
+    return slot
+
+
 def pack_weight(w, m, split=None):
-    """Packed weight for the conv engine: fp32 [n][kh*jp], or (split, the default under the
-    bf16x6 forward math) the pre-split bf16 h/m/l layout of fg_pack_weight_split, returned as a
-    bfloat16 tensor (conv problems built on it carry w_split = 1)."""
+    """Packed weight for the conv engine: fp32 [n][kh*jp]; or, by default under a split forward
+    math, the pre-split layout -- bf16 h/m/l pieces (bf16x6, fg_pack_weight_split) or scaled fp16
+    h/l pieces (f16x3, fg_pack_weight_f16; the tensor carries its scale source as `.absmax`).
+    Conv problems built on it carry w_split = 1 or 2 accordingly."""
     L.require_device(w, "weight")
     w = w.contiguous()
     s = wmap_struct(m)
     if split is None:
-        split = L.fwd_x6()
-    if split:
+        split = "f16x3" if L.fwd_f16x3() else ("bf16x6" if L.fwd_x6() else None)
+    elif split is True:
+        split = "f16x3" if L.fwd_f16x3() else "bf16x6"
+    if split == "f16x3":
+        amax = _SLOTS.take(w.device)        # weights change every step: never cached
+        L.check(_lib().fg_absmax(L.ptr(w), w.numel(), L.ptr(amax), L.stream_handle()), "absmax")
+        wp = torch.empty(2 * packed_numel(m), dtype=torch.float16, device=w.device)
+        L.check(_lib().fg_pack_weight_f16(L.ptr(w), C.byref(s), L.ptr(amax), L.ptr(wp), L.stream_handle()),
+                "pack_weight_f16")
+        wp.absmax = amax
+        return wp
+    if split == "bf16x6":
         wp = torch.empty(3 * packed_numel(m), dtype=torch.bfloat16, device=w.device)
         L.check(_lib().fg_pack_weight_split(L.ptr(w), C.byref(s), L.ptr(wp), L.stream_handle()), "pack_weight_split")
         return wp
@@ -114,14 +191,31 @@ def conv(probs, tag=None):
 
 def _conv(probs):
     arr = (L.fg_conv_problem * len(probs))()
+    f16 = L.fwd_f16x3()
+    keep = {}
     for i, p in enumerate(probs):
         s = arr[i]
         s.x, s.w, s.y = _addr(p["x"]), _addr(p["w"]), _addr(p["y"])
-        s.w_split = int(p["w"][0].dtype == torch.bfloat16)
+        wt = p["w"][0]
+        s.w_split = {torch.bfloat16: 1, torch.float16: 2}.get(wt.dtype, 0)
         s.bias = p["bias"].data_ptr() if p["bias"] is not None else None
         for k in _CONV_FIELDS:
             setattr(s, k, int(p[k]))
+        if f16:
+            xb = p["x"][0]
+            if id(xb) not in keep:
+                keep[id(xb)] = absmax(xb)
+            s.x_absmax = keep[id(xb)].data_ptr()
+            wa = getattr(wt, "absmax", None)
+            if wa is None:              # fp32 weights split on the fly: scale from their own max
+                if ("w", id(wt)) not in keep:
+                    keep[("w", id(wt))] = _SLOTS.take(wt.device)
+                    L.check(_lib().fg_absmax(L.ptr(wt), wt.numel(), L.ptr(keep[("w", id(wt))]),
+                                             L.stream_handle()), "absmax")
+                wa = keep[("w", id(wt))]
+            s.w_absmax = wa.data_ptr()
     L.check(_lib().fg_conv_fwd(arr, len(probs), L.stream_handle()), "conv_fwd")
+    _wrote(*[p["y"][0] for p in probs])
 
 
 _WG_FIELDS = ("spn", "spa", "spb", "sxn", "sxa", "sxb", "sxr", "m_img", "m_a", "m_b", "n_a", "kh", "j_valid",
@@ -136,6 +230,9 @@ def wgrad(prob, wmap, dw, accumulate=False):
     s.p, s.x, s.out = _addr(prob["p"]), _addr(prob["x"]), slab.data_ptr()
     for k in _WG_FIELDS:
         setattr(s, k, int(prob[k]))
+    if L.wgrad_f16x3():
+        pa, xa = absmax(prob["p"][0]), absmax(prob["x"][0])
+        s.p_absmax, s.x_absmax = pa.data_ptr(), xa.data_ptr()
     st = L.stream_handle()
     L.check(_lib().fg_conv_wgrad(C.byref(s), st), "conv_wgrad")
     m = wmap_struct(wmap)
@@ -146,15 +243,18 @@ def wgrad(prob, wmap, dw, accumulate=False):
 # ------------------------------------------------------------------ layout
 
 def pack_input(a, ca, b, cb, dst, img0, nimg, pad_mode):
+    _wrote(dst)
     L.check(_lib().fg_pack_input(sview(a), ca, sview(b), cb, view(dst), img0, nimg, pad_mode, L.stream_handle()),
             "pack_input")
 
 
 def zero_border(B):
+    _wrote(B)
     L.check(_lib().fg_zero_border(view(B), L.stream_handle()), "zero_border")
 
 
 def fold_add(gpad, fold_pad, add, dst):
+    _wrote(dst)
     L.check(_lib().fg_fold_add(view(gpad), fold_pad, view(add), view(dst), L.stream_handle()), "fold_add")
 
 
@@ -175,16 +275,17 @@ def in_stats(src):
 
 def in_apply(src, mean, rstd, act, residual, dst, pad_mode):
     L.check(_lib().fg_in_apply(view(src), L.ptr(mean), L.ptr(rstd), act, view(residual), view(dst), pad_mode,
-                               L.stream_handle()), "in_apply")
+                               L.ptr(_amax_out(dst)), L.stream_handle()), "in_apply")
 
 
 def in_bwd(gsrc, fold_pad, gadd, src, mean, rstd, act, dst, bias_grad=None):
     L.check(_lib().fg_in_bwd(view(gsrc), fold_pad, view(gadd), view(src), L.ptr(mean), L.ptr(rstd), act, view(dst),
-                             L.ptr(bias_grad), L.ptr(_work(src.n, src.c, src.t.device)), L.stream_handle()),
-            "in_bwd")
+                             L.ptr(bias_grad), L.ptr(_work(src.n, src.c, src.t.device)), L.ptr(_amax_out(dst)),
+                             L.stream_handle()), "in_bwd")
 
 
 def act_bwd(g, y, act):
+    # in place g *= act'(y) with act' in {0, 0.2, 1}: |g| cannot grow, a cached absmax stays valid
     L.check(_lib().fg_act_bwd(view(g), view(y), act, L.stream_handle()), "act_bwd")
 
 
@@ -197,10 +298,12 @@ def channel_sum(src, c_valid, out, accumulate=False):
 # ------------------------------------------------------------------ tail / losses / adam
 
 def tail_fwd(cl, al, x, out, mask):
+    _wrote(out, mask)
     L.check(_lib().fg_tail_fwd(view(cl), view(al), sview(x), L.ptr(out), L.ptr(mask), L.stream_handle()), "tail_fwd")
 
 
 def tail_bwd(cl, al, x, g_out, gc, ga):
+    _wrote(gc, ga)
     L.check(_lib().fg_tail_bwd(view(cl), view(al), sview(x), sview(g_out), view(gc), view(ga), L.stream_handle()),
             "tail_bwd")
 
@@ -208,6 +311,7 @@ def tail_bwd(cl, al, x, g_out, gc, ga):
 def mse_const(p, target, gscale, loss_out, g=None):
     """loss_out[0] = mean((p - target)^2); g = gscale * dL/dp (optional)"""
     work = torch.empty(1024, dtype=torch.float64, device=p.device)
+    _wrote(g)
     L.check(_lib().fg_mse_const(L.ptr(p), p.numel(), C.c_float(target), C.c_float(gscale), L.ptr(loss_out),
                                 L.ptr(g), L.ptr(work), L.stream_handle()), "mse")
 
@@ -216,6 +320,7 @@ def l1(a, b, gscale, loss_out, g=None, accumulate=False):
     """loss_out[0] = mean|a - b| over [N,C,H,W]; g (contiguous NCHW) = gscale * dL/da"""
     N, Cc, H, W = a.shape
     work = torch.empty(1024, dtype=torch.float64, device=a.device)
+    _wrote(g)
     L.check(_lib().fg_l1(sview(a), sview(b), N, Cc, H, W, C.c_float(gscale), L.ptr(loss_out), L.ptr(g),
                          int(accumulate), L.ptr(work), L.stream_handle()), "l1")
 

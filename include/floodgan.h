@@ -30,11 +30,25 @@ extern "C" {
 enum { FG_PAD_ZERO = 0, FG_PAD_REFLECT = 1 };
 enum { FG_ACT_NONE = 0, FG_ACT_RELU = 1, FG_ACT_LRELU = 2 };   /* LeakyReLU slope 0.2 */
 enum { FG_ERR_INVALID = -1 };
-/* Convolution arithmetic, per kernel family (bit mask): fp32 MFMA (v_mfma_f32_32x32x2_f32), or
- * fp32-equivalent split-bf16 (each fp32 operand = 3 bf16 pieces, the 6 exact bf16 products of
- * order >= 2^-16 accumulated in fp32) for the forward/input-gradient kernel and/or the
- * weight-gradient kernel. */
-enum { FG_MATH_FP32 = 0, FG_MATH_FWD_X6 = 1, FG_MATH_WGRAD_X6 = 2, FG_MATH_BF16X6 = 3 };
+/* An "absmax slot" (f16x3 operand scales) is FG_AMAX_SHARDS floats whose maximum bounds the
+ * operand's |values|; writers raise one shard each (blockIdx % FG_AMAX_SHARDS) to avoid a
+ * single-address atomic hot spot.  Slots are initialised to 0 by the caller. */
+enum { FG_AMAX_SHARDS = 64 };
+/* Convolution arithmetic, per kernel family (bit mask; at most one bit per family): fp32 MFMA
+ * (v_mfma_f32_32x32x2_f32); split-bf16 "bf16x6" (each fp32 operand = 3 bf16 pieces, the 6
+ * exact bf16 products of order >= 2^-16 accumulated in fp32); or split-fp16 "f16x3" (each
+ * operand scaled by a power of two from its absolute maximum and split into 2 fp16 pieces, the
+ * 3 exact products of order >= 2^-11 accumulated in fp32) -- for the forward/input-gradient
+ * kernel and the weight-gradient kernel independently. */
+enum {
+    FG_MATH_FP32 = 0,
+    FG_MATH_FWD_X6 = 1,
+    FG_MATH_WGRAD_X6 = 2,
+    FG_MATH_BF16X6 = 3,
+    FG_MATH_FWD_F16X3 = 4,
+    FG_MATH_WGRAD_F16X3 = 8,
+    FG_MATH_F16X3 = 12
+};
 
 /* An NHWC view: interior h x w, border `pad` on every side, c_alloc channels per pixel. */
 typedef struct fg_view {
@@ -69,7 +83,10 @@ typedef struct fg_conv_problem {
     int n_out, ldw;
     int act, accumulate;
     int w_split;          /* 0: w is fp32 [n][ldw] (fg_pack_weight); 1: w is the pre-split bf16 layout
-                             of fg_pack_weight_split (bf16x6 forward kernels only)                   */
+                             of fg_pack_weight_split (bf16x6 math); 2: the pre-split fp16 layout of
+                             fg_pack_weight_f16 (f16x3 math)                                         */
+    const float* x_absmax;   /* f16x3: absmax slot bounding |x| over every element the gather reads */
+    const float* w_absmax;   /* f16x3: absmax slot bounding |w| (the one fg_pack_weight_f16 used)  */
 } fg_conv_problem;
 
 /*
@@ -86,6 +103,8 @@ typedef struct fg_wgrad_problem {
     int m_img, m_a, m_b;
     int n_a, kh, j_valid;
     int splits, m_chunk;
+    const float* p_absmax;   /* f16x3: absmax slots bounding |p|, |x| over the elements read */
+    const float* x_absmax;
 } fg_wgrad_problem;
 
 /* Maps packed-K coordinates to PyTorch weight coordinates (see fg_pack_weight). */
@@ -118,10 +137,10 @@ int fg_conv_fwd(const fg_conv_problem* probs, int nprob, hipStream_t stream);
 int fg_set_conv_math(int mode);
 int fg_get_conv_math(void);
 
-/* Tuning hook: force one bf16x6 forward tile configuration (0..7, see conv_gemm.hip), or -1 for
+/* Tuning hook: force one split-math forward tile configuration (0..5, see conv_gemm.hip), or -1 for
  * the automatic choice by output-channel count (the default). */
 int fg_set_fwd_tile(int cfg);
-/* Same for the bf16x6 weight-gradient kernel (0..5). */
+/* Same for the split-math weight-gradient kernels (0..3). */
 int fg_set_wgrad_tile(int cfg);
 
 /* Weight gradient into partial slabs (see fg_wgrad_problem). */
@@ -140,6 +159,17 @@ int fg_pack_weight(const float* w, const fg_weight_map* map, float* wp, hipStrea
  * bf16 bit patterns) with w = h + m + l exactly.  Size n_out*kh*jp*3 bf16.  Conv problems that
  * read it set w_split = 1. */
 int fg_pack_weight_split(const float* w, const fg_weight_map* map, void* wps, hipStream_t stream);
+
+/* Pre-split for the f16x3 forward kernels: w * s (s = 2^(14 - e), max(w_absmax slot) < 2^e) split into
+ * fp16 pieces h, l at wps[(n*(kh*jp/8) + q)*16 + piece*8 + e] (fp16 bit patterns).  Size
+ * n_out*kh*jp*2 fp16.  Conv problems that read it set w_split = 2 and w_absmax. */
+int fg_pack_weight_f16(const float* w, const fg_weight_map* map, const float* w_absmax, void* wps,
+                       hipStream_t stream);
+
+/* Raise the absmax slot `out` (FG_AMAX_SHARDS floats, initialised by the caller) to bound
+ * max |x[i]| over n contiguous floats (bitwise max of |x|; NaN-propagating).  The operand-
+ * scale source of the f16x3 math. */
+int fg_absmax(const float* x, long long n, float* out, hipStream_t stream);
 
 /* ---------------------------------------------------------------------------------------- */
 /* layout / padding                                                                          */
@@ -167,9 +197,10 @@ int fg_in_stats(fg_view src, float eps, float* mean, float* rstd, double* work,
 
 /* dst = act((src - mean) * rstd) (+ residual), written over dst's full padded extent with
  * pad_mode (reflect or zero border).  Replaces instance_norm + relu/leaky_relu + F.pad
- * (+ the residual add of PairedAttentionBlock). */
+ * (+ the residual add of PairedAttentionBlock).  absmax (optional absmax slot, initialised by
+ * the caller) is raised to bound |dst| -- the f16x3 scale source of the convs reading dst. */
 int fg_in_apply(fg_view src, const float* mean, const float* rstd, int act, fg_view residual,
-                fg_view dst, int pad_mode, hipStream_t stream);
+                fg_view dst, int pad_mode, float* absmax, hipStream_t stream);
 
 /* Backward of fg_in_apply.  g is read from gsrc's interior, or folded through reflect
  * padding of width fold_pad when fold_pad > 0 (gsrc then holds the gradient of the padded
@@ -177,7 +208,7 @@ int fg_in_apply(fg_view src, const float* mean, const float* rstd, int act, fg_v
  * bias_grad (optional, [c]) receives sum over n,y,x of dst = grad of the conv bias that
  * feeds this norm. */
 int fg_in_bwd(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, const float* mean,
-              const float* rstd, int act, fg_view dst, float* bias_grad, double* work,
+              const float* rstd, int act, fg_view dst, float* bias_grad, double* work, float* absmax,
               hipStream_t stream);
 
 /* g *= act'(y) in place over the interior (y = saved activation output). */

@@ -46,10 +46,10 @@ def time_it(fn, reps=10):
     return ev[0].elapsed_time(ev[1]) / reps
 
 
-def accuracy(mode):
+def accuracy(mode, xscale=1.0):
     L.set_conv_math(mode)
     torch.manual_seed(0)
-    x = torch.randn(2, 256, 24, 24, dtype=torch.float64)
+    x = torch.randn(2, 256, 24, 24, dtype=torch.float64) * xscale
     w = torch.randn(256, 256, 3, 3, dtype=torch.float64) * 0.02
     ref = F.conv2d(F.pad(x, (1,) * 4, mode="reflect"), w)
     X = Buf(torch.zeros(2, 26, 26, 256).reshape(-1), 2, 24, 24, 256, 1)
@@ -61,16 +61,27 @@ def accuracy(mode):
     ops.conv([PL.conv_problem(X, 1, 3, 1, ops.pack_weight(wd, m), m, Y)])
     torch.cuda.synchronize()
     out = Y.interior().permute(0, 3, 1, 2).cpu()
+    # weight gradient of the same conv (gy = ref's shape, random) vs fp64
+    gy64 = torch.randn(2, 256, 24, 24, dtype=torch.float64) * xscale
+    gw_ref = torch.nn.grad.conv2d_weight(F.pad(x, (1,) * 4, mode="reflect"), w.shape, gy64)
+    GY = Buf.empty(2, 24, 24, 256, 0, "cuda")
+    GY.interior().copy_(gy64.float().permute(0, 2, 3, 1))
+    dw = torch.empty_like(wd)
+    ops.wgrad(PL.wgrad_conv(GY, X, 1, 3, 1, 256), PL.wmap_wgrad(wd.shape, True, 256, 3), dw)
+    torch.cuda.synchronize()
     # fp32 CPU reference of the same conv for scale
     ref32 = F.conv2d(F.pad(x.float(), (1,) * 4, mode="reflect"), w.float())
-    return nrel(out, ref), nrel(ref32, ref)
+    return nrel(out, ref), nrel(dw, gw_ref), nrel(ref32, ref)
 
 
 def main():
     L.load()
-    for mode in (("fp32", "bf16x6") if os.environ.get("ACCURACY", "1") == "1" else ()):
-        e, e32 = accuracy(mode)
-        print(f"accuracy {mode}: rel err vs fp64 {e:.3e}  (torch CPU fp32: {e32:.3e})", flush=True)
+    modes = os.environ.get("MODES", "bf16x6,f16x3").split(",")
+    for mode in (["fp32"] + modes if os.environ.get("ACCURACY", "1") == "1" else ()):
+        for xs in (1.0, 1e-7, 1e5):
+            e, ew, e32 = accuracy(mode, xs)
+            print(f"accuracy {mode} (x scale {xs:g}): fwd rel err vs fp64 {e:.3e}, wgrad {ew:.3e} "
+                  f"(torch CPU fp32 fwd: {e32:.3e})", flush=True)
     cases = {"resblock 3x3 256->256 @128": (8, 128, 256, 256, 3, 1, 1),
              "conv2 3x3s2 64->128 @512": (8, 512, 64, 128, 3, 2, 1),
              "D model.8 4x4 256->512 @64 (2N)": (16, 64, 256, 512, 4, 1, 1),
@@ -79,7 +90,7 @@ def main():
     tiles = [int(t) for t in os.environ.get("TILES", "0,1,2,3,4,5,6,7,8").split(",")]
     for name, c in cases.items():
         mk, flops, keep = make(*c)
-        variants = [("fp32", -1, False)] + [("bf16x6", t, True) for t in tiles] + [("bf16x6", -1, False)]
+        variants = [("fp32", -1, False)] + [(md, t, True) for md in modes for t in tiles]
         res = {}
         for rep in range(2):
             for mode, tile, split in variants:
@@ -101,7 +112,7 @@ def main():
         dw = torch.empty_like(w)
         wm = PL.wmap_wgrad(w.shape, True, X.c, k)
         wtiles = [int(t) for t in os.environ.get("WTILES", "-1").split(",")]
-        wvariants = [("fp32", -1)] + [("bf16x6", t) for t in wtiles]
+        wvariants = [("fp32", -1)] + [(md, t) for md in modes for t in wtiles]
         res = {}
         for rep in range(2):
             for mode, t in wvariants:
@@ -112,12 +123,13 @@ def main():
         L.set_wgrad_tile(-1)
         ops.wgrad(wprob, wm, dw)
         ref = dw.clone()
-        L.set_conv_math("bf16x6")
-        for t in wtiles:
-            L.set_wgrad_tile(t)
-            ops.wgrad(wprob, wm, dw)
-            torch.cuda.synchronize()
-            print(f"{name + ' wgrad':36s} x6 tile {t} vs fp32 rel diff {nrel(dw, ref):.2e}")
+        for md in modes:
+            L.set_conv_math(md)
+            for t in wtiles:
+                L.set_wgrad_tile(t)
+                ops.wgrad(wprob, wm, dw)
+                torch.cuda.synchronize()
+                print(f"{name + ' wgrad':36s} {md} tile {t} vs fp32 rel diff {nrel(dw, ref):.2e}")
         L.set_wgrad_tile(-1)
         for (mode, t), v in res.items():
             ms = min(v)

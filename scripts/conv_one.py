@@ -1,0 +1,42 @@
+"""Run one conv-engine launch shape repeatedly (for rocprofv3 counter passes).
+  python scripts/conv_one.py [fwd|wgrad] [reps]  -- resblock 3x3 256->256 @128, bs 8"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "flood-prediction-gan_amd"))
+import torch  # noqa: E402
+
+from floodgan import _lib as L, ops, plans as PL  # noqa: E402
+from floodgan.plans import Buf  # noqa: E402
+
+
+def main():
+    kind = sys.argv[1] if len(sys.argv) > 1 else "fwd"
+    reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+    L.load()
+    dev = "cuda"
+    N, H, C, k = 8, 128, 256, 3
+    X = Buf.empty(N, H, H, C, 1, dev)
+    X.t.uniform_(-1, 1)
+    w = torch.randn(C, C, k, k, device=dev) * 0.02
+    m = PL.wmap_conv_fwd(w.shape, C)
+    Y = Buf.empty(N, H, H, C, 0, dev)
+    Y.t.uniform_(-1, 1)
+    if kind == "fwd":
+        prob = PL.conv_problem(X, 1, k, 1, ops.pack_weight(w, m), m, Y, bias=torch.zeros(C, device=dev))
+        fn = lambda: ops.conv([prob])  # noqa: E731
+    else:
+        wprob = PL.wgrad_conv(Y, X, 1, k, 1, C)
+        dw = torch.empty_like(w)
+        wm = PL.wmap_wgrad(w.shape, True, X.c, k)
+        fn = lambda: ops.wgrad(wprob, wm, dw)  # noqa: E731
+    for _ in range(reps):
+        fn()
+    torch.cuda.synchronize()
+    print("done", kind, reps)
+
+
+if __name__ == "__main__":
+    main()

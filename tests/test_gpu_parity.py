@@ -15,6 +15,19 @@ KTOL = 1e-5     # single kernels vs fp64
 NTOL = 1e-3     # network / step (north-star tolerance)
 
 
+MATHS = ["fp32", "bf16x6", "f16x3"]
+
+
+@pytest.fixture
+def conv_math(request):
+    """Run a test under one conv math, restoring the library default afterwards."""
+    from floodgan import _lib as L
+    prev = L.get_conv_math()
+    L.set_conv_math(request.param)
+    yield request.param
+    L.set_conv_math(prev)
+
+
 def nrel(a, b):
     a = a.detach().double().cpu()
     b = b.detach().double().cpu()
@@ -60,26 +73,30 @@ CONV_CASES = [(9, 64, 7, 1, 3, "reflect", 24), (64, 128, 3, 2, 1, "constant", 20
               (128, 256, 4, 2, 1, "constant", 16), (256, 512, 4, 1, 1, "constant", 9), (512, 1, 4, 1, 1, "constant", 9)]
 
 
+@pytest.mark.parametrize("conv_math", MATHS, indirect=True)
 @pytest.mark.parametrize("case", CONV_CASES)
-def test_conv_fwd_wgrad_dgrad(case):
+def test_conv_fwd_wgrad_dgrad(case, conv_math):
+    """every conv geometry of the step: forward, weight gradient, input gradient vs fp64, in
+    each conv math (the f16x3 case also at gradient-like magnitudes: operands x 1e-9)"""
     from floodgan import ops, plans as PL
     from floodgan.plans import Buf
     cin, cout, k, s, p, mode, H = case
     torch.manual_seed(1)
-    x = torch.randn(2, cin, H, H, dtype=torch.float64)
+    mag = 1e-9 if conv_math == "f16x3" and cin == 256 else 1.0
+    x = torch.randn(2, cin, H, H, dtype=torch.float64) * mag
     w = (torch.randn(cout, cin, k, k, dtype=torch.float64) * 0.05).requires_grad_(True)
     b = torch.randn(cout, dtype=torch.float64)
     xr = x.clone().requires_grad_(True)
     xin = F.pad(xr, (p,) * 4, mode=mode) if p else xr
-    y = F.conv2d(xin, w, b, stride=s)
-    gy = torch.randn_like(y)
+    y = F.conv2d(xin, w, b * mag, stride=s)
+    gy = torch.randn_like(y) * mag
     gx_ref, gw_ref = torch.autograd.grad(y, (xr, w), gy)
     X = buf_from(x, p, mode)
     wd = w.detach().float().to(DEV)
     m = PL.wmap_conv_fwd(wd.shape, X.c)
     Ho = PL.out_size(H, k, s, p)
     Y = Buf.empty(2, Ho, Ho, cout, 0, DEV)
-    ops.conv([PL.conv_problem(X, p, k, s, ops.pack_weight(wd, m), m, Y, bias=b.float().to(DEV))])
+    ops.conv([PL.conv_problem(X, p, k, s, ops.pack_weight(wd, m), m, Y, bias=(b * mag).float().to(DEV))])
     assert nrel(nchw(Y), y) < KTOL
     # weight gradient
     GY = buf_from(gy, 0, "constant")
@@ -114,8 +131,9 @@ def test_conv_fwd_wgrad_dgrad(case):
     assert nrel(nchw(gx), gx_ref) < KTOL
 
 
+@pytest.mark.parametrize("conv_math", MATHS, indirect=True)
 @pytest.mark.parametrize("cin,cout,H", [(256, 128, 12), (128, 64, 20)])
-def test_convT(cin, cout, H):
+def test_convT(cin, cout, H, conv_math):
     from floodgan import ops, plans as PL
     from floodgan.plans import Buf
     torch.manual_seed(2)
