@@ -1217,12 +1217,15 @@ int launch_fwd_split_cfg(int cfg, const ConvBatch& b, int total, bool vec, bool 
         case 2: return launch_fwd_x6<SM, 128, 64, 32, 64, 3, 1, true>(b, total, vec, ws, stream);
         case 3: return launch_fwd_x6<SM, 128, 32, 32, 32, 2, 2, false>(b, total, vec, ws, stream);
         case 4: return launch_fwd_x6<SM, 128, 128, 64, 64, 3, 1, true>(b, total, vec, ws, stream);
-        default: return launch_fwd_x6<SM, 128, 32, 32, 32, 4, 1, true>(b, total, vec, ws, stream);
+        case 5: return launch_fwd_x6<SM, 128, 32, 32, 32, 4, 1, true>(b, total, vec, ws, stream);
+        case 6: return launch_fwd_x6<SM, 256, 256, 64, 128, 2, 1, true>(b, total, vec, ws, stream);
+        case 7: return launch_fwd_x6<SM, 256, 256, 128, 64, 2, 1, true>(b, total, vec, ws, stream);
+        default: return launch_fwd_x6<SM, 128, 256, 64, 128, 1, 1, true>(b, total, vec, ws, stream);
     }
 }
-constexpr int kFwdTiles = 6;
-constexpr int kFwdTileBM[kFwdTiles] = {128, 256, 128, 128, 128, 128};
-constexpr int kFwdTileBN[kFwdTiles] = {256, 128, 64, 32, 128, 32};
+constexpr int kFwdTiles = 9;
+constexpr int kFwdTileBM[kFwdTiles] = {128, 256, 128, 128, 128, 128, 256, 256, 128};
+constexpr int kFwdTileBN[kFwdTiles] = {256, 128, 64, 32, 128, 32, 256, 256, 256};
 
 }  // namespace
 

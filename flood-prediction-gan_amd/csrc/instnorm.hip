@@ -49,8 +49,25 @@ __global__ void in_stats_kernel(fg_view src, int chunks, double* __restrict__ wo
     f32x4 s = {0.f, 0.f, 0.f, 0.f}, ss = {0.f, 0.f, 0.f, 0.f};
     if (g < PG) {
         const f32x4 K = ld4(src.ptr + fg::vidx(src, n, 0, 0) + 4 * c4);
-        for (int p = p0 + g; p < p1; p += PG) {
-            const int y = p / src.w, x = p - (p / src.w) * src.w;
+        // pixel walk without divisions: (y, x) advance by PG per step; 2 loads in flight
+        int p = p0 + g, y = p / src.w, x = p - (p / src.w) * src.w;
+        auto next = [&]() {
+            p += PG;
+            x += PG;
+            while (x >= src.w) {
+                x -= src.w;
+                ++y;
+            }
+        };
+        for (; p + PG < p1;) {
+            const f32x4 v0 = ld4(src.ptr + fg::vidx(src, n, y, x) + 4 * c4) - K;
+            next();
+            const f32x4 v1 = ld4(src.ptr + fg::vidx(src, n, y, x) + 4 * c4) - K;
+            next();
+            s += v0 + v1;
+            ss += v0 * v0 + v1 * v1;
+        }
+        if (p < p1) {
             const f32x4 v = ld4(src.ptr + fg::vidx(src, n, y, x) + 4 * c4) - K;
             s += v;
             ss += v * v;
@@ -83,6 +100,7 @@ __global__ void in_finalize_kernel(fg_view src, int chunks, const double* __rest
     if (idx >= src.n * C) return;
     const int n = idx / C, c = idx - (idx / C) * C;
     double s1 = 0, s2 = 0;
+#pragma unroll 8
     for (int k = 0; k < chunks; ++k) {
         s1 += work[((size_t)(n * chunks + k) * C + c) * 2];
         s2 += work[((size_t)(n * chunks + k) * C + c) * 2 + 1];
@@ -167,8 +185,8 @@ __global__ void in_bwd_stats_kernel(fg_view g, int fp, fg_view gadd, fg_view src
     if (gi < PG) {
         const f32x4 m = ld4(mean + (size_t)n * C + 4 * c4);
         const f32x4 r = ld4(rstd + (size_t)n * C + 4 * c4);
+        int y = (p0 + gi) / w, x = (p0 + gi) - ((p0 + gi) / w) * w;   // walked without divisions
         for (int p = p0 + gi; p < p1; p += PG) {
-            const int y = p / w, x = p - (p / w) * w;
             const f32x4 xh = (ld4(src.ptr + fg::vidx(src, n, y, x) + 4 * c4) - m) * r;
             f32x4 gv = load_grad(g, fp, gadd, n, y, x, h, w, c4);
 #pragma unroll
@@ -176,6 +194,11 @@ __global__ void in_bwd_stats_kernel(fg_view g, int fp, fg_view gadd, fg_view src
             sg += gv;
             sgx += gv * xh;
             sx += xh;
+            x += PG;
+            while (x >= w) {
+                x -= w;
+                ++y;
+            }
         }
     }
 #pragma unroll
@@ -210,6 +233,7 @@ __global__ void in_bwd_finalize_kernel(int N, int C, int HWi, int chunks, const 
     const int n = idx / C, c = idx - (idx / C) * C;
     const double HW = (double)HWi;
     double sg = 0, sgx = 0, sx = 0;
+#pragma unroll 8
     for (int k = 0; k < chunks; ++k) {
         const double* wk = work + ((size_t)(n * chunks + k) * C + c) * 3;
         sg += wk[0];
