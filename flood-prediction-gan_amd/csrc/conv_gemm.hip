@@ -524,7 +524,23 @@ conv_fwd_x6_kernel(const ConvBatch batch) {
                     acc[tm][tn] = SM::mfma(af[tm][SM::PA[c]], bfr[tn][SM::PB[c]], acc[tm][tn]);
     };
     Stage R0, R1;
-    if constexpr (PF == 1) {
+    if constexpr (PF == 3) {
+        // write-after-barrier: ONE register set; at the top of stage kt the registers holding
+        // tile kt+1 (loaded during stage kt-1) go to the free LDS buffer and are refilled with
+        // tile kt+2 at once, so every global load has a whole stage to land
+        load(0, R0);
+        store(0, R0);
+        load(min(1, nkt - 1), R0);
+        __syncthreads();
+        for (int kt = 0; kt < nkt; ++kt) {
+            const int cur = kt & 1;
+            if (kt + 1 < nkt) store(cur ^ 1, R0);
+            load(min(kt + 2, nkt - 1), R0);
+            __builtin_amdgcn_sched_barrier(0);   // keep the loads issued ahead of this stage's MFMAs
+            compute(cur);
+            __syncthreads();
+        }
+    } else if constexpr (PF == 1) {
         load(0, R0);
         store(0, R0);
         __syncthreads();
@@ -797,7 +813,7 @@ __device__ __forceinline__ int wg_swz(int row) {
     else return 0;
 }
 
-template <class SM, int BA, int BKC, int WA, int WK, bool VX, bool VP, int MINW>
+template <class SM, int BA, int BKC, int WA, int WK, bool VX, bool VP, int MINW, bool WAB>
 __global__ void __launch_bounds__((BA / WA) * (BKC / WK) * 64, MINW)
 conv_wgrad_x6_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
     using T = typename SM::T;
@@ -969,10 +985,19 @@ conv_wgrad_x6_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
     const int swp = wg_swz<BA>(tr_row), swx = wg_swz<BKC>(tr_row);   // rows tr_row and tr_row+4 alike
     load();
     store(0);
+    if constexpr (WAB) load();
     __syncthreads();
     for (int it = 0; it < nit; ++it) {
         const int cur = it & 1;
-        load();                         // past the last stage: reads zeros (m >= mend), never stored
+        if constexpr (WAB) {
+            // write-after-barrier: the registers (tile it+1, loaded a stage ago) go to the free
+            // buffer first, then are refilled with tile it+2 ahead of this stage's MFMAs
+            if (it + 1 < nit) store(cur ^ 1);
+            load();
+            __builtin_amdgcn_sched_barrier(0);
+        } else {
+            load();                     // past the last stage: reads zeros (m >= mend), never stored
+        }
         V8 af[TM][NP], bfr[TN][NP];
 #pragma unroll
         for (int p = 0; p < NP; ++p) {
@@ -994,7 +1019,8 @@ conv_wgrad_x6_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
 #pragma unroll
                 for (int tn = 0; tn < TN; ++tn)
                     acc[tm][tn] = SM::mfma(af[tm][SM::PA[c]], bfr[tn][SM::PB[c]], acc[tm][tn]);
-        if (it + 1 < nit) store(cur ^ 1);
+        if constexpr (!WAB)
+            if (it + 1 < nit) store(cur ^ 1);
         __syncthreads();
     }
 
@@ -1158,20 +1184,20 @@ int launch_fwd(const ConvBatch& b, int total, bool vec, hipStream_t stream) {
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
-template <class SM, int BA, int BKC, int WA, int WK, int MINW>
+template <class SM, int BA, int BKC, int WA, int WK, int MINW, bool WAB = false>
 int launch_wgrad_x6(const fg_wgrad_problem& p, bool vx, bool vp, hipStream_t stream) {
     constexpr int NT = (BA / WA) * (BKC / WK) * 64;
     const int K = p.kh * p.j_valid;
     const int ta = (p.n_a + BA - 1) / BA, tk = (K + BKC - 1) / BKC;
     dim3 g(ta * tk * p.splits), blk(NT);
     if (vx && vp)
-        hipLaunchKernelGGL((conv_wgrad_x6_kernel<SM, BA, BKC, WA, WK, true, true, MINW>), g, blk, 0, stream, p, ta, tk);
+        hipLaunchKernelGGL((conv_wgrad_x6_kernel<SM, BA, BKC, WA, WK, true, true, MINW, WAB>), g, blk, 0, stream, p, ta, tk);
     else if (vx)
-        hipLaunchKernelGGL((conv_wgrad_x6_kernel<SM, BA, BKC, WA, WK, true, false, MINW>), g, blk, 0, stream, p, ta, tk);
+        hipLaunchKernelGGL((conv_wgrad_x6_kernel<SM, BA, BKC, WA, WK, true, false, MINW, WAB>), g, blk, 0, stream, p, ta, tk);
     else if (vp)
-        hipLaunchKernelGGL((conv_wgrad_x6_kernel<SM, BA, BKC, WA, WK, false, true, MINW>), g, blk, 0, stream, p, ta, tk);
+        hipLaunchKernelGGL((conv_wgrad_x6_kernel<SM, BA, BKC, WA, WK, false, true, MINW, WAB>), g, blk, 0, stream, p, ta, tk);
     else
-        hipLaunchKernelGGL((conv_wgrad_x6_kernel<SM, BA, BKC, WA, WK, false, false, MINW>), g, blk, 0, stream, p, ta, tk);
+        hipLaunchKernelGGL((conv_wgrad_x6_kernel<SM, BA, BKC, WA, WK, false, false, MINW, WAB>), g, blk, 0, stream, p, ta, tk);
     return fg::launched("conv_wgrad_x6");
 }
 
@@ -1183,10 +1209,12 @@ int launch_wgrad_split_cfg(int cfg, const fg_wgrad_problem& p, bool vx, bool vp,
         case 0: return launch_wgrad_x6<SM, 128, 128, 64, 64, 3>(p, vx, vp, stream);
         case 1: return launch_wgrad_x6<SM, 256, 128, 64, 64, 4>(p, vx, vp, stream);
         case 2: return launch_wgrad_x6<SM, 64, 256, 64, 64, 3>(p, vx, vp, stream);
-        default: return launch_wgrad_x6<SM, 32, 256, 32, 64, 3>(p, vx, vp, stream);
+        case 3: return launch_wgrad_x6<SM, 32, 256, 32, 64, 3>(p, vx, vp, stream);
+        case 4: return launch_wgrad_x6<SM, 256, 128, 64, 64, 4, true>(p, vx, vp, stream);
+        default: return launch_wgrad_x6<SM, 128, 128, 64, 64, 3, true>(p, vx, vp, stream);
     }
 }
-constexpr int kWgradTiles = 4;
+constexpr int kWgradTiles = 6;
 
 template <int BA, int BKC, int WA, int WK>
 int launch_wgrad(const fg_wgrad_problem& p, bool vx, bool vp, hipStream_t stream) {
@@ -1220,12 +1248,15 @@ int launch_fwd_split_cfg(int cfg, const ConvBatch& b, int total, bool vec, bool 
         case 5: return launch_fwd_x6<SM, 128, 32, 32, 32, 4, 1, true>(b, total, vec, ws, stream);
         case 6: return launch_fwd_x6<SM, 256, 256, 64, 128, 2, 1, true>(b, total, vec, ws, stream);
         case 7: return launch_fwd_x6<SM, 256, 256, 128, 64, 2, 1, true>(b, total, vec, ws, stream);
-        default: return launch_fwd_x6<SM, 128, 256, 64, 128, 1, 1, true>(b, total, vec, ws, stream);
+        case 8: return launch_fwd_x6<SM, 128, 256, 64, 128, 1, 1, true>(b, total, vec, ws, stream);
+        case 9: return launch_fwd_x6<SM, 128, 256, 64, 64, 2, 3, true>(b, total, vec, ws, stream);
+        case 10: return launch_fwd_x6<SM, 256, 128, 64, 64, 2, 3, true>(b, total, vec, ws, stream);
+        default: return launch_fwd_x6<SM, 128, 64, 32, 64, 3, 3, true>(b, total, vec, ws, stream);
     }
 }
-constexpr int kFwdTiles = 9;
-constexpr int kFwdTileBM[kFwdTiles] = {128, 256, 128, 128, 128, 128, 256, 256, 128};
-constexpr int kFwdTileBN[kFwdTiles] = {256, 128, 64, 32, 128, 32, 256, 256, 256};
+constexpr int kFwdTiles = 12;
+constexpr int kFwdTileBM[kFwdTiles] = {128, 256, 128, 128, 128, 128, 256, 256, 128, 128, 256, 128};
+constexpr int kFwdTileBN[kFwdTiles] = {256, 128, 64, 32, 128, 32, 256, 256, 256, 256, 128, 64};
 
 }  // namespace
 

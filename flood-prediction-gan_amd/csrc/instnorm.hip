@@ -29,8 +29,8 @@ constexpr int NT = 256;
 constexpr int MAX_CHUNKS = 256;
 
 int choose_chunks(int n, long long hw) {
-    long long c = (1024 + n - 1) / n;
-    if (c > hw / 256) c = hw / 256;
+    long long c = (2048 + n - 1) / n;      // ~2048 workgroups: enough loads in flight per CU
+    if (c > hw / 64) c = hw / 64;
     if (c > MAX_CHUNKS) c = MAX_CHUNKS;
     if (c < 1) c = 1;
     return (int)c;
@@ -93,23 +93,38 @@ __global__ void in_stats_kernel(fg_view src, int chunks, double* __restrict__ wo
     }
 }
 
-__global__ void in_finalize_kernel(fg_view src, int chunks, const double* __restrict__ work, float eps,
-                                   float* __restrict__ mean, float* __restrict__ rstd) {
+// finalize: block (n, 64-channel group), 64 x FG threads: thread (c, g) sums chunks g, g+FG, ...
+// (coalesced over c), then the FG partials are combined in LDS (fixed order: deterministic)
+constexpr int FG = 16;
+
+__global__ void __launch_bounds__(64 * FG) in_finalize_kernel(fg_view src, int chunks, const double* __restrict__ work,
+                                                               float eps, float* __restrict__ mean,
+                                                               float* __restrict__ rstd) {
     const int C = src.c_alloc;
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= src.n * C) return;
-    const int n = idx / C, c = idx - (idx / C) * C;
+    const int n = blockIdx.x, c = blockIdx.y * 64 + (threadIdx.x & 63), g = threadIdx.x >> 6;
+    __shared__ double red[FG][64][2];
     double s1 = 0, s2 = 0;
-#pragma unroll 8
-    for (int k = 0; k < chunks; ++k) {
-        s1 += work[((size_t)(n * chunks + k) * C + c) * 2];
-        s2 += work[((size_t)(n * chunks + k) * C + c) * 2 + 1];
+    if (c < C)
+        for (int k = g; k < chunks; k += FG) {
+            s1 += work[((size_t)(n * chunks + k) * C + c) * 2];
+            s2 += work[((size_t)(n * chunks + k) * C + c) * 2 + 1];
+        }
+    red[g][threadIdx.x & 63][0] = s1;
+    red[g][threadIdx.x & 63][1] = s2;
+    __syncthreads();
+    if (g != 0 || c >= C) return;
+    s1 = 0;
+    s2 = 0;
+    for (int gg = 0; gg < FG; ++gg) {
+        s1 += red[gg][threadIdx.x][0];
+        s2 += red[gg][threadIdx.x][1];
     }
     const double HW = (double)src.h * src.w;
     const double ms = s1 / HW;
     double var = s2 / HW - ms * ms;
     if (var < 0) var = 0;
     const double K = src.ptr[fg::vidx(src, n, 0, 0) + c];
+    const int idx = n * C + c;
     mean[idx] = (float)(K + ms);
     rstd[idx] = (float)(1.0 / sqrt(var + (double)eps));
 }
@@ -223,23 +238,36 @@ __global__ void in_bwd_stats_kernel(fg_view g, int fp, fg_view gadd, fg_view src
     }
 }
 
-// one thread per (n,c): coefficients of the apply pass and the per-plane part of the
-// (mathematically cancelled) conv-bias gradient
-__global__ void in_bwd_finalize_kernel(int N, int C, int HWi, int chunks, const double* __restrict__ work,
-                                       const float* __restrict__ rstd, float* __restrict__ coef,
-                                       double* __restrict__ bpart) {
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= N * C) return;
-    const int n = idx / C, c = idx - (idx / C) * C;
-    const double HW = (double)HWi;
+// block (n, 64-channel group) as in in_finalize_kernel: coefficients of the apply pass and the
+// per-plane part of the (mathematically cancelled) conv-bias gradient
+__global__ void __launch_bounds__(64 * FG) in_bwd_finalize_kernel(int N, int C, int HWi, int chunks,
+                                                                   const double* __restrict__ work,
+                                                                   const float* __restrict__ rstd,
+                                                                   float* __restrict__ coef,
+                                                                   double* __restrict__ bpart) {
+    const int n = blockIdx.x, c = blockIdx.y * 64 + (threadIdx.x & 63), g = threadIdx.x >> 6;
+    __shared__ double red[FG][64][3];
     double sg = 0, sgx = 0, sx = 0;
-#pragma unroll 8
-    for (int k = 0; k < chunks; ++k) {
-        const double* wk = work + ((size_t)(n * chunks + k) * C + c) * 3;
-        sg += wk[0];
-        sgx += wk[1];
-        sx += wk[2];
+    if (c < C)
+        for (int k = g; k < chunks; k += FG) {
+            const double* wk = work + ((size_t)(n * chunks + k) * C + c) * 3;
+            sg += wk[0];
+            sgx += wk[1];
+            sx += wk[2];
+        }
+    red[g][threadIdx.x & 63][0] = sg;
+    red[g][threadIdx.x & 63][1] = sgx;
+    red[g][threadIdx.x & 63][2] = sx;
+    __syncthreads();
+    if (g != 0 || c >= C) return;
+    sg = sgx = sx = 0;
+    for (int gg = 0; gg < FG; ++gg) {
+        sg += red[gg][threadIdx.x][0];
+        sgx += red[gg][threadIdx.x][1];
+        sx += red[gg][threadIdx.x][2];
     }
+    const double HW = (double)HWi;
+    const int idx = n * C + c;
     coef[(size_t)idx * 2] = (float)(sg / HW);
     coef[(size_t)idx * 2 + 1] = (float)(sgx / HW);
     // sum_hw rstd*(g' - mean g' - xhat*mean(g'xhat)) = -rstd * sx * sgx / HW
@@ -415,9 +443,8 @@ FG_API int fg_in_stats(fg_view src, float eps, float* mean, float* rstd, double*
     hipLaunchKernelGGL(in_stats_kernel, dim3(chunks, src.n), dim3(NT), 0, stream, src, chunks, work);
     int e = fg::launched("in_stats");
     if (e) return e;
-    const int tot = src.n * src.c_alloc;
-    hipLaunchKernelGGL(in_finalize_kernel, dim3((tot + 255) / 256), dim3(256), 0, stream, src, chunks, work, eps,
-                       mean, rstd);
+    hipLaunchKernelGGL(in_finalize_kernel, dim3(src.n, (src.c_alloc + 63) / 64), dim3(64 * FG), 0, stream, src,
+                       chunks, work, eps, mean, rstd);
     return fg::launched("in_finalize");
 }
 
@@ -456,8 +483,7 @@ FG_API int fg_in_bwd(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, cons
     int e = fg::launched("in_bwd_stats");
     if (e) return e;
     double* bpart = work + (size_t)src.n * C * MAX_CHUNKS * 3 + (size_t)src.n * C;
-    const int nc = src.n * C;
-    hipLaunchKernelGGL(in_bwd_finalize_kernel, dim3((nc + 255) / 256), dim3(256), 0, stream, src.n, C,
+    hipLaunchKernelGGL(in_bwd_finalize_kernel, dim3(src.n, (C + 63) / 64), dim3(64 * FG), 0, stream, src.n, C,
                        src.h * src.w, chunks, work, rstd, coef, bpart);
     e = fg::launched("in_bwd_finalize");
     if (e) return e;

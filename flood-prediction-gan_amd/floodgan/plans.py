@@ -210,7 +210,7 @@ def phase_maps(shape, k, p, c_alloc, n_base=0, n_out=None):
 # weight-gradient problems (fg_wgrad_problem)
 # ------------------------------------------------------------------------------------------
 
-WG_BLOCKS = 1024   # ~ one full wave of resident workgroups (256 CUs x 4)
+WG_BLOCKS = 512    # one wave of resident weight-gradient workgroups (256 CUs x 2): fewer fp32 slabs
 
 
 def wgrad_tile(n_a):

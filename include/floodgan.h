@@ -137,10 +137,10 @@ int fg_conv_fwd(const fg_conv_problem* probs, int nprob, hipStream_t stream);
 int fg_set_conv_math(int mode);
 int fg_get_conv_math(void);
 
-/* Tuning hook: force one split-math forward tile configuration (0..5, see conv_gemm.hip), or -1 for
+/* Tuning hook: force one split-math forward tile configuration (0..11, see conv_gemm.hip), or -1 for
  * the automatic choice by output-channel count (the default). */
 int fg_set_fwd_tile(int cfg);
-/* Same for the split-math weight-gradient kernels (0..3). */
+/* Same for the split-math weight-gradient kernels (0..5). */
 int fg_set_wgrad_tile(int cfg);
 
 /* Weight gradient into partial slabs (see fg_wgrad_problem). */

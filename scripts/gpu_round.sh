@@ -1,0 +1,18 @@
+#!/bin/bash
+# One GPU session: tile micro-bench, parity tests + smoke + bench, kernel profile, counter
+# passes on the resblock conv.  Every GPU step has its own limit; stop at the first failure.
+cd "$(dirname "$0")/.." || exit 1
+TAG=${TAG:-run}
+mkdir -p gpurun_out
+if [ -n "$TILES" ]; then
+  ACCURACY=${ACCURACY:-0} MODES=${MODES:-f16x3} timeout -k 10 600 python scripts/bench_conv.py > gpurun_out/bench_conv.log 2>&1 \
+    || { echo "bench_conv failed"; tail -20 gpurun_out/bench_conv.log; exit 1; }
+fi
+BENCH_ARGS=--no-cpu-baseline scripts/gpu_check.sh > gpurun_out/check.log 2>&1
+rc=$?; grep -a "passed\|failed\|smoke:\|rc=" gpurun_out/check.log; [ $rc -eq 0 ] || exit $rc
+grep -o '"value": [0-9.]*' gpurun_out/bench.log
+scripts/gpu_profile.sh $TAG > /dev/null 2>&1 || { echo "profile failed"; exit 1; }
+if [ -n "$PMC" ]; then
+  scripts/gpu_pmc.sh ${TAG}_fwd > /dev/null && KIND=wgrad scripts/gpu_pmc.sh ${TAG}_wgrad > /dev/null || { echo "pmc failed"; exit 1; }
+fi
+echo "round done"
