@@ -138,8 +138,9 @@ def main():
                        "parallelism": f"dp{world}"},
             "conv_math": math,
             "roofline": {"bound": "mfma",
-                         "kernel": (f"conv_fwd_x6_kernel<{'MathF16x3' if nprod == 3 else 'MathBF16x6'},128,256,64,64> "
-                                    "(8 waves, pre-split weights)" if fwd_x6 else
+                         "kernel": ("conv_fwd_f3_kernel<256,256,32,256,2> (LDS-DMA ring, 8 waves, 16x16x32 f16 MFMA)"
+                                    if nprod == 3 else
+                                    f"conv_fwd_x6_kernel<MathBF16x6,128,256,64,64>" if fwd_x6 else
                                     "conv_fwd_kernel<128,128,64,64>") + " resblock 3x3 256->256 @128x128",
                          "achieved": round(achieved, 2), "peak": round(peak, 2), "unit": "TFLOP/s",
                          "peak_basis": (f"16-bit dense MFMA 2500 TFLOP/s / {nprod} split products per fp32 MAC"

@@ -1,0 +1,60 @@
+// Shared pieces of the convolution engine (conv_gemm.hip: generic register-staged kernels;
+// conv_f3.hip: the LDS-DMA pipelined f16x3 forward kernel).
+#pragma once
+#include "fg_common.hpp"
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+namespace fgc {
+
+// Up to four fg_conv_problems sharing one launch (the four output phases of a stride-2
+// transposed conv); blocks [blk_start[i], blk_start[i+1]) belong to problem i.
+struct ConvBatch {
+    fg_conv_problem p[4];
+    int count;
+    int ntiles_n[4];
+    int blk_start[5];
+};
+
+__device__ __forceinline__ void decomp(int m, int mb, int mab, int& img, int& a, int& b) {
+    img = m / mab;
+    const int rem = m - img * mab;
+    a = rem / mb;
+    b = rem - a * mb;
+}
+
+// power-of-two operand scale from an absmax slot (max over its FG_AMAX_SHARDS shards, one per
+// lane, reduced across the wave): |v * s| < 2^14
+__device__ __forceinline__ float pow2_scale(const float* amax) {
+    unsigned b = amax ? __float_as_uint(amax[threadIdx.x & (FG_AMAX_SHARDS - 1)]) & 0x7fffffffu : 0u;
+#pragma unroll
+    for (int off = 1; off < FG_AMAX_SHARDS; off <<= 1) b = max(b, (unsigned)__shfl_xor((int)b, off));
+    const float m = __uint_as_float(b);
+    if (!(m > 0.f) || !(m < 3.0e38f)) return 1.f;
+    int e;
+    frexpf(m, &e);                                        // m < 2^e
+    return ldexpf(1.f, 14 - e);
+}
+
+// f16x3 split of 8 fp32 values: v*s = h + l, h = fp16(v*s), l = fp16(v*s - h)
+__device__ __forceinline__ void split_f16(const float (&v)[8], float s, f16x8& h, f16x8& l) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const f32x2 x = f32x2{v[2 * e], v[2 * e + 1]} * s;
+        const f16x2 hh = __builtin_convertvector(x, f16x2);
+        const f16x2 ll = __builtin_convertvector(x - __builtin_convertvector(hh, f32x2), f16x2);
+        h[2 * e] = hh[0];
+        h[2 * e + 1] = hh[1];
+        l[2 * e] = ll[0];
+        l[2 * e + 1] = ll[1];
+    }
+}
+
+// Pipelined f16x3 forward kernel (conv_f3.hip).  Returns 1 if it took the batch (launched or
+// failed: *rc holds the launch status), 0 if the batch does not fit its constraints.
+int launch_fwd_f3(const ConvBatch& b, int nprob, int max_n, hipStream_t stream, int* rc);
+
+}  // namespace fgc

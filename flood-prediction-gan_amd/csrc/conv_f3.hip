@@ -1,0 +1,315 @@
+// Pipelined f16x3 implicit-GEMM forward kernel for the wide convolutions of the hot path
+// (N >= 128: the resblock 3x3 convs and their input gradients, conv2/conv3, the deconv1 /
+// deconv2 phases, discriminator model.2/5/8): models/model_architectures.py:314-333, :407-410,
+// :426-435.
+//
+// Why a second kernel: the register-staged kernels of conv_gemm.hip stage a 16-deep k-tile
+// per barrier with a one-stage prefetch; rocprofv3 counters on the resblock conv (profiles/
+// round1/r1f_pmc_fwd.json) show the MFMA pipe busy 45 % of the cycles and waves parked on
+// s_waitcnt/barriers 51 % -- the im2col gather misses L2 (FETCH 9x the input) and one stage
+// of MFMA work does not cover that latency.  Here both operands travel global -> LDS by
+// LDS-DMA (buffer_load_dwordx4 ... lds) into a 3-deep ring of 32-deep k-stages, so every load
+// has two stages of MFMA work to land, no VGPRs hold staging data and the only barrier per
+// stage is a raw s_barrier after a counted vmcnt.
+//
+// Operands per stage (LDS, one __shared__ array):
+//   A: fp32 im2col rows [BM][32] (128 B rows), gathered with per-lane row addresses; the
+//      fp32 -> (h, l) fp16 split happens on the MFMA fragments after the LDS read.
+//   B: the pre-split fp16 weights (fg_pack_weight_f16) as [piece][BN][32] (64 B rows).
+// Both images are XOR-swizzled in 16-B chunks (the DMA writes lane-linear, so the swizzle is
+// applied to the per-lane SOURCE address) so that the 16x16x32 fragment reads
+// (ds_read_b128: lane l reads row l&15, k-chunk l>>4) are bank-conflict free.
+// MFMA: v_mfma_f32_16x16x32_f16, three products per fragment pair (lh, hl, hh).
+#include "conv_common.hpp"
+
+namespace {
+
+using fgc::ConvBatch;
+
+// 16-B chunk swizzles (found by exhaustive search over the ds_read_b128 lane groups)
+__device__ __forceinline__ int swz_a(int row) { return ((row >> 1) & 1) ^ (((row >> 3) & 1) << 2); }   // 8 chunks
+__device__ __forceinline__ int swz_b(int row) { return ((row >> 3) & 1) << 1; }                        // 4 chunks
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+// f16x3 split with scalar f32 arithmetic (packed-f32 VALU beside MFMAs costs extra issue
+// cycles): v*s = h + l, h = fp16(v*s), l = fp16(v*s - h), the residual exact in fp32
+__device__ __forceinline__ void split_scalar(const float (&v)[8], float s, f16x8& h, f16x8& l) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const float x0 = v[2 * e] * s, x1 = v[2 * e + 1] * s;
+        const f16x2 hh = __builtin_convertvector(f32x2{x0, x1}, f16x2);
+        const float r0 = x0 - (float)hh[0], r1 = x1 - (float)hh[1];
+        const f16x2 ll = __builtin_convertvector(f32x2{r0, r1}, f16x2);
+        h[2 * e] = hh[0];
+        h[2 * e + 1] = hh[1];
+        l[2 * e] = ll[0];
+        l[2 * e + 1] = ll[1];
+    }
+}
+
+// one stage of LDS-DMA: this wave's A_GL + B_GL 1-KiB pieces (per-lane byte offsets, per-stage
+// scalar offsets)
+template <int A_GL, int B_GL, int A_BYTES>
+__device__ __forceinline__ void dma_stage(char* sb, int wave, __amdgpu_buffer_rsrc_t xr, __amdgpu_buffer_rsrc_t wr,
+                                          const int* a_off, const int* b_off, int soff_a, int soff_b) {
+#pragma unroll
+    for (int i = 0; i < A_GL; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_void*)(sb + (wave * A_GL + i) * 1024), 16, a_off[i], soff_a,
+                                                 0, 0);
+#pragma unroll
+    for (int i = 0; i < B_GL; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (lds_void*)(sb + A_BYTES + (wave * B_GL + i) * 1024), 16, b_off[i],
+                                                 soff_b, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else static_assert(N < 0, "add the vmcnt immediate");
+}
+
+template <int BM, int BN, int WM, int WN, int NS>
+__global__ void __launch_bounds__((BM / WM) * (BN / WN) * 64, 1)
+conv_fwd_f3_kernel(const ConvBatch batch) {
+    constexpr int NWN = BN / WN;
+    constexpr int NW = (BM / WM) * NWN;
+    constexpr int TM = WM / 16, TN = WN / 16;
+    constexpr int A_BYTES = BM * 128;          // fp32 [BM][32]
+    constexpr int B_BYTES = 2 * BN * 64;       // fp16 [2][BN][32]
+    constexpr int STAGE = A_BYTES + B_BYTES;
+    constexpr int A_GL = A_BYTES / 1024 / NW;  // 1-KiB LDS-DMA instructions per wave per stage
+    constexpr int B_GL = B_BYTES / 1024 / NW;
+    static_assert(A_BYTES % (1024 * NW) == 0 && B_BYTES % (1024 * NW) == 0, "stage not a whole number of DMAs");
+
+    __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / NWN, wn = wave - (wave / NWN) * NWN;
+
+    const int wid = fg::xcd_remap(blockIdx.x, gridDim.x);
+    int pi = 0;
+    while (pi + 1 < batch.count && wid >= batch.blk_start[pi + 1]) ++pi;
+    const fg_conv_problem& P = batch.p[pi];
+    const int local = wid - batch.blk_start[pi];
+    const int ntn = batch.ntiles_n[pi];
+    const int mt = local / ntn, nt = local - (local / ntn) * ntn;
+    const int m0 = mt * BM, n0 = nt * BN;
+    const int mab = P.m_a * P.m_b;
+    const int M = P.m_img * mab;
+    const int nkt = P.kh * (P.jp / 32);
+    const int sxr = (int)P.sxr;
+
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)P.x, 0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)P.w, 0, 0x7fffffff, 0x00020000);
+
+    // ---- per-lane DMA sources (byte offsets; the per-stage k offset is a scalar soffset).
+    // A: instruction i of this wave fills rows (wave*A_GL+i)*8 + lane/8, physical chunk lane%8 <-
+    // logical chunk (lane%8) ^ swz_a(row).  Rows past M are clamped to a valid row (their
+    // results are never stored); jp == j_valid, so every k of a stage is a real tap.
+    int a_off[A_GL];
+#pragma unroll
+    for (int i = 0; i < A_GL; ++i) {
+        const int row = (wave * A_GL + i) * 8 + (lane >> 3);
+        const int cl = (lane & 7) ^ swz_a(row);
+        int img, a, b;
+        fgc::decomp(min(m0 + row, M - 1), P.m_b, mab, img, a, b);
+        a_off[i] = ((int)(img * P.sxn + a * P.sxa + b * P.sxb) + cl * 4) * 4;
+    }
+    // B: instruction q = wave*B_GL+i fills piece q / (BN/16), rows (q % (BN/16))*16 + lane/4,
+    // physical chunk lane%4 <- logical 8-k slot (lane%4) ^ swz_b(row); rows past n_out clamped
+    int b_off[B_GL];
+#pragma unroll
+    for (int i = 0; i < B_GL; ++i) {
+        const int q = wave * B_GL + i;
+        const int pc = q / (BN / 16);
+        const int row = (q - pc * (BN / 16)) * 16 + (lane >> 2);
+        const int cl = (lane & 3) ^ swz_b(row);
+        b_off[i] = min(n0 + row, P.n_out - 1) * (P.ldw / 8) * 32 + cl * 32 + pc * 16;
+    }
+
+    // stage kt covers packed k [32kt, 32kt+32) = kernel row r, run offset jb: kept incrementally
+    // in scalars (no per-stage vector address arithmetic)
+    auto issue = [&](int buf, int kt, int koff_bytes) {
+        dma_stage<A_GL, B_GL, A_BYTES>(smem + buf * STAGE, wave, xr, wr, a_off, b_off, koff_bytes, kt * 128);
+    };
+
+    const float sa = fgc::pow2_scale(P.x_absmax);
+    const float sb = fgc::pow2_scale(P.w_absmax);
+    const float out_scale = 1.f / (sa * sb);
+
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // fragment addressing: lane reads row (lane & 15) of each 16-row block, k-chunk g = lane >> 4
+    const int fr = lane & 15, g = lane >> 4;
+    // A rows wm*WM + tm*16 + fr: bits 1..3 of the row are those of fr
+    const int a_c0 = ((2 * g) ^ swz_a(fr)) * 16, a_c1 = ((2 * g + 1) ^ swz_a(fr)) * 16;
+    const int b_c = (g ^ swz_b(fr)) * 16;
+
+    // B fragments are read in column groups of TG blocks (bounded live registers); each group's
+    // three products are issued smallest first
+    constexpr int TG = TN < 4 ? TN : 4;
+    static_assert(TN % TG == 0, "column blocks per wave must be a multiple of the group");
+    auto compute = [&](int buf) {
+        const char* sbuf = smem + buf * STAGE;
+        f16x8 ah[TM], al[TM];
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) {
+            const char* rowp = sbuf + (wm * WM + tm * 16 + fr) * 128;
+            const f32x4 v0 = *reinterpret_cast<const f32x4*>(rowp + a_c0);
+            const f32x4 v1 = *reinterpret_cast<const f32x4*>(rowp + a_c1);
+            const float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+            split_scalar(v, sa, ah[tm], al[tm]);
+        }
+#pragma unroll
+        for (int t0 = 0; t0 < TN; t0 += TG) {
+            f16x8 bh[TG], bl[TG];
+#pragma unroll
+            for (int t = 0; t < TG; ++t) {
+                const char* rowp = sbuf + A_BYTES + (wn * WN + (t0 + t) * 16 + fr) * 64 + b_c;
+                bh[t] = *reinterpret_cast<const f16x8*>(rowp);
+                bl[t] = *reinterpret_cast<const f16x8*>(rowp + BN * 64);
+            }
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                for (int t = 0; t < TG; ++t)
+                    acc[tm][t0 + t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[tm], bh[t], acc[tm][t0 + t], 0, 0, 0);
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                for (int t = 0; t < TG; ++t)
+                    acc[tm][t0 + t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[tm], bl[t], acc[tm][t0 + t], 0, 0, 0);
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                for (int t = 0; t < TG; ++t)
+                    acc[tm][t0 + t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[tm], bh[t], acc[tm][t0 + t], 0, 0, 0);
+        }
+    };
+
+    // ---- NS-deep ring: stage kt+NS-1 is issued right after the barrier that retires stage kt-1's
+    // reads; before it, this wave waits for its own DMAs of stage kt (counted vmcnt: the younger
+    // NS-2 stages stay in flight) and the barrier makes everyone's visible
+    static_assert(NS == 2 || NS == 3, "ring depth");
+    const int jp = P.jp;
+    int ir = 0, ijb = 0;                     // (r, jb) of the next stage to issue
+    auto next_koff = [&]() {
+        const int k = (ir * sxr + ijb) * 4;
+        ijb += 32;
+        if (ijb == jp) { ijb = 0; ++ir; }
+        return k;
+    };
+#pragma unroll
+    for (int s0 = 0; s0 < NS - 1; ++s0)
+        if (s0 < nkt) issue(s0, s0, next_koff());
+    int cur = 0, nxt = NS - 1;
+    for (int kt = 0; kt < nkt; ++kt) {
+        if (NS == 3 && kt + 1 < nkt) wait_vmcnt<NS == 3 ? A_GL + B_GL : 0>();
+        else wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        if (kt + NS - 1 < nkt) issue(nxt, kt + NS - 1, next_koff());
+        compute(cur);
+        cur = cur == NS - 1 ? 0 : cur + 1;
+        nxt = nxt == NS - 1 ? 0 : nxt + 1;
+    }
+
+    // ---- epilogue: scale, bias, activation, strided store (or accumulate).  Column-invariant
+    // work (bias, n bounds) is hoisted; full tiles take a branch-free path.
+    const int act = P.act;
+    const bool accum = P.accumulate != 0;
+    float bias_v[TN];
+    int ncol[TN];
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+        ncol[tn] = n0 + wn * WN + tn * 16 + fr;
+        bias_v[tn] = P.bias ? P.bias[min(ncol[tn], P.n_out - 1)] : 0.f;
+    }
+    const bool full_n = n0 + BN <= P.n_out;
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) {
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {
+            const int m = m0 + wm * WM + tm * 16 + 4 * g + reg;
+            if (m >= M) continue;
+            int img, a, b;
+            fgc::decomp(m, P.m_b, mab, img, a, b);
+            float* yrow = P.y + img * P.syn + a * P.sya + b * P.syb;
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) {
+                if (!full_n && ncol[tn] >= P.n_out) continue;
+                float v = fg::act_fwd(acc[tm][tn][reg] * out_scale + bias_v[tn], act);
+                float* dst = yrow + ncol[tn] * P.syc;
+                if (accum) v += *dst;
+                *dst = v;
+            }
+        }
+    }
+}
+
+template <int BM, int BN, int WM, int WN, int NS = 3>
+int launch_cfg(const ConvBatch& in, int nprob, hipStream_t stream) {
+    constexpr int NT = (BM / WM) * (BN / WN) * 64;
+    ConvBatch b = in;
+    int total = 0;
+    for (int i = 0; i < nprob; ++i) {
+        const long long M = (long long)b.p[i].m_img * b.p[i].m_a * b.p[i].m_b;
+        b.ntiles_n[i] = (b.p[i].n_out + BN - 1) / BN;
+        b.blk_start[i] = total;
+        total += (int)((M + BM - 1) / BM) * b.ntiles_n[i];
+    }
+    for (int i = nprob; i < 4; ++i) { b.ntiles_n[i] = 1; b.blk_start[i] = total; }
+    b.blk_start[nprob] = total;
+    b.blk_start[4] = total;
+    if (total == 0) return 0;
+    hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS>), dim3(total), dim3(NT), 0, stream, b);
+    return fg::launched("conv_fwd_f3");
+}
+
+}  // namespace
+
+int g_f3_tile = -1;   // tuning hook (fg_set_f3_tile): -2 disables the kernel, >= 0 forces a config
+
+namespace fgc {
+
+int launch_fwd_f3(const ConvBatch& b, int nprob, int max_n, hipStream_t stream, int* rc) {
+    if (g_f3_tile == -2) return 0;
+    for (int i = 0; i < nprob; ++i) {
+        const fg_conv_problem& p = b.p[i];
+        // no K padding (every staged k is a real tap: padded j would gather past the row run)
+        if (p.w_split != 2 || p.jp % 32 || p.j_valid != p.jp || p.ldw != p.kh * p.jp || !p.x_absmax || !p.w_absmax ||
+            p.m_img * p.m_a * p.m_b < 1)
+            return 0;
+    }
+    int cfg = g_f3_tile >= 0 ? g_f3_tile : (max_n > 128 ? 4 : max_n > 64 ? 6 : -1);
+    switch (cfg) {
+        case 0: *rc = launch_cfg<128, 256, 32, 128>(b, nprob, stream); return 1;
+        case 1: *rc = launch_cfg<256, 128, 64, 64>(b, nprob, stream); return 1;
+        case 2: *rc = launch_cfg<128, 256, 64, 64>(b, nprob, stream); return 1;
+        case 3: *rc = launch_cfg<128, 128, 32, 64>(b, nprob, stream); return 1;
+        case 4: *rc = launch_cfg<256, 256, 32, 256, 2>(b, nprob, stream); return 1;
+        case 5: *rc = launch_cfg<256, 256, 64, 128, 2>(b, nprob, stream); return 1;
+        case 6: *rc = launch_cfg<256, 128, 32, 128, 2>(b, nprob, stream); return 1;
+        default: return 0;
+    }
+}
+
+}  // namespace fgc
+
+FG_API int fg_set_f3_tile(int cfg) {
+    if (cfg < -2 || cfg > 6) return fg::fail(FG_ERR_INVALID, "fg_set_f3_tile: %d", cfg);
+    g_f3_tile = cfg;
+    return 0;
+}

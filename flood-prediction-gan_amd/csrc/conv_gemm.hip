@@ -19,7 +19,7 @@
 // stay row(pixel)-major in LDS, split-M partial slabs are summed by wgrad_reduce.
 #include <algorithm>
 
-#include "fg_common.hpp"
+#include "conv_common.hpp"
 
 namespace {
 
@@ -27,19 +27,9 @@ constexpr int BK = 16;
 constexpr int LDK = BK + 4;
 int g_conv_math = FG_MATH_F16X3;    // default: scaled split-fp16 (accuracy: scripts/bench_conv.py, tests/)
 
-struct ConvBatch {
-    fg_conv_problem p[4];
-    int count;
-    int ntiles_n[4];
-    int blk_start[5];
-};
-
-__device__ __forceinline__ void decomp(int m, int mb, int mab, int& img, int& a, int& b) {
-    img = m / mab;
-    const int rem = m - img * mab;
-    a = rem / mb;
-    b = rem - a * mb;
-}
+using fgc::ConvBatch;
+using fgc::decomp;
+using fgc::pow2_scale;
 
 template <int BM, int BN, int WM, int WN, bool VEC>
 __global__ void __launch_bounds__((BM / WM) * (BN / WN) * 64)
@@ -222,7 +212,6 @@ conv_fwd_kernel(const ConvBatch batch) {
 // ------------------------------------------------------------------------------------------
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // Split of two fp32 values at once: v_cvt_pk_bf16_f32 (RNE) + v_pk_add_f32 (exact residuals).
 __device__ __forceinline__ void split3x2(float a, float b, bf16x2& h, bf16x2& m, bf16x2& l) {
@@ -257,22 +246,6 @@ __device__ __forceinline__ void split3(const float (&v)[8], bf16x8& h, bf16x8& m
 // 1/(s_a s_b).  Half the MFMAs and 2/3 of the staging of bf16x6, at ~4x its per-product error
 // (still far below the fp32 accumulation error of the convolution sums).
 // ------------------------------------------------------------------------------------------
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
-typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
-
-// power-of-two operand scale from an absmax slot (max over its FG_AMAX_SHARDS shards, one per
-// lane, reduced across the wave): |v * s| < 2^14
-__device__ __forceinline__ float pow2_scale(const float* amax) {
-    unsigned b = amax ? __float_as_uint(amax[threadIdx.x & (FG_AMAX_SHARDS - 1)]) & 0x7fffffffu : 0u;
-#pragma unroll
-    for (int off = 1; off < FG_AMAX_SHARDS; off <<= 1) b = max(b, (unsigned)__shfl_xor((int)b, off));
-    const float m = __uint_as_float(b);
-    if (!(m > 0.f) || !(m < 3.0e38f)) return 1.f;
-    int e;
-    frexpf(m, &e);                                        // m < 2^e
-    return ldexpf(1.f, 14 - e);
-}
 
 // split math traits: piece type, piece count, the products kept (PA[c] x PB[c], small first)
 struct MathBF16x6 {
@@ -1321,6 +1294,11 @@ FG_API int fg_conv_fwd(const fg_conv_problem* probs, int nprob, hipStream_t stre
             }
             return 0;
         }
+    }
+    if (f16 && vec && ws == 2 && g_fwd_tile < 0) {
+        // the LDS-DMA pipelined f16x3 kernel takes the wide convs (conv_f3.hip)
+        int rc = 0;
+        if (fgc::launch_fwd_f3(b, nprob, max_n, stream, &rc)) return rc;
     }
     int cfg = -1, BM, BN;
     if (x6) {

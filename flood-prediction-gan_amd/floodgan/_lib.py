@@ -71,6 +71,7 @@ SIGNATURES = {
     "fg_get_conv_math": [],
     "fg_set_fwd_tile": [C.c_int],
     "fg_set_wgrad_tile": [C.c_int],
+    "fg_set_f3_tile": [C.c_int],
     "fg_conv_wgrad": [C.POINTER(fg_wgrad_problem), C.c_void_p],
     "fg_wgrad_reduce": [C.c_void_p, C.c_int, C.POINTER(fg_weight_map), C.c_void_p, C.c_int, C.c_void_p],
     "fg_pack_weight": [C.c_void_p, C.POINTER(fg_weight_map), C.c_void_p, C.c_void_p],
@@ -150,6 +151,11 @@ def set_fwd_tile(cfg):
 def set_wgrad_tile(cfg):
     """Tuning hook: force a bf16x6 weight-gradient tile config (-1 = automatic)."""
     check(load().fg_set_wgrad_tile(int(cfg)), "set_wgrad_tile")
+
+
+def set_f3_tile(cfg):
+    """Tuning hook of the pipelined f16x3 forward kernel: -1 automatic, -2 off, 0..3 forced."""
+    check(load().fg_set_f3_tile(int(cfg)), "set_f3_tile")
 
 
 def get_conv_math():

@@ -142,6 +142,9 @@ int fg_get_conv_math(void);
 int fg_set_fwd_tile(int cfg);
 /* Same for the split-math weight-gradient kernels (0..5). */
 int fg_set_wgrad_tile(int cfg);
+/* Tuning hook of the LDS-DMA pipelined f16x3 forward kernel (conv_f3.hip, used for N > 64 when
+ * the operands allow): -1 automatic (default), -2 never use it, 0..3 force a tile config. */
+int fg_set_f3_tile(int cfg);
 
 /* Weight gradient into partial slabs (see fg_wgrad_problem). */
 int fg_conv_wgrad(const fg_wgrad_problem* prob, hipStream_t stream);

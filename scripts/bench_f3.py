@@ -1,0 +1,51 @@
+"""Micro-benchmark (GPU) of the LDS-DMA pipelined f16x3 forward kernel (conv_f3.hip) against
+the register-staged f16x3 kernel, at the real bs-8 512^2 geometries: per tile config, time and
+relative difference to the register-staged result.
+  F3_TILES=0,1,2,3 python scripts/bench_f3.py"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "flood-prediction-gan_amd"))
+import torch  # noqa: E402
+
+from floodgan import _lib as L, ops, plans as PL  # noqa: E402
+from bench_conv import make, nrel, time_it  # noqa: E402
+
+
+def main():
+    L.load()
+    L.set_conv_math("f16x3")
+    cases = {"resblock 3x3 256->256 @128": (8, 128, 256, 256, 3, 1, 1),
+             "conv3 3x3s2 128->256 @256": (8, 256, 128, 256, 3, 2, 1),
+             "conv2 3x3s2 64->128 @512": (8, 512, 64, 128, 3, 2, 1),
+             "D model.8 4x4 256->512 @64 (2N)": (16, 64, 256, 512, 4, 1, 1),
+             "D model.5 4x4s2 128->256 @128 (2N)": (16, 128, 128, 256, 4, 2, 1)}
+    tiles = [int(t) for t in os.environ.get("F3_TILES", "-1,0,1,2,3,4,5,6").split(",")]
+    for name, c in cases.items():
+        mk, flops, keep = make(*c)
+        X, w, Y = keep
+        prob = mk(True)
+        L.set_f3_tile(-2)
+        ops.conv([prob])
+        ref = Y.t.clone()
+        res = {}
+        for rep in range(2):
+            for t in [-2] + tiles:
+                L.set_f3_tile(t)
+                res.setdefault(t, []).append(time_it(lambda: ops.conv([prob])))
+        for t in [-2] + tiles:
+            L.set_f3_tile(t)
+            Y.t.zero_()
+            ops.conv([prob])
+            torch.cuda.synchronize()
+            d = nrel(Y.t, ref)
+            ms = min(res[t])
+            tag = "register-staged" if t == -2 else f"f3 tile {t}"
+            print(f"{name:36s} {tag:16s} {ms:8.3f} ms {flops / ms / 1e9:7.1f} TFLOP/s  rel diff {d:.2e}", flush=True)
+    L.set_f3_tile(-1)
+
+
+if __name__ == "__main__":
+    main()

@@ -160,6 +160,39 @@ def test_convT(cin, cout, H, conv_math):
     assert nrel(nchw(gx), gx_ref) < KTOL
 
 
+@pytest.mark.parametrize("cfg", [-2, 0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("case", [(256, 256, 3, 1, 1, "reflect", 20), (128, 256, 4, 2, 1, "constant", 22),
+                                  (64, 128, 3, 2, 1, "constant", 30), (256, 512, 4, 1, 1, "constant", 11)])
+def test_conv_f3_tiles(case, cfg):
+    """the pipelined f16x3 forward kernel (conv_f3.hip) in every tile config, ragged M / N
+    tiles included, against fp64 -- and the register-staged kernel it replaces (cfg -2)"""
+    from floodgan import _lib as L, ops, plans as PL
+    from floodgan.plans import Buf
+    cin, cout, k, s, p, mode, H = case
+    prev = L.get_conv_math()
+    L.set_conv_math("f16x3")
+    try:
+        L.set_f3_tile(cfg)
+        torch.manual_seed(3)
+        x = torch.randn(3, cin, H, H, dtype=torch.float64)
+        w = torch.randn(cout, cin, k, k, dtype=torch.float64) * 0.05
+        b = torch.randn(cout, dtype=torch.float64)
+        xin = F.pad(x, (p,) * 4, mode=mode) if p else x
+        y = F.conv2d(xin, w, b, stride=s)
+        X = buf_from(x, p, mode)
+        wd = w.float().to(DEV)
+        m = PL.wmap_conv_fwd(wd.shape, X.c)
+        Ho = PL.out_size(H, k, s, p)
+        Y = Buf.empty(3, Ho, Ho, cout, 0, DEV)
+        ops.conv([PL.conv_problem(X, p, k, s, ops.pack_weight(wd, m), m, Y, bias=b.float().to(DEV),
+                                  act=1)])
+        torch.cuda.synchronize()
+        assert nrel(nchw(Y), torch.relu(y)) < KTOL
+    finally:
+        L.set_f3_tile(-1)
+        L.set_conv_math(prev)
+
+
 # ------------------------------------------------------------------ instance norm
 
 @pytest.mark.parametrize("act,fold,residual", [(1, 0, False), (2, 0, False), (0, 0, True), (1, 1, False),
