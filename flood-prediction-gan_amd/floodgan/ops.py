@@ -87,12 +87,14 @@ def _tensor(obj):
 
 
 def _wrote(*objs):
-    """an op wrote these buffers: forget their cached absmax slots"""
+    """an op wrote these buffers: forget their cached absmax slots and split copies"""
     for o in objs:
         if o is not None:
             t = _tensor(o)
             if getattr(t, "_fg_amax", None) is not None:
                 t._fg_amax = None
+            if getattr(t, "_fg_split", None) is not None:
+                t._fg_split = None
 
 
 def absmax(t):
@@ -111,8 +113,8 @@ def absmax(t):
 
 def _amax_out(dst):
     """slot for a producer to raise to max |dst| (f16x3 only), recorded on dst"""
+    _wrote(dst)
     if not L.fwd_f16x3() and not L.wgrad_f16x3():
-        _wrote(dst)
         return None
     slot = _SLOTS.take(_dev(dst))
     _tensor(dst)._fg_amax = slot
@@ -177,8 +179,14 @@ class KernelTimer:
 _TIMER = None
 
 
+USE_WIN = True   # route eligible single convs to the row-strip kernel (fg_conv_win)
+
+
 def conv(probs, tag=None):
-    """Launch 1-4 fg_conv_problem dicts (plans.conv_problem / phase_problems) in one kernel."""
+    """Launch 1-4 fg_conv_problem dicts (plans.conv_problem / phase_problems) in one kernel
+    (the row-strip window kernel for a lone eligible 7x7 conv, see win_eligible)."""
+    if USE_WIN and len(probs) == 1 and win_eligible(probs[0]):
+        return conv_win(probs[0], tag)
     if _TIMER is not None and tag in _TIMER.tags:
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
@@ -216,6 +224,61 @@ def _conv(probs):
             s.w_absmax = wa.data_ptr()
     L.check(_lib().fg_conv_fwd(arr, len(probs), L.stream_handle()), "conv_fwd")
     _wrote(*[p["y"][0] for p in probs])
+
+
+def split_pixels(X):
+    """fg_split_pixels copy of a Buf (32 or 64 channels): fp16 h/l pieces of the scaled values,
+    the window-conv operand.  Cached on the buffer's tensor until an op writes it."""
+    t = X.t
+    cached = getattr(t, "_fg_split", None)
+    if cached is not None:
+        return cached
+    npix = X.n * X.hp * X.wp
+    out = torch.empty(npix * 2 * X.c, dtype=torch.float16, device=t.device)
+    L.check(_lib().fg_split_pixels(L.ptr(t), npix, X.c, X.wp, L.ptr(absmax(t)), L.ptr(out), L.stream_handle()),
+            "split_pixels")
+    out.absmax = absmax(t)
+    t._fg_split = out
+    return out
+
+
+def win_eligible(prob):
+    """True when fg_conv_win takes this conv (stride-1 7x7 over a 32/64-channel Buf whose full
+    border is the conv's padding, n_out within one 32/64-column tile, output rows >= 256 px)"""
+    X, off = prob["x"]
+    if not L.fwd_f16x3() or not isinstance(X, Buf) or X.c not in (32, 64):
+        return False
+    return (prob["kh"] == 7 and prob["j_valid"] == 7 * X.c and prob["jp"] == prob["j_valid"]
+            and prob["sxb"] == X.c and prob["sxa"] == prob["sxr"] == X.s_row and off == 0
+            and prob["n_out"] <= (32 if X.c == 64 else 64) and prob["m_b"] >= 256
+            and prob["w"][0].dtype == torch.float16)
+
+
+def conv_win(prob, tag=None):
+    """The row-strip window conv (fg_conv_win) of one plans.conv_problem."""
+    X, off = prob["x"]
+    xs = split_pixels(X)
+    arr = (L.fg_conv_problem * 1)()
+    s = arr[0]
+    s.x, s.w, s.y = _addr(prob["x"]), _addr(prob["w"]), _addr(prob["y"])
+    s.w_split = 2
+    s.bias = prob["bias"].data_ptr() if prob["bias"] is not None else None
+    for k in _CONV_FIELDS:
+        setattr(s, k, int(prob[k]))
+    s.x_absmax = xs.absmax.data_ptr()
+    s.w_absmax = prob["w"][0].absmax.data_ptr()
+
+    def run():
+        L.check(_lib().fg_conv_win(arr, L.ptr(xs), off // X.c, L.stream_handle()), "conv_win")
+    if _TIMER is not None and tag in _TIMER.tags:
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        run()
+        ev1.record()
+        _TIMER.events[tag].append((ev0, ev1))
+    else:
+        run()
+    _wrote(prob["y"][0])
 
 
 _WG_FIELDS = ("spn", "spa", "spb", "sxn", "sxa", "sxb", "sxr", "m_img", "m_a", "m_b", "n_a", "kh", "j_valid",

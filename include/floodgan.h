@@ -169,6 +169,20 @@ int fg_pack_weight_split(const float* w, const fg_weight_map* map, void* wps, hi
 int fg_pack_weight_f16(const float* w, const fg_weight_map* map, const float* w_absmax, void* wps,
                        hipStream_t stream);
 
+/* Pre-split operand for fg_conv_win: the npix NHWC pixels of c (32 or 64) fp32 channels at src,
+ * scaled by the power of two of the absmax slot (as fg_pack_weight_f16) and split into fp16
+ * pieces h, l; pixel p (padded-row column x = p % wp) becomes 2c fp16 whose 16-byte chunk k
+ * ([h | l] order) is stored at chunk k ^ swizzle(x).  Size npix*2c fp16. */
+int fg_split_pixels(const float* src, long long npix, int c, int wp, const float* amax, void* dst,
+                    hipStream_t stream);
+
+/* Row-strip f16x3 convolution (stride 1, 7x7, C = sxb in {32, 64}, n_out <= 32 / 64, output rows
+ * of >= 256 pixels): the same problem as fg_conv_fwd, with the input read from x_split (the
+ * fg_split_pixels copy of the buffer x points into; x_pix0 = pixel index of x's origin in it, at
+ * the start of a padded row).  Replaces the 7x7 content-head conv (models/model_architectures.py:328)
+ * and its input gradient. */
+int fg_conv_win(const fg_conv_problem* prob, const void* x_split, long long x_pix0, hipStream_t stream);
+
 /* Raise the absmax slot `out` (FG_AMAX_SHARDS floats, initialised by the caller) to bound
  * max |x[i]| over n contiguous floats (bitwise max of |x|; NaN-propagating).  The operand-
  * scale source of the f16x3 math. */

@@ -45,6 +45,31 @@ def main():
             tag = "register-staged" if t == -2 else f"f3 tile {t}"
             print(f"{name:36s} {tag:16s} {ms:8.3f} ms {flops / ms / 1e9:7.1f} TFLOP/s  rel diff {d:.2e}", flush=True)
     L.set_f3_tile(-1)
+    # the row-strip window kernel on the content head (fwd, and the input gradient's geometry)
+    from floodgan.plans import Buf
+    dev = "cuda"
+    for name, (cin_alloc, nout, pad) in {"content fwd 7x7 64->27 @512": (64, 27, 3),
+                                         "content dgrad 7x7 27(32)->64 @518": (32, 64, 6)}.items():
+        N, H = 8, 512
+        X = Buf.empty(N, H, H, cin_alloc, pad, dev)
+        X.t.uniform_(-1, 1)
+        if pad == 3:
+            w = torch.randn(nout, cin_alloc, 7, 7, device=dev) * 0.02
+            m = PL.wmap_conv_fwd(w.shape, cin_alloc)
+            Ho = H
+        else:
+            w = torch.randn(27, nout, 7, 7, device=dev) * 0.02
+            m = PL.wmap_conv_dgrad_s1(w.shape, cin_alloc)
+            Ho = H + 6
+        Y = Buf.empty(N, Ho, Ho, 32 if nout <= 32 else nout, 0, dev)
+        prob = PL.conv_problem(X, pad, 7, 1, ops.pack_weight(w, m), m, Y)
+        flops = 2.0 * N * Ho * Ho * nout * cin_alloc * 49
+        for use in (False, True, False, True):
+            ops.USE_WIN = use
+            ms = time_it(lambda: ops.conv([prob]))
+            print(f"{name:36s} {'window' if use else 'im2col':16s} {ms:8.3f} ms {flops / ms / 1e9:7.1f} TFLOP/s",
+                  flush=True)
+        ops.USE_WIN = True
 
 
 if __name__ == "__main__":

@@ -193,6 +193,55 @@ def test_conv_f3_tiles(case, cfg):
         L.set_conv_math(prev)
 
 
+@pytest.mark.parametrize("case", ["content_fwd", "content_dgrad"])
+def test_conv_window(case):
+    """the row-strip window kernel (fg_conv_win) on the content-head geometries -- 7x7 over 64
+    channels -> 27, and its input gradient 27(32) -> 64 over the 6-bordered gradient -- with
+    output rows of 256+ px (two-segment tiles, ragged last tile) against fp64"""
+    from floodgan import _lib as L, ops, plans as PL
+    from floodgan.plans import Buf
+    prev = L.get_conv_math()
+    L.set_conv_math("f16x3")
+    try:
+        torch.manual_seed(4)
+        if case == "content_fwd":
+            cin, cout, H, W = 64, 27, 6, 300
+            x = torch.randn(2, cin, H, W, dtype=torch.float64)
+            w = torch.randn(cout, cin, 7, 7, dtype=torch.float64) * 0.05
+            b = torch.randn(cout, dtype=torch.float64)
+            y = F.conv2d(F.pad(x, (3,) * 4, mode="reflect"), w, b)
+            X = buf_from(x, 3, "reflect")
+            wd = w.float().to(DEV)
+            m = PL.wmap_conv_fwd(wd.shape, X.c)
+            Y = Buf.empty(2, H, W, 32, 0, DEV)
+            prob = PL.conv_problem(X, 3, 7, 1, ops.pack_weight(wd, m), m, Y, bias=b.float().to(DEV))
+            ref = y
+        else:
+            cin, cout, H, W = 64, 27, 5, 290       # dgrad: gy has 27 (alloc 32) channels, output 64
+            gy = torch.randn(2, cout, H, W, dtype=torch.float64) * 1e-6
+            w = torch.randn(cout, cin, 7, 7, dtype=torch.float64) * 0.05
+            # gradient w.r.t. the 3-padded input = full correlation of gy with the flipped kernel
+            xp = torch.zeros(2, cin, H + 6, W + 6, dtype=torch.float64, requires_grad=True)
+            (ref,) = torch.autograd.grad(F.conv2d(xp, w), xp, gy)
+            GYP = buf_from(gy, 6, "constant", c_alloc=32)
+            wd = w.float().to(DEV)
+            md = PL.wmap_conv_dgrad_s1(wd.shape, GYP.c)
+            Y = Buf.empty(2, H + 6, W + 6, cin, 0, DEV)
+            prob = PL.conv_problem(GYP, 6, 7, 1, ops.pack_weight(wd, md), md, Y)
+        assert ops.win_eligible(prob)
+        ops.conv([prob])
+        torch.cuda.synchronize()
+        assert nrel(nchw(Y, ref.shape[1]), ref) < KTOL
+        ops.USE_WIN = False
+        Y.t.zero_()
+        ops.conv([prob])
+        torch.cuda.synchronize()
+        assert nrel(nchw(Y, ref.shape[1]), ref) < KTOL
+    finally:
+        ops.USE_WIN = True
+        L.set_conv_math(prev)
+
+
 # ------------------------------------------------------------------ instance norm
 
 @pytest.mark.parametrize("act,fold,residual", [(1, 0, False), (2, 0, False), (0, 0, True), (1, 1, False),
