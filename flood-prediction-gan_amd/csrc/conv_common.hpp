@@ -57,4 +57,7 @@ __device__ __forceinline__ void split_f16(const float (&v)[8], float s, f16x8& h
 // failed: *rc holds the launch status), 0 if the batch does not fit its constraints.
 int launch_fwd_f3(const ConvBatch& b, int nprob, int max_n, hipStream_t stream, int* rc);
 
+// Pipelined f16x3 weight-gradient kernel (conv_wgrad_f3.hip), same contract.
+int launch_wgrad_f3(const fg_wgrad_problem& p, hipStream_t stream, int* rc);
+
 }  // namespace fgc

@@ -1362,6 +1362,8 @@ FG_API int fg_conv_wgrad(const fg_wgrad_problem* prob, hipStream_t stream) {
         if (g_conv_math & FG_MATH_WGRAD_F16X3) {
             if (!p.p_absmax || !p.x_absmax)
                 return fg::fail(FG_ERR_INVALID, "fg_conv_wgrad: the f16x3 math needs p_absmax and x_absmax");
+            int rc = 0;
+            if (g_wgrad_tile < 0 && fgc::launch_wgrad_f3(p, stream, &rc)) return rc;   // conv_wgrad_f3.hip
             return launch_wgrad_split_cfg<MathF16x3>(cfg, p, vx, vp, stream);
         }
         return launch_wgrad_split_cfg<MathBF16x6>(cfg, p, vx, vp, stream);

@@ -1,0 +1,240 @@
+// Pipelined f16x3 weight-gradient kernel for the wide convolutions (the resblock 3x3 convs,
+// conv2/conv3, deconv1 and discriminator model.2/5/8 -- n_a >= 128 result rows, K >= 256):
+// convolution_backward's weight gradient of models/model_architectures.py:314-333, :407-410,
+// :426-435.
+//
+//   out[split][a][k] = sum over the split's pixels m of  P[m][a] * X[m][koff(k)]
+//
+// 256 x 256 (a x k) tiles, 8 waves as 4 (a) x 2 (k), each 64 x 128 in 16x16 blocks of
+// v_mfma_f32_16x16x32_f16 whose reduction index is 32 consecutive pixels.  Both operands stay in
+// their natural pixel-major layout: each stage loads 32 pixel rows of P (256 channels) and of the
+// X gather (256 k-columns) as float4 per slot, splits them into the scaled fp16 pieces (h, l) and
+// writes [piece][32 px][256] images; the MFMA fragments (8 consecutive pixels of one column per
+// lane) come out of ds_read_b64_tr_b16.  Write-after-barrier staging: at the top of stage t the
+// registers holding tile t+1 go to the free LDS buffer and are refilled with tile t+2, so every
+// global load has a whole stage of MFMAs to land.
+#include "conv_common.hpp"
+
+namespace {
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+constexpr int BR = 32;              // pixels per stage (the MFMA reduction depth)
+constexpr int TILE = 256;           // a and k extent of a tile
+constexpr int ROWB = TILE * 2;      // bytes per image row (256 fp16)
+constexpr int IMG = BR * ROWB;      // bytes per piece image (16 KiB)
+
+// 32-B column-pair swizzle: the 8 rows a 32-lane half of a transposed read touches land on
+// 8 distinct 32-B bank groups
+__device__ __forceinline__ int swz_tr(int row) { return ((row & 3) | (((row >> 3) & 1) << 2)) << 1; }   // in 16-B chunks
+
+__device__ __forceinline__ int img_off(int row, int col) {   // byte offset of fp16 column col of row
+    return row * ROWB + (((col >> 3) ^ swz_tr(row)) << 4) + ((col & 7) << 1);
+}
+
+__device__ __forceinline__ f16x8 tr_frag(const char* base, int a0, int a1) {
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + a0));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + a1));
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(f16x8, v);
+}
+
+__device__ __forceinline__ void split4(const f32x4& v, float s, f16x4& h, f16x4& l) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const float x = v[e] * s;
+        h[e] = (_Float16)x;
+        l[e] = (_Float16)(x - (float)h[e]);
+    }
+}
+
+__global__ void __launch_bounds__(512, 1)
+conv_wgrad_f3_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
+    constexpr int NT = 512, TM = 4, TN = 8;         // wave tile 64 (a) x 128 (k)
+    constexpr int SLOTS = BR * TILE / 4;            // float4 slots per operand per stage (2048)
+    constexpr int SPT = SLOTS / NT;                 // per thread (4)
+    constexpr int kOOB = 0x7fffffff;
+    __shared__ __attribute__((aligned(1024))) char smem[2 * 4 * IMG];   // [buf][P h, P l, X h, X l]
+
+    // wave-uniform by construction (readfirstlane): the pixel walks below live in SGPRs
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wa = wave >> 1, wk = wave & 1;
+    const int wid = fg::xcd_remap(blockIdx.x, gridDim.x);
+    const int ntile = tiles_a * tiles_k;
+    const int split = wid / ntile;
+    const int tile = wid - split * ntile;
+    const int ta = tile / tiles_k, tk = tile - (tile / tiles_k) * tiles_k;
+    const int a0 = ta * TILE, k0 = tk * TILE;
+    const int mab = P.m_a * P.m_b;
+    const int M = P.m_img * mab;
+    const int mbeg = split * P.m_chunk;
+    const int mend = min(M, mbeg + P.m_chunk);
+    const int K = P.kh * P.j_valid;
+    const int nst = mend > mbeg ? (mend - mbeg + BR - 1) / BR : 0;
+
+    const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc((void*)P.p, 0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)P.x, 0, 0x7fffffff, 0x00020000);
+    const float sp = fgc::pow2_scale(P.p_absmax);
+    const float sx = fgc::pow2_scale(P.x_absmax);
+
+    // ---- staging slots: slot s = tid + i*NT -> pixel row s / 64 of the stage, column group (s % 64)*4.
+    // Each thread's slots share one column group and walk pixel rows i*8 + tid/64, advanced by BR.
+    const int col = (tid & 63) * 4;
+    const int prow0 = wave;                         // + 8i
+    const bool p_col_ok = a0 + col < P.n_a;         // n_a % 4 == 0 (host check)
+    int x_koff = -1;                                // X column offset of this slot's k (k % 4 == 0 group)
+    {
+        const int k = k0 + col;
+        if (k < K) {
+            const int r = k / P.j_valid;
+            x_koff = r * (int)P.sxr + (k - r * P.j_valid);
+        }
+    }
+    // pixel walks (img, a, b) of the SPT slot rows
+    const int i32 = BR / mab, a32 = (BR - i32 * mab) / P.m_b, b32 = BR - i32 * mab - a32 * P.m_b;
+    int wm[SPT], wi[SPT], wa_[SPT], wb[SPT];
+#pragma unroll
+    for (int i = 0; i < SPT; ++i) {
+        wm[i] = mbeg + prow0 + 8 * i;
+        fgc::decomp(min(wm[i], M - 1), P.m_b, mab, wi[i], wa_[i], wb[i]);
+    }
+    f32x4 rp[SPT], rx[SPT];
+    auto load = [&]() {
+#pragma unroll
+        for (int i = 0; i < SPT; ++i) {
+            const bool ok = wm[i] < mend;
+            const int pb = wi[i] * (int)P.spn + wa_[i] * (int)P.spa + wb[i] * (int)P.spb + a0 + col;
+            const int xb = wi[i] * (int)P.sxn + wa_[i] * (int)P.sxa + wb[i] * (int)P.sxb + x_koff;
+            rp[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(pr, ok && p_col_ok ? pb * 4 : kOOB, 0, 0));
+            rx[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, ok && x_koff >= 0 ? xb * 4 : kOOB, 0, 0));
+            // advance by BR pixels
+            wm[i] += BR;
+            wb[i] += b32;
+            const int cb = wb[i] >= P.m_b;
+            wb[i] -= cb ? P.m_b : 0;
+            wa_[i] += a32 + cb;
+            const int ca = wa_[i] >= P.m_a;
+            wa_[i] -= ca ? P.m_a : 0;
+            wi[i] += i32 + ca;
+        }
+    };
+    auto store = [&](int buf) {
+        char* b = smem + buf * 4 * IMG;
+#pragma unroll
+        for (int i = 0; i < SPT; ++i) {
+            const int o = img_off(prow0 + 8 * i, col);
+            f16x4 h, l;
+            split4(rp[i], sp, h, l);
+            *reinterpret_cast<f16x4*>(b + o) = h;
+            *reinterpret_cast<f16x4*>(b + IMG + o) = l;
+            split4(rx[i], sx, h, l);
+            *reinterpret_cast<f16x4*>(b + 2 * IMG + o) = h;
+            *reinterpret_cast<f16x4*>(b + 3 * IMG + o) = l;
+        }
+    };
+
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // transposed-read lane roles: group g reads pixel rows 8g + q (and 8g + 4 + q), lane 4q+p of
+    // the group addresses columns 4p..4p+3 of the 16-column block
+    const int g = lane >> 4, q = (lane >> 2) & 3, p4 = (lane & 3) * 4;
+    auto compute = [&](int buf) {
+        const char* b = smem + buf * 4 * IMG;
+        f16x8 ah[TM], al[TM];
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) {
+            const int c = wa * 64 + tm * 16 + p4;
+            const int o0 = img_off(8 * g + q, c), o1 = img_off(8 * g + 4 + q, c);
+            ah[tm] = tr_frag(b, o0, o1);
+            al[tm] = tr_frag(b + IMG, o0, o1);
+        }
+#pragma unroll
+        for (int t0 = 0; t0 < TN; t0 += 4) {
+            f16x8 bh[4], bl[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int c = wk * 128 + (t0 + t) * 16 + p4;
+                const int o0 = img_off(8 * g + q, c), o1 = img_off(8 * g + 4 + q, c);
+                bh[t] = tr_frag(b + 2 * IMG, o0, o1);
+                bl[t] = tr_frag(b + 3 * IMG, o0, o1);
+            }
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+                    acc[tm][t0 + t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[tm], bh[t], acc[tm][t0 + t], 0, 0, 0);
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+                    acc[tm][t0 + t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[tm], bl[t], acc[tm][t0 + t], 0, 0, 0);
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+                    acc[tm][t0 + t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[tm], bh[t], acc[tm][t0 + t], 0, 0, 0);
+        }
+    };
+
+    // ---- write-after-barrier pipeline (one register set; loads past the range read zeros)
+    load();
+    store(0);
+    load();
+    __syncthreads();
+    for (int st = 0; st < nst; ++st) {
+        const int cur = st & 1;
+        if (st + 1 < nst) store(cur ^ 1);
+        load();
+        __builtin_amdgcn_sched_barrier(0);
+        compute(cur);
+        __syncthreads();
+    }
+
+    // ---- epilogue: scaled fp32 slab rows a, columns k
+    float* out = P.out + (size_t)split * P.n_a * K;
+    const float osc = 1.f / (sp * sx);
+    const int fr = lane & 15;
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {
+            const int a = a0 + wa * 64 + tm * 16 + 4 * g + reg;
+            if (a >= P.n_a) continue;
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) {
+                const int k = k0 + wk * 128 + tn * 16 + fr;
+                if (k < K) out[(size_t)a * K + k] = acc[tm][tn][reg] * osc;
+            }
+        }
+}
+
+}  // namespace
+
+int g_wgrad_f3 = 1;   // fg_set_wgrad_f3 (A/B hook)
+
+namespace fgc {
+
+// Returns 1 when the pipelined kernel took the problem (status in *rc), 0 when it does not apply.
+int launch_wgrad_f3(const fg_wgrad_problem& p, hipStream_t stream, int* rc) {
+    if (!g_wgrad_f3 || p.n_a < 256 || p.kh * p.j_valid < 256 || p.n_a % 4 || p.j_valid % 4 || !p.p_absmax ||
+        !p.x_absmax || ((uintptr_t)p.p & 15) || ((uintptr_t)p.x & 15) || (p.spn | p.spa | p.spb) % 4 ||
+        (p.sxn | p.sxa | p.sxb | p.sxr) % 4)
+        return 0;
+    const int ta = (p.n_a + TILE - 1) / TILE, tk = (p.kh * p.j_valid + TILE - 1) / TILE;
+    hipLaunchKernelGGL(conv_wgrad_f3_kernel, dim3(ta * tk * p.splits), dim3(512), 0, stream, p, ta, tk);
+    *rc = fg::launched("conv_wgrad_f3");
+    return 1;
+}
+
+}  // namespace fgc
+
+FG_API int fg_set_wgrad_f3(int on) {
+    g_wgrad_f3 = on != 0;
+    return 0;
+}

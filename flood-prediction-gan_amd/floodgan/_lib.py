@@ -72,6 +72,7 @@ SIGNATURES = {
     "fg_set_fwd_tile": [C.c_int],
     "fg_set_wgrad_tile": [C.c_int],
     "fg_set_f3_tile": [C.c_int],
+    "fg_set_wgrad_f3": [C.c_int],
     "fg_conv_wgrad": [C.POINTER(fg_wgrad_problem), C.c_void_p],
     "fg_wgrad_reduce": [C.c_void_p, C.c_int, C.POINTER(fg_weight_map), C.c_void_p, C.c_int, C.c_void_p],
     "fg_pack_weight": [C.c_void_p, C.POINTER(fg_weight_map), C.c_void_p, C.c_void_p],
@@ -158,6 +159,20 @@ def set_wgrad_tile(cfg):
 def set_f3_tile(cfg):
     """Tuning hook of the pipelined f16x3 forward kernel: -1 automatic, -2 off, 0..3 forced."""
     check(load().fg_set_f3_tile(int(cfg)), "set_f3_tile")
+
+
+_WGRAD_F3 = True
+
+
+def set_wgrad_f3(on):
+    """A/B hook of the pipelined f16x3 weight-gradient kernel."""
+    global _WGRAD_F3
+    check(load().fg_set_wgrad_f3(int(bool(on))), "set_wgrad_f3")
+    _WGRAD_F3 = bool(on)
+
+
+def wgrad_f3_on():
+    return _WGRAD_F3
 
 
 def get_conv_math():

@@ -7,7 +7,7 @@ import ctypes as C
 import torch
 
 from . import _lib as L
-from .plans import Buf, packed_numel, slab_numel
+from .plans import Buf, f3_wgrad_eligible, packed_numel, slab_numel, wgrad_splits
 
 EPS = 1e-5
 
@@ -288,6 +288,11 @@ _WG_FIELDS = ("spn", "spa", "spb", "sxn", "sxa", "sxb", "sxr", "m_img", "m_a", "
 def wgrad(prob, wmap, dw, accumulate=False):
     """weight gradient into the PyTorch-layout tensor dw (overwritten, or += if accumulate)"""
     dev = _dev(prob["p"][0])
+    if L.wgrad_f16x3() and L.wgrad_f3_on() and f3_wgrad_eligible(prob):
+        # re-split the pixel range for the pipelined kernel's tiles (one workgroup per CU)
+        splits, chunk = wgrad_splits(prob["n_a"], prob["kh"] * prob["j_valid"],
+                                     prob["m_img"] * prob["m_a"] * prob["m_b"], f3=True)
+        prob = dict(prob, splits=splits, m_chunk=chunk)
     slab = torch.empty(slab_numel(prob), dtype=torch.float32, device=dev)
     s = L.fg_wgrad_problem()
     s.p, s.x, s.out = _addr(prob["p"]), _addr(prob["x"]), slab.data_ptr()

@@ -220,13 +220,27 @@ def wgrad_tile(n_a):
     return (128, 128) if n_a > 64 else ((64, 256) if n_a > 32 else (32, 256))
 
 
-def wgrad_splits(n_a, K, M):
-    ba, bk = wgrad_tile(n_a)
+F3_WG_BLOCKS = 256  # the pipelined f16x3 weight-gradient kernel: 128 KiB LDS, one workgroup per CU
+
+
+def wgrad_splits(n_a, K, M, f3=False):
+    """(splits, pixels per split) of a weight-gradient problem: about one resident wave of
+    workgroups.  f3: the pipelined f16x3 kernel's 256 x 256 tiles and 32-pixel stages."""
+    if f3:
+        ba, bk, blocks, q = 256, 256, F3_WG_BLOCKS, 32
+    else:
+        (ba, bk), blocks, q = wgrad_tile(n_a), WG_BLOCKS, 16
     tiles = -(-n_a // ba) * -(-K // bk)
-    splits = max(1, min(WG_BLOCKS // max(tiles, 1), -(-M // 256)))
-    chunk = rup(-(-M // splits), 16)
+    splits = max(1, min(blocks // max(tiles, 1), -(-M // 256)))
+    chunk = rup(-(-M // splits), q)
     splits = -(-M // chunk)
     return splits, chunk
+
+
+def f3_wgrad_eligible(prob):
+    """the shapes the pipelined f16x3 weight-gradient kernel takes (conv_wgrad_f3.hip)"""
+    return prob["n_a"] >= 256 and prob["kh"] * prob["j_valid"] >= 256 and prob["n_a"] % 4 == 0 \
+        and prob["j_valid"] % 4 == 0
 
 
 def wgrad_problem(P, n_a, X, x_off_yx, sxa, sxb, k, slab=None):

@@ -145,6 +145,9 @@ int fg_set_wgrad_tile(int cfg);
 /* Tuning hook of the LDS-DMA pipelined f16x3 forward kernel (conv_f3.hip, used for N > 64 when
  * the operands allow): -1 automatic (default), -2 never use it, 0..3 force a tile config. */
 int fg_set_f3_tile(int cfg);
+/* A/B hook of the pipelined f16x3 weight-gradient kernel (conv_wgrad_f3.hip, n_a >= 256): 1 on
+ * (default), 0 off. */
+int fg_set_wgrad_f3(int on);
 
 /* Weight gradient into partial slabs (see fg_wgrad_problem). */
 int fg_conv_wgrad(const fg_wgrad_problem* prob, hipStream_t stream);

@@ -45,6 +45,33 @@ def main():
             tag = "register-staged" if t == -2 else f"f3 tile {t}"
             print(f"{name:36s} {tag:16s} {ms:8.3f} ms {flops / ms / 1e9:7.1f} TFLOP/s  rel diff {d:.2e}", flush=True)
     L.set_f3_tile(-1)
+    # weight gradients: pipelined f16x3 kernel vs the register-staged one
+    for name, c in {"resblock wgrad 3x3 256x256 @128": (8, 128, 256, 256, 3, 1, 1),
+                    "D model.8 wgrad 4x4 256->512 @64 (2N)": (16, 64, 256, 512, 4, 1, 1),
+                    "conv3 wgrad 3x3s2 128->256 @256": (8, 256, 128, 256, 3, 2, 1)}.items():
+        mk, flops, keep = make(*c)
+        X, w, Y = keep
+        Y.t.uniform_(-1, 1)
+        N, H, Cin, Cout, k, s_, p_ = c
+        wprob = PL.wgrad_conv(Y, X, p_, k, s_, Cout)
+        wm = PL.wmap_wgrad(w.shape, True, X.c, k)
+        dw = torch.empty_like(w)
+        res = {}
+        for rep in range(2):
+            for on in (0, 1):
+                L.set_wgrad_f3(on)
+                res.setdefault(on, []).append(time_it(lambda: ops.wgrad(wprob, wm, dw)))
+        outs = {}
+        for on in (0, 1):
+            L.set_wgrad_f3(on)
+            ops.wgrad(wprob, wm, dw)
+            torch.cuda.synchronize()
+            outs[on] = dw.clone()
+        for on in (0, 1):
+            ms = min(res[on])
+            print(f"{name:36s} {'f3' if on else 'register-staged':16s} {ms:8.3f} ms {flops / ms / 1e9:7.1f} TFLOP/s"
+                  f"  rel diff {nrel(outs[on], outs[0]):.2e}", flush=True)
+        L.set_wgrad_f3(1)
     # the row-strip window kernel on the content head (fwd, and the input gradient's geometry)
     from floodgan.plans import Buf
     dev = "cuda"

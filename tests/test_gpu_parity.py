@@ -193,6 +193,38 @@ def test_conv_f3_tiles(case, cfg):
         L.set_conv_math(prev)
 
 
+@pytest.mark.parametrize("on", [0, 1])
+@pytest.mark.parametrize("case", [(256, 256, 3, 1, 1, "reflect", 40), (128, 256, 4, 2, 1, "constant", 34),
+                                  (256, 512, 4, 1, 1, "constant", 17)])
+def test_wgrad_f3(case, on):
+    """the pipelined f16x3 weight-gradient kernel (conv_wgrad_f3.hip; on=0: the register-staged
+    kernel) on multi-split problems with ragged pixel chunks, against fp64"""
+    from floodgan import _lib as L, ops, plans as PL
+    cin, cout, k, s, p, mode, H = case
+    prev = L.get_conv_math()
+    L.set_conv_math("f16x3")
+    L.set_wgrad_f3(on)
+    try:
+        torch.manual_seed(5)
+        x = torch.randn(3, cin, H, H, dtype=torch.float64)
+        w = torch.randn(cout, cin, k, k, dtype=torch.float64) * 0.05
+        xin = F.pad(x, (p,) * 4, mode=mode) if p else x
+        Ho = PL.out_size(H, k, s, p)
+        gy = torch.randn(3, cout, Ho, Ho, dtype=torch.float64) * 1e-5
+        gw_ref = torch.nn.grad.conv2d_weight(xin, w.shape, gy, stride=s)
+        X = buf_from(x, p, mode)
+        GY = buf_from(gy, 0, "constant")
+        dw = torch.empty(w.shape, dtype=torch.float32, device=DEV)
+        prob = PL.wgrad_conv(GY, X, p, k, s, cout)
+        assert prob["splits"] > 1
+        ops.wgrad(prob, PL.wmap_wgrad(w.shape, True, X.c, k), dw)
+        torch.cuda.synchronize()
+        assert nrel(dw, gw_ref) < KTOL
+    finally:
+        L.set_wgrad_f3(1)
+        L.set_conv_math(prev)
+
+
 @pytest.mark.parametrize("case", ["content_fwd", "content_dgrad"])
 def test_conv_window(case):
     """the row-strip window kernel (fg_conv_win) on the content-head geometries -- 7x7 over 64
