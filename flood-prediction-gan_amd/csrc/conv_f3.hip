@@ -65,15 +65,23 @@ __device__ __forceinline__ void dma_stage(char* sb, int wave, __amdgpu_buffer_rs
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
+    static_assert(N >= 0 && N <= 15, "vmcnt immediate");
     if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
     else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
     else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
     else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if constexpr (N == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
     else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if constexpr (N == 9) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+    else if constexpr (N == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    else if constexpr (N == 11) asm volatile("s_waitcnt vmcnt(11)" ::: "memory");
     else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-    else static_assert(N < 0, "add the vmcnt immediate");
+    else if constexpr (N == 13) asm volatile("s_waitcnt vmcnt(13)" ::: "memory");
+    else if constexpr (N == 14) asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
+    else if constexpr (N == 15) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
 }
 
 template <int BM, int BN, int WM, int WN, int NS>
@@ -293,7 +301,7 @@ int launch_fwd_f3(const ConvBatch& b, int nprob, int max_n, hipStream_t stream, 
             p.m_img * p.m_a * p.m_b < 1)
             return 0;
     }
-    int cfg = g_f3_tile >= 0 ? g_f3_tile : (max_n > 128 ? 4 : max_n > 64 ? 6 : -1);
+    int cfg = g_f3_tile >= 0 ? g_f3_tile : (max_n > 128 ? 4 : max_n > 64 ? 6 : max_n > 32 ? 9 : -1);
     switch (cfg) {
         case 0: *rc = launch_cfg<128, 256, 32, 128>(b, nprob, stream); return 1;
         case 1: *rc = launch_cfg<256, 128, 64, 64>(b, nprob, stream); return 1;
@@ -302,6 +310,9 @@ int launch_fwd_f3(const ConvBatch& b, int nprob, int max_n, hipStream_t stream, 
         case 4: *rc = launch_cfg<256, 256, 32, 256, 2>(b, nprob, stream); return 1;
         case 5: *rc = launch_cfg<256, 256, 64, 128, 2>(b, nprob, stream); return 1;
         case 6: *rc = launch_cfg<256, 128, 32, 128, 2>(b, nprob, stream); return 1;
+        case 7: *rc = launch_cfg<256, 64, 32, 64, 3>(b, nprob, stream); return 1;
+        case 8: *rc = launch_cfg<256, 64, 64, 64, 3>(b, nprob, stream); return 1;
+        case 9: *rc = launch_cfg<128, 64, 32, 64, 3>(b, nprob, stream); return 1;
         default: return 0;
     }
 }
@@ -309,7 +320,7 @@ int launch_fwd_f3(const ConvBatch& b, int nprob, int max_n, hipStream_t stream, 
 }  // namespace fgc
 
 FG_API int fg_set_f3_tile(int cfg) {
-    if (cfg < -2 || cfg > 6) return fg::fail(FG_ERR_INVALID, "fg_set_f3_tile: %d", cfg);
+    if (cfg < -2 || cfg > 9) return fg::fail(FG_ERR_INVALID, "fg_set_f3_tile: %d", cfg);
     g_f3_tile = cfg;
     return 0;
 }

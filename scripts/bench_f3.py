@@ -21,7 +21,8 @@ def main():
              "conv3 3x3s2 128->256 @256": (8, 256, 128, 256, 3, 2, 1),
              "conv2 3x3s2 64->128 @512": (8, 512, 64, 128, 3, 2, 1),
              "D model.8 4x4 256->512 @64 (2N)": (16, 64, 256, 512, 4, 1, 1),
-             "D model.5 4x4s2 128->256 @128 (2N)": (16, 128, 128, 256, 4, 2, 1)}
+             "D model.5 4x4s2 128->256 @128 (2N)": (16, 128, 128, 256, 4, 2, 1),
+             "3x3 128->64 @256 (N=64 class)": (8, 256, 128, 64, 3, 1, 1)}
     tiles = [int(t) for t in os.environ.get("F3_TILES", "-1,0,1,2,3,4,5,6").split(",")]
     for name, c in cases.items():
         mk, flops, keep = make(*c)

@@ -160,9 +160,10 @@ def test_convT(cin, cout, H, conv_math):
     assert nrel(nchw(gx), gx_ref) < KTOL
 
 
-@pytest.mark.parametrize("cfg", [-2, 0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("cfg", [-2, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
 @pytest.mark.parametrize("case", [(256, 256, 3, 1, 1, "reflect", 20), (128, 256, 4, 2, 1, "constant", 22),
-                                  (64, 128, 3, 2, 1, "constant", 30), (256, 512, 4, 1, 1, "constant", 11)])
+                                  (64, 128, 3, 2, 1, "constant", 30), (256, 512, 4, 1, 1, "constant", 11),
+                                  (128, 64, 3, 1, 1, "constant", 21)])
 def test_conv_f3_tiles(case, cfg):
     """the pipelined f16x3 forward kernel (conv_f3.hip) in every tile config, ragged M / N
     tiles included, against fp64 -- and the register-staged kernel it replaces (cfg -2)"""
