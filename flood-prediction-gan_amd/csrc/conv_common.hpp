@@ -53,6 +53,15 @@ __device__ __forceinline__ void split_f16(const float (&v)[8], float s, f16x8& h
     }
 }
 
+// 16-B chunk swizzle of a pre-split pixel (fg_split_pixels): chunk k of [h | l] of the pixel in
+// padded column x is stored at k ^ swz_pixel(x) -- conflict-free shifted fragment reads
+// (exhaustive search over the ds_read_b128 lane groups and every row offset)
+template <int C>
+__device__ __forceinline__ int swz_pixel(int x) {
+    if constexpr (C == 64) return (x & 7) << 1;          // 16 chunks per 256-B pixel
+    else return ((x >> 1) & 3) << 1;                     // 8 chunks per 128-B pixel (C == 32)
+}
+
 // Pipelined f16x3 forward kernel (conv_f3.hip).  Returns 1 if it took the batch (launched or
 // failed: *rc holds the launch status), 0 if the batch does not fit its constraints.
 int launch_fwd_f3(const ConvBatch& b, int nprob, int max_n, hipStream_t stream, int* rc);

@@ -24,12 +24,10 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, int v
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds, 16, voff, soff, 0, 0);
 }
 
-// chunk swizzles (exhaustive search over the ds_read_b128 lane groups and every row offset)
+// chunk swizzles (exhaustive search over the ds_read_b128 lane groups and every row offset):
+// strip pixels use fgc::swz_pixel (the layout fg_split_pixels writes), weight rows this one
 template <int C>
-__device__ __forceinline__ int swz_strip(int x) {       // pixel column x -> XOR of its 16-B chunk index
-    if constexpr (C == 64) return (x & 7) << 1;          // 16 chunks per 256-B pixel
-    else return ((x >> 1) & 3) << 1;                     // 8 chunks per 128-B pixel (C == 32)
-}
+__device__ __forceinline__ int swz_strip(int x) { return fgc::swz_pixel<C>(x); }
 template <int C>
 __device__ __forceinline__ int swz_wrow(int n) {         // weight image row n
     if constexpr (C == 64) return (n >> 1) & 7;          // 8 chunks per 128-B row

@@ -81,6 +81,8 @@ SIGNATURES = {
     "fg_absmax": [C.c_void_p, C.c_longlong, C.c_void_p, C.c_void_p],
     "fg_split_pixels": [C.c_void_p, C.c_longlong, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p],
     "fg_conv_win": [C.POINTER(fg_conv_problem), C.c_void_p, C.c_longlong, C.c_void_p],
+    "fg_conv_wgrad_win": [C.POINTER(fg_wgrad_problem), C.c_void_p, C.c_longlong, C.c_int, C.c_int, C.c_void_p,
+                          C.c_longlong, C.c_int, C.c_void_p],
     "fg_pack_input": [fg_sview, C.c_int, fg_sview, C.c_int, fg_view, C.c_int, C.c_int, C.c_int, C.c_void_p],
     "fg_zero_border": [fg_view, C.c_void_p],
     "fg_fold_add": [fg_view, C.c_int, fg_view, fg_view, C.c_void_p],

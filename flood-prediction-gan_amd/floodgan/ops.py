@@ -250,7 +250,7 @@ def win_eligible(prob):
         return False
     return (prob["kh"] == 7 and prob["j_valid"] == 7 * X.c and prob["jp"] == prob["j_valid"]
             and prob["sxb"] == X.c and prob["sxa"] == prob["sxr"] == X.s_row and off == 0
-            and prob["n_out"] <= (32 if X.c == 64 else 64) and prob["m_b"] >= 256
+            and prob["n_out"] <= 32 and X.c == 64 and prob["m_b"] >= 256
             and prob["w"][0].dtype == torch.float16)
 
 
@@ -281,6 +281,40 @@ def conv_win(prob, tag=None):
     _wrote(prob["y"][0])
 
 
+WIN_WGRAD_SPLITS = 146   # x 7 kernel rows = ~1024 workgroups of 4 waves (several resident per CU)
+
+
+def wgrad_win_eligible(prob):
+    """the content-head weight gradient fg_conv_wgrad_win takes: 7x7 over a 64-channel Buf gathered
+    from a padded-row start, gradient a 32-channel Buf, n_a <= 32, output rows a multiple of 32 px"""
+    P, poff = prob["p"]
+    X, xoff = prob["x"]
+    return (isinstance(P, Buf) and isinstance(X, Buf) and P.c == 32 and X.c == 64 and prob["kh"] == 7
+            and prob["j_valid"] == 7 * 64 and prob["sxb"] == 64 and prob["sxa"] == prob["sxr"] == X.s_row
+            and prob["spb"] == 32 and prob["spa"] == P.s_row and prob["n_a"] <= 32 and prob["m_b"] % 32 == 0
+            and (xoff // X.c) % X.wp == 0 and xoff % X.c == 0 and poff % P.c == 0)
+
+
+def _wgrad_win(prob, wmap, dw, accumulate):
+    P, poff = prob["p"]
+    X, xoff = prob["x"]
+    ps, xs = split_pixels(P), split_pixels(X)
+    prob = dict(prob, splits=WIN_WGRAD_SPLITS, m_chunk=1)
+    slab = torch.empty(slab_numel(prob), dtype=torch.float32, device=P.t.device)
+    s = L.fg_wgrad_problem()
+    s.p, s.x, s.out = _addr(prob["p"]), _addr(prob["x"]), slab.data_ptr()
+    for k in _WG_FIELDS:
+        setattr(s, k, int(prob[k]))
+    s.p_absmax, s.x_absmax = ps.absmax.data_ptr(), xs.absmax.data_ptr()
+    st = L.stream_handle()
+    p_pix0 = poff // P.c
+    L.check(_lib().fg_conv_wgrad_win(C.byref(s), L.ptr(ps), p_pix0, p_pix0 % P.wp, P.wp, L.ptr(xs), xoff // X.c,
+                                     X.wp, st), "conv_wgrad_win")
+    m = wmap_struct(wmap)
+    L.check(_lib().fg_wgrad_reduce(L.ptr(slab), int(prob["splits"]), C.byref(m), L.ptr(dw), int(accumulate), st),
+            "wgrad_reduce")
+
+
 _WG_FIELDS = ("spn", "spa", "spb", "sxn", "sxa", "sxb", "sxr", "m_img", "m_a", "m_b", "n_a", "kh", "j_valid",
               "splits", "m_chunk")
 
@@ -288,6 +322,8 @@ _WG_FIELDS = ("spn", "spa", "spb", "sxn", "sxa", "sxb", "sxr", "m_img", "m_a", "
 def wgrad(prob, wmap, dw, accumulate=False):
     """weight gradient into the PyTorch-layout tensor dw (overwritten, or += if accumulate)"""
     dev = _dev(prob["p"][0])
+    if USE_WIN and L.wgrad_f16x3() and wgrad_win_eligible(prob):
+        return _wgrad_win(prob, wmap, dw, accumulate)
     if L.wgrad_f16x3() and L.wgrad_f3_on() and f3_wgrad_eligible(prob):
         # re-split the pixel range for the pipelined kernel's tiles (one workgroup per CU)
         splits, chunk = wgrad_splits(prob["n_a"], prob["kh"] * prob["j_valid"],

@@ -186,6 +186,15 @@ int fg_split_pixels(const float* src, long long npix, int c, int wp, const float
  * and its input gradient. */
 int fg_conv_win(const fg_conv_problem* prob, const void* x_split, long long x_pix0, hipStream_t stream);
 
+/* Row-strip f16x3 weight gradient of the 7x7 64 -> 32(27) content-head conv (the fg_wgrad_problem of
+ * its generic form: p = 32-channel gradient, x = 64-channel input gather, output rows of a multiple of
+ * 32 px), reading both operands from their fg_split_pixels copies: p_split (gradient; p_pix0 = pixel
+ * index of p's origin, p_col0 = its padded column, wp_p pixels per padded row) and x_split (input;
+ * x_pix0 at a padded-row start, wp_x).  Writes prob->splits slabs for fg_wgrad_reduce.  Replaces the
+ * content-head weight gradient of convolution_backward (models/model_architectures.py:328). */
+int fg_conv_wgrad_win(const fg_wgrad_problem* prob, const void* p_split, long long p_pix0, int p_col0,
+                      int wp_p, const void* x_split, long long x_pix0, int wp_x, hipStream_t stream);
+
 /* Raise the absmax slot `out` (FG_AMAX_SHARDS floats, initialised by the caller) to bound
  * max |x[i]| over n contiguous floats (bitwise max of |x|; NaN-propagating).  The operand-
  * scale source of the f16x3 math. */

@@ -98,6 +98,24 @@ def main():
             print(f"{name:36s} {'window' if use else 'im2col':16s} {ms:8.3f} ms {flops / ms / 1e9:7.1f} TFLOP/s",
                   flush=True)
         ops.USE_WIN = True
+    # content-head weight gradient: row-strip kernel vs the generic f16x3 one
+    N, H = 8, 512
+    X = Buf.empty(N, H, H, 64, 3, dev)
+    X.t.uniform_(-1, 1)
+    GY = Buf.empty(N, H, H, 32, 6, dev)
+    GY.t.uniform_(-1, 1)
+    wprob = PL.wgrad_conv(GY, X, 3, 7, 1, 27)
+    wm = PL.wmap_wgrad((27, 64, 7, 7), True, 64, 7)
+    dw = torch.empty(27, 64, 7, 7, device=dev)
+    flops = 2.0 * N * H * H * 27 * 64 * 49
+    outs = {}
+    for use in (False, True, False, True):
+        ops.USE_WIN = use
+        ms = time_it(lambda: ops.wgrad(wprob, wm, dw))
+        outs[use] = dw.clone()
+        print(f"{'content wgrad 7x7 64->27 @512':36s} {'window' if use else 'im2col':16s} {ms:8.3f} ms "
+              f"{flops / ms / 1e9:7.1f} TFLOP/s  rel diff {nrel(outs[use], outs[False]):.2e}", flush=True)
+    ops.USE_WIN = True
 
 
 if __name__ == "__main__":

@@ -2,7 +2,7 @@
 # f3 kernel iteration: its parity tests, the micro-benchmark, the full GPU suite, one bench.
 cd "$(dirname "$0")/.." || exit 1
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -k "f3_tiles or window or wgrad_f3" -x -q --timeout 120 --timeout-method thread > gpurun_out/f3_tests.log 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -k "f3_tiles or window or wgrad_f3 or wgrad_window" -x -q --timeout 120 --timeout-method thread > gpurun_out/f3_tests.log 2>&1
 rc=$?; echo "f3 tests rc=$rc"; tail -5 gpurun_out/f3_tests.log; [ $rc -eq 0 ] || exit $rc
 (cd scripts && timeout -k 10 300 python -u bench_f3.py) > gpurun_out/bench_f3.log 2>&1
 rc=$?; echo "bench_f3 rc=$rc"; cat gpurun_out/bench_f3.log; [ $rc -eq 0 ] || exit $rc

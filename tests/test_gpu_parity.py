@@ -226,6 +226,39 @@ def test_wgrad_f3(case, on):
         L.set_conv_math(prev)
 
 
+def test_wgrad_window():
+    """the row-strip content-head weight gradient (fg_conv_wgrad_win): gradient 27(32) channels
+    with its 6-wide zero border, input 64 channels reflect-padded by 3, against fp64 and against
+    the generic f16x3 weight-gradient kernel"""
+    from floodgan import _lib as L, ops, plans as PL
+    prev = L.get_conv_math()
+    L.set_conv_math("f16x3")
+    try:
+        torch.manual_seed(6)
+        H, W = 5, 288
+        x = torch.randn(2, 64, H, W, dtype=torch.float64)
+        gy = torch.randn(2, 27, H, W, dtype=torch.float64) * 1e-4
+        w = torch.zeros(27, 64, 7, 7, dtype=torch.float64)
+        gw_ref = torch.nn.grad.conv2d_weight(F.pad(x, (3,) * 4, mode="reflect"), w.shape, gy)
+        X = buf_from(x, 3, "reflect")
+        GY = buf_from(gy, 6, "constant", c_alloc=32)
+        prob = PL.wgrad_conv(GY, X, 3, 7, 1, 27)
+        assert ops.wgrad_win_eligible(prob)
+        wm = PL.wmap_wgrad(w.shape, True, X.c, 7)
+        dw = torch.empty(w.shape, dtype=torch.float32, device=DEV)
+        ops.wgrad(prob, wm, dw)
+        torch.cuda.synchronize()
+        assert nrel(dw, gw_ref) < KTOL
+        ops.USE_WIN = False
+        dw2 = torch.empty_like(dw)
+        ops.wgrad(prob, wm, dw2)
+        torch.cuda.synchronize()
+        assert nrel(dw2, gw_ref) < KTOL
+    finally:
+        ops.USE_WIN = True
+        L.set_conv_math(prev)
+
+
 @pytest.mark.parametrize("case", ["content_fwd", "content_dgrad"])
 def test_conv_window(case):
     """the row-strip window kernel (fg_conv_win) on the content-head geometries -- 7x7 over 64
@@ -261,8 +294,10 @@ def test_conv_window(case):
             md = PL.wmap_conv_dgrad_s1(wd.shape, GYP.c)
             Y = Buf.empty(2, H + 6, W + 6, cin, 0, DEV)
             prob = PL.conv_problem(GYP, 6, 7, 1, ops.pack_weight(wd, md), md, Y)
-        assert ops.win_eligible(prob)
-        ops.conv([prob])
+        # the step routes the forward here; the input gradient (N = 64) runs faster on the
+        # pipelined im2col kernel, so it is called directly
+        assert ops.win_eligible(prob) == (case == "content_fwd")
+        ops.conv_win(prob)
         torch.cuda.synchronize()
         assert nrel(nchw(Y, ref.shape[1]), ref) < KTOL
         ops.USE_WIN = False
