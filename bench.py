@@ -33,6 +33,25 @@ def resblock_conv_flops(batch, res):
     return 2.0 * m * 256 * (256 * 9)
 
 
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "round1", "r1h_pmc_resblock_fwd.json")
+
+
+def pmc_traffic(kernel_tag):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 counter passes
+    (scripts/gpu_pmc.sh + scripts/pmc_summary.py: FETCH_SIZE x2 per the gfx950 correction of
+    MI355X_MICROARCH.md, plus WRITE_SIZE), or None when that summary does not match the kernel."""
+    try:
+        with open(PMC_SUMMARY) as f:
+            s = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if s.get("kernel_tag") != kernel_tag or "hbm_bytes" not in s:
+        return None
+    return {"bytes_per_launch": s["hbm_bytes"], "read": s["hbm_read_bytes"], "write": s["hbm_write_bytes"],
+            "source": os.path.relpath(PMC_SUMMARY, ROOT), "l2_hit": s.get("l2_hit"),
+            "mfma_busy": s.get("mfma_busy"), "clock_ghz": s.get("clock_ghz")}
+
+
 def cpu_baseline(res, threads, steps=2):
     """Time the CPU oracle (the reference algorithm restated on PyTorch-CPU, pinned to the
     reference's own train_paired outputs) on a bounded sample: 1 warm-up + `steps` timed
@@ -145,7 +164,8 @@ def main():
                          "achieved": round(achieved, 2), "peak": round(peak, 2), "unit": "TFLOP/s",
                          "peak_basis": (f"16-bit dense MFMA 2500 TFLOP/s / {nprod} split products per fp32 MAC"
                                         if fwd_x6 else "fp32 MFMA dense peak"),
-                         "frac": round(achieved / peak, 4), "traffic": None,
+                         "frac": round(achieved / peak, 4),
+                         "traffic": pmc_traffic("conv_fwd_f3_kernel<256,256,32,256,2>" if nprod == 3 else None),
                          "avg_launch_ms": round(avg_ms, 4), "launches": len(durs),
                          "flop_per_launch": flops},
             "step_tflops": round(STEP_GFLOP_PER_IMG_512 * (R / 512) ** 2 * world * B * args.steps / elapsed / 1e3, 2),

@@ -86,7 +86,7 @@ __device__ __forceinline__ void wait_vmcnt() {
 
 template <int BM, int BN, int WM, int WN, int NS>
 __global__ void __launch_bounds__((BM / WM) * (BN / WN) * 64, 1)
-conv_fwd_f3_kernel(const ConvBatch batch) {
+conv_fwd_f3_kernel(const ConvBatch batch, int alt_order) {
     constexpr int NWN = BN / WN;
     constexpr int NW = (BM / WM) * NWN;
     constexpr int TM = WM / 16, TN = WN / 16;
@@ -212,23 +212,37 @@ conv_fwd_f3_kernel(const ConvBatch batch) {
     // NS-2 stages stay in flight) and the barrier makes everyone's visible
     static_assert(NS == 2 || NS == 3, "ring depth");
     const int jp = P.jp;
-    int ir = 0, ijb = 0;                     // (r, jb) of the next stage to issue
-    auto next_koff = [&]() {
-        const int k = (ir * sxr + ijb) * 4;
+    // (r, jb) of the next stage to issue.  alt_order: odd M tiles walk the kernel rows backwards,
+    // so two neighbouring tiles (output rows 2t, 2t+1 and 2t+2, 2t+3 at 128-px rows) gather the
+    // same input rows at the same time -- their first and last kernel rows -- and share L2 lines
+    const bool rev = alt_order && (mt & 1);
+    int ir = 0, ijb = 0;
+    auto next_stage = [&](int& kstage) {
+        const int r = rev ? P.kh - 1 - ir : ir;
+        const int k = (r * sxr + ijb) * 4;
+        kstage = r * (jp / 32) + ijb / 32;        // packed-weight stage of this (r, jb)
         ijb += 32;
         if (ijb == jp) { ijb = 0; ++ir; }
         return k;
     };
 #pragma unroll
     for (int s0 = 0; s0 < NS - 1; ++s0)
-        if (s0 < nkt) issue(s0, s0, next_koff());
+        if (s0 < nkt) {
+            int ks;
+            const int k = next_stage(ks);
+            issue(s0, ks, k);
+        }
     int cur = 0, nxt = NS - 1;
     for (int kt = 0; kt < nkt; ++kt) {
         if (NS == 3 && kt + 1 < nkt) wait_vmcnt<NS == 3 ? A_GL + B_GL : 0>();
         else wait_vmcnt<0>();
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
-        if (kt + NS - 1 < nkt) issue(nxt, kt + NS - 1, next_koff());
+        if (kt + NS - 1 < nkt) {
+            int ks;
+            const int k = next_stage(ks);
+            issue(nxt, ks, k);
+        }
         compute(cur);
         cur = cur == NS - 1 ? 0 : cur + 1;
         nxt = nxt == NS - 1 ? 0 : nxt + 1;
@@ -267,6 +281,8 @@ conv_fwd_f3_kernel(const ConvBatch batch) {
     }
 }
 
+int g_f3_alt = 1;     // fg_set_f3_order: alternate the kernel-row order of odd M tiles
+
 template <int BM, int BN, int WM, int WN, int NS = 3>
 int launch_cfg(const ConvBatch& in, int nprob, hipStream_t stream) {
     constexpr int NT = (BM / WM) * (BN / WN) * 64;
@@ -282,7 +298,7 @@ int launch_cfg(const ConvBatch& in, int nprob, hipStream_t stream) {
     b.blk_start[nprob] = total;
     b.blk_start[4] = total;
     if (total == 0) return 0;
-    hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS>), dim3(total), dim3(NT), 0, stream, b);
+    hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS>), dim3(total), dim3(NT), 0, stream, b, g_f3_alt);
     return fg::launched("conv_fwd_f3");
 }
 
@@ -322,5 +338,10 @@ int launch_fwd_f3(const ConvBatch& b, int nprob, int max_n, hipStream_t stream, 
 FG_API int fg_set_f3_tile(int cfg) {
     if (cfg < -2 || cfg > 9) return fg::fail(FG_ERR_INVALID, "fg_set_f3_tile: %d", cfg);
     g_f3_tile = cfg;
+    return 0;
+}
+
+FG_API int fg_set_f3_order(int alt) {
+    g_f3_alt = alt != 0;
     return 0;
 }

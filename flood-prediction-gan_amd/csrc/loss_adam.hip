@@ -84,6 +84,7 @@ __global__ void adam_kernel(const AdamGroup G) {
     const long long base = (long long)(blockIdx.x - G.blk_start[ti]) * ADAM_EPB;
     const float w = G.one_m_b1;
     const bool small_w = fabsf(w) < 0.5f;
+    unsigned amax = 0;
     for (int k = threadIdx.x; k < ADAM_EPB; k += NT) {
         const long long i = base + k;
         if (i >= T.numel) break;
@@ -96,9 +97,22 @@ __global__ void adam_kernel(const AdamGroup G) {
         v = v + G.one_m_b2 * g * g;
         // denom = exp_avg_sq.sqrt() / sqrt(bias_correction2) + eps ; param.addcdiv_(m, denom, -step_size)
         const float denom = sqrtf(v) / G.bc2_sqrt + G.eps;
-        T.param[i] = T.param[i] + G.lr_step * m / denom;
+        const float np = T.param[i] + G.lr_step * m / denom;
+        T.param[i] = np;
         T.exp_avg[i] = m;
         T.exp_avg_sq[i] = v;
+        amax = max(amax, __float_as_uint(np) & 0x7fffffffu);
+    }
+    if (T.absmax) {     // bitwise max of |param| (uint order = float order), one shard per block
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) amax = max(amax, (unsigned)__shfl_xor((int)amax, off));
+        __shared__ unsigned red[NT / 64];
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = amax;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int i = 1; i < NT / 64; ++i) amax = max(amax, red[i]);
+            atomicMax(reinterpret_cast<unsigned*>(T.absmax) + (blockIdx.x & (FG_AMAX_SHARDS - 1)), amax);
+        }
     }
 }
 

@@ -58,7 +58,7 @@ class fg_weight_map(C.Structure):
 
 class fg_adam_tensor(C.Structure):
     _fields_ = [("param", C.c_void_p), ("grad", C.c_void_p), ("exp_avg", C.c_void_p),
-                ("exp_avg_sq", C.c_void_p), ("numel", C.c_longlong)]
+                ("exp_avg_sq", C.c_void_p), ("numel", C.c_longlong), ("absmax", C.c_void_p)]
 
 
 # (name, argtypes) of every exported symbol; tests check the library exports all of them
@@ -72,6 +72,7 @@ SIGNATURES = {
     "fg_set_fwd_tile": [C.c_int],
     "fg_set_wgrad_tile": [C.c_int],
     "fg_set_f3_tile": [C.c_int],
+    "fg_set_f3_order": [C.c_int],
     "fg_set_wgrad_f3": [C.c_int],
     "fg_conv_wgrad": [C.POINTER(fg_wgrad_problem), C.c_void_p],
     "fg_wgrad_reduce": [C.c_void_p, C.c_int, C.POINTER(fg_weight_map), C.c_void_p, C.c_int, C.c_void_p],
@@ -79,6 +80,11 @@ SIGNATURES = {
     "fg_pack_weight_split": [C.c_void_p, C.POINTER(fg_weight_map), C.c_void_p, C.c_void_p],
     "fg_pack_weight_f16": [C.c_void_p, C.POINTER(fg_weight_map), C.c_void_p, C.c_void_p, C.c_void_p],
     "fg_absmax": [C.c_void_p, C.c_longlong, C.c_void_p, C.c_void_p],
+    "fg_conv_n1_fwd": [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+                       C.c_int, C.c_void_p],
+    "fg_conv_n1_wgrad_blocks": [C.c_int, C.c_int, C.c_int],
+    "fg_conv_n1_wgrad": [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int,
+                         C.c_void_p, C.c_void_p],
     "fg_split_pixels": [C.c_void_p, C.c_longlong, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p],
     "fg_conv_win": [C.POINTER(fg_conv_problem), C.c_void_p, C.c_longlong, C.c_void_p],
     "fg_conv_wgrad_win": [C.POINTER(fg_wgrad_problem), C.c_void_p, C.c_longlong, C.c_int, C.c_int, C.c_void_p,

@@ -311,7 +311,7 @@ def disc_forward(P, inp, save=True):
     m3, r3, a3 = _norm(e3, FG_ACT_LRELU, 1, FG_PAD_ZERO)
     h5, w5 = PL.out_size(h4, 4, 1, 1), PL.out_size(w4, 4, 1, 1)
     pred = torch.empty(N, 1, h5, w5, dtype=torch.float32, device=dev)
-    _conv_fwd(P, "model.11", a3, 1, 4, 1, Buf(pred.view(-1), N, h5, w5, 1, 0))
+    ops.conv_n1_fwd(a3, P["model.11.weight"], P["model.11.bias"], pred)      # GEMV-shaped: fp32 FMA kernel
     S = dict(inp=inp, e0=e0, e1=e1, m1=m1, r1=r1, a1=a1, e2=e2, m2=m2, r2=r2, a2=a2, e3=e3, m3=m3, r3=r3, a3=a3)
     return pred, (S if save else None)
 
@@ -328,10 +328,11 @@ def disc_backward(P, S, g_pred, param_grads=True, grads_into=None, input_grad=No
     dev = inp.t.device
     a3 = S["a3"]
     h5, w5 = g_pred.shape[2], g_pred.shape[3]
-    g11 = Buf.empty(N, h5, w5, 1, 2, dev)
+    g11 = Buf.empty(N, h5, w5, 1, 3, dev)              # zero border 3: the n1 weight-gradient kernel's reach
     ops.pack_input(g_pred, 1, None, 0, g11, 0, N, FG_PAD_ZERO)
     if param_grads:
-        _wgrad_conv(P, G, "model.11", g11, a3, 1, 4, 1)
+        w11 = P["model.11.weight"]
+        ops.conv_n1_wgrad(a3, g11, PL.wmap_wgrad(w11.shape, True, a3.c, 4), G.get("model.11.weight"))
         ops.channel_sum(g11, 1, G.get("model.11.bias"))
     g_a3 = Buf.empty(N, a3.h, a3.w, 512, 0, dev)
     _dgrad_s1(P, "model.11", g11, 2, 4, g_a3)

@@ -103,7 +103,7 @@ def absmax(t):
     cached on the tensor until an op writes it."""
     t = _tensor(t)
     cached = getattr(t, "_fg_amax", None)
-    if cached is not None:
+    if cached is not None and getattr(t, "_fg_amax_ver", t._version) == t._version:
         return cached
     out = _SLOTS.take(t.device)
     L.check(_lib().fg_absmax(L.ptr(t), t.numel(), L.ptr(out), L.stream_handle()), "absmax")
@@ -121,6 +121,19 @@ def _amax_out(dst):
     return slot
 
 
+def _weight_absmax(w):
+    """absmax slot of a parameter: the one FusedAdam's kernel raised with the last update while the
+    tensor's version counter shows no torch write since, else a fresh fg_absmax pass (recorded
+    with the version so the other packs of the same weights reuse it)"""
+    slot = getattr(w, "_fg_amax", None)
+    if slot is not None and getattr(w, "_fg_amax_ver", None) == w._version:
+        return slot
+    slot = _SLOTS.take(w.device)
+    L.check(_lib().fg_absmax(L.ptr(w), w.numel(), L.ptr(slot), L.stream_handle()), "absmax")
+    w._fg_amax, w._fg_amax_ver = slot, w._version
+    return slot
+
+
 def pack_weight(w, m, split=None):
     """Packed weight for the conv engine: fp32 [n][kh*jp]; or, by default under a split forward
     math, the pre-split layout -- bf16 h/m/l pieces (bf16x6, fg_pack_weight_split) or scaled fp16
@@ -134,8 +147,7 @@ def pack_weight(w, m, split=None):
     elif split is True:
         split = "f16x3" if L.fwd_f16x3() else "bf16x6"
     if split == "f16x3":
-        amax = _SLOTS.take(w.device)        # weights change every step: never cached
-        L.check(_lib().fg_absmax(L.ptr(w), w.numel(), L.ptr(amax), L.stream_handle()), "absmax")
+        amax = _weight_absmax(w)
         wp = torch.empty(2 * packed_numel(m), dtype=torch.float16, device=w.device)
         L.check(_lib().fg_pack_weight_f16(L.ptr(w), C.byref(s), L.ptr(amax), L.ptr(wp), L.stream_handle()),
                 "pack_weight_f16")
@@ -344,6 +356,29 @@ def wgrad(prob, wmap, dw, accumulate=False):
             "wgrad_reduce")
 
 
+# ------------------------------------------------------------------ discriminator head (model.11)
+
+N1_ROWS = 5   # input rows per weight-gradient block
+
+
+def conv_n1_fwd(X, w, b, y):
+    """model.11 forward: X Buf (512 ch, border 1), w (1, 512, 4, 4), y [N, 1, h-1, w-1] contiguous"""
+    _wrote(y)
+    L.check(_lib().fg_conv_n1_fwd(L.ptr(X.t), X.n, X.hp, X.wp, X.c, L.ptr(w.contiguous()), L.ptr(b), L.ptr(y),
+                                  y.shape[2], y.shape[3], L.stream_handle()), "conv_n1_fwd")
+
+
+def conv_n1_wgrad(X, G, wmap, dw):
+    """model.11 weight gradient: X Buf (512 ch, border 1), G output-gradient Buf (1 ch, border 3)"""
+    blocks = int(_lib().fg_conv_n1_wgrad_blocks(X.n, X.hp, N1_ROWS))
+    slab = torch.empty(blocks * 16 * X.c, dtype=torch.float32, device=X.t.device)
+    st = L.stream_handle()
+    L.check(_lib().fg_conv_n1_wgrad(L.ptr(X.t), X.n, X.hp, X.wp, X.c, L.ptr(G.t), G.hp, G.wp, N1_ROWS, L.ptr(slab),
+                                    st), "conv_n1_wgrad")
+    m = wmap_struct(wmap)
+    L.check(_lib().fg_wgrad_reduce(L.ptr(slab), blocks, C.byref(m), L.ptr(dw), 0, st), "wgrad_reduce")
+
+
 # ------------------------------------------------------------------ layout
 
 def pack_input(a, ca, b, cb, dst, img0, nimg, pad_mode):
@@ -430,13 +465,23 @@ def l1(a, b, gscale, loss_out, g=None, accumulate=False):
 
 
 def adam_step(entries, lr, beta1, beta2, eps, step):
-    """entries: list of (param, grad, exp_avg, exp_avg_sq) tensors sharing `step`"""
+    """entries: list of (param, grad, exp_avg, exp_avg_sq) tensors sharing `step`.  The kernel
+    also raises a fresh absmax slot per parameter (the next weight packing's scale source),
+    cached on the parameter with its version counter (see absmax)."""
     if not entries:
         return
     arr = (L.fg_adam_tensor * len(entries))()
+    slots = []
     for i, (p, g, m, v) in enumerate(entries):
         arr[i].param, arr[i].grad, arr[i].exp_avg, arr[i].exp_avg_sq = (
             p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr())
         arr[i].numel = p.numel()
+        slot = _SLOTS.take(p.device) if L.fwd_f16x3() else None
+        arr[i].absmax = slot.data_ptr() if slot is not None else None
+        slots.append(slot)
     L.check(_lib().fg_adam_step(arr, len(entries), float(lr), float(beta1), float(beta2), float(eps), int(step),
                                 L.stream_handle()), "adam_step")
+    for (p, _, _, _), slot in zip(entries, slots):
+        # the kernel wrote p through a raw pointer: torch's version counter did not move, so a
+        # later in-place torch write (another optimizer, load_state_dict) still invalidates this
+        p._fg_amax, p._fg_amax_ver = slot, p._version

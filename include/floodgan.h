@@ -145,6 +145,9 @@ int fg_set_wgrad_tile(int cfg);
 /* Tuning hook of the LDS-DMA pipelined f16x3 forward kernel (conv_f3.hip, used for N > 64 when
  * the operands allow): -1 automatic (default), -2 never use it, 0..3 force a tile config. */
 int fg_set_f3_tile(int cfg);
+/* Tuning hook: 1 = odd M tiles of the pipelined forward kernel walk the kernel rows backwards
+ * (L2 sharing between neighbouring tiles), 0 = one order for all tiles. */
+int fg_set_f3_order(int alt);
 /* A/B hook of the pipelined f16x3 weight-gradient kernel (conv_wgrad_f3.hip, n_a >= 256): 1 on
  * (default), 0 off. */
 int fg_set_wgrad_f3(int on);
@@ -194,6 +197,18 @@ int fg_conv_win(const fg_conv_problem* prob, const void* x_split, long long x_pi
  * content-head weight gradient of convolution_backward (models/model_architectures.py:328). */
 int fg_conv_wgrad_win(const fg_wgrad_problem* prob, const void* p_split, long long p_pix0, int p_col0,
                       int wp_p, const void* x_split, long long x_pix0, int wp_x, hipStream_t stream);
+
+/* The discriminator's last conv (Conv2d(512, 1, 4, 1, 1), models/model_architectures.py:437) in fp32:
+ * y[n][oy][ox] = bias[0] + sum_{c,r,s} x(n, oy+r, ox+s, c) * w[c*16 + r*4 + s] over the 1-padded NHWC
+ * input x (nimg images of hp x wp padded pixels, c = 512), y NCHW [nimg, 1, ho, wo], ho = hp-3. */
+int fg_conv_n1_fwd(const float* x, int nimg, int hp, int wp, int c, const float* w, const float* bias,
+                   float* y, int ho, int wo, hipStream_t stream);
+/* Its weight gradient into fg_conv_n1_wgrad_blocks(nimg, hp, rows_per_block) slabs of 16*c floats
+ * (the fg_conv_wgrad slab layout for n_a = 1; sum them with fg_wgrad_reduce).  gp: the output
+ * gradient [nimg][ghp][gwp] with a zero border of 3 (ghp = ho + 6). */
+int fg_conv_n1_wgrad_blocks(int nimg, int hp, int rows_per_block);
+int fg_conv_n1_wgrad(const float* x, int nimg, int hp, int wp, int c, const float* gp, int ghp, int gwp,
+                     int rows_per_block, float* slabs, hipStream_t stream);
 
 /* Raise the absmax slot `out` (FG_AMAX_SHARDS floats, initialised by the caller) to bound
  * max |x[i]| over n contiguous floats (bitwise max of |x|; NaN-propagating).  The operand-
@@ -278,6 +293,9 @@ typedef struct fg_adam_tensor {
     float* exp_avg;
     float* exp_avg_sq;
     long long numel;
+    float* absmax;        /* optional absmax slot (FG_AMAX_SHARDS floats, zeroed by the caller):
+                             raised to bound |param| after the update -- the f16x3 scale source of
+                             the next weight packing, at no extra pass                            */
 } fg_adam_tensor;
 /* One step for `count` tensors sharing (lr, betas, eps, step). */
 int fg_adam_step(const fg_adam_tensor* tensors, int count, double lr, double beta1,

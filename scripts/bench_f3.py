@@ -36,6 +36,12 @@ def main():
             for t in [-2] + tiles:
                 L.set_f3_tile(t)
                 res.setdefault(t, []).append(time_it(lambda: ops.conv([prob])))
+        for alt in (0, 1, 0, 1):
+            L.load().fg_set_f3_order(alt)
+            L.set_f3_tile(-1)
+            ms = time_it(lambda: ops.conv([prob]))
+            print(f"{name:36s} {'f3 alt-order ' + str(alt):16s} {ms:8.3f} ms {flops / ms / 1e9:7.1f} TFLOP/s", flush=True)
+        L.load().fg_set_f3_order(0)
         for t in [-2] + tiles:
             L.set_f3_tile(t)
             Y.t.zero_()

@@ -310,6 +310,30 @@ def test_conv_window(case):
         L.set_conv_math(prev)
 
 
+def test_disc_head_n1():
+    """model.11 (Conv2d(512, 1, 4, 1, 1)): the fp32 FMA forward and weight-gradient kernels vs fp64"""
+    from floodgan import ops, plans as PL
+    from floodgan.plans import Buf
+    torch.manual_seed(7)
+    N, H = 3, 11
+    x = torch.randn(N, 512, H, H, dtype=torch.float64)
+    w = torch.randn(1, 512, 4, 4, dtype=torch.float64) * 0.02
+    b = torch.randn(1, dtype=torch.float64)
+    y = F.conv2d(F.pad(x, (1,) * 4), w, b)
+    gy = torch.randn_like(y)
+    gw_ref = torch.nn.grad.conv2d_weight(F.pad(x, (1,) * 4), w.shape, gy)
+    X = buf_from(x, 1, "constant")
+    out = torch.empty(N, 1, H - 1, H - 1, dtype=torch.float32, device=DEV)
+    ops.conv_n1_fwd(X, w.float().to(DEV), b.float().to(DEV), out)
+    G = Buf.zeros(N, H - 1, H - 1, 1, 3, DEV)
+    G.interior().copy_(gy.float().permute(0, 2, 3, 1))
+    dw = torch.empty(1, 512, 4, 4, dtype=torch.float32, device=DEV)
+    ops.conv_n1_wgrad(X, G, PL.wmap_wgrad(w.shape, True, 512, 4), dw)
+    torch.cuda.synchronize()
+    assert nrel(out, y) < KTOL
+    assert nrel(dw, gw_ref) < KTOL
+
+
 # ------------------------------------------------------------------ instance norm
 
 @pytest.mark.parametrize("act,fold,residual", [(1, 0, False), (2, 0, False), (0, 0, True), (1, 1, False),
