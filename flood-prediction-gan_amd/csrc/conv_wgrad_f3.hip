@@ -21,16 +21,15 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 constexpr int BR = 32;              // pixels per stage (the MFMA reduction depth)
-constexpr int TILE = 256;           // a and k extent of a tile
-constexpr int ROWB = TILE * 2;      // bytes per image row (256 fp16)
-constexpr int IMG = BR * ROWB;      // bytes per piece image (16 KiB)
+constexpr int TK = 256;             // k extent of a tile (the a extent TA is 256 or 128)
 
 // 32-B column-pair swizzle: the 8 rows a 32-lane half of a transposed read touches land on
 // 8 distinct 32-B bank groups
 __device__ __forceinline__ int swz_tr(int row) { return ((row & 3) | (((row >> 3) & 1) << 2)) << 1; }   // in 16-B chunks
 
+template <int COLS>
 __device__ __forceinline__ int img_off(int row, int col) {   // byte offset of fp16 column col of row
-    return row * ROWB + (((col >> 3) ^ swz_tr(row)) << 4) + ((col & 7) << 1);
+    return row * (COLS * 2) + (((col >> 3) ^ swz_tr(row)) << 4) + ((col & 7) << 1);
 }
 
 __device__ __forceinline__ f16x8 tr_frag(const char* base, int a0, int a1) {
@@ -50,23 +49,26 @@ __device__ __forceinline__ void split4(const f32x4& v, float s, f16x4& h, f16x4&
     }
 }
 
+template <int TA>
 __global__ void __launch_bounds__(512, 1)
 conv_wgrad_f3_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
-    constexpr int NT = 512, TM = 4, TN = 8;         // wave tile 64 (a) x 128 (k)
-    constexpr int SLOTS = BR * TILE / 4;            // float4 slots per operand per stage (2048)
-    constexpr int SPT = SLOTS / NT;                 // per thread (4)
+    // 8 waves as NWA (a) x NWK (k); wave tile 64 (a) x WK (k): TA 256 -> 4 x 2, 64 x 128; TA 128 -> 2 x 4, 64 x 64
+    constexpr int NT = 512, NWA = TA / 64, NWK = 8 / NWA, WK = TK / NWK, TM = 4, TN = WK / 16;
+    constexpr int SPT = BR * TK / 4 / NT;           // float4 slots per thread per operand per stage (4)
+    constexpr int IMGP = BR * TA * 2, IMGX = BR * TK * 2;   // bytes per piece image
+    constexpr int BUF = 2 * IMGP + 2 * IMGX;
     constexpr int kOOB = 0x7fffffff;
-    __shared__ __attribute__((aligned(1024))) char smem[2 * 4 * IMG];   // [buf][P h, P l, X h, X l]
+    __shared__ __attribute__((aligned(1024))) char smem[2 * BUF];   // [buf][P h, P l, X h, X l]
 
     // wave-uniform by construction (readfirstlane): the pixel walks below live in SGPRs
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wa = wave >> 1, wk = wave & 1;
+    const int wa = wave / NWK, wk = wave - (wave / NWK) * NWK;
     const int wid = fg::xcd_remap(blockIdx.x, gridDim.x);
     const int ntile = tiles_a * tiles_k;
     const int split = wid / ntile;
     const int tile = wid - split * ntile;
     const int ta = tile / tiles_k, tk = tile - (tile / tiles_k) * tiles_k;
-    const int a0 = ta * TILE, k0 = tk * TILE;
+    const int a0 = ta * TA, k0 = tk * TK;
     const int mab = P.m_a * P.m_b;
     const int M = P.m_img * mab;
     const int mbeg = split * P.m_chunk;
@@ -83,7 +85,8 @@ conv_wgrad_f3_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
     // Each thread's slots share one column group and walk pixel rows i*8 + tid/64, advanced by BR.
     const int col = (tid & 63) * 4;
     const int prow0 = wave;                         // + 8i
-    const bool p_col_ok = a0 + col < P.n_a;         // n_a % 4 == 0 (host check)
+    const bool p_slot = col < TA;                   // P has TA columns: lanes past them stage nothing
+    const bool p_col_ok = p_slot && a0 + col < P.n_a;   // n_a % 4 == 0 (host check)
     int x_koff = -1;                                // X column offset of this slot's k (k % 4 == 0 group)
     {
         const int k = k0 + col;
@@ -121,17 +124,20 @@ conv_wgrad_f3_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
         }
     };
     auto store = [&](int buf) {
-        char* b = smem + buf * 4 * IMG;
+        char* b = smem + buf * BUF;
 #pragma unroll
         for (int i = 0; i < SPT; ++i) {
-            const int o = img_off(prow0 + 8 * i, col);
             f16x4 h, l;
-            split4(rp[i], sp, h, l);
-            *reinterpret_cast<f16x4*>(b + o) = h;
-            *reinterpret_cast<f16x4*>(b + IMG + o) = l;
+            if (p_slot) {
+                const int op = img_off<TA>(prow0 + 8 * i, col);
+                split4(rp[i], sp, h, l);
+                *reinterpret_cast<f16x4*>(b + op) = h;
+                *reinterpret_cast<f16x4*>(b + IMGP + op) = l;
+            }
+            const int ox = img_off<TK>(prow0 + 8 * i, col);
             split4(rx[i], sx, h, l);
-            *reinterpret_cast<f16x4*>(b + 2 * IMG + o) = h;
-            *reinterpret_cast<f16x4*>(b + 3 * IMG + o) = l;
+            *reinterpret_cast<f16x4*>(b + 2 * IMGP + ox) = h;
+            *reinterpret_cast<f16x4*>(b + 2 * IMGP + IMGX + ox) = l;
         }
     };
 
@@ -145,24 +151,24 @@ conv_wgrad_f3_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
     // the group addresses columns 4p..4p+3 of the 16-column block
     const int g = lane >> 4, q = (lane >> 2) & 3, p4 = (lane & 3) * 4;
     auto compute = [&](int buf) {
-        const char* b = smem + buf * 4 * IMG;
+        const char* b = smem + buf * BUF;
         f16x8 ah[TM], al[TM];
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm) {
             const int c = wa * 64 + tm * 16 + p4;
-            const int o0 = img_off(8 * g + q, c), o1 = img_off(8 * g + 4 + q, c);
+            const int o0 = img_off<TA>(8 * g + q, c), o1 = img_off<TA>(8 * g + 4 + q, c);
             ah[tm] = tr_frag(b, o0, o1);
-            al[tm] = tr_frag(b + IMG, o0, o1);
+            al[tm] = tr_frag(b + IMGP, o0, o1);
         }
 #pragma unroll
         for (int t0 = 0; t0 < TN; t0 += 4) {
             f16x8 bh[4], bl[4];
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
-                const int c = wk * 128 + (t0 + t) * 16 + p4;
-                const int o0 = img_off(8 * g + q, c), o1 = img_off(8 * g + 4 + q, c);
-                bh[t] = tr_frag(b + 2 * IMG, o0, o1);
-                bl[t] = tr_frag(b + 3 * IMG, o0, o1);
+                const int c = wk * WK + (t0 + t) * 16 + p4;
+                const int o0 = img_off<TK>(8 * g + q, c), o1 = img_off<TK>(8 * g + 4 + q, c);
+                bh[t] = tr_frag(b + 2 * IMGP, o0, o1);
+                bl[t] = tr_frag(b + 2 * IMGP + IMGX, o0, o1);
             }
 #pragma unroll
             for (int tm = 0; tm < TM; ++tm)
@@ -208,7 +214,7 @@ conv_wgrad_f3_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
             if (a >= P.n_a) continue;
 #pragma unroll
             for (int tn = 0; tn < TN; ++tn) {
-                const int k = k0 + wk * 128 + tn * 16 + fr;
+                const int k = k0 + wk * WK + tn * 16 + fr;
                 if (k < K) out[(size_t)a * K + k] = acc[tm][tn][reg] * osc;
             }
         }
@@ -222,12 +228,16 @@ namespace fgc {
 
 // Returns 1 when the pipelined kernel took the problem (status in *rc), 0 when it does not apply.
 int launch_wgrad_f3(const fg_wgrad_problem& p, hipStream_t stream, int* rc) {
-    if (!g_wgrad_f3 || p.n_a < 256 || p.kh * p.j_valid < 256 || p.n_a % 4 || p.j_valid % 4 || !p.p_absmax ||
+    if (!g_wgrad_f3 || p.n_a < 128 || p.kh * p.j_valid < 256 || p.n_a % 4 || p.j_valid % 4 || !p.p_absmax ||
         !p.x_absmax || ((uintptr_t)p.p & 15) || ((uintptr_t)p.x & 15) || (p.spn | p.spa | p.spb) % 4 ||
         (p.sxn | p.sxa | p.sxb | p.sxr) % 4)
         return 0;
-    const int ta = (p.n_a + TILE - 1) / TILE, tk = (p.kh * p.j_valid + TILE - 1) / TILE;
-    hipLaunchKernelGGL(conv_wgrad_f3_kernel, dim3(ta * tk * p.splits), dim3(512), 0, stream, p, ta, tk);
+    const int TA = p.n_a >= 256 ? 256 : 128;
+    const int ta = (p.n_a + TA - 1) / TA, tk = (p.kh * p.j_valid + TK - 1) / TK;
+    if (TA == 256)
+        hipLaunchKernelGGL(conv_wgrad_f3_kernel<256>, dim3(ta * tk * p.splits), dim3(512), 0, stream, p, ta, tk);
+    else
+        hipLaunchKernelGGL(conv_wgrad_f3_kernel<128>, dim3(ta * tk * p.splits), dim3(512), 0, stream, p, ta, tk);
     *rc = fg::launched("conv_wgrad_f3");
     return 1;
 }

@@ -55,7 +55,9 @@ def main():
     # weight gradients: pipelined f16x3 kernel vs the register-staged one
     for name, c in {"resblock wgrad 3x3 256x256 @128": (8, 128, 256, 256, 3, 1, 1),
                     "D model.8 wgrad 4x4 256->512 @64 (2N)": (16, 64, 256, 512, 4, 1, 1),
-                    "conv3 wgrad 3x3s2 128->256 @256": (8, 256, 128, 256, 3, 2, 1)}.items():
+                    "conv3 wgrad 3x3s2 128->256 @256": (8, 256, 128, 256, 3, 2, 1),
+                    "conv2 wgrad 3x3s2 64->128 @512": (8, 512, 64, 128, 3, 2, 1),
+                    "D model.2 wgrad 4x4s2 64->128 @256 (2N)": (16, 256, 64, 128, 4, 2, 1)}.items():
         mk, flops, keep = make(*c)
         X, w, Y = keep
         Y.t.uniform_(-1, 1)

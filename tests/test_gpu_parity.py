@@ -196,7 +196,8 @@ def test_conv_f3_tiles(case, cfg):
 
 @pytest.mark.parametrize("on", [0, 1])
 @pytest.mark.parametrize("case", [(256, 256, 3, 1, 1, "reflect", 40), (128, 256, 4, 2, 1, "constant", 34),
-                                  (256, 512, 4, 1, 1, "constant", 17)])
+                                  (256, 512, 4, 1, 1, "constant", 17), (64, 128, 3, 2, 1, "constant", 36),
+                                  (128, 128, 4, 2, 1, "constant", 30)])
 def test_wgrad_f3(case, on):
     """the pipelined f16x3 weight-gradient kernel (conv_wgrad_f3.hip; on=0: the register-staged
     kernel) on multi-split problems with ragged pixel chunks, against fp64"""
