@@ -20,6 +20,8 @@
 // applied to the per-lane SOURCE address) so that the 16x16x32 fragment reads
 // (ds_read_b128: lane l reads row l&15, k-chunk l>>4) are bank-conflict free.
 // MFMA: v_mfma_f32_16x16x32_f16, three products per fragment pair (lh, hl, hh).
+#include <algorithm>
+
 #include "conv_common.hpp"
 
 namespace {
@@ -86,7 +88,7 @@ __device__ __forceinline__ void wait_vmcnt() {
 
 template <int BM, int BN, int WM, int WN, int NS>
 __global__ void __launch_bounds__((BM / WM) * (BN / WN) * 64, 1)
-conv_fwd_f3_kernel(const ConvBatch batch, int alt_order) {
+conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
     constexpr int NWN = BN / WN;
     constexpr int NW = (BM / WM) * NWN;
     constexpr int TM = WM / 16, TN = WN / 16;
@@ -102,56 +104,92 @@ conv_fwd_f3_kernel(const ConvBatch batch, int alt_order) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave / NWN, wn = wave - (wave / NWN) * NWN;
 
-    const int wid = fg::xcd_remap(blockIdx.x, gridDim.x);
-    int pi = 0;
-    while (pi + 1 < batch.count && wid >= batch.blk_start[pi + 1]) ++pi;
-    const fg_conv_problem& P = batch.p[pi];
-    const int local = wid - batch.blk_start[pi];
-    const int ntn = batch.ntiles_n[pi];
-    const int mt = local / ntn, nt = local - (local / ntn) * ntn;
-    const int m0 = mt * BM, n0 = nt * BN;
-    const int mab = P.m_a * P.m_b;
-    const int M = P.m_img * mab;
-    const int nkt = P.kh * (P.jp / 32);
-    const int sxr = (int)P.sxr;
-
-    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)P.x, 0, 0x7fffffff, 0x00020000);
-    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)P.w, 0, 0x7fffffff, 0x00020000);
-
-    // ---- per-lane DMA sources (byte offsets; the per-stage k offset is a scalar soffset).
-    // A: instruction i of this wave fills rows (wave*A_GL+i)*8 + lane/8, physical chunk lane%8 <-
-    // logical chunk (lane%8) ^ swz_a(row).  Rows past M are clamped to a valid row (their
-    // results are never stored); jp == j_valid, so every k of a stage is a real tap.
-    int a_off[A_GL];
-#pragma unroll
-    for (int i = 0; i < A_GL; ++i) {
-        const int row = (wave * A_GL + i) * 8 + (lane >> 3);
-        const int cl = (lane & 7) ^ swz_a(row);
-        int img, a, b;
-        fgc::decomp(min(m0 + row, M - 1), P.m_b, mab, img, a, b);
-        a_off[i] = ((int)(img * P.sxn + a * P.sxa + b * P.sxb) + cl * 4) * 4;
-    }
-    // B: instruction q = wave*B_GL+i fills piece q / (BN/16), rows (q % (BN/16))*16 + lane/4,
-    // physical chunk lane%4 <- logical 8-k slot (lane%4) ^ swz_b(row); rows past n_out clamped
-    int b_off[B_GL];
-#pragma unroll
-    for (int i = 0; i < B_GL; ++i) {
-        const int q = wave * B_GL + i;
-        const int pc = q / (BN / 16);
-        const int row = (q - pc * (BN / 16)) * 16 + (lane >> 2);
-        const int cl = (lane & 3) ^ swz_b(row);
-        b_off[i] = min(n0 + row, P.n_out - 1) * (P.ldw / 8) * 32 + cl * 32 + pc * 16;
-    }
-
-    // stage kt covers packed k [32kt, 32kt+32) = kernel row r, run offset jb: kept incrementally
-    // in scalars (no per-stage vector address arithmetic)
-    auto issue = [&](int buf, int kt, int koff_bytes) {
-        dma_stage<A_GL, B_GL, A_BYTES>(smem + buf * STAGE, wave, xr, wr, a_off, b_off, koff_bytes, kt * 128);
+    // ---- persistent tile loop: workgroup w runs tiles w, w + G, w + 2G, ... (G = gridDim.x) as ONE
+    // stream of k-stages -- the DMAs of the next tile's first stages are in flight while the
+    // current tile finishes and writes its epilogue (short-K convs were prologue-bound).
+    const int G = gridDim.x;
+    const int first = fg::xcd_remap(blockIdx.x, G);
+    struct Geo {
+        int pi, mt, m0, n0, nkt;
+    };
+    auto geo = [&](int t) {
+        Geo q;
+        q.pi = 0;
+        while (q.pi + 1 < batch.count && t >= batch.blk_start[q.pi + 1]) ++q.pi;
+        const int local = t - batch.blk_start[q.pi];
+        const int ntn = batch.ntiles_n[q.pi];
+        q.mt = local / ntn;
+        q.m0 = q.mt * BM;
+        q.n0 = (local - q.mt * ntn) * BN;
+        q.nkt = batch.p[q.pi].kh * (batch.p[q.pi].jp / 32);
+        return q;
     };
 
-    const float sa = fgc::pow2_scale(P.x_absmax);
-    const float sb = fgc::pow2_scale(P.w_absmax);
-    const float out_scale = 1.f / (sa * sb);
+    // ---- issue side: the tile whose stages are being staged, its per-lane DMA sources (byte
+    // offsets; the per-stage k offset is a scalar soffset) and its (r, jb) walk.
+    // A: instruction i of this wave fills rows (wave*A_GL+i)*8 + lane/8, physical chunk lane%8 <-
+    // logical chunk (lane%8) ^ swz_a(row); rows past M are clamped to a valid row (never stored);
+    // jp == j_valid, so every k of a stage is a real tap.  B: instruction q = wave*B_GL+i fills
+    // piece q / (BN/16), rows (q % (BN/16))*16 + lane/4, chunk lane%4 <- slot (lane%4) ^ swz_b(row).
+    int it = first, ikt = 0, ir = 0, ijb = 0;
+    bool irev = false;
+    Geo ig;
+    __amdgpu_buffer_rsrc_t xr, wr;
+    int a_off[A_GL], b_off[B_GL];
+    auto setup_issue = [&]() {
+        ig = geo(it);
+        const fg_conv_problem& P = batch.p[ig.pi];
+        xr = __builtin_amdgcn_make_buffer_rsrc((void*)P.x, 0, 0x7fffffff, 0x00020000);
+        wr = __builtin_amdgcn_make_buffer_rsrc((void*)P.w, 0, 0x7fffffff, 0x00020000);
+        const int mab = P.m_a * P.m_b, M = P.m_img * mab;
+#pragma unroll
+        for (int i = 0; i < A_GL; ++i) {
+            const int row = (wave * A_GL + i) * 8 + (lane >> 3);
+            const int cl = (lane & 7) ^ swz_a(row);
+            int img, a, b;
+            fgc::decomp(min(ig.m0 + row, M - 1), P.m_b, mab, img, a, b);
+            a_off[i] = ((int)(img * P.sxn + a * P.sxa + b * P.sxb) + cl * 4) * 4;
+        }
+#pragma unroll
+        for (int i = 0; i < B_GL; ++i) {
+            const int q = wave * B_GL + i;
+            const int pc = q / (BN / 16);
+            const int row = (q - pc * (BN / 16)) * 16 + (lane >> 2);
+            const int cl = (lane & 3) ^ swz_b(row);
+            b_off[i] = min(ig.n0 + row, P.n_out - 1) * (P.ldw / 8) * 32 + cl * 32 + pc * 16;
+        }
+        // alt_order: odd M tiles walk the kernel rows backwards, so neighbouring tiles (output rows
+        // 2t, 2t+1 and 2t+2, 2t+3 at 128-px rows) gather the same input rows at the same time
+        irev = alt_order && (ig.mt & 1);
+        ikt = ir = ijb = 0;
+    };
+    // stage the next k-stage of the stream into ring buffer `buf`; false once the stream is done
+    auto issue_next = [&](int buf) {
+        if (it >= total_tiles) return false;
+        const fg_conv_problem& P = batch.p[ig.pi];
+        const int r = irev ? P.kh - 1 - ir : ir;
+        const int koff = (r * (int)P.sxr + ijb) * 4;
+        const int ks = r * (P.jp / 32) + ijb / 32;       // packed-weight stage of this (r, jb)
+        dma_stage<A_GL, B_GL, A_BYTES>(smem + buf * STAGE, wave, xr, wr, a_off, b_off, koff, ks * 128);
+        ijb += 32;
+        if (ijb == P.jp) { ijb = 0; ++ir; }
+        if (++ikt == ig.nkt) {
+            it += G;
+            if (it < total_tiles) setup_issue();
+        }
+        return true;
+    };
+
+    // ---- compute side
+    int ct = first, ckt = 0;
+    Geo cg = geo(ct);
+    float sa = 1.f, out_scale = 1.f;
+    auto setup_compute = [&]() {
+        cg = geo(ct);
+        sa = fgc::pow2_scale(batch.p[cg.pi].x_absmax);
+        out_scale = 1.f / (sa * fgc::pow2_scale(batch.p[cg.pi].w_absmax));
+        ckt = 0;
+    };
 
     f32x4 acc[TM][TN];
 #pragma unroll
@@ -207,81 +245,78 @@ conv_fwd_f3_kernel(const ConvBatch batch, int alt_order) {
         }
     };
 
-    // ---- NS-deep ring: stage kt+NS-1 is issued right after the barrier that retires stage kt-1's
-    // reads; before it, this wave waits for its own DMAs of stage kt (counted vmcnt: the younger
-    // NS-2 stages stay in flight) and the barrier makes everyone's visible
-    static_assert(NS == 2 || NS == 3, "ring depth");
-    const int jp = P.jp;
-    // (r, jb) of the next stage to issue.  alt_order: odd M tiles walk the kernel rows backwards,
-    // so two neighbouring tiles (output rows 2t, 2t+1 and 2t+2, 2t+3 at 128-px rows) gather the
-    // same input rows at the same time -- their first and last kernel rows -- and share L2 lines
-    const bool rev = alt_order && (mt & 1);
-    int ir = 0, ijb = 0;
-    auto next_stage = [&](int& kstage) {
-        const int r = rev ? P.kh - 1 - ir : ir;
-        const int k = (r * sxr + ijb) * 4;
-        kstage = r * (jp / 32) + ijb / 32;        // packed-weight stage of this (r, jb)
-        ijb += 32;
-        if (ijb == jp) { ijb = 0; ++ir; }
-        return k;
+    // ---- epilogue of the compute tile: scale, bias, activation, strided store (or accumulate)
+    auto epilogue = [&]() {
+        const fg_conv_problem& P = batch.p[cg.pi];
+        const int mab = P.m_a * P.m_b, M = P.m_img * mab;
+        const int act = P.act;
+        const bool accum = P.accumulate != 0;
+        float bias_v[TN];
+        int ncol[TN];
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+            ncol[tn] = cg.n0 + wn * WN + tn * 16 + fr;
+            bias_v[tn] = P.bias ? P.bias[min(ncol[tn], P.n_out - 1)] : 0.f;
+        }
+        const bool full_n = cg.n0 + BN <= P.n_out;
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) {
+#pragma unroll
+            for (int reg = 0; reg < 4; ++reg) {
+                const int m = cg.m0 + wm * WM + tm * 16 + 4 * g + reg;
+                if (m >= M) continue;
+                int img, a, b;
+                fgc::decomp(m, P.m_b, mab, img, a, b);
+                float* yrow = P.y + img * P.syn + a * P.sya + b * P.syb;
+#pragma unroll
+                for (int tn = 0; tn < TN; ++tn) {
+                    if (!full_n && ncol[tn] >= P.n_out) continue;
+                    float v = fg::act_fwd(acc[tm][tn][reg] * out_scale + bias_v[tn], act);
+                    float* dst = yrow + ncol[tn] * P.syc;
+                    if (accum) v += *dst;
+                    *dst = v;
+                }
+            }
+        }
     };
+
+    // ---- NS-deep ring over the stage stream: stage s+NS-1 is issued right after the barrier that
+    // retires stage s-1's reads; before it, this wave waits for its own DMAs of stage s (counted
+    // vmcnt: the younger NS-2 stages stay in flight) and the barrier makes everyone's visible
+    static_assert(NS == 2 || NS == 3, "ring depth");
+    if (first >= total_tiles) return;
+    setup_issue();
+    setup_compute();
+    int issued = 0, done = 0;
 #pragma unroll
     for (int s0 = 0; s0 < NS - 1; ++s0)
-        if (s0 < nkt) {
-            int ks;
-            const int k = next_stage(ks);
-            issue(s0, ks, k);
-        }
+        if (issue_next(s0)) ++issued;
     int cur = 0, nxt = NS - 1;
-    for (int kt = 0; kt < nkt; ++kt) {
-        if (NS == 3 && kt + 1 < nkt) wait_vmcnt<NS == 3 ? A_GL + B_GL : 0>();
+    while (true) {
+        if (NS == 3 && issued - done >= 2) wait_vmcnt<NS == 3 ? A_GL + B_GL : 0>();
         else wait_vmcnt<0>();
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
-        if (kt + NS - 1 < nkt) {
-            int ks;
-            const int k = next_stage(ks);
-            issue(nxt, ks, k);
-        }
+        if (issue_next(nxt)) ++issued;
         compute(cur);
+        ++done;
         cur = cur == NS - 1 ? 0 : cur + 1;
         nxt = nxt == NS - 1 ? 0 : nxt + 1;
-    }
-
-    // ---- epilogue: scale, bias, activation, strided store (or accumulate).  Column-invariant
-    // work (bias, n bounds) is hoisted; full tiles take a branch-free path.
-    const int act = P.act;
-    const bool accum = P.accumulate != 0;
-    float bias_v[TN];
-    int ncol[TN];
+        if (++ckt == cg.nkt) {
+            epilogue();
 #pragma unroll
-    for (int tn = 0; tn < TN; ++tn) {
-        ncol[tn] = n0 + wn * WN + tn * 16 + fr;
-        bias_v[tn] = P.bias ? P.bias[min(ncol[tn], P.n_out - 1)] : 0.f;
-    }
-    const bool full_n = n0 + BN <= P.n_out;
+            for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
-    for (int tm = 0; tm < TM; ++tm) {
-#pragma unroll
-        for (int reg = 0; reg < 4; ++reg) {
-            const int m = m0 + wm * WM + tm * 16 + 4 * g + reg;
-            if (m >= M) continue;
-            int img, a, b;
-            fgc::decomp(m, P.m_b, mab, img, a, b);
-            float* yrow = P.y + img * P.syn + a * P.sya + b * P.syb;
-#pragma unroll
-            for (int tn = 0; tn < TN; ++tn) {
-                if (!full_n && ncol[tn] >= P.n_out) continue;
-                float v = fg::act_fwd(acc[tm][tn][reg] * out_scale + bias_v[tn], act);
-                float* dst = yrow + ncol[tn] * P.syc;
-                if (accum) v += *dst;
-                *dst = v;
-            }
+                for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
+            ct += G;
+            if (ct >= total_tiles) break;
+            setup_compute();
         }
     }
 }
 
 int g_f3_alt = 1;     // fg_set_f3_order: alternate the kernel-row order of odd M tiles
+int g_f3_persist = 1; // fg_set_f3_persistent: resident workgroups loop over tiles
 
 template <int BM, int BN, int WM, int WN, int NS = 3>
 int launch_cfg(const ConvBatch& in, int nprob, hipStream_t stream) {
@@ -298,7 +333,11 @@ int launch_cfg(const ConvBatch& in, int nprob, hipStream_t stream) {
     b.blk_start[nprob] = total;
     b.blk_start[4] = total;
     if (total == 0) return 0;
-    hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS>), dim3(total), dim3(NT), 0, stream, b, g_f3_alt);
+    // persistent: as many workgroups as fit at once (LDS-limited), each looping over tiles
+    constexpr int LDS = NS * (BM * 128 + 2 * BN * 64);
+    const int per_cu = (160 * 1024) / LDS;
+    const int grid = g_f3_persist ? std::min(total, fg::num_cus() * per_cu) : total;
+    hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS>), dim3(grid), dim3(NT), 0, stream, b, total, g_f3_alt);
     return fg::launched("conv_fwd_f3");
 }
 
@@ -338,6 +377,11 @@ int launch_fwd_f3(const ConvBatch& b, int nprob, int max_n, hipStream_t stream, 
 FG_API int fg_set_f3_tile(int cfg) {
     if (cfg < -2 || cfg > 9) return fg::fail(FG_ERR_INVALID, "fg_set_f3_tile: %d", cfg);
     g_f3_tile = cfg;
+    return 0;
+}
+
+FG_API int fg_set_f3_persistent(int on) {
+    g_f3_persist = on != 0;
     return 0;
 }
 

@@ -20,6 +20,9 @@ int fail(int code, const char* fmt, ...);
 // Checks the most recent launch; returns 0 or the hipError_t (message recorded).
 int launched(const char* what);
 
+// Compute units of the current device (persistent-kernel grid sizing).
+int num_cus();
+
 // Blocks per XCD-aware remap: consecutive remapped ids land on the same XCD (blocks are
 // dealt round-robin over the 8 XCDs), bijective for any grid size (guide §5 T1).
 __device__ __forceinline__ int xcd_remap(int bid, int nblk) {

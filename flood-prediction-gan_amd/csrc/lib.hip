@@ -24,6 +24,20 @@ int launched(const char* what) {
     return 0;
 }
 
+int num_cus() {
+    // compute units of the current device (cached per device; 256 on MI355X)
+    static thread_local int cached_dev = -1, cached_cus = 256;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return cached_cus;
+    if (dev != cached_dev) {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
+            cached_cus = cus;
+        cached_dev = dev;
+    }
+    return cached_cus;
+}
+
 }  // namespace fg
 
 FG_API const char* fg_last_error(void) { return g_err; }

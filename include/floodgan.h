@@ -148,6 +148,10 @@ int fg_set_f3_tile(int cfg);
 /* Tuning hook: 1 = odd M tiles of the pipelined forward kernel walk the kernel rows backwards
  * (L2 sharing between neighbouring tiles), 0 = one order for all tiles. */
 int fg_set_f3_order(int alt);
+/* Tuning hook: 1 (default) = the pipelined forward kernel runs one resident wave of workgroups that
+ * loop over the tiles (the next tile's first k-stages stream in behind the current tile's last);
+ * 0 = one workgroup per tile. */
+int fg_set_f3_persistent(int on);
 /* A/B hook of the pipelined f16x3 weight-gradient kernel (conv_wgrad_f3.hip, n_a >= 256): 1 on
  * (default), 0 off. */
 int fg_set_wgrad_f3(int on);

@@ -1,0 +1,60 @@
+"""A/B of engine switches on the full bs-8 512^2 training step, interleaved in ONE process (device
+clocks and boxes differ by several percent, so separate bench runs cannot resolve small gains).
+  python scripts/ab_step.py f3_persistent [rounds] [steps]
+Switches: f3_persistent, f3_order, wgrad_f3, use_win."""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "flood-prediction-gan_amd"))
+import torch  # noqa: E402
+
+from floodgan import _lib as L, ops  # noqa: E402
+from floodgan.model import Model  # noqa: E402
+
+
+def switch(name, on):
+    lib = L.load()
+    if name == "f3_persistent":
+        lib.fg_set_f3_persistent(int(on))
+    elif name == "f3_order":
+        lib.fg_set_f3_order(int(on))
+    elif name == "wgrad_f3":
+        L.set_wgrad_f3(on)
+    elif name == "use_win":
+        ops.USE_WIN = bool(on)
+    else:
+        raise SystemExit(f"unknown switch {name}")
+
+
+def main():
+    name = sys.argv[1]
+    rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+    steps = int(sys.argv[3]) if len(sys.argv) > 3 else 5
+    dev = torch.device("cuda")
+    m = Model(model="PairedAttention", num_epochs=2, topography="all", device=dev)
+    g = torch.Generator().manual_seed(1234)
+    x = (torch.rand((8, 9, 512, 512), generator=g) * 2 - 1).to(dev)
+    y = (torch.rand((8, 3, 512, 512), generator=g) * 2 - 1).to(dev)
+    for on in (0, 1):
+        switch(name, on)
+        m.step_fn(x, y).cpu()
+    res = {0: [], 1: []}
+    for _ in range(rounds):
+        for on in (0, 1):
+            switch(name, on)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                m.step_fn(x, y).cpu()
+            torch.cuda.synchronize()
+            res[on].append((time.perf_counter() - t0) / steps * 1e3)
+    for on in (0, 1):
+        v = sorted(res[on])
+        print(f"{name}={on}: ms/step min {v[0]:.2f} median {v[len(v) // 2]:.2f}  ({8e3 / v[0]:.1f} img/s best)")
+
+
+if __name__ == "__main__":
+    main()

@@ -36,12 +36,12 @@ def main():
             for t in [-2] + tiles:
                 L.set_f3_tile(t)
                 res.setdefault(t, []).append(time_it(lambda: ops.conv([prob])))
-        for alt in (0, 1, 0, 1):
-            L.load().fg_set_f3_order(alt)
+        for pers in (0, 1, 0, 1):
+            L.load().fg_set_f3_persistent(pers)
             L.set_f3_tile(-1)
             ms = time_it(lambda: ops.conv([prob]))
-            print(f"{name:36s} {'f3 alt-order ' + str(alt):16s} {ms:8.3f} ms {flops / ms / 1e9:7.1f} TFLOP/s", flush=True)
-        L.load().fg_set_f3_order(0)
+            print(f"{name:36s} {'f3 persistent ' + str(pers):16s} {ms:8.3f} ms {flops / ms / 1e9:7.1f} TFLOP/s", flush=True)
+        L.load().fg_set_f3_persistent(1)
         for t in [-2] + tiles:
             L.set_f3_tile(t)
             Y.t.zero_()
@@ -52,6 +52,33 @@ def main():
             tag = "register-staged" if t == -2 else f"f3 tile {t}"
             print(f"{name:36s} {tag:16s} {ms:8.3f} ms {flops / ms / 1e9:7.1f} TFLOP/s  rel diff {d:.2e}", flush=True)
     L.set_f3_tile(-1)
+    # transposed-conv phase batches (deconv1 256->128 @128->256, deconv2 128->64 @256->512)
+    from floodgan.plans import Buf
+    for name, (cin, cout, Hin) in {"deconv1 ConvT 256->128 @128": (256, 128, 128),
+                                   "deconv2 ConvT 128->64 @256": (128, 64, 256)}.items():
+        N = 8
+        X = Buf.empty(N, Hin, Hin, cin, 1, "cuda")
+        X.t.uniform_(-1, 1)
+        w = torch.randn(cin, cout, 3, 3, device="cuda") * 0.02
+        Y = Buf.empty(N, 2 * Hin, 2 * Hin, cout, 0, "cuda")
+        maps = PL.phase_maps(w.shape, 3, 1, X.c)
+        probs = PL.phase_problems(X, w.shape, 3, 1, Y, [ops.pack_weight(w, m) for m, _, _ in maps], maps)
+        flops = 2.0 * N * (2 * Hin) ** 2 * cout * cin * 9 / 4
+        L.set_f3_tile(-2)
+        ops.conv(probs)
+        ref = Y.t.clone()
+        for pers in (-1, 0, 1, -1, 0, 1):
+            if pers < 0:
+                L.set_f3_tile(-2)
+            else:
+                L.set_f3_tile(-1)
+                L.load().fg_set_f3_persistent(pers)
+            ms = time_it(lambda: ops.conv(probs))
+            tag = "register-staged" if pers < 0 else f"f3 persistent {pers}"
+            print(f"{name:36s} {tag:16s} {ms:8.3f} ms {flops / ms / 1e9:7.1f} TFLOP/s  rel diff {nrel(Y.t, ref):.2e}",
+                  flush=True)
+        L.set_f3_tile(-1)
+        L.load().fg_set_f3_persistent(1)
     # weight gradients: pipelined f16x3 kernel vs the register-staged one
     for name, c in {"resblock wgrad 3x3 256x256 @128": (8, 128, 256, 256, 3, 1, 1),
                     "D model.8 wgrad 4x4 256->512 @64 (2N)": (16, 64, 256, 512, 4, 1, 1),
