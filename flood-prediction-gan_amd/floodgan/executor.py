@@ -34,6 +34,11 @@ def generator_param_names():
 DISC_LAYERS = ["model.0", "model.2", "model.5", "model.8", "model.11"]
 
 
+def disc_bucket_names():
+    """the discriminator's gradient buckets (one per layer) in the order disc_backward completes them"""
+    return [[f"{layer}.{k}" for k in ("weight", "bias")] for layer in reversed(DISC_LAYERS)]
+
+
 class _Grads:
     """Destination of parameter gradients: either fresh tensors (autograd path) or
     preallocated .grad tensors (fused step)."""
@@ -203,9 +208,20 @@ def _dgrad_s2(P, name, gy, k, Y=None, y_nchw=None, n_base=0, n_out=None, accumul
     ops.conv(PL.phase_problems(gy, w.shape, k, 1, Y, wps, maps, y_nchw=y_nchw, accumulate=accumulate))
 
 
-def gen_backward(P, S, g_out, grads_into=None):
+G_BUCKETS = ([f"{h}_{t}" for t in ("content", "attention") for h in ("deconv1", "deconv2", "deconv3")],) + \
+    tuple([_blk(i, 1), _blk(i, 2)] for i in reversed(range(N_BLOCKS))) + (["conv1", "conv2", "conv3"],)
+
+
+def gen_bucket_names():
+    """the generator's gradient buckets in the order gen_backward completes them (parallel.FlatGrads)"""
+    return [[f"{layer}.{k}" for layer in b for k in ("weight", "bias")] for b in G_BUCKETS]
+
+
+def gen_backward(P, S, g_out, grads_into=None, ready=None):
     """Explicit backward of gen_forward.  g_out: [N,3,H,W] (any strides).  Returns
-    {param name: grad} (written into grads_into[name] when given)."""
+    {param name: grad} (written into grads_into[name] when given).  ready(layer name), when
+    given, is called as soon as a gradient bucket (G_BUCKETS) is complete."""
+    ready = ready or (lambda name: None)
     G = _Grads(P, grads_into)
     x = S["x"]
     N, _, H, W = x.shape
@@ -247,9 +263,11 @@ def gen_backward(P, S, g_out, grads_into=None):
                   G.get(name + ".weight"))
         m = PL.wmap_convT_dgrad(w.shape, g_d1.c)
         ops.conv([PL.conv_problem(g_d1, 1, 3, 2, ops.pack_weight(w, m), m, g_h, accumulate=idx)])
+    ready("deconv1_content")
     # ---- resnet blocks in reverse: out = h + IN(conv2(pad(relu(IN(conv1(pad(h)))))))
     for i in reversed(range(N_BLOCKS)):
         g_h = _block_bwd(P, f"resnet_blocks.{i}.", S["blocks"][i], g_h, G)
+        ready(_blk(i, 1))
     # ---- encoder
     g_c3 = Buf.empty(N, H // 4, W // 4, 256, 1, dev)
     ops.in_bwd(g_h, 0, None, S["c3"], S["m3"], S["r3"], FG_ACT_RELU, g_c3, G.get("conv3.bias"))
@@ -264,6 +282,7 @@ def gen_backward(P, S, g_out, grads_into=None):
     g_c1 = Buf.empty(N, H, W, 64, 0, dev)
     ops.in_bwd(g_a1, 0, None, S["c1"], S["m1"], S["r1"], FG_ACT_RELU, g_c1, G.get("conv1.bias"))
     _wgrad_conv(P, G, "conv1", g_c1, S["X0"], 3, 7, 1)
+    ready("conv1")
     return G.out
 
 
@@ -317,11 +336,13 @@ def disc_forward(P, inp, save=True):
 
 
 def disc_backward(P, S, g_pred, param_grads=True, grads_into=None, input_grad=None, input_grad_channels=None,
-                  input_grad_accumulate=False):
+                  input_grad_accumulate=False, ready=None):
     """Explicit backward of disc_forward.
     param_grads: compute weight / bias gradients (False in the generator step, where D is
     frozen: models/model.py:636-637).  input_grad: NCHW tensor receiving dL/d(input
-    channels input_grad_channels=(start, count)), written or accumulated."""
+    channels input_grad_channels=(start, count)), written or accumulated.  ready(layer name), when
+    given, is called as each layer's gradients are complete (parallel.FlatGrads buckets)."""
+    ready = (ready if param_grads and ready is not None else (lambda name: None))
     G = _Grads(P, grads_into)
     inp = S["inp"]
     N = inp.n
@@ -334,6 +355,7 @@ def disc_backward(P, S, g_pred, param_grads=True, grads_into=None, input_grad=No
         w11 = P["model.11.weight"]
         ops.conv_n1_wgrad(a3, g11, PL.wmap_wgrad(w11.shape, True, a3.c, 4), G.get("model.11.weight"))
         ops.channel_sum(g11, 1, G.get("model.11.bias"))
+        ready("model.11")
     g_a3 = Buf.empty(N, a3.h, a3.w, 512, 0, dev)
     _dgrad_s1(P, "model.11", g11, 2, 4, g_a3)
     # model.8 (k4 s1 p1) + IN + LReLU
@@ -343,6 +365,7 @@ def disc_backward(P, S, g_pred, param_grads=True, grads_into=None, input_grad=No
     a2 = S["a2"]
     if param_grads:
         _wgrad_conv(P, G, "model.8", g_e3, a2, 1, 4, 1)
+        ready("model.8")
     g_a2 = Buf.empty(N, a2.h, a2.w, 256, 0, dev)
     _dgrad_s1(P, "model.8", g_e3, 2, 4, g_a2)
     # model.5 (k4 s2 p1)
@@ -352,6 +375,7 @@ def disc_backward(P, S, g_pred, param_grads=True, grads_into=None, input_grad=No
     a1 = S["a1"]
     if param_grads:
         _wgrad_conv(P, G, "model.5", g_e2, a1, 1, 4, 2)
+        ready("model.5")
     g_a1 = Buf.empty(N, a1.h, a1.w, 128, 0, dev)
     _dgrad_s2(P, "model.5", g_e2, 4, Y=g_a1)
     # model.2
@@ -361,6 +385,7 @@ def disc_backward(P, S, g_pred, param_grads=True, grads_into=None, input_grad=No
     e0 = S["e0"]
     if param_grads:
         _wgrad_conv(P, G, "model.2", g_e1, e0, 1, 4, 2)
+        ready("model.2")
     g_e0 = Buf.empty(N, e0.h, e0.w, 64, 1, dev)
     _dgrad_s2(P, "model.2", g_e1, 4, Y=g_e0)
     ops.zero_border(g_e0)
@@ -368,6 +393,7 @@ def disc_backward(P, S, g_pred, param_grads=True, grads_into=None, input_grad=No
     if param_grads:
         _wgrad_conv(P, G, "model.0", g_e0, inp, 1, 4, 2)
         ops.channel_sum(g_e0, 64, G.get("model.0.bias"))
+        ready("model.0")
     if input_grad is not None:
         c0, cn = input_grad_channels
         _dgrad_s2(P, "model.0", g_e0, 4, y_nchw=(input_grad.view(-1), cn, inp.h, inp.w), n_base=c0, n_out=cn,

@@ -32,7 +32,10 @@ class PairedStep:
         self.G, self.D = generator, discriminator
         self.opt_g, self.opt_d = opt_g, opt_d
         self.gp, self.dp = generator.param_dict(), discriminator.param_dict()
-        self.gflat, self.dflat = FlatGrads(self.gp.values()), FlatGrads(self.dp.values())
+        # gradient buffers laid out in the order the backward completes them: each bucket's RCCL
+        # all-reduce starts as soon as it is written and overlaps the rest of the backward
+        self.gflat = FlatGrads(self.gp, X.gen_bucket_names())
+        self.dflat = FlatGrads(self.dp, X.disc_bucket_names())
         self.group = group
         self.last_mask = None
         self.last_output = None
@@ -54,9 +57,11 @@ class PairedStep:
         g_pred = torch.empty_like(pred)
         ops.mse_const(pred[:N], 0.0, 0.5 * inv, losses[1:2], g_pred[:N])
         ops.mse_const(pred[N:], 1.0, 0.5 * inv, losses[0:1], g_pred[N:])
-        X.disc_backward(self.dp, dS, g_pred, param_grads=True, grads_into=self._grads(self.dp))
+        self.dflat.begin(self.group)
+        X.disc_backward(self.dp, dS, g_pred, param_grads=True, grads_into=self._grads(self.dp),
+                        ready=self.dflat.ready)
         del dS, dinp
-        self.dflat.allreduce_sum(self.group)
+        self.dflat.finish()
         self.opt_d.step()
         # ---- generator step against the updated discriminator                 (:636-646)
         dinp = X.disc_pack([(x, fake)], C + 3)
@@ -68,9 +73,10 @@ class PairedStep:
         X.disc_backward(self.dp, dS, g_pred, param_grads=False, input_grad=g_fake, input_grad_channels=(C, 3),
                         input_grad_accumulate=True)
         del dS, dinp
-        X.gen_backward(self.gp, gS, g_fake, grads_into=self._grads(self.gp))
+        self.gflat.begin(self.group)
+        X.gen_backward(self.gp, gS, g_fake, grads_into=self._grads(self.gp), ready=self.gflat.ready)
         del gS
-        self.gflat.allreduce_sum(self.group)
+        self.gflat.finish()
         self.opt_g.step()
         self.last_mask, self.last_output = mask, fake
         return losses * torch.tensor([1.0, 1.0, 1.0, 100.0], device=dev)

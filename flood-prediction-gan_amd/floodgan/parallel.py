@@ -23,10 +23,29 @@ def world():
 
 class FlatGrads:
     """Allocates one contiguous gradient buffer for `params` and points every p.grad at its
-    slice (views stay valid as long as nobody sets p.grad = None)."""
+    slice (views stay valid as long as nobody sets p.grad = None).
 
-    def __init__(self, params):
-        self.params = [p for p in params]
+    `params` is a list of tensors, or a {name: tensor} dict together with `buckets`: lists of
+    names in the order the backward finishes them.  The buffer is laid out bucket by bucket, so
+    each bucket is one contiguous slice and can be all-reduced as soon as the backward has
+    written it (`ready`), overlapping RCCL with the rest of the backward: ProcessGroupNCCL runs
+    the collective on its own stream after the current one, so the kernels queued after it
+    proceed in parallel; `finish` makes the current stream wait for all of them (before Adam)."""
+
+    def __init__(self, params, buckets=None):
+        if isinstance(params, dict):
+            named = params
+            order = buckets if buckets is not None else [list(named)]
+            listed = [n for b in order for n in b]
+            if sorted(listed) != sorted(named):
+                raise ValueError("buckets must list every parameter exactly once")
+            self.params = [named[n] for n in listed]
+            sizes = [sum(named[n].numel() for n in b) for b in order]
+            self.bucket_names = [tuple(b) for b in order]
+        else:
+            self.params = [p for p in params]
+            sizes = [sum(p.numel() for p in self.params)]
+            self.bucket_names = [None]
         n = sum(p.numel() for p in self.params)
         dev = self.params[0].device
         self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
@@ -36,6 +55,12 @@ class FlatGrads:
             v = self.flat[off:off + p.numel()].view_as(p)
             self.views.append(v)
             off += p.numel()
+        self.buckets = []
+        off = 0
+        for sz in sizes:
+            self.buckets.append(self.flat[off:off + sz])
+            off += sz
+        self._pending, self._handles, self._group = [], [], None
         self.attach()
 
     def attach(self):
@@ -49,6 +74,38 @@ class FlatGrads:
         ws, _ = world()
         if ws > 1:
             dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
+
+    # ---- bucketed, overlapped SUM all-reduce
+    def begin(self, group=None):
+        self._group = group
+        self._pending = list(range(len(self.buckets)))
+        self._handles = []
+
+    def ready(self, bucket):
+        """The backward has finished every gradient of `bucket` (index, or the name of one of its
+        parameters' bucket key): start its all-reduce asynchronously."""
+        i = bucket if isinstance(bucket, int) else self.bucket_index(bucket)
+        if i not in self._pending:
+            return
+        self._pending.remove(i)
+        ws, _ = world()
+        if ws > 1:
+            self._handles.append(dist.all_reduce(self.buckets[i], op=dist.ReduceOp.SUM, group=self._group,
+                                                 async_op=True))
+
+    def bucket_index(self, key):
+        for i, names in enumerate(self.bucket_names):
+            if names is not None and any(n == key or n.startswith(key + ".") for n in names):
+                return i
+        raise KeyError(key)
+
+    def finish(self):
+        """Start whatever was never marked ready, then wait for every bucket's all-reduce."""
+        for i in list(self._pending):
+            self.ready(i)
+        for h in self._handles:
+            h.wait()
+        self._handles = []
 
 
 def broadcast_params(module, src=0, group=None):
