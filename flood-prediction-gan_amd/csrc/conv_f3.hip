@@ -86,7 +86,13 @@ __device__ __forceinline__ void wait_vmcnt() {
     else if constexpr (N == 15) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
 }
 
-template <int BM, int BN, int WM, int WN, int NS>
+// SCH selects the per-stage instruction order: 0 = read+split all of A, then the three products
+// per column group smallest first; 1 = the A reads are issued before the next stage's DMA (their
+// LDS latency hides behind the DMA issue) and each column group's products run hh, hl, lh, so the
+// first MFMAs need only the cheap h half of the split and the l half overlaps them; 2 = as 1, with
+// the B fragments double-buffered in 2-block groups (group g+1 is read while group g's products
+// run; group 0 is read together with A, ahead of the DMA issue).
+template <int BM, int BN, int WM, int WN, int NS, int SCH>
 __global__ void __launch_bounds__((BM / WM) * (BN / WN) * 64, 1)
 conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
     constexpr int NWN = BN / WN;
@@ -132,6 +138,7 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
     // jp == j_valid, so every k of a stage is a real tap.  B: instruction q = wave*B_GL+i fills
     // piece q / (BN/16), rows (q % (BN/16))*16 + lane/4, chunk lane%4 <- slot (lane%4) ^ swz_b(row).
     int it = first, ikt = 0, ir = 0, ijb = 0;
+    int i_kh = 1, i_jp = 32, i_sxr = 0;     // the issue tile's kh, jp, sxr (no kernarg reloads per stage)
     bool irev = false;
     Geo ig;
     __amdgpu_buffer_rsrc_t xr, wr;
@@ -161,18 +168,20 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
         // alt_order: odd M tiles walk the kernel rows backwards, so neighbouring tiles (output rows
         // 2t, 2t+1 and 2t+2, 2t+3 at 128-px rows) gather the same input rows at the same time
         irev = alt_order && (ig.mt & 1);
+        i_kh = P.kh;
+        i_jp = P.jp;
+        i_sxr = (int)P.sxr;
         ikt = ir = ijb = 0;
     };
     // stage the next k-stage of the stream into ring buffer `buf`; false once the stream is done
     auto issue_next = [&](int buf) {
         if (it >= total_tiles) return false;
-        const fg_conv_problem& P = batch.p[ig.pi];
-        const int r = irev ? P.kh - 1 - ir : ir;
-        const int koff = (r * (int)P.sxr + ijb) * 4;
-        const int ks = r * (P.jp / 32) + ijb / 32;       // packed-weight stage of this (r, jb)
+        const int r = irev ? i_kh - 1 - ir : ir;
+        const int koff = (r * i_sxr + ijb) * 4;
+        const int ks = r * (i_jp / 32) + ijb / 32;       // packed-weight stage of this (r, jb)
         dma_stage<A_GL, B_GL, A_BYTES>(smem + buf * STAGE, wave, xr, wr, a_off, b_off, koff, ks * 128);
         ijb += 32;
-        if (ijb == P.jp) { ijb = 0; ++ir; }
+        if (ijb == i_jp) { ijb = 0; ++ir; }
         if (++ikt == ig.nkt) {
             it += G;
             if (it < total_tiles) setup_issue();
@@ -207,15 +216,22 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
     // three products are issued smallest first
     constexpr int TG = TN < 4 ? TN : 4;
     static_assert(TN % TG == 0, "column blocks per wave must be a multiple of the group");
-    auto compute = [&](int buf) {
+    auto load_a = [&](int buf, f32x4 (&va)[TM][2]) {
+        const char* sbuf = smem + buf * STAGE;
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) {
+            const char* rowp = sbuf + (wm * WM + tm * 16 + fr) * 128;
+            va[tm][0] = *reinterpret_cast<const f32x4*>(rowp + a_c0);
+            va[tm][1] = *reinterpret_cast<const f32x4*>(rowp + a_c1);
+        }
+    };
+    auto compute = [&](int buf, const f32x4 (&va)[TM][2]) {
         const char* sbuf = smem + buf * STAGE;
         f16x8 ah[TM], al[TM];
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm) {
-            const char* rowp = sbuf + (wm * WM + tm * 16 + fr) * 128;
-            const f32x4 v0 = *reinterpret_cast<const f32x4*>(rowp + a_c0);
-            const f32x4 v1 = *reinterpret_cast<const f32x4*>(rowp + a_c1);
-            const float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+            const float v[8] = {va[tm][0][0], va[tm][0][1], va[tm][0][2], va[tm][0][3],
+                                va[tm][1][0], va[tm][1][1], va[tm][1][2], va[tm][1][3]};
             split_scalar(v, sa, ah[tm], al[tm]);
         }
 #pragma unroll
@@ -227,21 +243,77 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
                 bh[t] = *reinterpret_cast<const f16x8*>(rowp);
                 bl[t] = *reinterpret_cast<const f16x8*>(rowp + BN * 64);
             }
+            if constexpr (SCH == 0) {
+#pragma unroll
+                for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                    for (int t = 0; t < TG; ++t)
+                        acc[tm][t0 + t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[tm], bh[t], acc[tm][t0 + t], 0, 0, 0);
+#pragma unroll
+                for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                    for (int t = 0; t < TG; ++t)
+                        acc[tm][t0 + t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[tm], bl[t], acc[tm][t0 + t], 0, 0, 0);
+#pragma unroll
+                for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                    for (int t = 0; t < TG; ++t)
+                        acc[tm][t0 + t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[tm], bh[t], acc[tm][t0 + t], 0, 0, 0);
+            } else {
+#pragma unroll
+                for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                    for (int t = 0; t < TG; ++t) {
+                        acc[tm][t0 + t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[tm], bh[t], acc[tm][t0 + t], 0, 0, 0);
+                        acc[tm][t0 + t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[tm], bl[t], acc[tm][t0 + t], 0, 0, 0);
+                    }
+#pragma unroll
+                for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                    for (int t = 0; t < TG; ++t)
+                        acc[tm][t0 + t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[tm], bh[t], acc[tm][t0 + t], 0, 0, 0);
+            }
+        }
+    };
+
+    constexpr int TG2 = TN < 2 ? TN : 2;
+    constexpr int NG2 = TN / TG2;
+    auto load_b = [&](int buf, int t0, f16x8 (&bh)[TG2], f16x8 (&bl)[TG2]) {
+        const char* sbuf = smem + buf * STAGE;
+#pragma unroll
+        for (int t = 0; t < TG2; ++t) {
+            const char* rowp = sbuf + A_BYTES + (wn * WN + (t0 + t) * 16 + fr) * 64 + b_c;
+            bh[t] = *reinterpret_cast<const f16x8*>(rowp);
+            bl[t] = *reinterpret_cast<const f16x8*>(rowp + BN * 64);
+        }
+    };
+    auto compute2 = [&](int buf, const f32x4 (&va)[TM][2], f16x8 (&bh)[2][TG2], f16x8 (&bl)[2][TG2]) {
+        f16x8 ah[TM], al[TM];
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) {
+            const float v[8] = {va[tm][0][0], va[tm][0][1], va[tm][0][2], va[tm][0][3],
+                                va[tm][1][0], va[tm][1][1], va[tm][1][2], va[tm][1][3]};
+            split_scalar(v, sa, ah[tm], al[tm]);
+        }
+#pragma unroll
+        for (int gi = 0; gi < NG2; ++gi) {
+            const int sl = gi & 1;
+            if (gi + 1 < NG2) load_b(buf, (gi + 1) * TG2, bh[sl ^ 1], bl[sl ^ 1]);
 #pragma unroll
             for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
-                for (int t = 0; t < TG; ++t)
-                    acc[tm][t0 + t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[tm], bh[t], acc[tm][t0 + t], 0, 0, 0);
+                for (int t = 0; t < TG2; ++t) {
+                    f32x4& c = acc[tm][gi * TG2 + t];
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[tm], bh[sl][t], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[tm], bl[sl][t], c, 0, 0, 0);
+                }
 #pragma unroll
             for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
-                for (int t = 0; t < TG; ++t)
-                    acc[tm][t0 + t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[tm], bl[t], acc[tm][t0 + t], 0, 0, 0);
-#pragma unroll
-            for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-                for (int t = 0; t < TG; ++t)
-                    acc[tm][t0 + t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[tm], bh[t], acc[tm][t0 + t], 0, 0, 0);
+                for (int t = 0; t < TG2; ++t) {
+                    f32x4& c = acc[tm][gi * TG2 + t];
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[tm], bh[sl][t], c, 0, 0, 0);
+                }
         }
     };
 
@@ -297,8 +369,22 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
         else wait_vmcnt<0>();
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
-        if (issue_next(nxt)) ++issued;
-        compute(cur);
+        f32x4 va[TM][2];
+        if constexpr (SCH == 0) {
+            if (issue_next(nxt)) ++issued;
+            load_a(cur, va);
+            compute(cur, va);
+        } else if constexpr (SCH == 1) {
+            load_a(cur, va);
+            if (issue_next(nxt)) ++issued;
+            compute(cur, va);
+        } else {
+            f16x8 bh[2][TG2], bl[2][TG2];
+            load_a(cur, va);
+            load_b(cur, 0, bh[0], bl[0]);
+            if (issue_next(nxt)) ++issued;
+            compute2(cur, va, bh, bl);
+        }
         ++done;
         cur = cur == NS - 1 ? 0 : cur + 1;
         nxt = nxt == NS - 1 ? 0 : nxt + 1;
@@ -317,6 +403,7 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
 
 int g_f3_alt = 1;     // fg_set_f3_order: alternate the kernel-row order of odd M tiles
 int g_f3_persist = 1; // fg_set_f3_persistent: resident workgroups loop over tiles
+int g_f3_sched = -1;  // fg_set_f3_sched: per-stage instruction order (kernel template SCH), -1 auto
 
 template <int BM, int BN, int WM, int WN, int NS = 3>
 int launch_cfg(const ConvBatch& in, int nprob, hipStream_t stream) {
@@ -337,7 +424,16 @@ int launch_cfg(const ConvBatch& in, int nprob, hipStream_t stream) {
     constexpr int LDS = NS * (BM * 128 + 2 * BN * 64);
     const int per_cu = (160 * 1024) / LDS;
     const int grid = g_f3_persist ? std::min(total, fg::num_cus() * per_cu) : total;
-    hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS>), dim3(grid), dim3(NT), 0, stream, b, total, g_f3_alt);
+    const int sched = g_f3_sched >= 0 ? g_f3_sched : (BN > 64 ? 1 : 0);
+    if (sched == 2)
+        hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 2>), dim3(grid), dim3(NT), 0, stream, b, total,
+                           g_f3_alt);
+    else if (sched == 1)
+        hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 1>), dim3(grid), dim3(NT), 0, stream, b, total,
+                           g_f3_alt);
+    else
+        hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 0>), dim3(grid), dim3(NT), 0, stream, b, total,
+                           g_f3_alt);
     return fg::launched("conv_fwd_f3");
 }
 
@@ -382,6 +478,12 @@ FG_API int fg_set_f3_tile(int cfg) {
 
 FG_API int fg_set_f3_persistent(int on) {
     g_f3_persist = on != 0;
+    return 0;
+}
+
+FG_API int fg_set_f3_sched(int sched) {
+    if (sched < -1 || sched > 2) return fg::fail(FG_ERR_INVALID, "fg_set_f3_sched: %d", sched);
+    g_f3_sched = sched;
     return 0;
 }
 

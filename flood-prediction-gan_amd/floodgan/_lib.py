@@ -73,6 +73,7 @@ SIGNATURES = {
     "fg_set_wgrad_tile": [C.c_int],
     "fg_set_f3_tile": [C.c_int],
     "fg_set_f3_order": [C.c_int],
+    "fg_set_f3_sched": [C.c_int],
     "fg_set_f3_persistent": [C.c_int],
     "fg_set_wgrad_f3": [C.c_int],
     "fg_conv_wgrad": [C.POINTER(fg_wgrad_problem), C.c_void_p],

@@ -148,6 +148,10 @@ int fg_set_f3_tile(int cfg);
 /* Tuning hook: 1 = odd M tiles of the pipelined forward kernel walk the kernel rows backwards
  * (L2 sharing between neighbouring tiles), 0 = one order for all tiles. */
 int fg_set_f3_order(int alt);
+/* Tuning hook: per-stage instruction order of the pipelined forward kernel: 0 = split all of A,
+ * then the products; 1 = A reads ahead of the DMA issue, h-half products first; 2 = as 1 with
+ * double-buffered B fragment groups; -1 (default) = the tuned choice per tile config. */
+int fg_set_f3_sched(int sched);
 /* Tuning hook: 1 (default) = the pipelined forward kernel runs one resident wave of workgroups that
  * loop over the tiles (the next tile's first k-stages stream in behind the current tile's last);
  * 0 = one workgroup per tile. */

@@ -1,7 +1,7 @@
 """A/B of engine switches on the full bs-8 512^2 training step, interleaved in ONE process (device
 clocks and boxes differ by several percent, so separate bench runs cannot resolve small gains).
-  python scripts/ab_step.py f3_persistent [rounds] [steps]
-Switches: f3_persistent, f3_order, wgrad_f3, use_win."""
+  python scripts/ab_step.py f3_persistent [rounds] [steps] [values, default 0,1]
+Switches: f3_persistent, f3_sched, f3_order, wgrad_f3, use_win."""
 import os
 import sys
 import time
@@ -19,6 +19,8 @@ def switch(name, on):
     lib = L.load()
     if name == "f3_persistent":
         lib.fg_set_f3_persistent(int(on))
+    elif name == "f3_sched":
+        lib.fg_set_f3_sched(int(on))
     elif name == "f3_order":
         lib.fg_set_f3_order(int(on))
     elif name == "wgrad_f3":
@@ -33,17 +35,18 @@ def main():
     name = sys.argv[1]
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 3
     steps = int(sys.argv[3]) if len(sys.argv) > 3 else 5
+    vals = [int(v) for v in sys.argv[4].split(",")] if len(sys.argv) > 4 else [0, 1]
     dev = torch.device("cuda")
     m = Model(model="PairedAttention", num_epochs=2, topography="all", device=dev)
     g = torch.Generator().manual_seed(1234)
     x = (torch.rand((8, 9, 512, 512), generator=g) * 2 - 1).to(dev)
     y = (torch.rand((8, 3, 512, 512), generator=g) * 2 - 1).to(dev)
-    for on in (0, 1):
+    for on in vals:
         switch(name, on)
         m.step_fn(x, y).cpu()
-    res = {0: [], 1: []}
+    res = {v: [] for v in vals}
     for _ in range(rounds):
-        for on in (0, 1):
+        for on in vals:
             switch(name, on)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
@@ -51,7 +54,7 @@ def main():
                 m.step_fn(x, y).cpu()
             torch.cuda.synchronize()
             res[on].append((time.perf_counter() - t0) / steps * 1e3)
-    for on in (0, 1):
+    for on in vals:
         v = sorted(res[on])
         print(f"{name}={on}: ms/step min {v[0]:.2f} median {v[len(v) // 2]:.2f}  ({8e3 / v[0]:.1f} img/s best)")
 
