@@ -90,8 +90,8 @@ __device__ __forceinline__ void wait_vmcnt() {
 // per column group smallest first; 1 = the A reads are issued before the next stage's DMA (their
 // LDS latency hides behind the DMA issue) and each column group's products run hh, hl, lh, so the
 // first MFMAs need only the cheap h half of the split and the l half overlaps them; 2 = as 1, with
-// the B fragments double-buffered in 2-block groups (group g+1 is read while group g's products
-// run; group 0 is read together with A, ahead of the DMA issue).
+// the B fragments double-buffered in 2-block groups, pinned (group g+1 is read while group g's
+// products run; group 0 is read together with A, ahead of the DMA issue).
 template <int BM, int BN, int WM, int WN, int NS, int SCH>
 __global__ void __launch_bounds__((BM / WM) * (BN / WN) * 64, 1)
 conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
@@ -109,6 +109,9 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave / NWN, wn = wave - (wave / NWN) * NWN;
+    // order bit 2: static priority for the second half of the waves (the arbitration losers of
+    // the two waves sharing each SIMD)
+    if ((alt_order & 4) && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
 
     // ---- persistent tile loop: workgroup w runs tiles w, w + G, w + 2G, ... (G = gridDim.x) as ONE
     // stream of k-stages -- the DMAs of the next tile's first stages are in flight while the
@@ -137,8 +140,12 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
     // logical chunk (lane%8) ^ swz_a(row); rows past M are clamped to a valid row (never stored);
     // jp == j_valid, so every k of a stage is a real tap.  B: instruction q = wave*B_GL+i fills
     // piece q / (BN/16), rows (q % (BN/16))*16 + lane/4, chunk lane%4 <- slot (lane%4) ^ swz_b(row).
-    int it = first, ikt = 0, ir = 0, ijb = 0;
-    int i_kh = 1, i_jp = 32, i_sxr = 0;     // the issue tile's kh, jp, sxr (no kernarg reloads per stage)
+    // k walk of a tile: channel chunk ic (outer), kernel row ir, tap is (inner), so the kw taps of
+    // one 32-channel chunk -- the same input pixels shifted by one -- and then the kh rows are
+    // gathered back to back while still in L2 (the input itself is far larger than L2).  Without a
+    // usable jc (channels per pixel) the run is walked as kw = jp/32 pseudo-taps of 32 (r outer).
+    int it = first, ikt = 0, ic = 0, ir = 0, is = 0;
+    int i_kh = 1, i_jp = 32, i_sxr = 0, i_c = 32, i_kw = 1, i_nc = 1;   // per issue tile (no kernarg reloads)
     bool irev = false;
     Geo ig;
     __amdgpu_buffer_rsrc_t xr, wr;
@@ -167,21 +174,30 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
         }
         // alt_order: odd M tiles walk the kernel rows backwards, so neighbouring tiles (output rows
         // 2t, 2t+1 and 2t+2, 2t+3 at 128-px rows) gather the same input rows at the same time
-        irev = alt_order && (ig.mt & 1);
+        irev = (alt_order & 1) && (ig.mt & 1);
         i_kh = P.kh;
         i_jp = P.jp;
         i_sxr = (int)P.sxr;
-        ikt = ir = ijb = 0;
+        i_c = ((alt_order & 2) && P.jc > 0 && P.jc % 32 == 0 && P.jp % P.jc == 0) ? P.jc : 32;
+        i_kw = P.jp / i_c;
+        i_nc = i_c / 32;
+        ikt = ic = ir = is = 0;
     };
     // stage the next k-stage of the stream into ring buffer `buf`; false once the stream is done
     auto issue_next = [&](int buf) {
         if (it >= total_tiles) return false;
         const int r = irev ? i_kh - 1 - ir : ir;
-        const int koff = (r * i_sxr + ijb) * 4;
-        const int ks = r * (i_jp / 32) + ijb / 32;       // packed-weight stage of this (r, jb)
+        const int jb = is * i_c + ic * 32;
+        const int koff = (r * i_sxr + jb) * 4;
+        const int ks = r * (i_jp / 32) + jb / 32;        // packed-weight stage of this (r, jb)
+#ifdef FG_F3_DIAG
+        if (!((alt_order >> 4) & 1) || ikt < NS)         // diag bit 0: no DMA after the first stages
+#endif
         dma_stage<A_GL, B_GL, A_BYTES>(smem + buf * STAGE, wave, xr, wr, a_off, b_off, koff, ks * 128);
-        ijb += 32;
-        if (ijb == i_jp) { ijb = 0; ++ir; }
+        if (++is == i_kw) {
+            is = 0;
+            if (++ir == i_kh) { ir = 0; ++ic; }
+        }
         if (++ikt == ig.nkt) {
             it += G;
             if (it < total_tiles) setup_issue();
@@ -287,18 +303,40 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
             bl[t] = *reinterpret_cast<const f16x8*>(rowp + BN * 64);
         }
     };
+    // SCH 2: the instruction order is pinned with sched_barriers (the compiler otherwise sinks
+    // every fragment read to just before its first use): region g holds group g+1's B reads, then
+    // group g's MFMAs; the l half of the A split sits in region 0 among group 0's MFMAs.
     auto compute2 = [&](int buf, const f32x4 (&va)[TM][2], f16x8 (&bh)[2][TG2], f16x8 (&bl)[2][TG2]) {
         f16x8 ah[TM], al[TM];
+        float xs[TM][8];
 #pragma unroll
-        for (int tm = 0; tm < TM; ++tm) {
-            const float v[8] = {va[tm][0][0], va[tm][0][1], va[tm][0][2], va[tm][0][3],
-                                va[tm][1][0], va[tm][1][1], va[tm][1][2], va[tm][1][3]};
-            split_scalar(v, sa, ah[tm], al[tm]);
-        }
+        for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float x0 = va[tm][e >> 1][(e & 1) * 2] * sa, x1 = va[tm][e >> 1][(e & 1) * 2 + 1] * sa;
+                xs[tm][2 * e] = x0;
+                xs[tm][2 * e + 1] = x1;
+                const f16x2 hh = __builtin_convertvector(f32x2{x0, x1}, f16x2);
+                ah[tm][2 * e] = hh[0];
+                ah[tm][2 * e + 1] = hh[1];
+            }
 #pragma unroll
         for (int gi = 0; gi < NG2; ++gi) {
             const int sl = gi & 1;
             if (gi + 1 < NG2) load_b(buf, (gi + 1) * TG2, bh[sl ^ 1], bl[sl ^ 1]);
+            __builtin_amdgcn_sched_barrier(0);
+            if (gi == 0) {
+#pragma unroll
+                for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const float r0 = xs[tm][2 * e] - (float)ah[tm][2 * e];
+                        const float r1 = xs[tm][2 * e + 1] - (float)ah[tm][2 * e + 1];
+                        const f16x2 ll = __builtin_convertvector(f32x2{r0, r1}, f16x2);
+                        al[tm][2 * e] = ll[0];
+                        al[tm][2 * e + 1] = ll[1];
+                    }
+            }
 #pragma unroll
             for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
@@ -370,6 +408,11 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
         f32x4 va[TM][2];
+#ifdef FG_F3_DIAG
+        if ((alt_order >> 5) & 1) {                      // diag bit 1: DMA and barriers only
+            if (issue_next(nxt)) ++issued;
+        } else
+#endif
         if constexpr (SCH == 0) {
             if (issue_next(nxt)) ++issued;
             load_a(cur, va);
@@ -401,7 +444,9 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
     }
 }
 
-int g_f3_alt = 1;     // fg_set_f3_order: alternate the kernel-row order of odd M tiles
+int g_f3_alt = 7;     // fg_set_f3_order: bit 0 alternates the kernel-row order of odd M tiles,
+                      // bit 1 walks k chunk-outer (taps of one channel chunk back to back),
+                      // bit 2 raises the priority of the second half of the waves
 int g_f3_persist = 1; // fg_set_f3_persistent: resident workgroups loop over tiles
 int g_f3_sched = -1;  // fg_set_f3_sched: per-stage instruction order (kernel template SCH), -1 auto
 
@@ -425,6 +470,12 @@ int launch_cfg(const ConvBatch& in, int nprob, hipStream_t stream) {
     const int per_cu = (160 * 1024) / LDS;
     const int grid = g_f3_persist ? std::min(total, fg::num_cus() * per_cu) : total;
     const int sched = g_f3_sched >= 0 ? g_f3_sched : (BN > 64 ? 1 : 0);
+#ifdef FG_F3_DIAG
+    // timing-only diagnostic build (outputs are wrong): FG_F3_DIAG=1 compute without data movement,
+    // 2 data movement without compute
+    const char* dg = getenv("FG_F3_DIAG");
+    const int g_f3_alt = ::g_f3_alt | ((dg ? atoi(dg) : 0) << 4);
+#endif
     if (sched == 2)
         hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 2>), dim3(grid), dim3(NT), 0, stream, b, total,
                            g_f3_alt);
@@ -488,6 +539,7 @@ FG_API int fg_set_f3_sched(int sched) {
 }
 
 FG_API int fg_set_f3_order(int alt) {
-    g_f3_alt = alt != 0;
+    if (alt < 0 || alt > 7) return fg::fail(FG_ERR_INVALID, "fg_set_f3_order: %d", alt);
+    g_f3_alt = alt;
     return 0;
 }

@@ -37,7 +37,7 @@ class fg_conv_problem(C.Structure):
                 ("m_img", C.c_int), ("m_a", C.c_int), ("m_b", C.c_int),
                 ("kh", C.c_int), ("j_valid", C.c_int), ("jp", C.c_int),
                 ("n_out", C.c_int), ("ldw", C.c_int), ("act", C.c_int), ("accumulate", C.c_int),
-                ("w_split", C.c_int), ("x_absmax", C.c_void_p), ("w_absmax", C.c_void_p)]
+                ("w_split", C.c_int), ("x_absmax", C.c_void_p), ("w_absmax", C.c_void_p), ("jc", C.c_int)]
 
 
 class fg_wgrad_problem(C.Structure):

@@ -221,6 +221,7 @@ def _conv(probs):
         s.bias = p["bias"].data_ptr() if p["bias"] is not None else None
         for k in _CONV_FIELDS:
             setattr(s, k, int(p[k]))
+        s.jc = getattr(p["x"][0], "c", 0)
         if f16:
             xb = p["x"][0]
             if id(xb) not in keep:

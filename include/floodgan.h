@@ -87,6 +87,9 @@ typedef struct fg_conv_problem {
                              fg_pack_weight_f16 (f16x3 math)                                         */
     const float* x_absmax;   /* f16x3: absmax slot bounding |x| over every element the gather reads */
     const float* w_absmax;   /* f16x3: absmax slot bounding |w| (the one fg_pack_weight_f16 used)  */
+    int jc;               /* channels per pixel of the j run (j = s*jc + ch), or 0 if unknown: lets the
+                             pipelined kernel walk the taps of one channel chunk back to back (the
+                             gathered input rows are re-read while still in L2)                  */
 } fg_conv_problem;
 
 /*
@@ -143,10 +146,12 @@ int fg_set_fwd_tile(int cfg);
 /* Same for the split-math weight-gradient kernels (0..5). */
 int fg_set_wgrad_tile(int cfg);
 /* Tuning hook of the LDS-DMA pipelined f16x3 forward kernel (conv_f3.hip, used for N > 64 when
- * the operands allow): -1 automatic (default), -2 never use it, 0..3 force a tile config. */
+ * the operands allow): -1 automatic (default), -2 never use it, 0..9 force a tile config. */
 int fg_set_f3_tile(int cfg);
-/* Tuning hook: 1 = odd M tiles of the pipelined forward kernel walk the kernel rows backwards
- * (L2 sharing between neighbouring tiles), 0 = one order for all tiles. */
+/* Tuning hook, k-walk order of the pipelined forward kernel: bit 0 = odd M tiles walk the kernel
+ * rows backwards (L2 sharing between neighbouring tiles); bit 1 = channel-chunk-outer walk (the
+ * taps of one 32-channel chunk back to back, needs fg_conv_problem.jc); bit 2 = static priority
+ * for the second half of the waves.  Default 7. */
 int fg_set_f3_order(int alt);
 /* Tuning hook: per-stage instruction order of the pipelined forward kernel: 0 = split all of A,
  * then the products; 1 = A reads ahead of the DMA issue, h-half products first; 2 = as 1 with

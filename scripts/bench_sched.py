@@ -1,6 +1,6 @@
-"""Interleaved A/B (GPU) of the pipelined forward kernel's stage schedules (fg_set_f3_sched 0/1)
-on the bs-8 512^2 forward geometries, with the relative difference between the two results.
-  python scripts/bench_sched.py"""
+"""Interleaved A/B (GPU) of a pipelined-forward-kernel switch (fg_set_f3_sched / fg_set_f3_order)
+on the bs-8 512^2 forward geometries, with the relative difference between the results.
+  python scripts/bench_sched.py [sched|order] [values]"""
 import os
 import sys
 
@@ -15,24 +15,32 @@ from floodgan.plans import Buf  # noqa: E402
 from bench_conv import make, nrel, time_it  # noqa: E402
 
 
+SW = sys.argv[1] if len(sys.argv) > 1 else "sched"
+VALS = [int(v) for v in sys.argv[2].split(",")] if len(sys.argv) > 2 else [0, 1, 2]
+DEFAULT = {"sched": -1, "order": 7}[SW]
+
+
+def setsw(v):
+    getattr(L.load(), "fg_set_f3_" + SW)(v)
+
+
 def ab(name, run, out, flops, reps=3):
-    lib = L.load()
-    res, outs = {0: [], 1: [], 2: []}, {}
+    res, outs = {v: [] for v in VALS}, {}
     for _ in range(reps):
-        for sch in (0, 1, 2):
-            lib.fg_set_f3_sched(sch)
-            res[sch].append(time_it(run))
-    for sch in (0, 1, 2):
-        lib.fg_set_f3_sched(sch)
+        for v in VALS:
+            setsw(v)
+            res[v].append(time_it(run))
+    for v in VALS:
+        setsw(v)
         out.zero_()
         run()
         torch.cuda.synchronize()
-        outs[sch] = out.clone()
-    lib.fg_set_f3_sched(-1)
-    for sch in (0, 1, 2):
-        ms = min(res[sch])
-        print(f"{name:36s} sched {sch} {ms:8.3f} ms {flops / ms / 1e9:7.1f} TFLOP/s"
-              f"  rel diff {nrel(outs[sch], outs[0]):.2e}", flush=True)
+        outs[v] = out.clone()
+    setsw(DEFAULT)
+    for v in VALS:
+        ms = min(res[v])
+        print(f"{name:36s} {SW} {v} {ms:8.3f} ms {flops / ms / 1e9:7.1f} TFLOP/s"
+              f"  rel diff {nrel(outs[v], outs[VALS[0]]):.2e}", flush=True)
 
 
 def main():

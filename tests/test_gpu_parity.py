@@ -160,14 +160,15 @@ def test_convT(cin, cout, H, conv_math):
     assert nrel(nchw(gx), gx_ref) < KTOL
 
 
-@pytest.mark.parametrize("persistent,sched", [(0, 2), (1, 2), (1, 1), (1, 0)])
+@pytest.mark.parametrize("persistent,sched,order", [(0, 2, 3), (1, 2, 3), (1, 1, 3), (1, 0, 3), (1, 1, 2),
+                                                    (1, 1, 1), (1, 1, 0), (1, 1, 7)])
 @pytest.mark.parametrize("cfg", [-2, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
 @pytest.mark.parametrize("case", [(256, 256, 3, 1, 1, "reflect", 20), (128, 256, 4, 2, 1, "constant", 22),
                                   (64, 128, 3, 2, 1, "constant", 30), (256, 512, 4, 1, 1, "constant", 11),
                                   (128, 64, 3, 1, 1, "constant", 21)])
-def test_conv_f3_tiles(case, cfg, persistent, sched):
-    """the pipelined f16x3 forward kernel (conv_f3.hip) in every tile config and both stage
-    schedules, ragged M / N tiles included, against fp64 -- and the register-staged kernel it
+def test_conv_f3_tiles(case, cfg, persistent, sched, order):
+    """the pipelined f16x3 forward kernel (conv_f3.hip) in every tile config, stage schedule and
+    k-walk order, ragged M / N tiles included, against fp64 -- and the register-staged kernel it
     replaces (cfg -2)"""
     from floodgan import _lib as L, ops, plans as PL
     from floodgan.plans import Buf
@@ -178,6 +179,7 @@ def test_conv_f3_tiles(case, cfg, persistent, sched):
         L.set_f3_tile(cfg)
         L.load().fg_set_f3_persistent(persistent)
         L.load().fg_set_f3_sched(sched)
+        L.load().fg_set_f3_order(order)
         torch.manual_seed(3)
         x = torch.randn(3, cin, H, H, dtype=torch.float64)
         w = torch.randn(cout, cin, k, k, dtype=torch.float64) * 0.05
@@ -197,6 +199,7 @@ def test_conv_f3_tiles(case, cfg, persistent, sched):
         L.set_f3_tile(-1)
         L.load().fg_set_f3_persistent(1)
         L.load().fg_set_f3_sched(-1)
+        L.load().fg_set_f3_order(7)
         L.set_conv_math(prev)
 
 
