@@ -65,6 +65,11 @@ __device__ __forceinline__ void dma_stage(char* sb, int wave, __amdgpu_buffer_rs
                                                  soff_b, 0, 0);
 }
 
+// one 1-KiB LDS-DMA piece (per-lane byte offset, per-stage scalar offset)
+__device__ __forceinline__ void dma_piece(char* dst, __amdgpu_buffer_rsrc_t r, int voff, int soff) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)dst, 16, voff, soff, 0, 0);
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
     static_assert(N >= 0 && N <= 15, "vmcnt immediate");
@@ -91,7 +96,8 @@ __device__ __forceinline__ void wait_vmcnt() {
 // LDS latency hides behind the DMA issue) and each column group's products run hh, hl, lh, so the
 // first MFMAs need only the cheap h half of the split and the l half overlaps them; 2 = as 1, with
 // the B fragments double-buffered in 2-block groups, pinned (group g+1 is read while group g's
-// products run; group 0 is read together with A, ahead of the DMA issue).
+// products run; group 0 is read together with A, ahead of the DMA issue); 3 = as 1, with the
+// next stage's LDS-DMA pieces spread between the column groups instead of one burst.
 template <int BM, int BN, int WM, int WN, int NS, int SCH>
 __global__ void __launch_bounds__((BM / WM) * (BN / WN) * 64, 1)
 conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
@@ -205,6 +211,45 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
         return true;
     };
 
+    // SCH 3: the same stage split into prep / pieces / advance, so that the pieces can be issued
+    // one or two at a time between the MFMA groups of the current stage (an LDS-DMA piece costs
+    // ~60 issue cycles among MFMAs but 100-185 in a burst beside the fragment reads)
+    int p_koff = 0, p_soffb = 0, p_buf = 0;   // p_buf: byte offset of the target stage in smem
+    bool p_on = false;
+    auto issue_prep = [&](int buf) {
+        p_on = it < total_tiles;
+        if (!p_on) return;
+        const int r = irev ? i_kh - 1 - ir : ir;
+        const int jb = is * i_c + ic * 32;
+        p_koff = __builtin_amdgcn_readfirstlane((r * i_sxr + jb) * 4);        // scalar offsets: wave-uniform
+        p_soffb = __builtin_amdgcn_readfirstlane((r * (i_jp / 32) + jb / 32) * 128);
+        p_buf = buf * STAGE;
+#ifdef FG_F3_DIAG
+        if (((alt_order >> 4) & 1) && ikt >= NS) p_on = false;
+#endif
+    };
+    auto issue_piece = [&](int i) {
+        if (!p_on) return;
+        // the LDS destination is wave-uniform (M0): say so, or the compiler emits a waterfall loop
+        if (i < A_GL)
+            dma_piece(smem + __builtin_amdgcn_readfirstlane(p_buf + (wave * A_GL + i) * 1024), xr, a_off[i], p_koff);
+        else
+            dma_piece(smem + __builtin_amdgcn_readfirstlane(p_buf + A_BYTES + (wave * B_GL + (i - A_GL)) * 1024), wr,
+                      b_off[i - A_GL], p_soffb);
+    };
+    auto issue_advance = [&]() {
+        if (it >= total_tiles) return false;
+        if (++is == i_kw) {
+            is = 0;
+            if (++ir == i_kh) { ir = 0; ++ic; }
+        }
+        if (++ikt == ig.nkt) {
+            it += G;
+            if (it < total_tiles) setup_issue();
+        }
+        return true;
+    };
+
     // ---- compute side
     int ct = first, ckt = 0;
     Geo cg = geo(ct);
@@ -258,6 +303,11 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
                 const char* rowp = sbuf + A_BYTES + (wn * WN + (t0 + t) * 16 + fr) * 64 + b_c;
                 bh[t] = *reinterpret_cast<const f16x8*>(rowp);
                 bl[t] = *reinterpret_cast<const f16x8*>(rowp + BN * 64);
+            }
+            if constexpr (SCH == 3) {
+                constexpr int NP = A_GL + B_GL, NGR = TN / TG, PPG = (NP + NGR - 1) / NGR;
+#pragma unroll
+                for (int i = (t0 / TG) * PPG; i < (t0 / TG + 1) * PPG && i < NP; ++i) issue_piece(i);
             }
             if constexpr (SCH == 0) {
 #pragma unroll
@@ -421,6 +471,11 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
             load_a(cur, va);
             if (issue_next(nxt)) ++issued;
             compute(cur, va);
+        } else if constexpr (SCH == 3) {
+            load_a(cur, va);
+            issue_prep(nxt);
+            compute(cur, va);
+            if (issue_advance()) ++issued;
         } else {
             f16x8 bh[2][TG2], bl[2][TG2];
             load_a(cur, va);
@@ -469,14 +524,17 @@ int launch_cfg(const ConvBatch& in, int nprob, hipStream_t stream) {
     constexpr int LDS = NS * (BM * 128 + 2 * BN * 64);
     const int per_cu = (160 * 1024) / LDS;
     const int grid = g_f3_persist ? std::min(total, fg::num_cus() * per_cu) : total;
-    const int sched = g_f3_sched >= 0 ? g_f3_sched : (BN > 64 ? 1 : 0);
+    const int sched = g_f3_sched >= 0 ? g_f3_sched : 3;
 #ifdef FG_F3_DIAG
     // timing-only diagnostic build (outputs are wrong): FG_F3_DIAG=1 compute without data movement,
     // 2 data movement without compute
     const char* dg = getenv("FG_F3_DIAG");
     const int g_f3_alt = ::g_f3_alt | ((dg ? atoi(dg) : 0) << 4);
 #endif
-    if (sched == 2)
+    if (sched == 3)
+        hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 3>), dim3(grid), dim3(NT), 0, stream, b, total,
+                           g_f3_alt);
+    else if (sched == 2)
         hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 2>), dim3(grid), dim3(NT), 0, stream, b, total,
                            g_f3_alt);
     else if (sched == 1)
@@ -533,7 +591,7 @@ FG_API int fg_set_f3_persistent(int on) {
 }
 
 FG_API int fg_set_f3_sched(int sched) {
-    if (sched < -1 || sched > 2) return fg::fail(FG_ERR_INVALID, "fg_set_f3_sched: %d", sched);
+    if (sched < -1 || sched > 3) return fg::fail(FG_ERR_INVALID, "fg_set_f3_sched: %d", sched);
     g_f3_sched = sched;
     return 0;
 }

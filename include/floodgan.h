@@ -155,7 +155,8 @@ int fg_set_f3_tile(int cfg);
 int fg_set_f3_order(int alt);
 /* Tuning hook: per-stage instruction order of the pipelined forward kernel: 0 = split all of A,
  * then the products; 1 = A reads ahead of the DMA issue, h-half products first; 2 = as 1 with
- * double-buffered B fragment groups; -1 (default) = the tuned choice per tile config. */
+ * double-buffered B fragment groups; 3 = as 1 with the next stage's DMA pieces spread between
+ * the MFMA groups; -1 (default) = the tuned choice per tile config. */
 int fg_set_f3_sched(int sched);
 /* Tuning hook: 1 (default) = the pipelined forward kernel runs one resident wave of workgroups that
  * loop over the tiles (the next tile's first k-stages stream in behind the current tile's last);

@@ -161,7 +161,7 @@ def test_convT(cin, cout, H, conv_math):
 
 
 @pytest.mark.parametrize("persistent,sched,order", [(0, 2, 3), (1, 2, 3), (1, 1, 3), (1, 0, 3), (1, 1, 2),
-                                                    (1, 1, 1), (1, 1, 0), (1, 1, 7)])
+                                                    (1, 1, 1), (1, 1, 0), (1, 1, 7), (1, 3, 7), (0, 3, 7)])
 @pytest.mark.parametrize("cfg", [-2, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
 @pytest.mark.parametrize("case", [(256, 256, 3, 1, 1, "reflect", 20), (128, 256, 4, 2, 1, "constant", 22),
                                   (64, 128, 3, 2, 1, "constant", 30), (256, 512, 4, 1, 1, "constant", 11),
