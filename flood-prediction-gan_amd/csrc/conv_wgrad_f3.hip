@@ -49,7 +49,11 @@ __device__ __forceinline__ void split4(const f32x4& v, float s, f16x4& h, f16x4&
     }
 }
 
-template <int TA>
+// SCH 0: each stage = store (split + LDS writes of the staged registers) and the next global
+// loads as one burst, then the MFMAs; SCH 1: the stage's MFMAs in four column groups with one
+// staging slot's store + reload in front of each (the VALU split and the LDS writes run beside
+// the partner wave's MFMAs instead of stalling the SIMD at the top of every stage).
+template <int TA, int SCH>
 __global__ void __launch_bounds__(512, 1)
 conv_wgrad_f3_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
     // 8 waves as NWA (a) x NWK (k); wave tile 64 (a) x WK (k): TA 256 -> 4 x 2, 64 x 128; TA 128 -> 2 x 4, 64 x 64
@@ -104,9 +108,8 @@ conv_wgrad_f3_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
         fgc::decomp(min(wm[i], M - 1), P.m_b, mab, wi[i], wa_[i], wb[i]);
     }
     f32x4 rp[SPT], rx[SPT];
-    auto load = [&]() {
-#pragma unroll
-        for (int i = 0; i < SPT; ++i) {
+    auto load_slot = [&](int i) {
+        {
             const bool ok = wm[i] < mend;
             const int pb = wi[i] * (int)P.spn + wa_[i] * (int)P.spa + wb[i] * (int)P.spb + a0 + col;
             const int xb = wi[i] * (int)P.sxn + wa_[i] * (int)P.sxa + wb[i] * (int)P.sxb + x_koff;
@@ -123,10 +126,13 @@ conv_wgrad_f3_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
             wi[i] += i32 + ca;
         }
     };
-    auto store = [&](int buf) {
-        char* b = smem + buf * BUF;
+    auto load = [&]() {
 #pragma unroll
-        for (int i = 0; i < SPT; ++i) {
+        for (int i = 0; i < SPT; ++i) load_slot(i);
+    };
+    auto store_slot = [&](int buf, int i) {
+        char* b = smem + buf * BUF;
+        {
             f16x4 h, l;
             if (p_slot) {
                 const int op = img_off<TA>(prow0 + 8 * i, col);
@@ -140,6 +146,10 @@ conv_wgrad_f3_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
             *reinterpret_cast<f16x4*>(b + 2 * IMGP + IMGX + ox) = l;
         }
     };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < SPT; ++i) store_slot(buf, i);
+    };
 
     f32x4 acc[TM][TN];
 #pragma unroll
@@ -150,7 +160,9 @@ conv_wgrad_f3_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
     // transposed-read lane roles: group g reads pixel rows 8g + q (and 8g + 4 + q), lane 4q+p of
     // the group addresses columns 4p..4p+3 of the 16-column block
     const int g = lane >> 4, q = (lane >> 2) & 3, p4 = (lane & 3) * 4;
-    auto compute = [&](int buf) {
+    constexpr int TG = SCH == 0 ? 4 : TN / SPT;          // column blocks per group (SCH 1: one slot per group)
+    static_assert(TN % TG == 0 && (SCH == 0 || TN / TG == SPT), "groups");
+    auto compute = [&](int buf, bool stage_next) {
         const char* b = smem + buf * BUF;
         f16x8 ah[TM], al[TM];
 #pragma unroll
@@ -161,29 +173,35 @@ conv_wgrad_f3_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
             al[tm] = tr_frag(b + IMGP, o0, o1);
         }
 #pragma unroll
-        for (int t0 = 0; t0 < TN; t0 += 4) {
-            f16x8 bh[4], bl[4];
+        for (int t0 = 0; t0 < TN; t0 += TG) {
+            f16x8 bh[TG], bl[TG];
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
+            for (int t = 0; t < TG; ++t) {
                 const int c = wk * WK + (t0 + t) * 16 + p4;
                 const int o0 = img_off<TK>(8 * g + q, c), o1 = img_off<TK>(8 * g + 4 + q, c);
                 bh[t] = tr_frag(b + 2 * IMGP, o0, o1);
                 bl[t] = tr_frag(b + 2 * IMGP + IMGX, o0, o1);
             }
+            if constexpr (SCH == 1) {
+                // this group's staging slot: split + write the registers of the next stage into the
+                // free buffer, then refill them with the stage after
+                if (stage_next) store_slot(buf ^ 1, t0 / TG);
+                load_slot(t0 / TG);
+            }
 #pragma unroll
             for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
-                for (int t = 0; t < 4; ++t)
+                for (int t = 0; t < TG; ++t)
                     acc[tm][t0 + t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[tm], bh[t], acc[tm][t0 + t], 0, 0, 0);
 #pragma unroll
             for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
-                for (int t = 0; t < 4; ++t)
+                for (int t = 0; t < TG; ++t)
                     acc[tm][t0 + t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[tm], bl[t], acc[tm][t0 + t], 0, 0, 0);
 #pragma unroll
             for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
-                for (int t = 0; t < 4; ++t)
+                for (int t = 0; t < TG; ++t)
                     acc[tm][t0 + t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[tm], bh[t], acc[tm][t0 + t], 0, 0, 0);
         }
     };
@@ -195,10 +213,14 @@ conv_wgrad_f3_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
     __syncthreads();
     for (int st = 0; st < nst; ++st) {
         const int cur = st & 1;
-        if (st + 1 < nst) store(cur ^ 1);
-        load();
-        __builtin_amdgcn_sched_barrier(0);
-        compute(cur);
+        if constexpr (SCH == 0) {
+            if (st + 1 < nst) store(cur ^ 1);
+            load();
+            __builtin_amdgcn_sched_barrier(0);
+            compute(cur, false);
+        } else {
+            compute(cur, st + 1 < nst);
+        }
         __syncthreads();
     }
 
@@ -222,7 +244,7 @@ conv_wgrad_f3_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
 
 }  // namespace
 
-int g_wgrad_f3 = 1;   // fg_set_wgrad_f3 (A/B hook)
+int g_wgrad_f3 = 2;   // fg_set_wgrad_f3 (A/B hook): 0 off, 1 stage schedule 0, 2 auto, 3 stage schedule 1
 
 namespace fgc {
 
@@ -234,10 +256,17 @@ int launch_wgrad_f3(const fg_wgrad_problem& p, hipStream_t stream, int* rc) {
         return 0;
     const int TA = p.n_a >= 256 ? 256 : 128;
     const int ta = (p.n_a + TA - 1) / TA, tk = (p.kh * p.j_valid + TK - 1) / TK;
-    if (TA == 256)
-        hipLaunchKernelGGL(conv_wgrad_f3_kernel<256>, dim3(ta * tk * p.splits), dim3(512), 0, stream, p, ta, tk);
+    const dim3 grid(ta * tk * p.splits);
+    // measured: the interleaved staging pays off on the 128-row tiles only
+    const int sch = g_wgrad_f3 == 3 || (g_wgrad_f3 == 2 && TA == 128) ? 1 : 0;
+    if (TA == 256 && sch == 1)
+        hipLaunchKernelGGL((conv_wgrad_f3_kernel<256, 1>), grid, dim3(512), 0, stream, p, ta, tk);
+    else if (TA == 256)
+        hipLaunchKernelGGL((conv_wgrad_f3_kernel<256, 0>), grid, dim3(512), 0, stream, p, ta, tk);
+    else if (sch == 1)
+        hipLaunchKernelGGL((conv_wgrad_f3_kernel<128, 1>), grid, dim3(512), 0, stream, p, ta, tk);
     else
-        hipLaunchKernelGGL(conv_wgrad_f3_kernel<128>, dim3(ta * tk * p.splits), dim3(512), 0, stream, p, ta, tk);
+        hipLaunchKernelGGL((conv_wgrad_f3_kernel<128, 0>), grid, dim3(512), 0, stream, p, ta, tk);
     *rc = fg::launched("conv_wgrad_f3");
     return 1;
 }
@@ -245,6 +274,7 @@ int launch_wgrad_f3(const fg_wgrad_problem& p, hipStream_t stream, int* rc) {
 }  // namespace fgc
 
 FG_API int fg_set_wgrad_f3(int on) {
-    g_wgrad_f3 = on != 0;
+    if (on < 0 || on > 3) return fg::fail(FG_ERR_INVALID, "fg_set_wgrad_f3: %d", on);
+    g_wgrad_f3 = on;
     return 0;
 }

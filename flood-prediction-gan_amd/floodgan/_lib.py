@@ -174,11 +174,13 @@ def set_f3_tile(cfg):
 _WGRAD_F3 = True
 
 
-def set_wgrad_f3(on):
-    """A/B hook of the pipelined f16x3 weight-gradient kernel."""
+def set_wgrad_f3(mode):
+    """A/B hook of the pipelined f16x3 weight-gradient kernel: 0 off, 1 stage schedule 0,
+    3 stage schedule 1, 2 (default, also True) the measured choice per tile."""
     global _WGRAD_F3
-    check(load().fg_set_wgrad_f3(int(bool(on))), "set_wgrad_f3")
-    _WGRAD_F3 = bool(on)
+    mode = 2 if mode is True else int(mode)
+    check(load().fg_set_wgrad_f3(mode), "set_wgrad_f3")
+    _WGRAD_F3 = mode != 0
 
 
 def wgrad_f3_on():

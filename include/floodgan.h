@@ -162,8 +162,9 @@ int fg_set_f3_sched(int sched);
  * loop over the tiles (the next tile's first k-stages stream in behind the current tile's last);
  * 0 = one workgroup per tile. */
 int fg_set_f3_persistent(int on);
-/* A/B hook of the pipelined f16x3 weight-gradient kernel (conv_wgrad_f3.hip, n_a >= 256): 1 on
- * (default), 0 off. */
+/* A/B hook of the pipelined f16x3 weight-gradient kernel (conv_wgrad_f3.hip, n_a >= 128): 0 off,
+ * 1 = staging as one burst per stage, 3 = staging slots interleaved with the MFMA groups,
+ * 2 (default) = the measured choice per tile (interleaved for 128-row tiles). */
 int fg_set_wgrad_f3(int on);
 
 /* Weight gradient into partial slabs (see fg_wgrad_problem). */

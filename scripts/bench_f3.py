@@ -94,20 +94,20 @@ def main():
         dw = torch.empty_like(w)
         res = {}
         for rep in range(2):
-            for on in (0, 1):
+            for on in (0, 1, 2):
                 L.set_wgrad_f3(on)
                 res.setdefault(on, []).append(time_it(lambda: ops.wgrad(wprob, wm, dw)))
         outs = {}
-        for on in (0, 1):
+        for on in (0, 1, 2):
             L.set_wgrad_f3(on)
             ops.wgrad(wprob, wm, dw)
             torch.cuda.synchronize()
             outs[on] = dw.clone()
-        for on in (0, 1):
+        for on in (0, 1, 2):
             ms = min(res[on])
-            print(f"{name:36s} {'f3' if on else 'register-staged':16s} {ms:8.3f} ms {flops / ms / 1e9:7.1f} TFLOP/s"
+            print(f"{name:36s} {('f3 sched ' + str(on - 1)) if on else 'register-staged':16s} {ms:8.3f} ms {flops / ms / 1e9:7.1f} TFLOP/s"
                   f"  rel diff {nrel(outs[on], outs[0]):.2e}", flush=True)
-        L.set_wgrad_f3(1)
+        L.set_wgrad_f3(2)
     # the row-strip window kernel on the content head (fwd, and the input gradient's geometry)
     from floodgan.plans import Buf
     dev = "cuda"

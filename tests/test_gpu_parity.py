@@ -203,7 +203,7 @@ def test_conv_f3_tiles(case, cfg, persistent, sched, order):
         L.set_conv_math(prev)
 
 
-@pytest.mark.parametrize("on", [0, 1])
+@pytest.mark.parametrize("on", [0, 1, 2, 3])
 @pytest.mark.parametrize("case", [(256, 256, 3, 1, 1, "reflect", 40), (128, 256, 4, 2, 1, "constant", 34),
                                   (256, 512, 4, 1, 1, "constant", 17), (64, 128, 3, 2, 1, "constant", 36),
                                   (128, 128, 4, 2, 1, "constant", 30)])
@@ -232,7 +232,7 @@ def test_wgrad_f3(case, on):
         torch.cuda.synchronize()
         assert nrel(dw, gw_ref) < KTOL
     finally:
-        L.set_wgrad_f3(1)
+        L.set_wgrad_f3(2)
         L.set_conv_math(prev)
 
 
