@@ -346,13 +346,18 @@ def test_disc_head_n1():
 
 # ------------------------------------------------------------------ instance norm
 
-@pytest.mark.parametrize("act,fold,residual", [(1, 0, False), (2, 0, False), (0, 0, True), (1, 1, False),
-                                               (1, 3, False)])
-def test_instnorm_fwd_bwd(act, fold, residual):
+@pytest.mark.parametrize("act,fold,residual,C,gadd", [(1, 0, False, 64, False), (2, 0, False, 64, False),
+                                                       (0, 0, True, 64, False), (1, 1, False, 64, False),
+                                                       (1, 3, False, 64, False), (1, 1, False, 256, True),
+                                                       (2, 1, False, 16, True), (1, 3, False, 32, True),
+                                                       (0, 0, False, 128, True)])
+def test_instnorm_fwd_bwd(act, fold, residual, C, gadd):
+    """IN forward (stats, apply with activation / residual / padding) and backward (fold of the
+    reflect-pad gradient, the added residual gradient `gadd`) against fp64 autograd"""
     from floodgan import ops
     from floodgan.plans import Buf
     torch.manual_seed(3)
-    C, H = 64, 20
+    H = 20
     c = (torch.randn(2, C, H, H, dtype=torch.float64) * 2 + 0.7).requires_grad_(True)
     r = torch.randn(2, C, H, H, dtype=torch.float64)
     y = F.instance_norm(c, eps=1e-5)
@@ -362,7 +367,13 @@ def test_instnorm_fwd_bwd(act, fold, residual):
     pad_mode = "reflect" if fold else "constant"
     yp = F.pad(y, (max(fold, 1),) * 4, mode=pad_mode if fold else "constant")
     gy = torch.randn_like(yp)
-    (gc_ref,) = torch.autograd.grad(yp, c, gy)
+    if gadd:      # a second gradient on the (unpadded) block output, e.g. from the residual branch
+        ga = torch.randn(2, C, H, H, dtype=torch.float64)
+        (gc_ref,) = torch.autograd.grad([yp, y], c, [gy, ga])
+        gab = buf_from(ga, 0, "constant")
+    else:
+        (gc_ref,) = torch.autograd.grad(yp, c, gy)
+        gab = None
     cb = buf_from(c.detach(), 0, "constant")
     rb = buf_from(r, 0, "constant") if residual else None
     mean, rstd = ops.in_stats(cb)
@@ -376,10 +387,10 @@ def test_instnorm_fwd_bwd(act, fold, residual):
     if fold:
         gsrc = buf_from(gy, 0, "constant")
         gsrc = Buf(gsrc.t, 2, H + 2 * fold, H + 2 * fold, C, 0)
-        ops.in_bwd(gsrc, fold, None, cb, mean, rstd, act, gdst, bias_g)
+        ops.in_bwd(gsrc, fold, gab, cb, mean, rstd, act, gdst, bias_g)
     else:
         gsrc = buf_from(gy[:, :, pad:-pad, pad:-pad], 0, "constant")
-        ops.in_bwd(gsrc, 0, None, cb, mean, rstd, act, gdst, bias_g)
+        ops.in_bwd(gsrc, 0, gab, cb, mean, rstd, act, gdst, bias_g)
     torch.cuda.synchronize()
     assert nrel(nchw(gdst), gc_ref) < 1e-5
     assert float(gdst.nhwc()[:, 0].abs().max()) == 0.0       # zero border
