@@ -33,7 +33,7 @@ def resblock_conv_flops(batch, res):
     return 2.0 * m * 256 * (256 * 9)
 
 
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "round1", "r1h_pmc_resblock_fwd.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "round1", "r1l_pmc_resblock_fwd.json")
 
 
 def pmc_traffic(kernel_tag):

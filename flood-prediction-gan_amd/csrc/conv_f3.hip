@@ -304,8 +304,11 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
                 bh[t] = *reinterpret_cast<const f16x8*>(rowp);
                 bl[t] = *reinterpret_cast<const f16x8*>(rowp + BN * 64);
             }
-            if constexpr (SCH == 3) {
-                constexpr int NP = A_GL + B_GL, NGR = TN / TG, PPG = (NP + NGR - 1) / NGR;
+            if constexpr (SCH >= 3) {
+                // SCH 3: pieces spread over all column groups; 4: over the first half; 5: all in the
+                // first group (each piece needs time to land before the stage-end vmcnt)
+                constexpr int NGA = TN / TG, NGR = SCH == 3 ? NGA : SCH == 4 ? (NGA + 1) / 2 : 1;
+                constexpr int NP = A_GL + B_GL, PPG = (NP + NGR - 1) / NGR;
 #pragma unroll
                 for (int i = (t0 / TG) * PPG; i < (t0 / TG + 1) * PPG && i < NP; ++i) issue_piece(i);
             }
@@ -471,7 +474,7 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
             load_a(cur, va);
             if (issue_next(nxt)) ++issued;
             compute(cur, va);
-        } else if constexpr (SCH == 3) {
+        } else if constexpr (SCH >= 3) {
             load_a(cur, va);
             issue_prep(nxt);
             compute(cur, va);
@@ -531,7 +534,13 @@ int launch_cfg(const ConvBatch& in, int nprob, hipStream_t stream) {
     const char* dg = getenv("FG_F3_DIAG");
     const int g_f3_alt = ::g_f3_alt | ((dg ? atoi(dg) : 0) << 4);
 #endif
-    if (sched == 3)
+    if (sched == 5)
+        hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 5>), dim3(grid), dim3(NT), 0, stream, b, total,
+                           g_f3_alt);
+    else if (sched == 4)
+        hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 4>), dim3(grid), dim3(NT), 0, stream, b, total,
+                           g_f3_alt);
+    else if (sched == 3)
         hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 3>), dim3(grid), dim3(NT), 0, stream, b, total,
                            g_f3_alt);
     else if (sched == 2)
@@ -591,7 +600,7 @@ FG_API int fg_set_f3_persistent(int on) {
 }
 
 FG_API int fg_set_f3_sched(int sched) {
-    if (sched < -1 || sched > 3) return fg::fail(FG_ERR_INVALID, "fg_set_f3_sched: %d", sched);
+    if (sched < -1 || sched > 5) return fg::fail(FG_ERR_INVALID, "fg_set_f3_sched: %d", sched);
     g_f3_sched = sched;
     return 0;
 }

@@ -5,6 +5,8 @@
 // Statistics: per-(n,c) plane sums over chunked pixel ranges, shifted by the plane's first
 // value (robust E[x^2]-E[x]^2), accumulated per thread in fp32, combined in fp64.
 // Backward: dL/dx = rstd * (g' - mean(g') - xhat * mean(g' xhat)), g' = g * act'(xhat).
+#include <algorithm>
+
 #include "fg_common.hpp"
 
 namespace {
@@ -27,6 +29,7 @@ __device__ __forceinline__ unsigned absbits4(const f32x4& v) {
 
 constexpr int NT = 256;
 constexpr int MAX_CHUNKS = 256;
+constexpr int CS_CHUNKS = 1024;     // channel-sum blocks (workspace: fg_channel_sum_workspace_doubles)
 
 int choose_chunks(int n, long long hw) {
     long long c = (2048 + n - 1) / n;      // ~2048 workgroups: enough loads in flight per CU
@@ -317,6 +320,22 @@ __global__ void in_bwd_apply_kernel(fg_view g, int fp, fg_view gadd, fg_view src
     if (amax) absmax_flush(am, amax);
 }
 
+// float4 form: block = interior row (n, yy), threads over (x, channel quad) of the row
+__global__ void __launch_bounds__(256) act_bwd4_kernel(fg_view g, fg_view y, int act) {
+    const int C = g.c_alloc, C4 = C / 4, W4 = g.w * C4;
+    const int n = blockIdx.x / g.h, yy = blockIdx.x - (blockIdx.x / g.h) * g.h;
+    float* grow = g.ptr + fg::vidx(g, n, yy, 0);
+    const float* yrow = y.ptr + fg::vidx(y, n, yy, 0);
+    for (int i = threadIdx.x; i < W4; i += 256) {
+        const int x = i / C4, c = (i - x * C4) * 4;
+        f32x4 gv = ld4(grow + (size_t)x * C + c);
+        const f32x4 yv = ld4(yrow + (size_t)x * C + c);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) gv[e] *= fg::act_grad(yv[e], act);
+        *reinterpret_cast<f32x4*>(grow + (size_t)x * C + c) = gv;
+    }
+}
+
 __global__ void act_bwd_kernel(fg_view g, fg_view y, int act) {
     const int C = g.c_alloc;
     const long long total = (long long)g.n * g.h * g.w * C;
@@ -371,33 +390,38 @@ __global__ void channel_sum_kernel(fg_view src, int c_valid, int chunks, double*
     }
 }
 
-__global__ void channel_sum4_kernel(fg_view src, int chunks, double* __restrict__ work) {
-    // c_alloc % 4 == 0: threads = (pixel lane g, float4 channel group c4)
+__global__ void __launch_bounds__(256) channel_sum4_kernel(fg_view src, int chunks, double* __restrict__ work) {
+    // c_alloc % 4 == 0: threads = (pixel lane gi, float4 channel group c4); the block's pixel range is
+    // walked as (n, y, x) without divisions, two pixels per trip
     const int C = src.c_alloc, L = C / 4, PG = NT / L;
     const int gi = threadIdx.x / L, c4 = threadIdx.x - (threadIdx.x / L) * L;
     const long long P = (long long)src.n * src.h * src.w;
     const long long per = (P + chunks - 1) / chunks;
     const long long p0 = blockIdx.x * per, p1 = min(P, p0 + per);
     __shared__ double red[NT][4];
-    double acc[4] = {0, 0, 0, 0};
-    if (gi < PG) {
-        f32x4 s = {0.f, 0.f, 0.f, 0.f};
-        int cnt = 0;
-        for (long long p = p0 + gi; p < p1; p += PG) {
-            const int x = (int)(p % src.w);
-            const long long t = p / src.w;
-            const int y = (int)(t % src.h);
-            const int n = (int)(t / src.h);
-            s += ld4(src.ptr + fg::vidx(src, n, y, x) + 4 * c4);
-            if (++cnt == 64) {
-                for (int e = 0; e < 4; ++e) acc[e] += s[e];
-                s = f32x4{0.f, 0.f, 0.f, 0.f};
-                cnt = 0;
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+    if (gi < PG && p0 + gi < p1) {
+        const long long q = p0 + gi;
+        int x = (int)(q % src.w), y = (int)((q / src.w) % src.h), n = (int)(q / ((long long)src.w * src.h));
+        auto step = [&]() {
+            x += PG;
+            while (x >= src.w) {
+                x -= src.w;
+                if (++y == src.h) { y = 0; ++n; }
             }
+        };
+        const int cnt = (int)((p1 - q + PG - 1) / PG);       // pixels of this lane (per <= 4096: fp32-safe)
+        int k = 0;
+        for (; k + 1 < cnt; k += 2) {
+            const f32x4 a = ld4(src.ptr + fg::vidx(src, n, y, x) + 4 * c4);
+            step();
+            const f32x4 b = ld4(src.ptr + fg::vidx(src, n, y, x) + 4 * c4);
+            step();
+            s += a + b;
         }
-        for (int e = 0; e < 4; ++e) acc[e] += s[e];
+        if (k < cnt) s += ld4(src.ptr + fg::vidx(src, n, y, x) + 4 * c4);
     }
-    for (int e = 0; e < 4; ++e) red[threadIdx.x][e] = acc[e];
+    for (int e = 0; e < 4; ++e) red[threadIdx.x][e] = s[e];
     __syncthreads();
     if (threadIdx.x < L) {
         double a[4] = {0, 0, 0, 0};
@@ -407,15 +431,25 @@ __global__ void channel_sum4_kernel(fg_view src, int chunks, double* __restrict_
     }
 }
 
-__global__ void channel_sum4_finalize(int C, int c_valid, int chunks, const double* __restrict__ work, float* out,
-                                      int accumulate) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= c_valid) return;
+// block = one channel: 256 lanes sum the chunk partials (strided), then a fixed-order tree
+__global__ void __launch_bounds__(256) channel_sum4_finalize(int C, int c_valid, int chunks,
+                                                             const double* __restrict__ work, float* out,
+                                                             int accumulate) {
+    const int c = blockIdx.x;
+    __shared__ double red[256];
     double s = 0;
-    for (int k = 0; k < chunks; ++k) s += work[(size_t)k * C + c];
-    float v = (float)s;
-    if (accumulate) v += out[c];
-    out[c] = v;
+    for (int k = threadIdx.x; k < chunks; k += 256) s += work[(size_t)k * C + c];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int off = 128; off > 0; off >>= 1) {
+        if (threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        float v = (float)red[0];
+        if (accumulate) v += out[c];
+        out[c] = v;
+    }
 }
 
 __global__ void channel_sum_finalize(int c_valid, int chunks, const double* __restrict__ work, float* out,
@@ -502,26 +536,36 @@ FG_API int fg_in_bwd(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, cons
 FG_API int fg_act_bwd(fg_view g, fg_view y, int act, hipStream_t stream) {
     if (!ok_view(g) || !ok_view(y) || g.c_alloc != y.c_alloc || g.h != y.h || g.w != y.w || g.n != y.n)
         return fg::fail(FG_ERR_INVALID, "fg_act_bwd: bad args");
+    if (g.c_alloc % 4 == 0) {
+        hipLaunchKernelGGL(act_bwd4_kernel, dim3(g.n * g.h), dim3(256), 0, stream, g, y, act);
+        return fg::launched("act_bwd4");
+    }
     const long long total = (long long)g.n * g.h * g.w * g.c_alloc;
     hipLaunchKernelGGL(act_bwd_kernel, dim3(fg::blocks_for(total, 256, 16384)), dim3(256), 0, stream, g, y, act);
     return fg::launched("act_bwd");
+}
+
+FG_API long long fg_channel_sum_workspace_doubles(int c_alloc) {
+    return (long long)std::max(CS_CHUNKS, MAX_CHUNKS) * c_alloc + 64;
 }
 
 FG_API int fg_channel_sum(fg_view src, int c_valid, float* out, int accumulate, double* work, hipStream_t stream) {
     if (!ok_view(src) || !out || !work || c_valid < 1 || c_valid > src.c_alloc)
         return fg::fail(FG_ERR_INVALID, "fg_channel_sum: bad args");
     const long long P = (long long)src.n * src.h * src.w;
-    int chunks = (int)((P + 4095) / 4096);
-    if (chunks > MAX_CHUNKS) chunks = MAX_CHUNKS;
-    if (chunks < 1) chunks = 1;
     if (src.c_alloc % 4 == 0 && NT % (src.c_alloc / 4) == 0) {
+        // ~2048 pixels per block, at most CS_CHUNKS blocks (the workspace bound)
+        int chunks = (int)std::min<long long>(CS_CHUNKS, std::max<long long>(1, (P + 2047) / 2048));
         hipLaunchKernelGGL(channel_sum4_kernel, dim3(chunks), dim3(NT), 0, stream, src, chunks, work);
         int e = fg::launched("channel_sum4");
         if (e) return e;
-        hipLaunchKernelGGL(channel_sum4_finalize, dim3((c_valid + 255) / 256), dim3(256), 0, stream, src.c_alloc,
-                           c_valid, chunks, work, out, accumulate);
+        hipLaunchKernelGGL(channel_sum4_finalize, dim3(c_valid), dim3(256), 0, stream, src.c_alloc, c_valid, chunks,
+                           work, out, accumulate);
         return fg::launched("channel_sum4_finalize");
     }
+    int chunks = (int)((P + 4095) / 4096);
+    if (chunks > MAX_CHUNKS) chunks = MAX_CHUNKS;
+    if (chunks < 1) chunks = 1;
     const int groups = (c_valid + NT - 1) / NT;
     hipLaunchKernelGGL(channel_sum_kernel, dim3(chunks, groups), dim3(NT), 0, stream, src, c_valid, chunks, work);
     int e = fg::launched("channel_sum");

@@ -101,6 +101,7 @@ SIGNATURES = {
                   C.c_void_p, C.c_void_p, C.c_void_p],
     "fg_act_bwd": [fg_view, fg_view, C.c_int, C.c_void_p],
     "fg_channel_sum": [fg_view, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p],
+    "fg_channel_sum_workspace_doubles": [C.c_int],
     "fg_tail_fwd": [fg_view, fg_view, fg_sview, C.c_void_p, C.c_void_p, C.c_void_p],
     "fg_tail_bwd": [fg_view, fg_view, fg_sview, fg_sview, fg_view, fg_view, C.c_void_p],
     "fg_mse_const": [C.c_void_p, C.c_longlong, C.c_float, C.c_float, C.c_void_p, C.c_void_p, C.c_void_p,
@@ -110,7 +111,8 @@ SIGNATURES = {
     "fg_adam_step": [C.POINTER(fg_adam_tensor), C.c_int, C.c_double, C.c_double, C.c_double, C.c_double,
                      C.c_longlong, C.c_void_p],
 }
-RESTYPES = {"fg_last_error": C.c_char_p, "fg_in_workspace_doubles": C.c_longlong}
+RESTYPES = {"fg_last_error": C.c_char_p, "fg_in_workspace_doubles": C.c_longlong,
+            "fg_channel_sum_workspace_doubles": C.c_longlong}
 
 _lib = None
 

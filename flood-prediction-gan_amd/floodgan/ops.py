@@ -430,7 +430,7 @@ def act_bwd(g, y, act):
 
 
 def channel_sum(src, c_valid, out, accumulate=False):
-    work = torch.empty(256 * c_valid + 64, dtype=torch.float64, device=src.t.device)
+    work = torch.empty(_lib().fg_channel_sum_workspace_doubles(src.c), dtype=torch.float64, device=src.t.device)
     L.check(_lib().fg_channel_sum(view(src), c_valid, L.ptr(out), int(accumulate), L.ptr(work), L.stream_handle()),
             "channel_sum")
 

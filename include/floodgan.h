@@ -273,9 +273,11 @@ int fg_in_bwd(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, const float
 /* g *= act'(y) in place over the interior (y = saved activation output). */
 int fg_act_bwd(fg_view g, fg_view y, int act, hipStream_t stream);
 
-/* out[c] (+)= sum over n,y,x of src(n,y,x,c) for c < c_valid.  Bias gradients. */
+/* out[c] (+)= sum over n,y,x of src(n,y,x,c) for c < c_valid.  Bias gradients.  `work` holds
+ * fg_channel_sum_workspace_doubles(src.c_alloc) doubles. */
 int fg_channel_sum(fg_view src, int c_valid, float* out, int accumulate, double* work,
                    hipStream_t stream);
+long long fg_channel_sum_workspace_doubles(int c_alloc);
 
 /* ---------------------------------------------------------------------------------------- */
 /* generator tail: tanh(27) + softmax(10) + attention composite                              */

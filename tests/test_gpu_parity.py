@@ -687,3 +687,39 @@ def test_reference_loop_with_dropin_modules(golden):
         out = G(x)
     env = _reference_envelope(g)[0][0]
     assert nrel(out, torch.from_numpy(g["it0_g_out"])) < max(NTOL, 2 * env)
+
+
+# ------------------------------------------------------------------ bias-gradient sums, activation backward
+
+@pytest.mark.parametrize("N,H,C,c_valid,pad", [(2, 33, 32, 27, 3), (2, 40, 16, 10, 0), (3, 17, 64, 64, 1),
+                                               (2, 64, 4, 1, 0), (1, 9, 12, 12, 2)])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_channel_sum(N, H, C, c_valid, pad, accumulate):
+    """fg_channel_sum (bias gradients: models/model_architectures.py conv biases without a following
+    IN) against an fp64 sum, padded views and partial channel ranges included"""
+    from floodgan import ops
+    torch.manual_seed(5)
+    x = torch.randn(N, C, H, H, dtype=torch.float64)
+    b = buf_from(x, pad, "constant")
+    out = torch.randn(C, device=DEV)
+    prev = out.clone()
+    ops.channel_sum(b, c_valid, out, accumulate)
+    torch.cuda.synchronize()
+    ref = x.float().double().sum((0, 2, 3))[:c_valid] + (prev[:c_valid].double().cpu() if accumulate else 0)
+    assert nrel(out[:c_valid], ref) < 1e-5
+    assert torch.equal(out[c_valid:].cpu(), prev[c_valid:].cpu())
+
+
+@pytest.mark.parametrize("C,act", [(64, 2), (16, 1), (3, 2)])
+def test_act_bwd(C, act):
+    """fg_act_bwd: g *= act'(y) over the interior of padded views (ReLU / LeakyReLU(0.2))"""
+    from floodgan import ops
+    torch.manual_seed(6)
+    g = torch.randn(2, C, 21, 21, dtype=torch.float64)
+    y = torch.randn(2, C, 21, 21, dtype=torch.float64)
+    gb, yb = buf_from(g, 1, "constant"), buf_from(y, 2, "constant")
+    ops.act_bwd(gb, yb, act)
+    torch.cuda.synchronize()
+    slope = 0.0 if act == 1 else 0.2
+    ref = g.float().double() * torch.where(y.float() > 0, torch.ones_like(y), torch.full_like(y, slope))
+    assert nrel(nchw(gb), ref) < 1e-6
