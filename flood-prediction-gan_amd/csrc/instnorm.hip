@@ -277,12 +277,13 @@ __global__ void __launch_bounds__(64 * FG) in_bwd_finalize_kernel(int N, int C, 
     bpart[idx] = -(double)rstd[idx] * sx * sgx / HW;
 }
 
-__global__ void in_bwd_bias_kernel(int N, int C, const double* __restrict__ bpart, float* __restrict__ bias_grad) {
+__global__ void in_bwd_bias_kernel(int N, int C, const double* __restrict__ bpart, float* __restrict__ bias_grad,
+                                   int accumulate) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= C) return;
     double s = 0;
     for (int n = 0; n < N; ++n) s += bpart[(size_t)n * C + c];
-    bias_grad[c] = (float)s;
+    bias_grad[c] = accumulate ? bias_grad[c] + (float)s : (float)s;
 }
 
 __global__ void in_bwd_apply_kernel(fg_view g, int fp, fg_view gadd, fg_view src, const float* __restrict__ mean,
@@ -498,7 +499,8 @@ FG_API int fg_in_apply(fg_view src, const float* mean, const float* rstd, int ac
 }
 
 FG_API int fg_in_bwd(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, const float* mean, const float* rstd,
-                     int act, fg_view dst, float* bias_grad, double* work, float* absmax, hipStream_t stream) {
+                     int act, fg_view dst, float* bias_grad, int bias_accumulate, double* work, float* absmax,
+                     hipStream_t stream) {
     if (!ok_view(gsrc) || !ok_view(src) || !ok_view(dst) || !mean || !rstd || !work || src.c_alloc % 4 ||
         (NT % (src.c_alloc / 4)) != 0 || gsrc.c_alloc != src.c_alloc || dst.c_alloc != src.c_alloc ||
         dst.h != src.h || dst.w != src.w || dst.n != src.n)
@@ -523,7 +525,7 @@ FG_API int fg_in_bwd(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, cons
     if (e) return e;
     if (bias_grad) {
         hipLaunchKernelGGL(in_bwd_bias_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, src.n, C, bpart,
-                           bias_grad);
+                           bias_grad, bias_accumulate);
         e = fg::launched("in_bwd_bias");
         if (e) return e;
     }

@@ -95,6 +95,29 @@ __global__ void fold_add_kernel(fg_view g, int fp, fg_view add, fg_view dst) {
     }
 }
 
+// One thread per (n, ch, y, x) of the NCHW destination, x fastest (coalesced stores; the
+// 9-channel NHWC source rows are read at a 36-byte pixel stride, all within a few lines).
+__global__ void unfold_nchw_kernel(fg_view g, int fp, int c, fg_wview dst, int h, int w, int acc) {
+    const long long total = (long long)g.n * c * h * w;
+    for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const int x = (int)(idx % w);
+        long long q = idx / w;
+        const int y = (int)(q % h);
+        q /= h;
+        const int ch = (int)(q % c);
+        const int n = (int)(q / c);
+        int ys[3], xs[3];
+        const int ny = fp > 0 ? fold_src(y, h, fp, ys) : (ys[0] = y, 1);
+        const int nx = fp > 0 ? fold_src(x, w, fp, xs) : (xs[0] = x, 1);
+        float v = 0.f;
+        for (int iy = 0; iy < ny; ++iy)
+            for (int ix = 0; ix < nx; ++ix) v += g.ptr[fg::vidx(g, n, ys[iy], xs[ix]) + ch];
+        float* d = dst.ptr + n * dst.sn + ch * dst.sc + y * dst.sy + x * dst.sx;
+        *d = ch < acc ? *d + v : v;
+    }
+}
+
 }  // namespace
 
 FG_API int fg_pack_input(fg_sview a, int ca, fg_sview b, int cb, fg_view dst, int img0, int nimg, int pad_mode,
@@ -133,4 +156,19 @@ FG_API int fg_fold_add(fg_view gpad, int fold_pad, fg_view add, fg_view dst, hip
     hipLaunchKernelGGL(fold_add_kernel, dim3(fg::blocks_for(total, 256, 16384)), dim3(256), 0, stream, gpad,
                        fold_pad, add, dst);
     return fg::launched("fold_add");
+}
+
+FG_API int fg_unfold_nchw(fg_view gpad, int fold_pad, int c, fg_wview dst, int h, int w, int acc_channels,
+                          hipStream_t stream) {
+    if (!gpad.ptr || !dst.ptr || c <= 0 || c > gpad.c_alloc || fold_pad < 0 || h <= 0 || w <= 0)
+        return fg::fail(FG_ERR_INVALID, "fg_unfold_nchw: bad args");
+    if (gpad.h != h + 2 * fold_pad || gpad.w != w + 2 * fold_pad)
+        return fg::fail(FG_ERR_INVALID, "fg_unfold_nchw: gpad %dx%d vs dst %dx%d fold %d", gpad.h, gpad.w, h, w,
+                        fold_pad);
+    if (fold_pad >= h || fold_pad >= w) return fg::fail(FG_ERR_INVALID, "fg_unfold_nchw: fold too wide");
+    const long long total = (long long)gpad.n * c * h * w;
+    if (total == 0) return 0;
+    hipLaunchKernelGGL(unfold_nchw_kernel, dim3(fg::blocks_for(total, 256, 16384)), dim3(256), 0, stream, gpad,
+                       fold_pad, c, dst, h, w, acc_channels);
+    return fg::launched("unfold_nchw");
 }

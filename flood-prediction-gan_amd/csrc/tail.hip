@@ -69,7 +69,8 @@ __global__ void tail_fwd_kernel(fg_view cl, fg_view al, fg_sview x, float* __res
     }
 }
 
-__global__ void tail_bwd_kernel(fg_view cl, fg_view al, fg_sview x, fg_sview gout, fg_view gc, fg_view ga) {
+__global__ void tail_bwd_kernel(fg_view cl, fg_view al, fg_sview x, fg_sview gout, fg_view gc, fg_view ga,
+                                fg_wview gx) {
     // iterate over gc's padded extent so its zero border is written too
     const int H = cl.h, W = cl.w;
     const int hp = H + 2 * gc.pad, wp = W + 2 * gc.pad;
@@ -112,6 +113,10 @@ __global__ void tail_bwd_kernel(fg_view cl, fg_view al, fg_sview x, fg_sview gou
             *reinterpret_cast<f32x4*>(gcp + 4 * q) = f32x4{go[4 * q], go[4 * q + 1], go[4 * q + 2], go[4 * q + 3]};
         for (int i = 32; i < gc.c_alloc; i += 4) *reinterpret_cast<f32x4*>(gcp + i) = f32x4{0.f, 0.f, 0.f, 0.f};
         gatt[9] = g[0] * xin[0] + g[1] * xin[1] + g[2] * xin[2];
+        if (gx.ptr) {  // d(output10)/d(input[:, :3]) = attention10 (models/model_architectures.py:393, :251)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) gx.ptr[n * gx.sn + c * gx.sc + yy * gx.sy + xx * gx.sx] = g[c] * v.a[9];
+        }
         float dot = 0.f;
 #pragma unroll
         for (int i = 0; i < NATT; ++i) dot += v.a[i] * gatt[i];
@@ -143,7 +148,7 @@ FG_API int fg_tail_fwd(fg_view content_logits, fg_view att_logits, fg_sview x, f
 }
 
 FG_API int fg_tail_bwd(fg_view content_logits, fg_view att_logits, fg_sview x, fg_sview g_out, fg_view g_content,
-                       fg_view g_att, hipStream_t stream) {
+                       fg_view g_att, fg_wview g_x, hipStream_t stream) {
     if (!content_logits.ptr || !att_logits.ptr || !x.ptr || !g_out.ptr || !g_content.ptr || !g_att.ptr ||
         content_logits.c_alloc < 28 || content_logits.c_alloc % 4 || att_logits.c_alloc < 12 ||
         att_logits.c_alloc % 4 || g_content.c_alloc < 32 || g_content.c_alloc % 4 || g_att.c_alloc < 16 ||
@@ -154,6 +159,6 @@ FG_API int fg_tail_bwd(fg_view content_logits, fg_view att_logits, fg_sview x, f
     const long long total = (long long)content_logits.n * (content_logits.h + 2 * g_content.pad) *
                             (content_logits.w + 2 * g_content.pad);
     hipLaunchKernelGGL(tail_bwd_kernel, dim3(fg::blocks_for(total, 256, 16384)), dim3(256), 0, stream,
-                       content_logits, att_logits, x, g_out, g_content, g_att);
+                       content_logits, att_logits, x, g_out, g_content, g_att, g_x);
     return fg::launched("tail_bwd");
 }

@@ -6,7 +6,9 @@ the Model/train_paired API mirror the reference, the arithmetic runs in hand-wri
 kernels (libfloodgan.so, C-ABI in include/floodgan.h).
 """
 from ._lib import load as load_library  # noqa: F401
-from .model_architectures import (PairedAttentionBlock, PairedAttentionDiscriminator,  # noqa: F401
+from .model_architectures import (AttentionGANBlock, AttentionGANDiscriminator,  # noqa: F401
+                                  AttentionGANGenerator, PairedAttentionBlock, PairedAttentionDiscriminator,
                                   PairedAttentionGenerator)
 
-__all__ = ["PairedAttentionGenerator", "PairedAttentionBlock", "PairedAttentionDiscriminator", "load_library"]
+__all__ = ["PairedAttentionGenerator", "PairedAttentionBlock", "PairedAttentionDiscriminator",
+           "AttentionGANGenerator", "AttentionGANBlock", "AttentionGANDiscriminator", "load_library"]

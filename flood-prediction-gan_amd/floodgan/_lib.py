@@ -30,6 +30,9 @@ class fg_sview(C.Structure):
                 ("sy", C.c_longlong), ("sx", C.c_longlong)]
 
 
+fg_wview = fg_sview   # same layout (float* + 4 strides), writable on the C side
+
+
 class fg_conv_problem(C.Structure):
     _fields_ = [("x", C.c_void_p), ("w", C.c_void_p), ("bias", C.c_void_p), ("y", C.c_void_p),
                 ("sxn", C.c_longlong), ("sxa", C.c_longlong), ("sxb", C.c_longlong), ("sxr", C.c_longlong),
@@ -94,16 +97,17 @@ SIGNATURES = {
     "fg_pack_input": [fg_sview, C.c_int, fg_sview, C.c_int, fg_view, C.c_int, C.c_int, C.c_int, C.c_void_p],
     "fg_zero_border": [fg_view, C.c_void_p],
     "fg_fold_add": [fg_view, C.c_int, fg_view, fg_view, C.c_void_p],
+    "fg_unfold_nchw": [fg_view, C.c_int, C.c_int, fg_wview, C.c_int, C.c_int, C.c_int, C.c_void_p],
     "fg_in_workspace_doubles": [C.c_int, C.c_int],
     "fg_in_stats": [fg_view, C.c_float, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p],
     "fg_in_apply": [fg_view, C.c_void_p, C.c_void_p, C.c_int, fg_view, fg_view, C.c_int, C.c_void_p, C.c_void_p],
     "fg_in_bwd": [fg_view, C.c_int, fg_view, fg_view, C.c_void_p, C.c_void_p, C.c_int, fg_view, C.c_void_p,
-                  C.c_void_p, C.c_void_p, C.c_void_p],
+                  C.c_int, C.c_void_p, C.c_void_p, C.c_void_p],
     "fg_act_bwd": [fg_view, fg_view, C.c_int, C.c_void_p],
     "fg_channel_sum": [fg_view, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p],
     "fg_channel_sum_workspace_doubles": [C.c_int],
     "fg_tail_fwd": [fg_view, fg_view, fg_sview, C.c_void_p, C.c_void_p, C.c_void_p],
-    "fg_tail_bwd": [fg_view, fg_view, fg_sview, fg_sview, fg_view, fg_view, C.c_void_p],
+    "fg_tail_bwd": [fg_view, fg_view, fg_sview, fg_sview, fg_view, fg_view, fg_wview, C.c_void_p],
     "fg_mse_const": [C.c_void_p, C.c_longlong, C.c_float, C.c_float, C.c_void_p, C.c_void_p, C.c_void_p,
                      C.c_void_p],
     "fg_l1": [fg_sview, fg_sview, C.c_int, C.c_int, C.c_int, C.c_int, C.c_float, C.c_void_p, C.c_void_p,

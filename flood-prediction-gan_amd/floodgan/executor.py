@@ -43,8 +43,9 @@ class _Grads:
     """Destination of parameter gradients: either fresh tensors (autograd path) or
     preallocated .grad tensors (fused step)."""
 
-    def __init__(self, params, into=None):
+    def __init__(self, params, into=None, accumulate=False):
         self.params, self.into = params, into
+        self.acc = accumulate       # raise existing gradients (a network used several times per step)
         self.out = {}
 
     def get(self, name):
@@ -82,16 +83,24 @@ def _norm(c, act, pad, mode, residual=None):
     return mean, rstd, out
 
 
-def gen_forward(P, x, save=True):
-    """x: [N, C, H, W] fp32 (any strides) on the device.  Returns (out [N,3,H,W], mask [N,H,W], saved)."""
+def gen_forward(P, x, save=True, x_extra=None):
+    """x: [N, C, H, W] fp32 (any strides) on the device.  Returns (out [N,3,H,W], mask [N,H,W], saved).
+    x_extra (optional [N, Ce, H, W]): the generator input is cat((x, x_extra), 1), packed without
+    materialising the cat (the cycle path's `torch.cat((image, conditions), 1)`, models/model.py:682-689);
+    x must then hold >= 3 channels (the tail composites input[:, :3])."""
     require_device(x, "generator input")
     N, Cin, H, W = x.shape
+    Ce = 0
+    if x_extra is not None:
+        require_device(x_extra, "generator input")
+        Ce = x_extra.shape[1]
+        assert x_extra.shape[0] == N and tuple(x_extra.shape[2:]) == (H, W) and Cin >= 3
     if H % 4 or W % 4 or H < 8 or W < 8:
         raise RuntimeError(f"PairedAttentionGenerator needs H, W divisible by 4 and >= 8 (got {H}x{W})")
     dev = x.device
     S = {}
-    X0 = Buf.empty(N, H, W, Cin, 3, dev)
-    ops.pack_input(x, Cin, None, 0, X0, 0, N, FG_PAD_REFLECT)                 # F.pad(input, 3, reflect)
+    X0 = Buf.empty(N, H, W, Cin + Ce, 3, dev)
+    ops.pack_input(x, Cin, x_extra, Ce, X0, 0, N, FG_PAD_REFLECT)             # F.pad(input, 3, reflect)
     c1 = Buf.empty(N, H, W, 64, 0, dev)
     _conv_fwd(P, "conv1", X0, 3, 7, 1, c1)
     m1, r1, a1 = _norm(c1, FG_ACT_RELU, 1, FG_PAD_ZERO)
@@ -148,12 +157,12 @@ def _block_bwd(P, pre, b, g_h, G):
     N, Hh, Ww, Cc = g_h.n, g_h.h, g_h.w, g_h.c
     dev = g_h.t.device
     g_cb2 = Buf.empty(N, Hh, Ww, Cc, 2, dev)          # zero border 2: full correlation of a 3x3
-    ops.in_bwd(g_h, 0, None, b["cb2"], b["mb2"], b["rb2"], FG_ACT_NONE, g_cb2, G.get(pre + "conv2.bias"))
+    ops.in_bwd(g_h, 0, None, b["cb2"], b["mb2"], b["rb2"], FG_ACT_NONE, g_cb2, G.get(pre + "conv2.bias"), G.acc)
     _wgrad_conv(P, G, pre + "conv2", g_cb2, b["rb"], 1, 3, 1)
     g_rbp = Buf.empty(N, Hh + 2, Ww + 2, Cc, 0, dev)  # gradient w.r.t. the reflect-padded relu output
     _dgrad_s1(P, pre + "conv2", g_cb2, 2, 3, g_rbp)
     g_cb1 = Buf.empty(N, Hh, Ww, Cc, 2, dev)
-    ops.in_bwd(g_rbp, 1, None, b["cb1"], b["mb1"], b["rb1"], FG_ACT_RELU, g_cb1, G.get(pre + "conv1.bias"))
+    ops.in_bwd(g_rbp, 1, None, b["cb1"], b["mb1"], b["rb1"], FG_ACT_RELU, g_cb1, G.get(pre + "conv1.bias"), G.acc)
     _wgrad_conv(P, G, pre + "conv1", g_cb1, b["h"], 1, 3, 1)
     g_hp = Buf.empty(N, Hh + 2, Ww + 2, Cc, 0, dev)
     _dgrad_s1(P, pre + "conv1", g_cb1, 2, 3, g_hp)
@@ -192,7 +201,7 @@ def block_backward_nchw(S, g, need_input=True):
 def _wgrad_conv(P, G, name, gy, X, pad, k, stride):
     w = P[name + ".weight"]
     ops.wgrad(PL.wgrad_conv(gy, X, pad, k, stride, w.shape[0]), PL.wmap_wgrad(w.shape, True, X.c, k),
-              G.get(name + ".weight"))
+              G.get(name + ".weight"), accumulate=G.acc)
 
 
 def _dgrad_s1(P, name, gyp, pad_used, k, Y):
@@ -217,29 +226,35 @@ def gen_bucket_names():
     return [[f"{layer}.{k}" for layer in b for k in ("weight", "bias")] for b in G_BUCKETS]
 
 
-def gen_backward(P, S, g_out, grads_into=None, ready=None):
+def gen_backward(P, S, g_out, grads_into=None, ready=None, input_grad=None, accumulate=False):
     """Explicit backward of gen_forward.  g_out: [N,3,H,W] (any strides).  Returns
     {param name: grad} (written into grads_into[name] when given).  ready(layer name), when
-    given, is called as soon as a gradient bucket (G_BUCKETS) is complete."""
+    given, is called as soon as a gradient bucket (G_BUCKETS) is complete.  input_grad (optional
+    [N,C,H,W] tensor, any strides) receives dL/d(input): the cycle path back-propagates through
+    one generator into the other (models/model.py:677-706); the paired step never asks for it.
+    accumulate: add into grads_into instead of overwriting (a generator applied several times in
+    one cycle iteration)."""
     ready = ready or (lambda name: None)
-    G = _Grads(P, grads_into)
+    G = _Grads(P, grads_into, accumulate)
+    assert not accumulate or grads_into is not None
     x = S["x"]
     N, _, H, W = x.shape
+    Cin = S["X0"].c            # input channels, including a fused x_extra
     dev = x.device
     # ---- tail: tanh / softmax / composite backward (models/model_architectures.py:352-399)
     cl, al = S["cl"], S["al"]
     gcl = Buf.empty(N, H, W, CONTENT_ALLOC, 6, dev)     # zero border 6 = full correlation of a 7x7
     gal = Buf.empty(N, H, W, ATT_ALLOC, 0, dev)
-    ops.tail_bwd(cl, al, x, g_out, gcl, gal)
+    ops.tail_bwd(cl, al, x, g_out, gcl, gal, gx=input_grad)     # input_grad[:, :3] = g_out * attention10
     hc, ha = S["heads"]["content"], S["heads"]["attention"]
     # ---- deconv3_content: 7x7 over reflect-padded (3) ad2
     _wgrad_conv(P, G, "deconv3_content", gcl, hc["ad2"], 3, 7, 1)
-    ops.channel_sum(gcl, 27, G.get("deconv3_content.bias"))
+    ops.channel_sum(gcl, 27, G.get("deconv3_content.bias"), G.acc)
     g_ad2c = Buf.empty(N, H + 6, W + 6, 64, 0, dev)     # gradient w.r.t. the PADDED input
     _dgrad_s1(P, "deconv3_content", gcl, 6, 7, g_ad2c)
     # ---- deconv3_attention: 1x1
     _wgrad_conv(P, G, "deconv3_attention", gal, ha["ad2"], 0, 1, 1)
-    ops.channel_sum(gal, 10, G.get("deconv3_attention.bias"))
+    ops.channel_sum(gal, 10, G.get("deconv3_attention.bias"), G.acc)
     g_ad2a = Buf.empty(N, H, W, 64, 0, dev)
     _dgrad_s1(P, "deconv3_attention", gal, 0, 1, g_ad2a)
     # ---- deconv2 / deconv1 of both heads
@@ -247,20 +262,21 @@ def gen_backward(P, S, g_out, grads_into=None, ready=None):
     for idx, (tag, hd, g_ad2, fold) in enumerate((("content", hc, g_ad2c, 3), ("attention", ha, g_ad2a, 0))):
         g_d2 = Buf.empty(N, H, W, 64, 1, dev)
         ops.in_bwd(g_ad2, fold, None, hd["d2"], hd["md2"], hd["rd2"], FG_ACT_RELU, g_d2,
-                   G.get(f"deconv2_{tag}.bias"))
+                   G.get(f"deconv2_{tag}.bias"), G.acc)
         name = f"deconv2_{tag}"
         w = P[name + ".weight"]
         ops.wgrad(PL.wgrad_convT(hd["ad1"], g_d2, 3, 1, w.shape[0]), PL.wmap_wgrad(w.shape, True, g_d2.c, 3),
-                  G.get(name + ".weight"))
+                  G.get(name + ".weight"), accumulate=G.acc)
         g_ad1 = Buf.empty(N, H // 2, W // 2, 128, 0, dev)
         m = PL.wmap_convT_dgrad(w.shape, g_d2.c)
         ops.conv([PL.conv_problem(g_d2, 1, 3, 2, ops.pack_weight(w, m), m, g_ad1)])
         g_d1 = Buf.empty(N, H // 2, W // 2, 128, 1, dev)
-        ops.in_bwd(g_ad1, 0, None, hd["d1"], hd["md1"], hd["rd1"], FG_ACT_RELU, g_d1, G.get(f"deconv1_{tag}.bias"))
+        ops.in_bwd(g_ad1, 0, None, hd["d1"], hd["md1"], hd["rd1"], FG_ACT_RELU, g_d1, G.get(f"deconv1_{tag}.bias"),
+                   G.acc)
         name = f"deconv1_{tag}"
         w = P[name + ".weight"]
         ops.wgrad(PL.wgrad_convT(S["h"], g_d1, 3, 1, w.shape[0]), PL.wmap_wgrad(w.shape, True, g_d1.c, 3),
-                  G.get(name + ".weight"))
+                  G.get(name + ".weight"), accumulate=G.acc)
         m = PL.wmap_convT_dgrad(w.shape, g_d1.c)
         ops.conv([PL.conv_problem(g_d1, 1, 3, 2, ops.pack_weight(w, m), m, g_h, accumulate=idx)])
     ready("deconv1_content")
@@ -270,19 +286,26 @@ def gen_backward(P, S, g_out, grads_into=None, ready=None):
         ready(_blk(i, 1))
     # ---- encoder
     g_c3 = Buf.empty(N, H // 4, W // 4, 256, 1, dev)
-    ops.in_bwd(g_h, 0, None, S["c3"], S["m3"], S["r3"], FG_ACT_RELU, g_c3, G.get("conv3.bias"))
+    ops.in_bwd(g_h, 0, None, S["c3"], S["m3"], S["r3"], FG_ACT_RELU, g_c3, G.get("conv3.bias"), G.acc)
     _wgrad_conv(P, G, "conv3", g_c3, S["a2"], 1, 3, 2)
     g_a2 = Buf.empty(N, H // 2, W // 2, 128, 0, dev)
     _dgrad_s2(P, "conv3", g_c3, 3, Y=g_a2)
     g_c2 = Buf.empty(N, H // 2, W // 2, 128, 1, dev)
-    ops.in_bwd(g_a2, 0, None, S["c2"], S["m2"], S["r2"], FG_ACT_RELU, g_c2, G.get("conv2.bias"))
+    ops.in_bwd(g_a2, 0, None, S["c2"], S["m2"], S["r2"], FG_ACT_RELU, g_c2, G.get("conv2.bias"), G.acc)
     _wgrad_conv(P, G, "conv2", g_c2, S["a1"], 1, 3, 2)
     g_a1 = Buf.empty(N, H, W, 64, 0, dev)
     _dgrad_s2(P, "conv2", g_c2, 3, Y=g_a1)
-    g_c1 = Buf.empty(N, H, W, 64, 0, dev)
-    ops.in_bwd(g_a1, 0, None, S["c1"], S["m1"], S["r1"], FG_ACT_RELU, g_c1, G.get("conv1.bias"))
+    # zero border 6 = the full correlation of the 7x7 stem when the input gradient is wanted
+    g_c1 = Buf.empty(N, H, W, 64, 0 if input_grad is None else 6, dev)
+    ops.in_bwd(g_a1, 0, None, S["c1"], S["m1"], S["r1"], FG_ACT_RELU, g_c1, G.get("conv1.bias"), G.acc)
     _wgrad_conv(P, G, "conv1", g_c1, S["X0"], 3, 7, 1)
     ready("conv1")
+    if input_grad is not None:
+        # gradient of the reflect-padded input (9 -> 12 channels: aligned rows), then the pad's
+        # adjoint into NCHW, accumulated onto the tail's x[:, :3] term
+        g_x0 = Buf.empty(N, H + 6, W + 6, PL.rup(Cin, 4), 0, dev)
+        _dgrad_s1(P, "conv1", g_c1, 6, 7, g_x0)
+        ops.unfold_nchw(g_x0, 3, Cin, input_grad, acc_channels=3)
     return G.out
 
 
@@ -339,8 +362,8 @@ def disc_backward(P, S, g_pred, param_grads=True, grads_into=None, input_grad=No
                   input_grad_accumulate=False, ready=None):
     """Explicit backward of disc_forward.
     param_grads: compute weight / bias gradients (False in the generator step, where D is
-    frozen: models/model.py:636-637).  input_grad: NCHW tensor receiving dL/d(input
-    channels input_grad_channels=(start, count)), written or accumulated.  ready(layer name), when
+    frozen: models/model.py:636-637).  input_grad: contiguous NCHW tensor whose channels 0 .. count
+    receive dL/d(input channels input_grad_channels=(start, count)), written or accumulated.  ready(layer name), when
     given, is called as each layer's gradients are complete (parallel.FlatGrads buckets)."""
     ready = (ready if param_grads and ready is not None else (lambda name: None))
     G = _Grads(P, grads_into)
@@ -396,6 +419,8 @@ def disc_backward(P, S, g_pred, param_grads=True, grads_into=None, input_grad=No
         ready("model.0")
     if input_grad is not None:
         c0, cn = input_grad_channels
-        _dgrad_s2(P, "model.0", g_e0, 4, y_nchw=(input_grad.view(-1), cn, inp.h, inp.w), n_base=c0, n_out=cn,
-                  accumulate=int(input_grad_accumulate))
+        # input_grad: contiguous [N, Ctot, H, W]; D-input channels c0 .. c0+cn land in its channels 0 .. cn
+        assert input_grad.is_contiguous() and input_grad.shape[1] >= cn
+        _dgrad_s2(P, "model.0", g_e0, 4, y_nchw=(input_grad.view(-1), input_grad.shape[1], inp.h, inp.w), n_base=c0,
+                  n_out=cn, accumulate=int(input_grad_accumulate))
     return G.out

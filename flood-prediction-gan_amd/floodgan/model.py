@@ -8,6 +8,7 @@ no autograd graph, one fused 2N-image discriminator pass for the D step (Instanc
 per-sample, so D(fake) and D(real) in one batch is the same computation), fused losses and
 FusedAdam.  With torch.distributed initialised it performs batch-DP over RCCL.
 """
+import itertools
 import time
 
 import numpy as np
@@ -17,7 +18,9 @@ from torch.optim import lr_scheduler
 
 from . import executor as X
 from . import ops
-from .model_architectures import PairedAttentionDiscriminator, PairedAttentionGenerator
+from .cycle import IDENTITY_KEYS, LOSS_KEYS, CycleStep
+from .model_architectures import (AttentionGANDiscriminator, AttentionGANGenerator, PairedAttentionDiscriminator,
+                                  PairedAttentionGenerator)
 from .optim import FusedAdam
 from .parallel import FlatGrads, world
 
@@ -87,17 +90,18 @@ class PairedStep:
 
 
 class Model:
-    """Paired-path subset of the reference's Model (models/model.py:26-160) with identical
-    construction semantics (seed, initialise_weights, Adam(2e-4, (0.5, 0.999)), LambdaLR)."""
+    """The reference's Model (models/model.py:26-160) for its two attention models, with identical
+    construction semantics (seed, initialise_weights, Adam(2e-4, (0.5, 0.999)), LambdaLR):
+    "PairedAttention" (train_paired, the hot path) and "AttentionGAN" (train_cycle, §8(f))."""
 
     def __init__(self, model="PairedAttention", dataset_subset="all", dataset_dem="best", data_path=None,
                  num_epochs=1, topography="all", resize=256, crop=None, save_model_interval=0,
                  save_images_interval=0, verbose=False, load_pretrained_model=False, pretrained_model_path=None,
                  add_identity_loss=False, training_model=True, seed=47, device="cuda", train_loader=None):
         self.model = model.lower()
-        if self.model != "pairedattention":
-            raise NotImplementedError("floodgan implements the PairedAttention paired training path; "
-                                      f"'{model}' is out of scope (SURVEY.md §2)")
+        if self.model not in ("pairedattention", "attentiongan"):
+            raise NotImplementedError("floodgan implements the PairedAttention (paired) and AttentionGAN (cycle) "
+                                      f"training paths; '{model}' is out of scope (SURVEY.md §2)")
         saved = None
         if load_pretrained_model:
             saved = torch.load(pretrained_model_path, map_location="cpu", weights_only=True)
@@ -110,21 +114,33 @@ class Model:
         self.load_pretrained_model, self.data_path = load_pretrained_model, data_path
         self.dataset_subset, self.dataset_dem, self.resize, self.crop = dataset_subset, dataset_dem, resize, crop
         self.training_model, self.seed, self.device = training_model, seed, device
-        self.model_is_cycle, self.model_is_attention = False, True
+        self.model_is_cycle, self.model_is_attention = self.model == "attentiongan", True
 
         input_channels = TOPOGRAPHY_CHANNELS[self.topography]
         torch.manual_seed(self.seed)
-        self.generator = PairedAttentionGenerator(input_channels=input_channels).apply(
-            self.initialise_weights).to(device)
-        if self.training_model:
+        if self.model_is_cycle:                                   # models/model.py:96-100, :108-115
+            self._init_cycle(input_channels, device)
+        else:
+            self.generator = PairedAttentionGenerator(input_channels=input_channels).apply(
+                self.initialise_weights).to(device)
+        if self.training_model and not self.model_is_cycle:
             self.discriminator = PairedAttentionDiscriminator(input_channels=input_channels).apply(
                 self.initialise_weights).to(device)
             self.optimizer_discriminator = FusedAdam(self.discriminator.parameters(), lr=0.0002, betas=(0.5, 0.999))
             self.optimizer_generator = FusedAdam(self.generator.parameters(), lr=0.0002, betas=(0.5, 0.999))
+        if self.training_model:
             self.scheduler_generator = lr_scheduler.LambdaLR(self.optimizer_generator, lr_lambda=self.lambda_rule)
             self.scheduler_discriminator = lr_scheduler.LambdaLR(self.optimizer_discriminator,
                                                                  lr_lambda=self.lambda_rule)
-        if saved is not None:
+        if saved is not None and self.model_is_cycle:
+            self.starting_epoch, self.all_losses = saved["starting_epoch"], saved["all_losses"]
+            for name in self._cycle_nets():
+                getattr(self, name).load_state_dict(saved[name])
+            if self.training_model:
+                for name in ("optimizer_generator", "optimizer_discriminator", "scheduler_generator",
+                             "scheduler_discriminator"):
+                    getattr(self, name).load_state_dict(saved[name])
+        elif saved is not None:
             self.starting_epoch, self.all_losses = saved["starting_epoch"], saved["all_losses"]
             self.generator.load_state_dict(saved["generator"])
             if self.training_model:
@@ -141,6 +157,23 @@ class Model:
         # build's scope: assign any iterable of (input [N,C,H,W], target [N,3,H,W], names).
         self.train_loader = train_loader
         self._step = None
+
+    def _cycle_nets(self):
+        nets = ["pre_to_post_generator", "post_to_pre_generator"]
+        return nets + (["pre_discriminator", "post_discriminator"] if self.training_model else [])
+
+    def _init_cycle(self, input_channels, device):
+        """models/model.py:96-100 (construction order = RNG order) and :108-115 (optimisers)."""
+        for name in self._cycle_nets():
+            cls = AttentionGANGenerator if name.endswith("generator") else AttentionGANDiscriminator
+            setattr(self, name, cls(input_channels=input_channels).apply(self.initialise_weights).to(device))
+        if self.training_model:
+            self.optimizer_generator = FusedAdam(itertools.chain(self.pre_to_post_generator.parameters(),
+                                                                 self.post_to_pre_generator.parameters()),
+                                                 lr=0.0002, betas=(0.5, 0.999))
+            self.optimizer_discriminator = FusedAdam(itertools.chain(self.post_discriminator.parameters(),
+                                                                     self.pre_discriminator.parameters()),
+                                                     lr=0.0002, betas=(0.5, 0.999))
 
     @staticmethod
     def initialise_weights(m):
@@ -159,7 +192,11 @@ class Model:
         return 1.0 - max(0, epoch + 1 - (self.num_epochs / 2)) / float((self.num_epochs / 2) + 1)
 
     def initialise_loss_storage(self, overall):
+        """models/model.py:183-205"""
         pre = "all_" if overall else ""
+        if self.model_is_cycle:
+            keys = LOSS_KEYS + (IDENTITY_KEYS if self.add_identity_loss else [])
+            return {pre + k: [] for k in keys}
         return {f"{pre}losses_discriminator_real": [], f"{pre}losses_discriminator_synthetic": [],
                 f"{pre}losses_generator_synthetic": [], f"{pre}l1_losses_generator_synthetic": []}
 
@@ -192,6 +229,36 @@ class Model:
             self.scheduler_generator.step()
             self.save_results(epoch, losses, t0)
 
+    @property
+    def cycle_step_fn(self):
+        if self._step is None:
+            self._step = CycleStep(self.pre_to_post_generator, self.post_to_pre_generator, self.pre_discriminator,
+                                   self.post_discriminator, self.optimizer_generator, self.optimizer_discriminator,
+                                   identity=self.add_identity_loss)
+        return self._step
+
+    def train_cycle(self):
+        """models/model.py:660-758 on the fused device step (CycleStep)."""
+        if not self.model_is_cycle:
+            raise RuntimeError("train_cycle needs model='AttentionGAN'")
+        if self.train_loader is None:
+            raise RuntimeError("assign Model.train_loader (iterable of (input, target, names)) first")
+        for epoch in range(self.starting_epoch, self.num_epochs + 1):
+            t0 = time.time()
+            losses = self.initialise_loss_storage(overall=False)
+            for name in self._cycle_nets():
+                getattr(self, name).train()
+            torch.manual_seed(epoch)
+            for input_stack, output_image, _ in self.train_loader:
+                input_stack = input_stack.to(self.device, non_blocking=True)
+                output_image = output_image.to(self.device, non_blocking=True)
+                vals = self.cycle_step_fn(input_stack, output_image).cpu().tolist()
+                for k, v in zip(losses.keys(), vals):
+                    losses[k].append(v)
+            self.scheduler_generator.step()
+            self.scheduler_discriminator.step()
+            self.save_results(epoch, losses, t0)
+
     def save_results(self, epoch, losses, epoch_start_time):
         """models/model.py:322-358 (loss bookkeeping + checkpoint; plots are out of scope)."""
         self.current_epoch = epoch
@@ -201,9 +268,18 @@ class Model:
             print(f"Epoch {epoch} ({time.time() - epoch_start_time:.2f} seconds) | "
                   + " | ".join(f"{k} = {v[-1]:.2f}" for k, v in self.all_losses.items()))
         if self.save_model_interval != 0 and epoch % self.save_model_interval == 0:
-            torch.save(self.checkpoint(epoch), f"{self.data_path}/models/PairedAttention_epoch{epoch}.pth.tar")
+            name = "AttentionGAN" if self.model_is_cycle else "PairedAttention"
+            torch.save(self.checkpoint(epoch), f"{self.data_path}/models/{name}_epoch{epoch}.pth.tar")
 
     def checkpoint(self, epoch):
+        if self.model_is_cycle:                                   # models/model.py:335-355 (cycle keys)
+            ck = {"model": self.model, "starting_epoch": epoch + 1, "num_epochs": self.num_epochs,
+                  "topography": self.topography, "all_losses": self.all_losses,
+                  "add_identity_loss": self.add_identity_loss}
+            for name in self._cycle_nets() + ["optimizer_generator", "optimizer_discriminator",
+                                              "scheduler_generator", "scheduler_discriminator"]:
+                ck[name] = getattr(self, name).state_dict()
+            return ck
         return {"model": self.model, "starting_epoch": epoch + 1, "num_epochs": self.num_epochs,
                 "topography": self.topography,
                 "optimizer_generator": self.optimizer_generator.state_dict(),

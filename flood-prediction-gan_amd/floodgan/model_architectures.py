@@ -45,13 +45,13 @@ class _GeneratorFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g_out, _g_mask):
-        if ctx.needs_input_grad[0]:
-            raise NotImplementedError("gradient w.r.t. the generator input is not part of the paired "
-                                      "training step (models/model.py:615-646)")
-        grads = X.gen_backward(ctx.P, ctx.S, g_out)
+        gx = None
+        if ctx.needs_input_grad[0]:   # the cycle path: G(cat(G'(x), conditions)) (models/model.py:677-706)
+            gx = torch.empty(ctx.S["x"].shape, dtype=torch.float32, device=g_out.device)
+        grads = X.gen_backward(ctx.P, ctx.S, g_out, input_grad=gx)
         ctx.S = None
-        return (None,) + tuple(grads[k] if need else None
-                               for k, need in zip(GEN_KEYS, ctx.needs_input_grad[1:]))
+        return (gx,) + tuple(grads[k] if need else None
+                             for k, need in zip(GEN_KEYS, ctx.needs_input_grad[1:]))
 
 
 class _DiscriminatorFn(torch.autograd.Function):
@@ -80,6 +80,8 @@ class PairedAttentionGenerator(nn.Module):
     """models/model_architectures.py:305-400 -- ResNet-9 encoder/decoder with a tanh content
     head (27 ch) and a softmax attention head (10 ch) composited with input[:, :3]."""
 
+    _block = None   # the residual block class (set below: PairedAttentionBlock)
+
     def __init__(self, input_channels):
         super().__init__()
         self.input_channels = input_channels
@@ -90,8 +92,7 @@ class PairedAttentionGenerator(nn.Module):
         self.conv2_norm = nn.InstanceNorm2d(128)
         self.conv3 = nn.Conv2d(128, 256, kernel_size=3, stride=2, padding=1)
         self.conv3_norm = nn.InstanceNorm2d(256)
-        self.resnet_blocks = nn.Sequential(*[PairedAttentionBlock(channel=256, kernel=3, stride=1, padding=1)
-                                             for _ in range(9)])
+        self.resnet_blocks = nn.Sequential(*[self._block(256, 3, 1, 1) for _ in range(9)])
         self.deconv1_content = nn.ConvTranspose2d(256, 128, kernel_size=3, stride=2, padding=1, output_padding=1)
         self.deconv1_norm_content = nn.InstanceNorm2d(128)
         self.deconv2_content = nn.ConvTranspose2d(128, 64, kernel_size=3, stride=2, padding=1, output_padding=1)
@@ -151,9 +152,12 @@ class _BlockFn(torch.autograd.Function):
 class PairedAttentionDiscriminator(nn.Module):
     """models/model_architectures.py:420-441 -- 70x70 PatchGAN over input_channels + 3."""
 
+    _extra_channels = 3   # D sees cat(input, image) in the paired path (models/model.py:616-617)
+
     def __init__(self, input_channels):
         super().__init__()
-        sequence = [nn.Conv2d(input_channels + 3, 64, kernel_size=4, stride=2, padding=1), nn.LeakyReLU(0.2, True)]
+        c0 = input_channels + self._extra_channels
+        sequence = [nn.Conv2d(c0, 64, kernel_size=4, stride=2, padding=1), nn.LeakyReLU(0.2, True)]
         nf_mult = 1
         for n in range(1, 3):
             nf_prev, nf_mult = nf_mult, min(2 ** n, 8)
@@ -170,3 +174,29 @@ class PairedAttentionDiscriminator(nn.Module):
 
     def forward(self, x):
         return _DiscriminatorFn.apply(x, *self.param_dict().values())
+
+
+PairedAttentionGenerator._block = PairedAttentionBlock
+
+
+# ------------------------------------------------------------------------------------------
+# AttentionGAN (cycle path): the same generator graph, a PatchGAN over input_channels
+# ------------------------------------------------------------------------------------------
+
+class AttentionGANBlock(PairedAttentionBlock):
+    """models/model_architectures.py:260-276 -- identical to PairedAttentionBlock."""
+
+
+class AttentionGANGenerator(PairedAttentionGenerator):
+    """models/model_architectures.py:163-258 -- layer for layer the PairedAttention generator
+    (same names, shapes, registration order, forward :197-258 and last_attention_mask), so it
+    runs on the same executor; train_cycle additionally needs its input gradient."""
+
+    _block = AttentionGANBlock
+
+
+class AttentionGANDiscriminator(PairedAttentionDiscriminator):
+    """models/model_architectures.py:278-299 -- the PatchGAN over `input_channels` (the cycle
+    path feeds it 9-channel images, models/model.py:693-727), not input_channels + 3."""
+
+    _extra_channels = 0

@@ -398,6 +398,16 @@ def fold_add(gpad, fold_pad, add, dst):
     L.check(_lib().fg_fold_add(view(gpad), fold_pad, view(add), view(dst), L.stream_handle()), "fold_add")
 
 
+def unfold_nchw(gpad, fold_pad, c, dst, acc_channels=0):
+    """dst [N, c', H, W] (any strides): channels < c get the reflect-pad adjoint of gpad (accumulated for
+    channels < acc_channels)"""
+    _wrote(dst)
+    N, _, H, W = dst.shape
+    assert gpad.n == N and dst.shape[1] >= c
+    L.check(_lib().fg_unfold_nchw(view(gpad), fold_pad, c, sview(dst), H, W, acc_channels, L.stream_handle()),
+            "unfold_nchw")
+
+
 # ------------------------------------------------------------------ instance norm
 
 def _work(n, c, dev):
@@ -418,10 +428,10 @@ def in_apply(src, mean, rstd, act, residual, dst, pad_mode):
                                L.ptr(_amax_out(dst)), L.stream_handle()), "in_apply")
 
 
-def in_bwd(gsrc, fold_pad, gadd, src, mean, rstd, act, dst, bias_grad=None):
+def in_bwd(gsrc, fold_pad, gadd, src, mean, rstd, act, dst, bias_grad=None, bias_accumulate=False):
     L.check(_lib().fg_in_bwd(view(gsrc), fold_pad, view(gadd), view(src), L.ptr(mean), L.ptr(rstd), act, view(dst),
-                             L.ptr(bias_grad), L.ptr(_work(src.n, src.c, src.t.device)), L.ptr(_amax_out(dst)),
-                             L.stream_handle()), "in_bwd")
+                             L.ptr(bias_grad), int(bias_accumulate), L.ptr(_work(src.n, src.c, src.t.device)),
+                             L.ptr(_amax_out(dst)), L.stream_handle()), "in_bwd")
 
 
 def act_bwd(g, y, act):
@@ -442,10 +452,11 @@ def tail_fwd(cl, al, x, out, mask):
     L.check(_lib().fg_tail_fwd(view(cl), view(al), sview(x), L.ptr(out), L.ptr(mask), L.stream_handle()), "tail_fwd")
 
 
-def tail_bwd(cl, al, x, g_out, gc, ga):
-    _wrote(gc, ga)
-    L.check(_lib().fg_tail_bwd(view(cl), view(al), sview(x), sview(g_out), view(gc), view(ga), L.stream_handle()),
-            "tail_bwd")
+def tail_bwd(cl, al, x, g_out, gc, ga, gx=None):
+    """gx (optional [N, C, H, W] tensor): channels 0..2 receive the background term's input gradient"""
+    _wrote(gc, ga, gx)
+    L.check(_lib().fg_tail_bwd(view(cl), view(al), sview(x), sview(g_out), view(gc), view(ga), sview(gx),
+                               L.stream_handle()), "tail_bwd")
 
 
 def mse_const(p, target, gscale, loss_out, g=None):

@@ -62,6 +62,12 @@ typedef struct fg_sview {
     long long sn, sc, sy, sx;
 } fg_sview;
 
+/* The same strided 4-D view, writable (gradient outputs in the caller's memory format). */
+typedef struct fg_wview {
+    float* ptr;
+    long long sn, sc, sy, sx;
+} fg_wview;
+
 /*
  * Implicit-GEMM convolution problem (forward conv, stride-1 dgrad, and one phase of a
  * stride-2 transposed conv / stride-2 dgrad).  Rows m = (img, a, b) of an m_img x m_a x m_b
@@ -246,6 +252,14 @@ int fg_zero_border(fg_view dst, hipStream_t stream);
  * plus an optional residual-gradient add (models/model_architectures.py:418 `input + x`). */
 int fg_fold_add(fg_view gpad, int fold_pad, fg_view add, fg_view dst, hipStream_t stream);
 
+/* dst(n, ch, y, x) (+)= fold_reflect(gpad)(n, y, x, ch) for ch < c: the adjoint of the
+ * generator's `F.pad(input, 3, reflect)` (models/model_architectures.py:342) written into
+ * the caller's strided NCHW input-gradient tensor.  gpad's interior is (h + 2 fold_pad) x
+ * (w + 2 fold_pad) where h x w is dst's spatial size; channels ch < acc_channels are
+ * accumulated onto dst (the tail's direct x[:, :3] term), the rest overwritten. */
+int fg_unfold_nchw(fg_view gpad, int fold_pad, int c, fg_wview dst, int h, int w, int acc_channels,
+                   hipStream_t stream);
+
 /* ---------------------------------------------------------------------------------------- */
 /* instance norm (nn.InstanceNorm2d, affine=False, eps 1e-5) fused with activation           */
 /* ---------------------------------------------------------------------------------------- */
@@ -264,11 +278,11 @@ int fg_in_apply(fg_view src, const float* mean, const float* rstd, int act, fg_v
 /* Backward of fg_in_apply.  g is read from gsrc's interior, or folded through reflect
  * padding of width fold_pad when fold_pad > 0 (gsrc then holds the gradient of the padded
  * tensor); optional gadd (compact) is added.  dst receives dL/dsrc (border zeroed);
- * bias_grad (optional, [c]) receives sum over n,y,x of dst = grad of the conv bias that
- * feeds this norm. */
+ * bias_grad (optional, [c]) receives (or, with bias_accumulate, is raised by) sum over n,y,x
+ * of dst = grad of the conv bias that feeds this norm. */
 int fg_in_bwd(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, const float* mean,
-              const float* rstd, int act, fg_view dst, float* bias_grad, double* work, float* absmax,
-              hipStream_t stream);
+              const float* rstd, int act, fg_view dst, float* bias_grad, int bias_accumulate, double* work,
+              float* absmax, hipStream_t stream);
 
 /* g *= act'(y) in place over the interior (y = saved activation output). */
 int fg_act_bwd(fg_view g, fg_view y, int act, hipStream_t stream);
@@ -286,9 +300,12 @@ long long fg_channel_sum_workspace_doubles(int c_alloc);
 int fg_tail_fwd(fg_view content_logits, fg_view att_logits, fg_sview x, float* out,
                 float* mask, hipStream_t stream);
 /* g_out: strided [N,3,H,W].  g_content: dst view (27 used of c_alloc, zero border/channels),
- * g_att: dst view (10 used).  g_x (optional strided, may be NULL ptr) += grad wrt x[:, :3]. */
+ * g_att: dst view (10 used).  g_x (optional, NULL ptr = skip): channels 0..2 of a strided
+ * [N,C,H,W] tensor receive the direct gradient w.r.t. input[:, :3] of the background term
+ * `input[:, :3] * attention10` (models/model_architectures.py:393, :251) -- the input
+ * gradient that the cycle path (models/model.py:677-706) back-propagates into G. */
 int fg_tail_bwd(fg_view content_logits, fg_view att_logits, fg_sview x, fg_sview g_out,
-                fg_view g_content, fg_view g_att, hipStream_t stream);
+                fg_view g_content, fg_view g_att, fg_wview g_x, hipStream_t stream);
 
 /* ---------------------------------------------------------------------------------------- */
 /* losses (nn.MSELoss vs a constant target, nn.L1Loss; models/model.py:626-644)             */

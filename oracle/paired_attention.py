@@ -52,9 +52,10 @@ def generator_layout(c_in=9):
     return L
 
 
-def discriminator_layout(c_in=9):
-    """models/model_architectures.py:424-438: Sequential indices 0, 2, 5, 8, 11 hold convs."""
-    return [("model.0", "conv", (64, c_in + 3, 4, 4)),
+def discriminator_layout(c_in=9, extra=3):
+    """models/model_architectures.py:424-438: Sequential indices 0, 2, 5, 8, 11 hold convs.
+    extra = 3 for the paired D (input_channels + 3, :424), 0 for AttentionGAN's (:281)."""
+    return [("model.0", "conv", (64, c_in + extra, 4, 4)),
             ("model.2", "conv", (128, 64, 4, 4)),
             ("model.5", "conv", (256, 128, 4, 4)),
             ("model.8", "conv", (512, 256, 4, 4)),

@@ -19,8 +19,8 @@ def pytest_configure(config):
 def golden():
     import numpy as np
 
-    def load(R):
-        path = os.path.join(ROOT, "tests", "golden", f"paired_step_{R}.npz")
+    def load(R, kind="paired_step"):
+        path = os.path.join(ROOT, "tests", "golden", f"{kind}_{R}.npz")
         z = np.load(path, allow_pickle=False)
         return {k.replace("__", "."): z[k] for k in z.files}
 
