@@ -133,6 +133,53 @@ __global__ void tail_bwd_kernel(fg_view cl, fg_view al, fg_sview x, fg_sview gou
     }
 }
 
+// CycleGAN head (models/model_architectures.py:115-117: conv 7x7 64->3 then nn.Tanh): one thread
+// per output element, x fastest (coalesced NCHW stores).
+__global__ void tanh_head_fwd_kernel(fg_view logits, int c, fg_wview out) {
+    const int H = logits.h, W = logits.w;
+    const long long total = (long long)logits.n * c * H * W;
+    for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const int xx = (int)(idx % W);
+        long long q = idx / W;
+        const int yy = (int)(q % H);
+        q /= H;
+        const int ch = (int)(q % c);
+        const int n = (int)(q / c);
+        out.ptr[n * out.sn + ch * out.sc + yy * out.sy + xx * out.sx] = tanhf(logits.ptr[fg::vidx(logits, n, yy, xx) + ch]);
+    }
+}
+
+// g_logits = g_out * (1 - tanh^2), written over g_logits' full padded extent (zero border and
+// zero channels >= c: the 7x7 input-gradient conv reads them).  One thread per padded pixel.
+__global__ void tanh_head_bwd_kernel(fg_view logits, int c, fg_sview gout, fg_view gl) {
+    const int H = logits.h, W = logits.w;
+    const int hp = H + 2 * gl.pad, wp = W + 2 * gl.pad;
+    const long long total = (long long)logits.n * hp * wp;
+    for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const int xp = (int)(idx % wp);
+        const long long t = idx / wp;
+        const int yp = (int)(t % hp);
+        const int n = (int)(t / hp);
+        const int yy = yp - gl.pad, xx = xp - gl.pad;
+        float* gp = gl.ptr + ((size_t)(n * hp + yp) * wp + xp) * gl.c_alloc;
+        const bool inside = yy >= 0 && yy < H && xx >= 0 && xx < W;
+        for (int i = 0; i < gl.c_alloc; i += 4) {
+            float v[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                v[j] = 0.f;
+                if (inside && i + j < c) {
+                    const float th = tanhf(logits.ptr[fg::vidx(logits, n, yy, xx) + i + j]);
+                    v[j] = gout.ptr[n * gout.sn + (i + j) * gout.sc + yy * gout.sy + xx * gout.sx] * (1.f - th * th);
+                }
+            }
+            *reinterpret_cast<f32x4*>(gp + i) = f32x4{v[0], v[1], v[2], v[3]};
+        }
+    }
+}
+
 }  // namespace
 
 FG_API int fg_tail_fwd(fg_view content_logits, fg_view att_logits, fg_sview x, float* out, float* mask,
@@ -161,4 +208,24 @@ FG_API int fg_tail_bwd(fg_view content_logits, fg_view att_logits, fg_sview x, f
     hipLaunchKernelGGL(tail_bwd_kernel, dim3(fg::blocks_for(total, 256, 16384)), dim3(256), 0, stream,
                        content_logits, att_logits, x, g_out, g_content, g_att, g_x);
     return fg::launched("tail_bwd");
+}
+
+FG_API int fg_tanh_head_fwd(fg_view logits, int c, fg_wview out, hipStream_t stream) {
+    if (!logits.ptr || !out.ptr || c <= 0 || c > logits.c_alloc) return fg::fail(FG_ERR_INVALID, "fg_tanh_head_fwd: bad args");
+    const long long total = (long long)logits.n * c * logits.h * logits.w;
+    if (total == 0) return 0;
+    hipLaunchKernelGGL(tanh_head_fwd_kernel, dim3(fg::blocks_for(total, 256, 16384)), dim3(256), 0, stream, logits, c,
+                       out);
+    return fg::launched("tanh_head_fwd");
+}
+
+FG_API int fg_tanh_head_bwd(fg_view logits, int c, fg_sview g_out, fg_view g_logits, hipStream_t stream) {
+    if (!logits.ptr || !g_out.ptr || !g_logits.ptr || c <= 0 || c > logits.c_alloc || g_logits.c_alloc % 4 ||
+        g_logits.c_alloc < c || g_logits.h != logits.h || g_logits.w != logits.w || g_logits.n != logits.n)
+        return fg::fail(FG_ERR_INVALID, "fg_tanh_head_bwd: bad args");
+    const long long total = (long long)logits.n * (logits.h + 2 * g_logits.pad) * (logits.w + 2 * g_logits.pad);
+    if (total == 0) return 0;
+    hipLaunchKernelGGL(tanh_head_bwd_kernel, dim3(fg::blocks_for(total, 256, 16384)), dim3(256), 0, stream, logits, c,
+                       g_out, g_logits);
+    return fg::launched("tanh_head_bwd");
 }

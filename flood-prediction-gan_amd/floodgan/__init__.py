@@ -7,8 +7,9 @@ kernels (libfloodgan.so, C-ABI in include/floodgan.h).
 """
 from ._lib import load as load_library  # noqa: F401
 from .model_architectures import (AttentionGANBlock, AttentionGANDiscriminator,  # noqa: F401
-                                  AttentionGANGenerator, PairedAttentionBlock, PairedAttentionDiscriminator,
+                                  AttentionGANGenerator, CycleGANBlock, CycleGANDiscriminator, CycleGANGenerator, PairedAttentionBlock, PairedAttentionDiscriminator,
                                   PairedAttentionGenerator)
 
 __all__ = ["PairedAttentionGenerator", "PairedAttentionBlock", "PairedAttentionDiscriminator",
-           "AttentionGANGenerator", "AttentionGANBlock", "AttentionGANDiscriminator", "load_library"]
+           "AttentionGANGenerator", "AttentionGANBlock", "AttentionGANDiscriminator",
+           "CycleGANGenerator", "CycleGANBlock", "CycleGANDiscriminator", "load_library"]

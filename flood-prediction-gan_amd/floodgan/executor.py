@@ -83,11 +83,18 @@ def _norm(c, act, pad, mode, residual=None):
     return mean, rstd, out
 
 
+def has_attention(P):
+    """PairedAttention / AttentionGAN generators carry the attention head; CycleGAN's does not"""
+    return "deconv3_attention.weight" in P
+
+
 def gen_forward(P, x, save=True, x_extra=None):
     """x: [N, C, H, W] fp32 (any strides) on the device.  Returns (out [N,3,H,W], mask [N,H,W], saved).
     x_extra (optional [N, Ce, H, W]): the generator input is cat((x, x_extra), 1), packed without
     materialising the cat (the cycle path's `torch.cat((image, conditions), 1)`, models/model.py:682-689);
-    x must then hold >= 3 channels (the tail composites input[:, :3])."""
+    x must then hold >= 3 channels (the tail composites input[:, :3]).
+    The same graph serves the CycleGAN ResNet generator (models/model_architectures.py:91-120) when
+    P has no attention head: one decoder and a tanh head (conv 7x7 64->3); mask is then None."""
     require_device(x, "generator input")
     N, Cin, H, W = x.shape
     Ce = 0
@@ -119,7 +126,8 @@ def gen_forward(P, x, save=True, x_extra=None):
         blocks.append(b)
     S.update(blocks=blocks, h=h)
     heads = {}
-    for tag, pad2, mode2 in (("content", 3, FG_PAD_REFLECT), ("attention", 0, FG_PAD_ZERO)):
+    attention = has_attention(P)
+    for tag, pad2, mode2 in (("content", 3, FG_PAD_REFLECT), ("attention", 0, FG_PAD_ZERO))[:1 + attention]:
         d1 = Buf.empty(N, H // 2, W // 2, 128, 0, dev)
         _convT_fwd(P, f"deconv1_{tag}", h, d1)
         md1, rd1, ad1 = _norm(d1, FG_ACT_RELU, 1, FG_PAD_ZERO)
@@ -129,9 +137,13 @@ def gen_forward(P, x, save=True, x_extra=None):
         heads[tag] = dict(d1=d1, md1=md1, rd1=rd1, ad1=ad1, d2=d2, md2=md2, rd2=rd2, ad2=ad2)
     cl = Buf.empty(N, H, W, CONTENT_ALLOC, 0, dev)
     _conv_fwd(P, "deconv3_content", heads["content"]["ad2"], 3, 7, 1, cl)
+    out = torch.empty(N, 3, H, W, dtype=torch.float32, device=dev)
+    if not attention:                                 # CycleGAN: nn.Tanh() on the 3 logits (:115-117)
+        ops.tanh_head_fwd(cl, 3, out)
+        S.update(heads=heads, cl=cl)
+        return out, None, (S if save else None)
     al = Buf.empty(N, H, W, ATT_ALLOC, 0, dev)
     _conv_fwd(P, "deconv3_attention", heads["attention"]["ad2"], 0, 1, 1, al)
-    out = torch.empty(N, 3, H, W, dtype=torch.float32, device=dev)
     mask = torch.empty(N, H, W, dtype=torch.float32, device=dev)
     ops.tail_fwd(cl, al, x, out, mask)
     S.update(heads=heads, cl=cl, al=al)
@@ -241,25 +253,36 @@ def gen_backward(P, S, g_out, grads_into=None, ready=None, input_grad=None, accu
     N, _, H, W = x.shape
     Cin = S["X0"].c            # input channels, including a fused x_extra
     dev = x.device
-    # ---- tail: tanh / softmax / composite backward (models/model_architectures.py:352-399)
-    cl, al = S["cl"], S["al"]
+    attention = has_attention(P)
+    n_content = 27 if attention else 3
+    # ---- tail: tanh / softmax / composite backward (models/model_architectures.py:352-399), or the
+    # CycleGAN tanh head (:115-117)
+    cl = S["cl"]
     gcl = Buf.empty(N, H, W, CONTENT_ALLOC, 6, dev)     # zero border 6 = full correlation of a 7x7
-    gal = Buf.empty(N, H, W, ATT_ALLOC, 0, dev)
-    ops.tail_bwd(cl, al, x, g_out, gcl, gal, gx=input_grad)     # input_grad[:, :3] = g_out * attention10
-    hc, ha = S["heads"]["content"], S["heads"]["attention"]
+    hc = S["heads"]["content"]
+    if attention:
+        al = S["al"]
+        gal = Buf.empty(N, H, W, ATT_ALLOC, 0, dev)
+        ops.tail_bwd(cl, al, x, g_out, gcl, gal, gx=input_grad)     # input_grad[:, :3] = g_out * attention10
+        ha = S["heads"]["attention"]
+    else:
+        ops.tanh_head_bwd(cl, 3, g_out, gcl)
     # ---- deconv3_content: 7x7 over reflect-padded (3) ad2
     _wgrad_conv(P, G, "deconv3_content", gcl, hc["ad2"], 3, 7, 1)
-    ops.channel_sum(gcl, 27, G.get("deconv3_content.bias"), G.acc)
+    ops.channel_sum(gcl, n_content, G.get("deconv3_content.bias"), G.acc)
     g_ad2c = Buf.empty(N, H + 6, W + 6, 64, 0, dev)     # gradient w.r.t. the PADDED input
     _dgrad_s1(P, "deconv3_content", gcl, 6, 7, g_ad2c)
-    # ---- deconv3_attention: 1x1
-    _wgrad_conv(P, G, "deconv3_attention", gal, ha["ad2"], 0, 1, 1)
-    ops.channel_sum(gal, 10, G.get("deconv3_attention.bias"), G.acc)
-    g_ad2a = Buf.empty(N, H, W, 64, 0, dev)
-    _dgrad_s1(P, "deconv3_attention", gal, 0, 1, g_ad2a)
+    heads = [("content", hc, g_ad2c, 3)]
+    if attention:
+        # ---- deconv3_attention: 1x1
+        _wgrad_conv(P, G, "deconv3_attention", gal, ha["ad2"], 0, 1, 1)
+        ops.channel_sum(gal, 10, G.get("deconv3_attention.bias"), G.acc)
+        g_ad2a = Buf.empty(N, H, W, 64, 0, dev)
+        _dgrad_s1(P, "deconv3_attention", gal, 0, 1, g_ad2a)
+        heads.append(("attention", ha, g_ad2a, 0))
     # ---- deconv2 / deconv1 of both heads
     g_h = Buf.empty(N, H // 4, W // 4, 256, 0, dev)
-    for idx, (tag, hd, g_ad2, fold) in enumerate((("content", hc, g_ad2c, 3), ("attention", ha, g_ad2a, 0))):
+    for idx, (tag, hd, g_ad2, fold) in enumerate(heads):
         g_d2 = Buf.empty(N, H, W, 64, 1, dev)
         ops.in_bwd(g_ad2, fold, None, hd["d2"], hd["md2"], hd["rd2"], FG_ACT_RELU, g_d2,
                    G.get(f"deconv2_{tag}.bias"), G.acc)
@@ -305,7 +328,7 @@ def gen_backward(P, S, g_out, grads_into=None, ready=None, input_grad=None, accu
         # adjoint into NCHW, accumulated onto the tail's x[:, :3] term
         g_x0 = Buf.empty(N, H + 6, W + 6, PL.rup(Cin, 4), 0, dev)
         _dgrad_s1(P, "conv1", g_c1, 6, 7, g_x0)
-        ops.unfold_nchw(g_x0, 3, Cin, input_grad, acc_channels=3)
+        ops.unfold_nchw(g_x0, 3, Cin, input_grad, acc_channels=3 if attention else 0)
     return G.out
 
 

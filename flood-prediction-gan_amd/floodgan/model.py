@@ -19,8 +19,8 @@ from torch.optim import lr_scheduler
 from . import executor as X
 from . import ops
 from .cycle import IDENTITY_KEYS, LOSS_KEYS, CycleStep
-from .model_architectures import (AttentionGANDiscriminator, AttentionGANGenerator, PairedAttentionDiscriminator,
-                                  PairedAttentionGenerator)
+from .model_architectures import (AttentionGANDiscriminator, AttentionGANGenerator, CycleGANDiscriminator,
+                                  CycleGANGenerator, PairedAttentionDiscriminator, PairedAttentionGenerator)
 from .optim import FusedAdam
 from .parallel import FlatGrads, world
 
@@ -90,18 +90,18 @@ class PairedStep:
 
 
 class Model:
-    """The reference's Model (models/model.py:26-160) for its two attention models, with identical
-    construction semantics (seed, initialise_weights, Adam(2e-4, (0.5, 0.999)), LambdaLR):
-    "PairedAttention" (train_paired, the hot path) and "AttentionGAN" (train_cycle, §8(f))."""
+    """The reference's Model (models/model.py:26-160) with identical construction semantics (seed,
+    initialise_weights, Adam(2e-4, (0.5, 0.999)), LambdaLR) for "PairedAttention" (train_paired,
+    the hot path) and the cycle models "AttentionGAN" / "CycleGAN" (train_cycle)."""
 
     def __init__(self, model="PairedAttention", dataset_subset="all", dataset_dem="best", data_path=None,
                  num_epochs=1, topography="all", resize=256, crop=None, save_model_interval=0,
                  save_images_interval=0, verbose=False, load_pretrained_model=False, pretrained_model_path=None,
                  add_identity_loss=False, training_model=True, seed=47, device="cuda", train_loader=None):
         self.model = model.lower()
-        if self.model not in ("pairedattention", "attentiongan"):
-            raise NotImplementedError("floodgan implements the PairedAttention (paired) and AttentionGAN (cycle) "
-                                      f"training paths; '{model}' is out of scope (SURVEY.md §2)")
+        if self.model not in ("pairedattention", "attentiongan", "cyclegan"):
+            raise NotImplementedError("floodgan implements the PairedAttention (paired), AttentionGAN and CycleGAN "
+                                      f"(cycle) training paths; '{model}' is out of scope (SURVEY.md §2)")
         saved = None
         if load_pretrained_model:
             saved = torch.load(pretrained_model_path, map_location="cpu", weights_only=True)
@@ -114,7 +114,8 @@ class Model:
         self.load_pretrained_model, self.data_path = load_pretrained_model, data_path
         self.dataset_subset, self.dataset_dem, self.resize, self.crop = dataset_subset, dataset_dem, resize, crop
         self.training_model, self.seed, self.device = training_model, seed, device
-        self.model_is_cycle, self.model_is_attention = self.model == "attentiongan", True
+        self.model_is_cycle = self.model in ("attentiongan", "cyclegan")
+        self.model_is_attention = self.model != "cyclegan"
 
         input_channels = TOPOGRAPHY_CHANNELS[self.topography]
         torch.manual_seed(self.seed)
@@ -164,8 +165,10 @@ class Model:
 
     def _init_cycle(self, input_channels, device):
         """models/model.py:96-100 (construction order = RNG order) and :108-115 (optimisers)."""
+        gcls, dcls = ((AttentionGANGenerator, AttentionGANDiscriminator) if self.model == "attentiongan"
+                      else (CycleGANGenerator, CycleGANDiscriminator))
         for name in self._cycle_nets():
-            cls = AttentionGANGenerator if name.endswith("generator") else AttentionGANDiscriminator
+            cls = gcls if name.endswith("generator") else dcls
             setattr(self, name, cls(input_channels=input_channels).apply(self.initialise_weights).to(device))
         if self.training_model:
             self.optimizer_generator = FusedAdam(itertools.chain(self.pre_to_post_generator.parameters(),
@@ -240,7 +243,7 @@ class Model:
     def train_cycle(self):
         """models/model.py:660-758 on the fused device step (CycleStep)."""
         if not self.model_is_cycle:
-            raise RuntimeError("train_cycle needs model='AttentionGAN'")
+            raise RuntimeError("train_cycle needs model='AttentionGAN' or 'CycleGAN'")
         if self.train_loader is None:
             raise RuntimeError("assign Model.train_loader (iterable of (input, target, names)) first")
         for epoch in range(self.starting_epoch, self.num_epochs + 1):
@@ -268,7 +271,7 @@ class Model:
             print(f"Epoch {epoch} ({time.time() - epoch_start_time:.2f} seconds) | "
                   + " | ".join(f"{k} = {v[-1]:.2f}" for k, v in self.all_losses.items()))
         if self.save_model_interval != 0 and epoch % self.save_model_interval == 0:
-            name = "AttentionGAN" if self.model_is_cycle else "PairedAttention"
+            name = {"attentiongan": "AttentionGAN", "cyclegan": "CycleGAN"}.get(self.model, "PairedAttention")
             torch.save(self.checkpoint(epoch), f"{self.data_path}/models/{name}_epoch{epoch}.pth.tar")
 
     def checkpoint(self, epoch):

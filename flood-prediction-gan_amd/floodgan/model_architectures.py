@@ -34,24 +34,29 @@ DISC_KEYS = _disc_keys()
 
 
 class _GeneratorFn(torch.autograd.Function):
+    """keys: the executor's names of `params` (GEN_KEYS, or CYCLEGAN_GEN_KEYS for the tanh-head
+    generator, which returns an empty mask)."""
+
     @staticmethod
-    def forward(ctx, x, *params):
-        P = dict(zip(GEN_KEYS, params))
+    def forward(ctx, keys, x, *params):
+        P = dict(zip(keys, params))
         save = any(ctx.needs_input_grad)
         out, mask, S = X.gen_forward(P, x, save=save)
-        ctx.P, ctx.S = P, S
+        if mask is None:
+            mask = out.new_empty(0)
+        ctx.keys, ctx.P, ctx.S = keys, P, S
         ctx.mark_non_differentiable(mask)
         return out, mask
 
     @staticmethod
     def backward(ctx, g_out, _g_mask):
         gx = None
-        if ctx.needs_input_grad[0]:   # the cycle path: G(cat(G'(x), conditions)) (models/model.py:677-706)
+        if ctx.needs_input_grad[1]:   # the cycle path: G(cat(G'(x), conditions)) (models/model.py:677-706)
             gx = torch.empty(ctx.S["x"].shape, dtype=torch.float32, device=g_out.device)
         grads = X.gen_backward(ctx.P, ctx.S, g_out, input_grad=gx)
         ctx.S = None
-        return (gx,) + tuple(grads[k] if need else None
-                             for k, need in zip(GEN_KEYS, ctx.needs_input_grad[1:]))
+        return (None, gx) + tuple(grads[k] if need else None
+                                  for k, need in zip(ctx.keys, ctx.needs_input_grad[2:]))
 
 
 class _DiscriminatorFn(torch.autograd.Function):
@@ -112,7 +117,7 @@ class PairedAttentionGenerator(nn.Module):
 
     def forward(self, input):
         params = [p for p in self.param_dict().values()]
-        out, mask = _GeneratorFn.apply(input, *params)
+        out, mask = _GeneratorFn.apply(tuple(GEN_KEYS), input, *params)
         self.last_attention_mask = mask
         return out
 
@@ -200,3 +205,76 @@ class AttentionGANDiscriminator(PairedAttentionDiscriminator):
     path feeds it 9-channel images, models/model.py:693-727), not input_channels + 3."""
 
     _extra_channels = 0
+
+
+# ------------------------------------------------------------------------------------------
+# CycleGAN (cycle path): ResNet-9 generator with a single tanh head, the same PatchGAN
+# ------------------------------------------------------------------------------------------
+
+def _cyclegan_names():
+    """executor name -> CycleGANGenerator parameter prefix (nn.Sequential indices of
+    models/model_architectures.py:95-117: 1, 4, 7 convs; 10-18 blocks with conv_block.1 / .5;
+    19, 22 transposed convs; 26 the 7x7 head)"""
+    m = {"conv1": "model.1", "conv2": "model.4", "conv3": "model.7"}
+    for i in range(9):
+        m[f"resnet_blocks.{i}.conv1"] = f"model.{10 + i}.conv_block.1"
+        m[f"resnet_blocks.{i}.conv2"] = f"model.{10 + i}.conv_block.5"
+    m.update({"deconv1_content": "model.19", "deconv2_content": "model.22", "deconv3_content": "model.26"})
+    return m
+
+
+CYCLEGAN_NAMES = _cyclegan_names()
+CYCLEGAN_GEN_KEYS = tuple(f"{n}.{s}" for n in CYCLEGAN_NAMES for s in ("weight", "bias"))
+
+
+class CycleGANGenerator(nn.Module):
+    """models/model_architectures.py:91-120 -- the same encoder / 9 residual blocks / decoder as the
+    attention generators, one decoder, reflect-pad 3 + conv 7x7 64->3 + tanh.  Same Sequential
+    layout (state_dict keys `model.<i>...`) and construction order (RNG parity); the whole network
+    is one autograd node on the native executor (which sees it under its own layer names)."""
+
+    def __init__(self, input_channels):
+        super().__init__()
+        model = [nn.ReflectionPad2d(3), nn.Conv2d(input_channels, 64, kernel_size=7, padding=0, bias=True),
+                 nn.InstanceNorm2d(64), nn.ReLU(True)]
+        for i in range(2):
+            mult = 2 ** i
+            model += [nn.Conv2d(64 * mult, 64 * mult * 2, kernel_size=3, stride=2, padding=1, bias=True),
+                      nn.InstanceNorm2d(64 * mult * 2), nn.ReLU(True)]
+        model += [CycleGANBlock(dim=256) for _ in range(9)]
+        for i in range(2):
+            mult = 2 ** (2 - i)
+            model += [nn.ConvTranspose2d(64 * mult, int(64 * mult / 2), kernel_size=3, stride=2, padding=1,
+                                         output_padding=1, bias=True),
+                      nn.InstanceNorm2d(int(64 * mult / 2)), nn.ReLU(True)]
+        model += [nn.ReflectionPad2d(3), nn.Conv2d(64, 3, kernel_size=7, padding=0), nn.Tanh()]
+        self.model = nn.Sequential(*model)
+
+    def param_dict(self):
+        """parameters under the executor's layer names (CYCLEGAN_GEN_KEYS order)"""
+        sd = dict(self.named_parameters())
+        return {f"{n}.{s}": sd[f"{p}.{s}"] for n, p in CYCLEGAN_NAMES.items() for s in ("weight", "bias")}
+
+    def forward(self, x):
+        out, _ = _GeneratorFn.apply(CYCLEGAN_GEN_KEYS, x, *self.param_dict().values())
+        return out
+
+
+class CycleGANBlock(nn.Module):
+    """models/model_architectures.py:122-134 -- x + IN(conv(pad(ReLU(IN(conv(pad(x))))))), the
+    PairedAttentionBlock computation under Sequential names (conv_block.1 / conv_block.5)."""
+
+    def __init__(self, dim):
+        super().__init__()
+        self.conv_block = nn.Sequential(nn.ReflectionPad2d(1), nn.Conv2d(dim, dim, kernel_size=3, padding=0, bias=True),
+                                        nn.InstanceNorm2d(dim), nn.ReLU(True), nn.ReflectionPad2d(1),
+                                        nn.Conv2d(dim, dim, kernel_size=3, padding=0, bias=True),
+                                        nn.InstanceNorm2d(dim))
+
+    def forward(self, x):
+        c1, c2 = self.conv_block[1], self.conv_block[5]
+        return _BlockFn.apply(x, c1.weight, c1.bias, c2.weight, c2.bias)
+
+
+class CycleGANDiscriminator(AttentionGANDiscriminator):
+    """models/model_architectures.py:136-157 -- the same PatchGAN over input_channels."""

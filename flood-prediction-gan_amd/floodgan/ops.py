@@ -459,6 +459,17 @@ def tail_bwd(cl, al, x, g_out, gc, ga, gx=None):
                                L.stream_handle()), "tail_bwd")
 
 
+def tanh_head_fwd(logits, c, out):
+    _wrote(out)
+    L.check(_lib().fg_tanh_head_fwd(view(logits), c, sview(out), L.stream_handle()), "tanh_head_fwd")
+
+
+def tanh_head_bwd(logits, c, g_out, g_logits):
+    _wrote(g_logits)
+    L.check(_lib().fg_tanh_head_bwd(view(logits), c, sview(g_out), view(g_logits), L.stream_handle()),
+            "tanh_head_bwd")
+
+
 def mse_const(p, target, gscale, loss_out, g=None):
     """loss_out[0] = mean((p - target)^2); g = gscale * dL/dp (optional)"""
     work = torch.empty(1024, dtype=torch.float64, device=p.device)

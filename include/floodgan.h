@@ -307,6 +307,13 @@ int fg_tail_fwd(fg_view content_logits, fg_view att_logits, fg_sview x, float* o
 int fg_tail_bwd(fg_view content_logits, fg_view att_logits, fg_sview x, fg_sview g_out,
                 fg_view g_content, fg_view g_att, fg_wview g_x, hipStream_t stream);
 
+/* CycleGAN generator head (models/model_architectures.py:115-117, conv 7x7 64->3 + nn.Tanh):
+ * out (strided [N,c,H,W]) = tanh(logits[..., :c]). */
+int fg_tanh_head_fwd(fg_view logits, int c, fg_wview out, hipStream_t stream);
+/* g_logits = g_out * (1 - tanh(logits)^2) for channels < c; zero border and zero channels >= c
+ * (g_logits feeds the 7x7 input-gradient conv with its full-correlation border). */
+int fg_tanh_head_bwd(fg_view logits, int c, fg_sview g_out, fg_view g_logits, hipStream_t stream);
+
 /* ---------------------------------------------------------------------------------------- */
 /* losses (nn.MSELoss vs a constant target, nn.L1Loss; models/model.py:626-644)             */
 /* ---------------------------------------------------------------------------------------- */

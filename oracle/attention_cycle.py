@@ -6,8 +6,10 @@ Like oracle/paired_attention.py this is the checker, never the product: only `te
 Functional restatement on PyTorch-CPU of:
 
   generator     models/model_architectures.py:163-258 (AttentionGANGenerator: layer for layer the
-                PairedAttention generator, so generator_forward is shared)
-  discriminator models/model_architectures.py:278-299 (PatchGAN over input_channels, not +3)
+                PairedAttention generator, so generator_forward is shared); CycleGAN's ResNet
+                generator :91-134 (cyclegan_generator_forward)
+  discriminator models/model_architectures.py:278-299 (PatchGAN over input_channels, not +3; CycleGAN's
+                :136-157 is the same network)
   init          models/model.py:80, :97-100 (pre_to_post G, post_to_pre G, pre D, post D, each
                 constructed then .apply(initialise_weights)), :162-173
   optimisers    models/model.py:110-115 (Adam over chain(G_pre_to_post, G_post_to_pre) and over
@@ -15,7 +17,8 @@ Functional restatement on PyTorch-CPU of:
   train step    models/model.py:677-752 (Model.train_cycle inner iteration)
   image buffer  models/model.py:275-294 (get_buffer_image; < 50 stored images => returns the new one)
 
-Parity pin: tests/test_oracle_golden.py checks it against tests/golden/cycle_step_32[_id].npz,
+Parity pin: tests/test_oracle_cycle_golden.py checks it against tests/golden/cycle_step_32[_id].npz
+and cyclegan_step_32.npz,
 produced by tests/golden/make_golden_cycle.py from the reference's unmodified train_cycle().
 """
 import random
@@ -30,11 +33,55 @@ from .paired_attention import (_construct, _initialise, discriminator_forward, d
 NETS = ("pre_to_post", "post_to_pre", "pre_d", "post_d")
 
 
-def init_cycle_params(seed=47, c_in=9):
+def cyclegan_generator_layout(c_in=9):
+    """models/model_architectures.py:95-117 in construction (= registration) order; the
+    nn.Sequential indices: 1, 4, 7 convs, 10..18 CycleGANBlocks (conv_block.1 / .5), 19, 22
+    transposed convs, 26 the 7x7 head."""
+    L = [("model.1", "conv", (64, c_in, 7, 7)), ("model.4", "conv", (128, 64, 3, 3)),
+         ("model.7", "conv", (256, 128, 3, 3))]
+    for i in range(9):
+        L += [(f"model.{10 + i}.conv_block.1", "conv", (256, 256, 3, 3)),
+              (f"model.{10 + i}.conv_block.5", "conv", (256, 256, 3, 3))]
+    L += [("model.19", "convT", (256, 128, 3, 3)), ("model.22", "convT", (128, 64, 3, 3)),
+          ("model.26", "conv", (3, 64, 7, 7))]
+    return L
+
+
+def _in(x):
+    return F.instance_norm(x, eps=1e-5)
+
+
+def cyclegan_generator_forward(P, x):
+    """models/model_architectures.py:95-120 (CycleGANBlock.forward :132-134)."""
+    def conv(name, h, stride=1, padding=0):
+        return F.conv2d(h, P[name + ".weight"], P[name + ".bias"], stride=stride, padding=padding)
+
+    def convT(name, h):
+        return F.conv_transpose2d(h, P[name + ".weight"], P[name + ".bias"], stride=2, padding=1, output_padding=1)
+
+    h = F.relu(_in(conv("model.1", F.pad(x, (3, 3, 3, 3), mode="reflect"))))
+    h = F.relu(_in(conv("model.4", h, 2, 1)))
+    h = F.relu(_in(conv("model.7", h, 2, 1)))
+    for i in range(9):
+        pre = f"model.{10 + i}.conv_block."
+        r = F.relu(_in(conv(pre + "1", F.pad(h, (1, 1, 1, 1), mode="reflect"))))
+        h = h + _in(conv(pre + "5", F.pad(r, (1, 1, 1, 1), mode="reflect")))
+    h = F.relu(_in(convT("model.19", h)))
+    h = F.relu(_in(convT("model.22", h)))
+    return torch.tanh(conv("model.26", F.pad(h, (3, 3, 3, 3), mode="reflect")))
+
+
+def cyclegan_cancelled_biases():
+    """conv biases feeding an InstanceNorm in the CycleGAN generator (all but model.26)"""
+    return {n + ".bias" for n, _, _ in cyclegan_generator_layout()[:-1]}
+
+
+def init_cycle_params(seed=47, c_in=9, model="attentiongan"):
     """models/model.py:80, :97-100: manual_seed(seed) then G_pre_to_post, G_post_to_pre, D_pre,
     D_post, each built (nn.Conv2d RNG) and re-initialised (N(0, 0.02)) before the next."""
     torch.manual_seed(seed)
-    gl, dl = generator_layout(c_in), discriminator_layout(c_in, extra=0)
+    gl = generator_layout(c_in) if model == "attentiongan" else cyclegan_generator_layout(c_in)
+    dl = discriminator_layout(c_in, extra=0)
     return OrderedDict((n, _initialise(_construct(L), L)) for n, L in zip(NETS, (gl, gl, dl, dl)))
 
 
@@ -60,8 +107,10 @@ class CycleStepOracle:
     """Holds the four networks + the two Adam optimisers and performs reference train_cycle
     iterations (models/model.py:677-752) with autograd on the CPU."""
 
-    def __init__(self, params=None, seed=47, c_in=9, lr=2e-4, identity=False, dtype=torch.float32):
-        params = params or init_cycle_params(seed, c_in)
+    def __init__(self, params=None, seed=47, c_in=9, lr=2e-4, identity=False, dtype=torch.float32,
+                 model="attentiongan"):
+        params = params or init_cycle_params(seed, c_in, model)
+        self.model = model
         self.P = OrderedDict((n, OrderedDict((k, v.detach().clone().to(dtype).requires_grad_(True))
                                              for k, v in params[n].items())) for n in NETS)
         G1, G2, D1, D2 = (list(self.P[n].values()) for n in NETS)
@@ -76,6 +125,8 @@ class CycleStepOracle:
                 g["lr"] = lr
 
     def _g(self, name, x):
+        if self.model == "cyclegan":
+            return cyclegan_generator_forward(self.P[name], x)
         return generator_forward(self.P[name], x)[0]
 
     def _d(self, name, x):

@@ -5,7 +5,8 @@ with the same inert stand-ins for tifffile / torchvision.transforms / torchmetri
 make_golden.py.  It builds `Model(model="attentiongan", topography="all", ...)` and drives
 the UNMODIFIED `Model.train_cycle()` (models/model.py:660-758) over synthetic tiles.
 
-Only numeric results are written (tests/golden/cycle_step_<R>[_id].npz, no pickles).
+Only numeric results are written (tests/golden/cycle_step_<R>[_id].npz for AttentionGAN,
+tests/golden/cyclegan_step_<R>.npz for CycleGAN (models/model_architectures.py:91-157); no pickles).
 
 Recorded per case (R = 32, batch N = 2, input_channels = 9, seed 47):
   * inputs x0, y0, x1, y1 ~ U[-1, 1) from torch.Generator().manual_seed(1234)
@@ -37,9 +38,11 @@ def _eval(m, x0, y0, rec, pre):
     post = torch.cat((y0, x0[:, 3:]), 1)
     with torch.no_grad():
         rec[pre + "g_pre_to_post"] = m.pre_to_post_generator(x0).numpy()
-        rec[pre + "mask_pre_to_post"] = m.pre_to_post_generator.last_attention_mask.numpy()
+        if m.model == "attentiongan":
+            rec[pre + "mask_pre_to_post"] = m.pre_to_post_generator.last_attention_mask.numpy()
         rec[pre + "g_post_to_pre"] = m.post_to_pre_generator(post).numpy()
-        rec[pre + "mask_post_to_pre"] = m.post_to_pre_generator.last_attention_mask.numpy()
+        if m.model == "attentiongan":
+            rec[pre + "mask_post_to_pre"] = m.post_to_pre_generator.last_attention_mask.numpy()
         rec[pre + "d_pre"] = m.pre_discriminator(x0).numpy()
         rec[pre + "d_post"] = m.post_discriminator(post).numpy()
     for net in NETS:
@@ -47,11 +50,11 @@ def _eval(m, x0, y0, rec, pre):
             rec[f"{pre}{net}/{k}"] = v
 
 
-def run(R, N=2, identity=False):
+def run(R, N=2, identity=False, model="attentiongan"):
     from models import model as M  # noqa: E402  (reference, imported read-only)
 
     torch.set_num_threads(8)
-    m = M.Model(model="attentiongan", dataset_subset="usa", dataset_dem="same", data_path="/nonexistent",
+    m = M.Model(model=model, dataset_subset="usa", dataset_dem="same", data_path="/nonexistent",
                 num_epochs=2, topography="all", resize=R, verbose=False, add_identity_loss=identity)
     gen = torch.Generator().manual_seed(1234)
     x0, y0 = synth(R, N, gen)
@@ -101,9 +104,10 @@ def main():
     cwd = os.getcwd()
     os.chdir(REF)  # models/data.py reads metadata/dataset_split.csv relative to cwd
     try:
-        for R, identity in ((32, False), (32, True)):
-            rec = run(R, identity=identity)
-            out = os.path.join(HERE, f"cycle_step_{R}{'_id' if identity else ''}.npz")
+        for model, R, identity in (("attentiongan", 32, False), ("attentiongan", 32, True), ("cyclegan", 32, False)):
+            rec = run(R, identity=identity, model=model)
+            kind = "cycle_step" if model == "attentiongan" else "cyclegan_step"
+            out = os.path.join(HERE, f"{kind}_{R}{'_id' if identity else ''}.npz")
             np.savez_compressed(out, **{k.replace(".", "__"): v for k, v in rec.items()})
             print("wrote", out, "losses it0", rec["it0_losses"], "it1", rec["it1_losses"])
     finally:

@@ -67,3 +67,25 @@ def test_image_pool_semantics():
             assert float(a[0, 0, 0, 0]) == -float(b[0, 0, 0, 0])      # pairs stay together
     assert swapped > 5 and kept > 5
     assert len(pool.images) == 3
+
+
+def test_cyclegan_modules_match_reference_layout_and_init(golden):
+    """CycleGAN: Sequential state_dict keys / shapes in the reference's order, bit-identical
+    seed-47 initial weights (golden from the reference's own construction)."""
+    from floodgan.model import Model
+    from floodgan.model_architectures import CYCLEGAN_GEN_KEYS
+    g = golden(32, "cyclegan_step")
+    m = Model(model="CycleGAN", num_epochs=2, topography="all", device="cpu")
+    lay = OC.cyclegan_generator_layout(9)
+    want = [(n + s, shape if s == ".weight" else ((shape[1],) if k == "convT" else (shape[0],)))
+            for n, k, shape in lay for s in (".weight", ".bias")]
+    sd = m.pre_to_post_generator.state_dict()
+    assert [(k, tuple(v.shape)) for k, v in sd.items()] == [(k, tuple(s)) for k, s in want]
+    assert len(m.pre_to_post_generator.param_dict()) == len(CYCLEGAN_GEN_KEYS) == len(sd)
+    for net in NETS:
+        for name, t in getattr(m, net).state_dict().items():
+            ref = g[f"init_{net}/{name}"]
+            t = t.double().flatten()
+            n8 = min(8, t.numel())
+            assert np.array_equal(t[:n8].numpy(), ref[2:2 + n8]), (net, name)
+            assert abs(t.sum().item() - ref[0]) <= 1e-9 * max(1.0, abs(ref[1])), (net, name)

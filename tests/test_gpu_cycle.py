@@ -79,75 +79,107 @@ def test_generator_x_extra_equals_cat():
     assert torch.equal(a, b) and torch.equal(ma, mb)
 
 
-def test_generator_input_gradient_vs_fp64(report):
-    """The cycle path's new backward: d loss / d input through the drop-in AttentionGAN generator
-    (autograd over the fused node) vs the fp64 oracle; a smooth loss so no kink decides the sign."""
+def _gen_fwd(model, P, x):
+    return OC.cyclegan_generator_forward(P, x) if model == "cyclegan" else O.generator_forward(P, x)[0]
+
+
+def _skip_g(model):
+    return OC.cyclegan_cancelled_biases() if model == "cyclegan" else O.cancelled_biases()[0]
+
+
+@pytest.mark.parametrize("model", ["attentiongan", "cyclegan"])
+def test_generator_input_gradient_vs_fp64(model, report):
+    """The cycle path's new backward: d loss / d input through the drop-in generator (autograd over
+    the fused node) vs the fp64 oracle; a smooth loss so no kink decides the sign."""
     from floodgan.model import Model
     R = 32
     torch.manual_seed(12)
     x = torch.rand(2, 9, R, R) * 2 - 1
     y = torch.rand(2, 3, R, R) * 2 - 1
-    m = Model(model="AttentionGAN", num_epochs=2, topography="all")
-    P = OC.init_cycle_params()
+    m = Model(model=model, num_epochs=2, topography="all")
+    P = OC.init_cycle_params(model=model)
     Gd = {k: v.double().requires_grad_(True) for k, v in P["pre_to_post"].items()}
     xr = x.double().requires_grad_(True)
-    out_r, _ = O.generator_forward(Gd, xr)
+    out_r = _gen_fwd(model, Gd, xr)
     F.mse_loss(out_r, y.double()).backward()
     xd = x.to(DEV).requires_grad_(True)
     out = m.pre_to_post_generator(xd)
     F.mse_loss(out, y.to(DEV)).backward()
     e_x = nrel(xd.grad, xr.grad)
-    skip_g, _ = O.cancelled_biases()
+    skip_g = _skip_g(model)
     eg = [(k, nrel(p.grad, Gd[k].grad)) for k, p in m.pre_to_post_generator.named_parameters() if k not in skip_g]
-    report("cycle_generator_input_grad_vs_fp64", R=R, input_grad=e_x, worst_G=_worst(eg))
+    report("cycle_generator_input_grad_vs_fp64", model=model, R=R, input_grad=e_x, worst_G=_worst(eg))
     assert e_x < 1e-4 and _worst(eg)[1] < 1e-4, (e_x, _worst(eg))
 
 
-def _cycle_model(identity):
+def _cycle_model(identity, model="attentiongan"):
     from floodgan.model import Model
-    return Model(model="AttentionGAN", num_epochs=2, topography="all", add_identity_loss=identity)
+    return Model(model=model, num_epochs=2, topography="all", add_identity_loss=identity)
 
 
-@pytest.mark.parametrize("identity", [False, True])
-def test_cycle_step_gradients_vs_fp64(identity, report):
+CASES = [("attentiongan", False), ("attentiongan", True), ("cyclegan", False)]
+
+
+@pytest.mark.parametrize("model,identity", CASES)
+def test_cycle_step_gradients_vs_fp64(model, identity, report):
     """First CycleStep iteration: every G and D gradient vs the fp64 oracle iteration (all of
     them are computed before any parameter update), and all iteration-0 losses."""
     torch.manual_seed(13)
     R = 32
     x = torch.rand(2, 9, R, R) * 2 - 1
     y = torch.rand(2, 3, R, R) * 2 - 1
-    st = OC.CycleStepOracle(identity=identity, dtype=torch.float64)
+    st = OC.CycleStepOracle(identity=identity, dtype=torch.float64, model=model)
     rec = {}
     ref_losses = np.array(st.step(x, y, record=rec))
-    m = _cycle_model(identity)
+    m = _cycle_model(identity, model)
     losses = m.cycle_step_fn(x.to(DEV), y.to(DEV)).cpu().numpy().astype(np.float64)
     lrel = np.abs(losses - ref_losses) / np.abs(ref_losses)
-    skip_g, skip_d = O.cancelled_biases()
-    errs = {}
+    skip_g, skip_d = _skip_g(model), O.cancelled_biases()[1]
+
+    def grads_of(r, net):
+        return r["g_grads" if "_to_" in net else "d_grads"][net]
+
+    # The reference's own fp32 envelope: at 32x32 the residual blocks run at 8x8, so a weight
+    # gradient sums 64 pixels and one ReLU whose pre-activation is ~1e-6 (decided differently by
+    # any two fp32 evaluations) moves it by ~1e-2 (DESIGN.md §4, P3).  Measure it with the fp32
+    # oracle under 1e-6 relative input noise and allow max(1e-3, 2x) of it per tensor.
+    env = {}
+    for trial in range(3):
+        torch.manual_seed(100 + trial)
+        r32 = {}
+        OC.CycleStepOracle(identity=identity, model=model).step(x * (1 + 1e-6 * trial * torch.randn_like(x)), y,
+                                                                record=r32)
+        for net in OC.NETS:
+            for k, v in grads_of(r32, net).items():
+                env[(net, k)] = max(env.get((net, k), 0.0), nrel(v, grads_of(rec, net)[k]))
+    errs, bad = {}, []
     for net, mod, skip in (("pre_to_post", m.pre_to_post_generator, skip_g),
                            ("post_to_pre", m.post_to_pre_generator, skip_g),
                            ("pre_d", m.pre_discriminator, skip_d), ("post_d", m.post_discriminator, skip_d)):
-        ref = rec["g_grads" if "_to_" in net else "d_grads"][net]
-        errs[net] = _worst([(k, nrel(p.grad, ref[k])) for k, p in mod.named_parameters() if k not in skip])
-    report("cycle_step_grads_vs_fp64", R=R, identity=identity, loss_rel=lrel.tolist(),
-           worst={k: list(v) for k, v in errs.items()})
+        ref = grads_of(rec, net)
+        es = [(k, nrel(p.grad, ref[k])) for k, p in mod.named_parameters() if k not in skip]
+        errs[net] = _worst(es)
+        bad += [(net, k, e, env[(net, k)]) for k, e in es if e >= max(NTOL, 2 * env[(net, k)])]
+    report("cycle_step_grads_vs_fp64", model=model, R=R, identity=identity, loss_rel=lrel.tolist(),
+           worst={k: list(v) for k, v in errs.items()},
+           fp32_envelope_worst={net: max(v for (n, k), v in env.items() if n == net and k not in skip_g | skip_d)
+                                for net in OC.NETS})
     assert lrel.max() < 1e-5, lrel
-    for net, (k, e) in errs.items():
-        assert e < NTOL, (net, k, e)
+    assert not bad, bad
 
 
-@pytest.mark.parametrize("identity", [False, True])
-def test_cycle_train_vs_reference_golden(golden, identity, report):
+@pytest.mark.parametrize("model,identity", CASES)
+def test_cycle_train_vs_reference_golden(golden, model, identity, report):
     """Model.train_cycle (two epochs, one batch each) vs the REFERENCE's own train_cycle run
     (tests/golden/cycle_step_32[_id].npz): iteration-0 losses are pre-update (P1, 1e-5);
     iteration-1 losses and post-update outputs are held to the P3 bound max(1e-3, 2x the
     reference's own fp32 envelope under 1e-6 input noise)."""
-    g = golden("32_id" if identity else 32, "cycle_step")
+    g = golden("32_id" if identity else 32, "cycle_step" if model == "attentiongan" else "cyclegan_step")
     env = [0.0, 0.0, 0.0, 0.0]      # loss it0, loss it1, G out after it1, D out after it1
     x0c = torch.from_numpy(g["x0"])
     for trial in range(1, 3):
         torch.manual_seed(trial)
-        st = OC.CycleStepOracle(identity=identity)
+        st = OC.CycleStepOracle(identity=identity, model=model)
         lr = 2e-4
         for it in range(2):
             st.set_lr(lr)
@@ -156,10 +188,10 @@ def test_cycle_train_vs_reference_golden(golden, identity, report):
             env[it] = max(env[it], float((np.abs(ls - g[f"it{it}_losses"]) / np.abs(g[f"it{it}_losses"])).max()))
             lr = float(g[f"it{it}_lr_after"][0])
         with torch.no_grad():
-            env[2] = max(env[2], nrel(O.generator_forward(st.P["pre_to_post"], x0c)[0],
+            env[2] = max(env[2], nrel(_gen_fwd(model, st.P["pre_to_post"], x0c),
                                       torch.from_numpy(g["it1_g_pre_to_post"])))
             env[3] = max(env[3], nrel(O.discriminator_forward(st.P["pre_d"], x0c), torch.from_numpy(g["it1_d_pre"])))
-    m = _cycle_model(identity)
+    m = _cycle_model(identity, model)
 
     class _Loader:
         def __init__(self):
@@ -183,7 +215,7 @@ def test_cycle_train_vs_reference_golden(golden, identity, report):
     e_d = nrel(d, torch.from_numpy(g["it1_d_pre"]))
     lrel = [np.abs(np.array([m.all_losses["all_" + k][it] for k in keys]) - g[f"it{it}_losses"])
             / np.abs(g[f"it{it}_losses"]) for it in range(2)]
-    report("cycle_train_vs_reference_golden", identity=identity, loss_rel_it0=lrel[0].tolist(),
+    report("cycle_train_vs_reference_golden", model=model, identity=identity, loss_rel_it0=lrel[0].tolist(),
            loss_rel_it1=lrel[1].tolist(), g_out_after=e_g, d_out_after=e_d, reference_envelope=env)
     assert lrel[0].max() < 1e-5, lrel[0]
     assert lrel[1].max() < max(NTOL, 2 * env[1]), (lrel[1], env)

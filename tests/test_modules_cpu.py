@@ -70,7 +70,7 @@ def test_fused_adam_state_format_matches_torch_adam():
 def test_model_rejects_out_of_scope_models():
     from floodgan.model import Model
     with pytest.raises(NotImplementedError):
-        Model(model="CycleGAN", device="cpu")
+        Model(model="Pix2Pix", device="cpu")
 
 
 def test_lambda_rule_matches_reference():

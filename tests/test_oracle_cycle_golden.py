@@ -12,13 +12,18 @@ GOLD_NETS = dict(zip(OC.NETS, ("pre_to_post_generator", "post_to_pre_generator",
                                "post_discriminator")))
 
 
-def _outputs(P, x0, y0):
+def _outputs(P, x0, y0, model="attentiongan"):
     post = torch.cat((y0, x0[:, 3:]), 1)
     with torch.no_grad():
-        a, ma = O.generator_forward(P["pre_to_post"], x0)
-        b, mb = O.generator_forward(P["post_to_pre"], post)
-        return dict(g_pre_to_post=a, mask_pre_to_post=ma, g_post_to_pre=b, mask_post_to_pre=mb,
-                    d_pre=O.discriminator_forward(P["pre_d"], x0), d_post=O.discriminator_forward(P["post_d"], post))
+        out = dict(d_pre=O.discriminator_forward(P["pre_d"], x0), d_post=O.discriminator_forward(P["post_d"], post))
+        if model == "cyclegan":
+            out.update(g_pre_to_post=OC.cyclegan_generator_forward(P["pre_to_post"], x0),
+                       g_post_to_pre=OC.cyclegan_generator_forward(P["post_to_pre"], post))
+        else:
+            a, ma = O.generator_forward(P["pre_to_post"], x0)
+            b, mb = O.generator_forward(P["post_to_pre"], post)
+            out.update(g_pre_to_post=a, mask_pre_to_post=ma, g_post_to_pre=b, mask_post_to_pre=mb)
+        return out
 
 
 def test_cycle_init_rng_parity(golden):
@@ -56,6 +61,37 @@ def test_cycle_two_training_iterations(golden, kind, identity):
         assert np.allclose(losses, g[f"it{it}_losses"], rtol=1e-4, atol=1e-6), (it, losses, g[f"it{it}_losses"])
         # after an Adam update the fp32 reference is itself chaotic at ~1e-3
         for k, v in _outputs(st.P, x0, y0).items():
+            assert nrel(v, g[f"it{it}_{k}"]) < 1e-4, (it, k)
+        for net, gname in GOLD_NETS.items():
+            _check_checksums(g, f"it{it}_{gname}", st.P[net], skip_g if net in ("pre_to_post", "post_to_pre") else skip_d)
+        lr = float(g[f"it{it}_lr_after"][0])
+
+
+def test_cyclegan_init_and_forward(golden):
+    g = golden(32, "cyclegan_step")
+    P = OC.init_cycle_params(model="cyclegan")
+    for net, gname in GOLD_NETS.items():
+        for name, t in P[net].items():
+            ref = g[f"init_{gname}/{name}"]
+            t = t.double().flatten()
+            assert np.array_equal(t[:min(8, t.numel())].numpy(), ref[2:2 + min(8, t.numel())]), (net, name)
+    assert [k for k in P["pre_to_post"]] == [f"{n}.{s}" for n, _, _ in OC.cyclegan_generator_layout() for s in ("weight", "bias")]
+    x0, y0 = torch.from_numpy(g["x0"]), torch.from_numpy(g["y0"])
+    for k, v in _outputs(P, x0, y0, "cyclegan").items():
+        assert nrel(v, g["init_" + k]) < 1e-6, k
+
+
+def test_cyclegan_two_training_iterations(golden):
+    g = golden(32, "cyclegan_step")
+    st = OC.CycleStepOracle(model="cyclegan")
+    skip_g, (_, skip_d) = OC.cyclegan_cancelled_biases(), O.cancelled_biases()
+    x0, y0 = torch.from_numpy(g["x0"]), torch.from_numpy(g["y0"])
+    lr = 2e-4
+    for it in range(2):
+        st.set_lr(lr)
+        losses = st.step(torch.from_numpy(g[f"x{it}"]), torch.from_numpy(g[f"y{it}"]))
+        assert np.allclose(losses, g[f"it{it}_losses"], rtol=1e-4, atol=1e-6), (it, losses, g[f"it{it}_losses"])
+        for k, v in _outputs(st.P, x0, y0, "cyclegan").items():
             assert nrel(v, g[f"it{it}_{k}"]) < 1e-4, (it, k)
         for net, gname in GOLD_NETS.items():
             _check_checksums(g, f"it{it}_{gname}", st.P[net], skip_g if net in ("pre_to_post", "post_to_pre") else skip_d)
