@@ -8,6 +8,11 @@ batch already resident in HBM.  Prints ONE JSON line (rank 0).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 8] [--res 512]
   N>1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+
+--workload attentiongan | cyclegan times the cycle path instead (SURVEY.md §8(f) row 1,
+BASELINE.json configs[3]/[4]): one iteration of models/model.py:677-752 (two generators, the
+recreated images through the other generator, two discriminators, both Adam steps, the eight
+logged losses read back).  The default (paired) is the headline line.
 """
 import argparse
 import json
@@ -52,24 +57,25 @@ def pmc_traffic(kernel_tag):
             "mfma_busy": s.get("mfma_busy"), "clock_ghz": s.get("clock_ghz")}
 
 
-def cpu_baseline(res, threads, steps=2):
+def cpu_baseline(res, threads, steps=2, workload="paired"):
     """Time the CPU oracle (the reference algorithm restated on PyTorch-CPU, pinned to the
-    reference's own train_paired outputs) on a bounded sample: 1 warm-up + `steps` timed
-    iterations at batch 1, res x res."""
-    from oracle import paired_attention as O  # the checker / CPU baseline only
+    reference's own train_paired / train_cycle outputs) on a bounded sample: 1 warm-up + `steps`
+    timed iterations at batch 1, res x res."""
+    from oracle import attention_cycle as OC  # the checker / CPU baseline only
+    from oracle import paired_attention as O
 
     torch.set_num_threads(threads)
     g = torch.Generator().manual_seed(4321)
     x = torch.rand((1, 9, res, res), generator=g) * 2 - 1
     y = torch.rand((1, 3, res, res), generator=g) * 2 - 1
-    st = O.PairedStepOracle()
+    st = O.PairedStepOracle() if workload == "paired" else OC.CycleStepOracle(model=workload)
     st.step(x, y)
     t0 = time.perf_counter()
     for _ in range(steps):
         st.step(x, y)
     dt = time.perf_counter() - t0
     return {"value": round(steps / dt, 4), "unit": "img/s", "cores": threads, "kind": "port",
-            "sample": f"{steps} timed iterations (+1 warm-up) of the CPU oracle paired step at batch 1, "
+            "sample": f"{steps} timed iterations (+1 warm-up) of the CPU oracle {workload} step at batch 1, "
                       f"{res}x{res}, torch-CPU fp32 with {threads} threads"}
 
 
@@ -82,6 +88,7 @@ def main():
     ap.add_argument("--res", type=int, default=512)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--workload", choices=["paired", "attentiongan", "cyclegan"], default="paired")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -97,11 +104,15 @@ def main():
     from floodgan.parallel import broadcast_params
 
     B, R = args.batch, args.res
-    m = Model(model="PairedAttention", num_epochs=2, topography="all", device=dev)
+    cycle = args.workload != "paired"
+    m = Model(model={"paired": "PairedAttention", "attentiongan": "AttentionGAN", "cyclegan": "CycleGAN"}[args.workload],
+              num_epochs=2, topography="all", device=dev)
+    nets = ([m.pre_to_post_generator, m.post_to_pre_generator, m.pre_discriminator, m.post_discriminator] if cycle
+            else [m.generator, m.discriminator])
     if world > 1:
-        broadcast_params(m.generator)
-        broadcast_params(m.discriminator)
-    step = m.step_fn
+        for net in nets:
+            broadcast_params(net)
+    step = m.cycle_step_fn if cycle else m.step_fn
     g = torch.Generator().manual_seed(1234 + rank)
     x = (torch.rand((B, 9, R, R), generator=g) * 2 - 1).to(dev)
     y = (torch.rand((B, 3, R, R), generator=g) * 2 - 1).to(dev)
@@ -139,7 +150,8 @@ def main():
     if rank == 0:
         img_s = world * B * args.steps / elapsed
         out = {
-            "metric": "GAN training images/sec (512x512, PairedAttention)",
+            "metric": ("GAN training images/sec (512x512, PairedAttention)" if not cycle else
+                       f"GAN training images/sec ({R}x{R}, {m.model} cycle)"),
             "value": round(img_s, 3),
             "unit": "img/s",
             "n_gpus": world,
@@ -151,8 +163,10 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic U[-1,1) tiles resident in HBM, seed-47 weights (models/model.py:80)",
-            "config": {"workload": f"PairedAttention paired train step, {R}x{R}, topography=all "
-                                   f"(9-ch G input, 12-ch D input), batch {B}/GPU",
+            "config": {"workload": (f"PairedAttention paired train step, {R}x{R}, topography=all "
+                                    f"(9-ch G input, 12-ch D input), batch {B}/GPU" if not cycle else
+                                    f"{m.model} train_cycle step (2 G + 2 D, recreated images, Adam x2), {R}x{R}, "
+                                    f"topography=all (9-ch G and D inputs), batch {B}/GPU"),
                        "global_batch": world * B, "per_gpu_batch": B, "resolution": R,
                        "parallelism": f"dp{world}"},
             "conv_math": math,
@@ -168,12 +182,13 @@ def main():
                          "traffic": pmc_traffic("conv_fwd_f3_kernel<256,256,32,256,2>" if nprod == 3 else None),
                          "avg_launch_ms": round(avg_ms, 4), "launches": len(durs),
                          "flop_per_launch": flops},
-            "step_tflops": round(STEP_GFLOP_PER_IMG_512 * (R / 512) ** 2 * world * B * args.steps / elapsed / 1e3, 2),
+            "step_tflops": (None if cycle else
+                            round(STEP_GFLOP_PER_IMG_512 * (R / 512) ** 2 * world * B * args.steps / elapsed / 1e3, 2)),
             "losses_last_step": [round(float(v), 5) for v in losses],
         }
         if world == 1 and not args.no_cpu_baseline:
             threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
-            out["cpu_baseline"] = cpu_baseline(R, threads)
+            out["cpu_baseline"] = cpu_baseline(R, threads, steps=1 if cycle else 2, workload=args.workload)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
