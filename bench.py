@@ -30,12 +30,37 @@ import torch.distributed as dist  # noqa: E402
 FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak (spec)
 BF16_MFMA_PEAK_TFLOPS = 2500.0    # MI355X_MICROARCH.md: bf16 / fp16 dense MFMA peak (spec)
 STEP_GFLOP_PER_IMG_512 = 1593.5   # conv fwd 546.1 + conv bwd 1047.3 GFLOP per image
+STEP_GB_PER_IMG_512 = 3.96        # algorithmic conv-operand bytes per image at batch 8
+HBM_PEAK_TBS = 8.0                # MI355X_MICROARCH.md: HBM3E peak (spec)
 
 
 def resblock_conv_flops(batch, res):
     """3x3 s1 256->256 conv over (res/4)^2 pixels: 2*M*N*K per launch."""
     m = batch * (res // 4) ** 2
     return 2.0 * m * 256 * (256 * 9)
+
+
+def resblock_conv_bytes(batch, res):
+    """algorithmic HBM bytes of one resblock conv launch: the reflect-padded input read once, the
+    pre-split fp16 (h, l) weights, the output written once"""
+    hw = res // 4
+    return 4.0 * batch * ((hw + 2) ** 2 * 256 + hw * hw * 256) + 2 * 2 * 256 * 2304
+
+
+def step_roofline(img_s_per_gpu, res, peak_conv):
+    """The whole step against its ceilings: the conv math's MFMA roof
+    (1593.5 GFLOP per 512^2 image), the exact-fp32 MFMA roof, and HBM (3.96 GB per image)."""
+    f = STEP_GFLOP_PER_IMG_512 * (res / 512) ** 2 * 1e9
+    b = STEP_GB_PER_IMG_512 * (res / 512) ** 2 * 1e9
+    ceil_conv = peak_conv * 1e12 / f
+    ceil_fp32 = FP32_MFMA_PEAK_TFLOPS * 1e12 / f
+    ceil_hbm = HBM_PEAK_TBS * 1e12 / b
+    return {"img_s_per_gpu": round(img_s_per_gpu, 3),
+            "ceiling_conv_math_img_s": round(ceil_conv, 1), "frac_conv_math": round(img_s_per_gpu / ceil_conv, 4),
+            "ceiling_fp32_mfma_img_s": round(ceil_fp32, 1), "frac_fp32_mfma": round(img_s_per_gpu / ceil_fp32, 4),
+            "ceiling_hbm_img_s": round(ceil_hbm, 1), "frac_hbm": round(img_s_per_gpu / ceil_hbm, 4),
+            "basis": "SURVEY.md §8(d): 1593.5 GFLOP and 3.96 GB per 512x512 image-step; HBM 8 TB/s; the conv "
+                     "math's MFMA roof (f16x3: 2500/3 TFLOP/s) and the exact-fp32 MFMA roof 157.3 TFLOP/s"}
 
 
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "round1", "r1l_pmc_resblock_fwd.json")
@@ -57,26 +82,50 @@ def pmc_traffic(kernel_tag):
             "mfma_busy": s.get("mfma_busy"), "clock_ghz": s.get("clock_ghz")}
 
 
-def cpu_baseline(res, threads, steps=2, workload="paired"):
+def host_cpus():
+    """What the host offers: lscpu's sockets x cores per socket (physical cores), logical CPUs, and the
+    CPU share this process may use (affinity; OMP_NUM_THREADS on the GPU box = the box's share)."""
+    info = {"logical": os.cpu_count(), "affinity": len(os.sched_getaffinity(0))}
+    try:
+        import subprocess
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        kv = dict(line.split(":", 1) for line in out.splitlines() if ":" in line)
+        kv = {k.strip(): v.strip() for k, v in kv.items()}
+        info["model"] = kv.get("Model name")
+        info["physical_cores"] = int(kv.get("Socket(s)", 1)) * int(kv.get("Core(s) per socket", 0)) or None
+    except (OSError, ValueError):
+        pass
+    return info
+
+
+def cpu_baseline(res, threads, steps=3, workload="paired", batches=(1, 8)):
     """Time the CPU oracle (the reference algorithm restated on PyTorch-CPU, pinned to the
-    reference's own train_paired / train_cycle outputs) on a bounded sample: 1 warm-up + `steps`
-    timed iterations at batch 1, res x res."""
+    reference's own train_paired / train_cycle outputs; its speed matches the reference's own
+    train_paired within the margin recorded in profiles/round2/oracle_vs_reference_speed.log) on a
+    bounded sample: `steps` timed iterations at each batch size (1 warm-up iteration at batch 1)."""
     from oracle import attention_cycle as OC  # the checker / CPU baseline only
     from oracle import paired_attention as O
 
     torch.set_num_threads(threads)
-    g = torch.Generator().manual_seed(4321)
-    x = torch.rand((1, 9, res, res), generator=g) * 2 - 1
-    y = torch.rand((1, 3, res, res), generator=g) * 2 - 1
     st = O.PairedStepOracle() if workload == "paired" else OC.CycleStepOracle(model=workload)
-    st.step(x, y)
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        st.step(x, y)
-    dt = time.perf_counter() - t0
-    return {"value": round(steps / dt, 4), "unit": "img/s", "cores": threads, "kind": "port",
-            "sample": f"{steps} timed iterations (+1 warm-up) of the CPU oracle {workload} step at batch 1, "
-                      f"{res}x{res}, torch-CPU fp32 with {threads} threads"}
+    rates = {}
+    for bs in batches:
+        g = torch.Generator().manual_seed(4321)
+        x = torch.rand((bs, 9, res, res), generator=g) * 2 - 1
+        y = torch.rand((bs, 3, res, res), generator=g) * 2 - 1
+        if bs == batches[0]:
+            st.step(x, y)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            st.step(x, y)
+        rates[bs] = bs * steps / (time.perf_counter() - t0)
+    host = host_cpus()
+    return {"value": round(rates[batches[-1]], 4), "unit": "img/s", "cores": threads, "kind": "port",
+            "by_batch": {str(b): round(v, 4) for b, v in rates.items()}, "host": host,
+            "sample": f"{steps} timed iterations at batch " + " and ".join(map(str, batches)) +
+                      f" (+1 warm-up) of the CPU oracle {workload} step, {res}x{res}, torch-CPU fp32 with {threads} "
+                      f"threads (the box's CPU share; host: {host.get('physical_cores')} physical cores, "
+                      f"{host.get('logical')} logical); value = the batch-{batches[-1]} rate"}
 
 
 def main():
@@ -184,11 +233,17 @@ def main():
                          "flop_per_launch": flops},
             "step_tflops": (None if cycle else
                             round(STEP_GFLOP_PER_IMG_512 * (R / 512) ** 2 * world * B * args.steps / elapsed / 1e3, 2)),
+            "step_roofline": (None if cycle else step_roofline(img_s / world, R, peak)),
             "losses_last_step": [round(float(v), 5) for v in losses],
         }
+        tr = out["roofline"]["traffic"]
+        if tr:
+            tr["over_algorithmic"] = round(tr["bytes_per_launch"] / resblock_conv_bytes(B, R), 3)
+            tr["algorithmic_bytes"] = resblock_conv_bytes(B, R)
         if world == 1 and not args.no_cpu_baseline:
-            threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
-            out["cpu_baseline"] = cpu_baseline(R, threads, steps=1 if cycle else 2, workload=args.workload)
+            threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", 0)) or len(os.sched_getaffinity(0))
+            out["cpu_baseline"] = cpu_baseline(R, threads, steps=1 if cycle else 3, workload=args.workload,
+                                               batches=(1,) if cycle else (1, 8))
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -505,7 +505,10 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
 int g_f3_alt = 7;     // fg_set_f3_order: bit 0 alternates the kernel-row order of odd M tiles,
                       // bit 1 walks k chunk-outer (taps of one channel chunk back to back),
                       // bit 2 raises the priority of the second half of the waves
-int g_f3_persist = 1; // fg_set_f3_persistent: resident workgroups loop over tiles
+int g_f3_persist = 1; // fg_set_f3_persistent: 1 resident workgroups loop over tiles, 0 one workgroup per
+                      // tile, n >= 2 at most n workgroups (test hook: forces the tile-crossing stream
+                      // -- setup_issue() mid-stream, next tile's stages in flight over an epilogue --
+                      // at small sizes)
 int g_f3_sched = -1;  // fg_set_f3_sched: per-stage instruction order (kernel template SCH), -1 auto
 
 template <int BM, int BN, int WM, int WN, int NS = 3>
@@ -526,7 +529,7 @@ int launch_cfg(const ConvBatch& in, int nprob, hipStream_t stream) {
     // persistent: as many workgroups as fit at once (LDS-limited), each looping over tiles
     constexpr int LDS = NS * (BM * 128 + 2 * BN * 64);
     const int per_cu = (160 * 1024) / LDS;
-    const int grid = g_f3_persist ? std::min(total, fg::num_cus() * per_cu) : total;
+    const int grid = g_f3_persist ? std::min(total, g_f3_persist > 1 ? g_f3_persist : fg::num_cus() * per_cu) : total;
     const int sched = g_f3_sched >= 0 ? g_f3_sched : 3;
 #ifdef FG_F3_DIAG
     // timing-only diagnostic build (outputs are wrong): FG_F3_DIAG=1 compute without data movement,
@@ -595,7 +598,8 @@ FG_API int fg_set_f3_tile(int cfg) {
 }
 
 FG_API int fg_set_f3_persistent(int on) {
-    g_f3_persist = on != 0;
+    if (on < 0) return fg::fail(FG_ERR_INVALID, "fg_set_f3_persistent: %d", on);
+    g_f3_persist = on;
     return 0;
 }
 

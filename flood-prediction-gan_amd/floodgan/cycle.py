@@ -45,7 +45,8 @@ class ImagePool:
         self.size, self.images, self.rng = size, [], rng or random
 
     def __call__(self, image, conditions):
-        item = (image, conditions.clone())      # the caller may reuse its input tensor next step
+        # the caller may reuse its input tensor next step; conditions is None without topography
+        item = (image, None if conditions is None else conditions.clone())
         if len(self.images) < self.size:
             self.images.append(item)
             return image, conditions
@@ -66,8 +67,16 @@ class CycleStep:
         self.dpre, self.dpost = d_pre.param_dict(), d_post.param_dict()
         self.opt_g, self.opt_d = opt_g, opt_d
         self.identity, self.group = identity, group
-        self.gflat = FlatGrads(list(self.g1.values()) + list(self.g2.values()))
-        self.dflat = FlatGrads(list(self.dpost.values()) + list(self.dpre.values()))
+        # one flat gradient buffer per optimiser group, laid out bucket by bucket in the order the
+        # backward completes them (each generator's buckets complete in its LAST backward pass of
+        # the iteration, each discriminator's in its D-step backward); each bucket's all-reduce
+        # starts as soon as it is written (parallel.FlatGrads)
+        gnamed = {f"{t}.{k}": v for t, P in (("g1", self.g1), ("g2", self.g2)) for k, v in P.items()}
+        gb = [[f"{t}.{n}" for n in b] for t in ("g1", "g2") for b in X.gen_bucket_names(self.g1)]
+        self.gflat = FlatGrads(gnamed, gb)
+        dnamed = {f"{t}.{k}": v for t, P in (("dpre", self.dpre), ("dpost", self.dpost)) for k, v in P.items()}
+        db = [[f"{t}.{n}" for n in b] for t in ("dpre", "dpost") for b in X.disc_bucket_names()]
+        self.dflat = FlatGrads(dnamed, db)
         self.pre_pool, self.post_pool = ImagePool(rng=pool_rng), ImagePool(rng=pool_rng)
         self.last = {}
 
@@ -80,13 +89,16 @@ class CycleStep:
         inv = 1.0 / ws
         N, C, H, W = x.shape
         dev = x.device
-        if C < 4:
-            raise RuntimeError("the cycle step concatenates conditions: needs topography channels (C > 3)")
-        cond = x[:, 3:]
+        # models/model.py:682-689: with topography the conditions (input channels 3..) are cat'ed to
+        # every image a generator or discriminator sees; without (C == 3) nothing is cat'ed
+        cond = x[:, 3:] if C > 3 else None
         losses = torch.zeros(10, dtype=torch.float32, device=dev)
         self.gflat.attach()
         self.dflat.attach()
         g1g, g2g = self._grads(self.g1), self._grads(self.g2)
+
+        def ready(flat, tag):
+            return lambda name: flat.ready(f"{tag}.{name}")
         # ---- generators forward                                                 (:685-692)
         sp, mask_p, S_a = X.gen_forward(self.g1, x)                       # synthetic post
         spre, mask_q, S_b = X.gen_forward(self.g2, y, x_extra=cond)       # synthetic pre
@@ -104,7 +116,11 @@ class CycleStep:
             ops.mse_const(pred, 1.0, inv, losses[slot:slot + 1], g_pred)
             preds.append((params, dS, g_pred))
         # ---- generator backward: second round first; its input gradient, plus the frozen
-        # discriminator's, is d/d(first-round output)
+        # discriminator's, is d/d(first-round output).  A generator's gradient buckets are complete
+        # (and start their all-reduce) in its last backward of the iteration.
+        self.gflat.begin(self.group)
+        last1 = None if self.identity else ready(self.gflat, "g1")
+        last2 = None if self.identity else ready(self.gflat, "g2")
         gx_d = torch.empty(N, C, H, W, dtype=torch.float32, device=dev)
         X.gen_backward(self.g2, S_d, g_rq, grads_into=g2g, input_grad=gx_d)
         del S_d
@@ -118,33 +134,33 @@ class CycleStep:
         X.disc_backward(params, dS, g_pred, param_grads=False, input_grad=gx_c, input_grad_channels=(0, 3),
                         input_grad_accumulate=True)
         del preds, dS
-        X.gen_backward(self.g1, S_a, gx_d[:, :3], grads_into=g1g, accumulate=True)
+        X.gen_backward(self.g1, S_a, gx_d[:, :3], grads_into=g1g, accumulate=True, ready=last1)
         del S_a
-        X.gen_backward(self.g2, S_b, gx_c[:, :3], grads_into=g2g, accumulate=True)
+        X.gen_backward(self.g2, S_b, gx_c[:, :3], grads_into=g2g, accumulate=True, ready=last2)
         del S_b, gx_c, gx_d
         if self.identity:                                                     # (:700-702)
-            for params, grads, a, b, target, slot in ((self.g1, g1g, y, cond, y, 8),
-                                                      (self.g2, g2g, x, None, x[:, :3], 9)):
+            for params, grads, a, b, target, slot, tag in ((self.g1, g1g, y, cond, y, 8, "g1"),
+                                                           (self.g2, g2g, x, None, x[:, :3], 9, "g2")):
                 out, _, S_i = X.gen_forward(params, a, x_extra=b)
                 g_i = torch.empty_like(g_rq)
                 ops.l1(out, target, 5.0 * inv, losses[slot:slot + 1], g_i)
-                X.gen_backward(params, S_i, g_i, grads_into=grads, accumulate=True)
+                X.gen_backward(params, S_i, g_i, grads_into=grads, accumulate=True, ready=ready(self.gflat, tag))
                 del S_i
-        self.gflat.begin(self.group)
         self.gflat.finish()
         self.opt_g.step()
         # ---- discriminators: real and pooled synthetic in one 2N batch each    (:715-739)
         spre_b, cq = self.pre_pool(spre, cond)
         sp_b, cp = self.post_pool(sp, cond)
-        for params, real, real_extra, syn, syn_extra, slots in ((self.dpre, x, None, spre_b, cq, (4, 6)),
-                                                                (self.dpost, y, cond, sp_b, cp, (5, 7))):
+        self.dflat.begin(self.group)
+        for params, real, real_extra, syn, syn_extra, slots, tag in (
+                (self.dpre, x, None, spre_b, cq, (4, 6), "dpre"), (self.dpost, y, cond, sp_b, cp, (5, 7), "dpost")):
             pred, dS = X.disc_forward(params, X.disc_pack([(real, real_extra), (syn, syn_extra)], C), save=True)
             g_pred = torch.empty_like(pred)
             ops.mse_const(pred[:N], 1.0, 0.5 * inv, losses[slots[0]:slots[0] + 1], g_pred[:N])
             ops.mse_const(pred[N:], 0.0, 0.5 * inv, losses[slots[1]:slots[1] + 1], g_pred[N:])
-            X.disc_backward(params, dS, g_pred, param_grads=True, grads_into=self._grads(params))
+            X.disc_backward(params, dS, g_pred, param_grads=True, grads_into=self._grads(params),
+                            ready=ready(self.dflat, tag))
             del dS
-        self.dflat.begin(self.group)
         self.dflat.finish()
         self.opt_d.step()
         self.last = dict(synthetic_post=sp, synthetic_pre=spre, mask_pre_to_post=mask_p, mask_post_to_pre=mask_q,

@@ -233,9 +233,17 @@ G_BUCKETS = ([f"{h}_{t}" for t in ("content", "attention") for h in ("deconv1", 
     tuple([_blk(i, 1), _blk(i, 2)] for i in reversed(range(N_BLOCKS))) + (["conv1", "conv2", "conv3"],)
 
 
-def gen_bucket_names():
-    """the generator's gradient buckets in the order gen_backward completes them (parallel.FlatGrads)"""
-    return [[f"{layer}.{k}" for layer in b for k in ("weight", "bias")] for b in G_BUCKETS]
+def gen_bucket_names(P=None):
+    """the generator's gradient buckets in the order gen_backward completes them (parallel.FlatGrads);
+    with P, only the layers P holds (the CycleGAN generator has no attention head)"""
+    out = []
+    for b in G_BUCKETS:
+        names = [f"{layer}.{k}" for layer in b for k in ("weight", "bias")]
+        if P is not None:
+            names = [n for n in names if n in P]
+        if names:
+            out.append(names)
+    return out
 
 
 def gen_backward(P, S, g_out, grads_into=None, ready=None, input_grad=None, accumulate=False):

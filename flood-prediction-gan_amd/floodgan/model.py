@@ -98,13 +98,16 @@ class Model:
                  num_epochs=1, topography="all", resize=256, crop=None, save_model_interval=0,
                  save_images_interval=0, verbose=False, load_pretrained_model=False, pretrained_model_path=None,
                  add_identity_loss=False, training_model=True, seed=47, device="cuda", train_loader=None):
+        saved = None
+        if load_pretrained_model:
+            # models/model.py:52-57: the checkpoint, not the `model` argument, names the architecture
+            saved = torch.load(pretrained_model_path, map_location="cpu", weights_only=True)
+            model = saved["model"]
         self.model = model.lower()
         if self.model not in ("pairedattention", "attentiongan", "cyclegan"):
             raise NotImplementedError("floodgan implements the PairedAttention (paired), AttentionGAN and CycleGAN "
                                       f"(cycle) training paths; '{model}' is out of scope (SURVEY.md §2)")
-        saved = None
-        if load_pretrained_model:
-            saved = torch.load(pretrained_model_path, map_location="cpu", weights_only=True)
+        if saved is not None:
             self.num_epochs, self.topography = saved["num_epochs"], saved["topography"]
             self.add_identity_loss = saved["add_identity_loss"]
         else:

@@ -45,11 +45,15 @@ class _GeneratorFn(torch.autograd.Function):
         if mask is None:
             mask = out.new_empty(0)
         ctx.keys, ctx.P, ctx.S = keys, P, S
+        # the caller-visible tensors the backward reads (input, parameters) go through
+        # save_for_backward so an in-place change between forward and backward raises
+        ctx.save_for_backward(x, *params)
         ctx.mark_non_differentiable(mask)
         return out, mask
 
     @staticmethod
     def backward(ctx, g_out, _g_mask):
+        _ = ctx.saved_tensors          # version check of the input and the parameters
         gx = None
         if ctx.needs_input_grad[1]:   # the cycle path: G(cat(G'(x), conditions)) (models/model.py:677-706)
             gx = torch.empty(ctx.S["x"].shape, dtype=torch.float32, device=g_out.device)
@@ -66,10 +70,12 @@ class _DiscriminatorFn(torch.autograd.Function):
         buf = X.disc_pack([(x, None)], x.shape[1])
         pred, S = X.disc_forward(P, buf, save=any(ctx.needs_input_grad))
         ctx.P, ctx.S, ctx.xshape = P, S, tuple(x.shape)
+        ctx.save_for_backward(*params)
         return pred
 
     @staticmethod
     def backward(ctx, g_pred):
+        _ = ctx.saved_tensors          # version check of the parameters
         need_params = any(ctx.needs_input_grad[1:])
         gx = None
         if ctx.needs_input_grad[0]:
@@ -144,10 +150,12 @@ class _BlockFn(torch.autograd.Function):
     def forward(ctx, x, w1, b1, w2, b2):
         out, S = X.block_forward_nchw(x, {"w1": w1, "b1": b1, "w2": w2, "b2": b2}, save=any(ctx.needs_input_grad))
         ctx.S = S
+        ctx.save_for_backward(w1, b1, w2, b2)
         return out
 
     @staticmethod
     def backward(ctx, g):
+        _ = ctx.saved_tensors          # version check of the parameters
         gx, grads = X.block_backward_nchw(ctx.S, g, need_input=ctx.needs_input_grad[0])
         ctx.S = None
         return (gx,) + tuple(grads[k] if need else None

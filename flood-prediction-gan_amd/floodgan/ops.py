@@ -103,11 +103,13 @@ def absmax(t):
     cached on the tensor until an op writes it."""
     t = _tensor(t)
     cached = getattr(t, "_fg_amax", None)
-    if cached is not None and getattr(t, "_fg_amax_ver", t._version) == t._version:
+    # a slot is valid only together with the version counter it was recorded at: an in-place torch
+    # write since then (or a slot recorded without a version) means it may no longer bound t
+    if cached is not None and getattr(t, "_fg_amax_ver", None) == t._version:
         return cached
     out = _SLOTS.take(t.device)
     L.check(_lib().fg_absmax(L.ptr(t), t.numel(), L.ptr(out), L.stream_handle()), "absmax")
-    t._fg_amax = out
+    t._fg_amax, t._fg_amax_ver = out, t._version
     return out
 
 
@@ -117,7 +119,10 @@ def _amax_out(dst):
     if not L.fwd_f16x3() and not L.wgrad_f16x3():
         return None
     slot = _SLOTS.take(_dev(dst))
-    _tensor(dst)._fg_amax = slot
+    t = _tensor(dst)
+    # the kernel writes through a raw pointer (torch's counter does not move): record the version
+    # now, so a later in-place torch write invalidates the slot
+    t._fg_amax, t._fg_amax_ver = slot, t._version
     return slot
 
 
@@ -244,14 +249,14 @@ def split_pixels(X):
     the window-conv operand.  Cached on the buffer's tensor until an op writes it."""
     t = X.t
     cached = getattr(t, "_fg_split", None)
-    if cached is not None:
+    if cached is not None and getattr(t, "_fg_split_ver", None) == t._version:
         return cached
     npix = X.n * X.hp * X.wp
     out = torch.empty(npix * 2 * X.c, dtype=torch.float16, device=t.device)
     L.check(_lib().fg_split_pixels(L.ptr(t), npix, X.c, X.wp, L.ptr(absmax(t)), L.ptr(out), L.stream_handle()),
             "split_pixels")
     out.absmax = absmax(t)
-    t._fg_split = out
+    t._fg_split, t._fg_split_ver = out, t._version
     return out
 
 
@@ -435,7 +440,13 @@ def in_bwd(gsrc, fold_pad, gadd, src, mean, rstd, act, dst, bias_grad=None, bias
 
 
 def act_bwd(g, y, act):
-    # in place g *= act'(y) with act' in {0, 0.2, 1}: |g| cannot grow, a cached absmax stays valid
+    # in place g *= act'(y) with act' in {0, 0.2, 1}: |g| cannot grow, so a cached absmax slot still
+    # bounds it and is kept; a cached pre-split copy no longer matches the contents and is dropped
+    t = _tensor(g)
+    slot, ver = getattr(t, "_fg_amax", None), getattr(t, "_fg_amax_ver", None)
+    _wrote(g)
+    if slot is not None:
+        t._fg_amax, t._fg_amax_ver = slot, ver
     L.check(_lib().fg_act_bwd(view(g), view(y), act, L.stream_handle()), "act_bwd")
 
 

@@ -166,7 +166,8 @@ int fg_set_f3_order(int alt);
 int fg_set_f3_sched(int sched);
 /* Tuning hook: 1 (default) = the pipelined forward kernel runs one resident wave of workgroups that
  * loop over the tiles (the next tile's first k-stages stream in behind the current tile's last);
- * 0 = one workgroup per tile. */
+ * 0 = one workgroup per tile; n >= 2 = at most n resident workgroups (test hook: every workgroup then
+ * streams many tiles back to back even at small problem sizes). */
 int fg_set_f3_persistent(int on);
 /* A/B hook of the pipelined f16x3 weight-gradient kernel (conv_wgrad_f3.hip, n_a >= 128): 0 off,
  * 1 = staging as one burst per stage, 3 = staging slots interleaved with the MFMA groups,

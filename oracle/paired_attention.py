@@ -181,9 +181,24 @@ class PairedStepOracle:
             for g in opt.param_groups:
                 g["lr"] = lr
 
-    def step(self, x, y, record=None):
+    def load_state(self, G, D, opt_g_state=None, opt_d_state=None):
+        """Teacher forcing: continue from another implementation's state -- parameters (name ->
+        tensor) and torch.optim.Adam-format optimiser state dicts (FusedAdam writes that format)."""
+        with torch.no_grad():
+            for P, src in ((self.G, G), (self.D, D)):
+                for k, v in P.items():
+                    v.copy_(src[k].detach().to(v.device, v.dtype))
+        if opt_g_state is not None:
+            self.opt_g.load_state_dict(opt_g_state)
+        if opt_d_state is not None:
+            self.opt_d.load_state_dict(opt_d_state)
+
+    def step(self, x, y, record=None, d_after=None):
         """One iteration of models/model.py:615-646. Returns the four losses (D real,
-        D synthetic, G synthetic, raw L1 before x100) as floats."""
+        D synthetic, G synthetic, raw L1 before x100) as floats.
+        d_after (teacher forcing, tests only): discriminator parameters to continue the G step
+        with instead of this oracle's own Adam(D) result, so that the G half is compared on the
+        same D as the implementation under test."""
         x, y = x.to(self.dtype), y.to(self.dtype)
         fake, mask = generator_forward(self.G, x)
         cat_real = torch.cat((x, y), 1)
@@ -200,6 +215,12 @@ class PairedStepOracle:
         if record is not None:
             record["d_grads"] = OrderedDict((k, v.grad.detach().clone()) for k, v in self.D.items())
         self.opt_d.step()
+        if record is not None:
+            record["d_after_own"] = OrderedDict((k, v.detach().clone()) for k, v in self.D.items())
+        if d_after is not None:
+            with torch.no_grad():
+                for k, v in self.D.items():
+                    v.copy_(d_after[k].detach().to(v.device, v.dtype))
         for p in self.D.values():
             p.requires_grad_(False)
         self.opt_g.zero_grad()

@@ -112,26 +112,29 @@ def test_generator_input_gradient_vs_fp64(model, report):
     assert e_x < 1e-4 and _worst(eg)[1] < 1e-4, (e_x, _worst(eg))
 
 
-def _cycle_model(identity, model="attentiongan"):
+def _cycle_model(identity, model="attentiongan", topography="all"):
     from floodgan.model import Model
-    return Model(model=model, num_epochs=2, topography="all", add_identity_loss=identity)
+    return Model(model=model, num_epochs=2, topography=topography, add_identity_loss=identity)
 
 
 CASES = [("attentiongan", False), ("attentiongan", True), ("cyclegan", False)]
+# topography=None (models/model.py:682-689: no conditions cat, 3-channel generators and discriminators)
+CASES_TOPO = [(m, i, "all") for m, i in CASES] + [("attentiongan", True, None), ("cyclegan", False, None)]
 
 
-@pytest.mark.parametrize("model,identity", CASES)
-def test_cycle_step_gradients_vs_fp64(model, identity, report):
+@pytest.mark.parametrize("model,identity,topography", CASES_TOPO)
+def test_cycle_step_gradients_vs_fp64(model, identity, topography, report):
     """First CycleStep iteration: every G and D gradient vs the fp64 oracle iteration (all of
     them are computed before any parameter update), and all iteration-0 losses."""
     torch.manual_seed(13)
     R = 32
-    x = torch.rand(2, 9, R, R) * 2 - 1
+    c_in = 9 if topography else 3
+    x = torch.rand(2, c_in, R, R) * 2 - 1
     y = torch.rand(2, 3, R, R) * 2 - 1
-    st = OC.CycleStepOracle(identity=identity, dtype=torch.float64, model=model)
+    st = OC.CycleStepOracle(identity=identity, dtype=torch.float64, model=model, c_in=c_in)
     rec = {}
     ref_losses = np.array(st.step(x, y, record=rec))
-    m = _cycle_model(identity, model)
+    m = _cycle_model(identity, model, topography)
     losses = m.cycle_step_fn(x.to(DEV), y.to(DEV)).cpu().numpy().astype(np.float64)
     lrel = np.abs(losses - ref_losses) / np.abs(ref_losses)
     skip_g, skip_d = _skip_g(model), O.cancelled_biases()[1]
@@ -147,8 +150,8 @@ def test_cycle_step_gradients_vs_fp64(model, identity, report):
     for trial in range(3):
         torch.manual_seed(100 + trial)
         r32 = {}
-        OC.CycleStepOracle(identity=identity, model=model).step(x * (1 + 1e-6 * trial * torch.randn_like(x)), y,
-                                                                record=r32)
+        OC.CycleStepOracle(identity=identity, model=model, c_in=c_in).step(
+            x * (1 + 1e-6 * trial * torch.randn_like(x)), y, record=r32)
         for net in OC.NETS:
             for k, v in grads_of(r32, net).items():
                 env[(net, k)] = max(env.get((net, k), 0.0), nrel(v, grads_of(rec, net)[k]))
@@ -160,7 +163,8 @@ def test_cycle_step_gradients_vs_fp64(model, identity, report):
         es = [(k, nrel(p.grad, ref[k])) for k, p in mod.named_parameters() if k not in skip]
         errs[net] = _worst(es)
         bad += [(net, k, e, env[(net, k)]) for k, e in es if e >= max(NTOL, 2 * env[(net, k)])]
-    report("cycle_step_grads_vs_fp64", model=model, R=R, identity=identity, loss_rel=lrel.tolist(),
+    report("cycle_step_grads_vs_fp64", model=model, R=R, identity=identity, topography=topography,
+           loss_rel=lrel.tolist(),
            worst={k: list(v) for k, v in errs.items()},
            fp32_envelope_worst={net: max(v for (n, k), v in env.items() if n == net and k not in skip_g | skip_d)
                                 for net in OC.NETS})

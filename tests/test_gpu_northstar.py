@@ -1,0 +1,407 @@
+"""Parity at the north-star configuration (BASELINE.json configs[1]: PairedAttention, 512x512,
+topography=all) and the pinned-update criterion, against the CPU oracle (oracle/paired_attention.py,
+pinned to the reference's own train_paired by tests/test_oracle_golden.py).
+
+  P1  everything computed before the first update (G output, attention mask, D outputs, the D
+      losses and the L1 term) vs the fp32 oracle: norm-relative <= 1e-5.
+  P2  every G and D gradient under a smooth loss vs the fp64 oracle: <= 1e-4.
+  U   the optimiser update itself, teacher-forced: the oracle continues from the HIP state
+      (parameters + Adam moments) and, for the G half, from the HIP discriminator after Adam(D)
+      (models/model.py:633, :646).  Every element whose first moment is decided well above the
+      gradient's rounding-level disagreement must move in the same direction (fraction 1.0) and the
+      update of the decided elements agrees to 1e-3 norm-relative; undecided elements (|m| within
+      10x the gradient noise: IN-cancelled biases, flipped ReLU kinks) are reported, not asserted.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import attention_cycle as OC
+from oracle import paired_attention as O
+from test_gpu_parity import DEV, KTOL, NTOL, buf_from, nchw, nrel
+
+pytestmark = pytest.mark.gpu
+
+R = 512
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from floodgan import _lib as L
+    L.check(L.load().fg_device_ok(), "device_ok")
+    torch.set_num_threads(min(16, max(1, len(__import__("os").sched_getaffinity(0)))))
+
+
+def _model(**kw):
+    from floodgan.model import Model
+    return Model(model="PairedAttention", num_epochs=2, topography=kw.pop("topography", "all"), **kw)
+
+
+def _inputs(n, c=9, res=R, seed=1234):
+    g = torch.Generator().manual_seed(seed)
+    return torch.rand((n, c, res, res), generator=g) * 2 - 1, torch.rand((n, 3, res, res), generator=g) * 2 - 1
+
+
+# ---------------------------------------------------------------------------------------------- P1
+
+def test_p1_forward_and_losses_512(report):
+    """512x512, batch 2: G output, attention mask, D(real), D(synthetic) at the seed-47 weights and the
+    three pre-update losses of the fused training step (models/model.py:615-631, :643) vs the fp32 oracle."""
+    x, y = _inputs(2)
+    Gp, Dp = O.init_params()
+    with torch.no_grad():
+        fake_r, mask_r = O.generator_forward(Gp, x)
+        dr_r = O.discriminator_forward(Dp, torch.cat((x, y), 1))
+        df_r = O.discriminator_forward(Dp, torch.cat((x, fake_r), 1))
+    ref = np.array([float(F.mse_loss(dr_r, torch.ones_like(dr_r))), float(F.mse_loss(df_r, torch.zeros_like(df_r))),
+                    100 * float(F.l1_loss(fake_r, y))])
+    m = _model()
+    xd, yd = x.to(DEV), y.to(DEV)
+    with torch.no_grad():
+        out = m.generator(xd)
+        mask = m.generator.last_attention_mask
+        dr = m.discriminator(torch.cat((xd, yd), 1))
+        df = m.discriminator(torch.cat((xd, out), 1))
+    e = dict(g_out=nrel(out, fake_r), mask=nrel(mask, mask_r), d_real=nrel(dr, dr_r), d_synthetic=nrel(df, df_r))
+    losses = m.step_fn(xd, yd).cpu().numpy().astype(np.float64)
+    lrel = np.abs(losses[[0, 1, 3]] - ref) / np.abs(ref)
+    report("p1_512_vs_oracle_fp32", R=R, batch=2, loss_rel=lrel.tolist(), **e)
+    assert max(e.values()) < KTOL, e
+    assert lrel.max() < KTOL, lrel
+
+
+# ---------------------------------------------------------------------------------------------- P2
+
+def _worst(pairs):
+    return max(pairs, key=lambda t: t[1])
+
+
+def test_p2_gradients_512(report):
+    """512x512, batch 1: every G and D gradient through the drop-in modules under a smooth loss
+    MSE(D(cat(x, G(x))), 1) + 100*MSE(G(x), y) vs the fp64 oracle (IN-cancelled biases excluded:
+    their gradients are pure rounding noise)."""
+    x, y = _inputs(1, seed=99)
+    Gp, Dp = O.init_params()
+    Gd = {k: v.double().requires_grad_(True) for k, v in Gp.items()}
+    Dd = {k: v.double().requires_grad_(True) for k, v in Dp.items()}
+    fake_r, _ = O.generator_forward(Gd, x.double())
+    pr = O.discriminator_forward(Dd, torch.cat((x.double(), fake_r), 1))
+    (F.mse_loss(pr, torch.ones_like(pr)) + 100 * F.mse_loss(fake_r, y.double())).backward()
+    m = _model()
+    xd, yd = x.to(DEV), y.to(DEV)
+    fake = m.generator(xd)
+    pred = m.discriminator(torch.cat((xd, fake), 1))
+    (F.mse_loss(pred, torch.ones_like(pred)) + 100 * F.mse_loss(fake, yd)).backward()
+    skip_g, skip_d = O.cancelled_biases()
+    eg = [(k, nrel(p.grad, Gd[k].grad)) for k, p in m.generator.named_parameters() if k not in skip_g]
+    ed = [(k, nrel(p.grad, Dd[k].grad)) for k, p in m.discriminator.named_parameters() if k not in skip_d]
+    report("p2_512_grads_vs_fp64", R=R, worst_G=_worst(eg), worst_D=_worst(ed))
+    assert _worst(eg)[1] < 1e-4 and _worst(ed)[1] < 1e-4, (_worst(eg), _worst(ed))
+
+
+# ---------------------------------------------------------------------------------------------- batch 8
+
+def test_bs8_per_sample_equals_bs1_512(report):
+    """The bench's own shape (batch 8 at 512x512: the resblock convs' persistent workgroups stream two
+    tiles each, the tile-crossing path of conv_fwd_f3).  InstanceNorm is per sample, so each sample's
+    G output / mask / D output at batch 8 equals a batch-1 run of that sample; two samples are also
+    checked against the fp32 oracle, and the fused step's pre-update losses at batch 8 equal the torch
+    losses (models/model.py:626-631, :643) of the validated module outputs."""
+    x, y = _inputs(8, seed=7)
+    m = _model()
+    xd, yd = x.to(DEV), y.to(DEV)
+    with torch.no_grad():
+        out8 = m.generator(xd)
+        mask8 = m.generator.last_attention_mask.clone()
+        dr8 = m.discriminator(torch.cat((xd, yd), 1))
+        df8 = m.discriminator(torch.cat((xd, out8), 1))
+        errs = []
+        for i in (0, 3, 7):
+            o1 = m.generator(xd[i:i + 1])
+            k1 = m.generator.last_attention_mask
+            d1 = m.discriminator(torch.cat((xd[i:i + 1], yd[i:i + 1]), 1))
+            errs.append((i, nrel(out8[i:i + 1], o1), nrel(mask8[i:i + 1], k1), nrel(dr8[i:i + 1], d1)))
+    Gp, Dp = O.init_params()
+    oerr = []
+    with torch.no_grad():
+        for i in (0, 7):
+            fr, mr = O.generator_forward(Gp, x[i:i + 1])
+            oerr.append((i, nrel(out8[i:i + 1], fr), nrel(mask8[i:i + 1], mr)))
+    ref = np.array([float(F.mse_loss(dr8, torch.ones_like(dr8))), float(F.mse_loss(df8, torch.zeros_like(df8))),
+                    100 * float(F.l1_loss(out8, yd))])
+    losses = m.step_fn(xd, yd).cpu().numpy().astype(np.float64)
+    lrel = np.abs(losses[[0, 1, 3]] - ref) / np.abs(ref)
+    report("bs8_512_per_sample", per_sample_vs_bs1=errs, vs_oracle=oerr, step_loss_rel=lrel.tolist(),
+           losses=losses.tolist())
+    assert max(max(e[1:]) for e in errs) < KTOL, errs
+    assert max(max(e[1:]) for e in oerr) < KTOL, oerr
+    assert lrel.max() < KTOL, lrel
+    assert np.isfinite(losses).all()
+
+
+# ---------------------------------------------------------------------------------------------- U
+
+BETA1 = 0.5
+
+
+def _update_agreement(p0, p_hip, p_ref, g_hip, g_ref, m_ref):
+    """(fraction of decided elements whose update direction agrees, norm-relative update error over
+    the decided elements, fraction decided, norm-relative error of the whole updated tensor)"""
+    d_hip = (p_hip.double().cpu() - p0.double().cpu()).flatten()
+    d_ref = (p_ref.double().cpu() - p0.double().cpu()).flatten()
+    sigma = float((g_hip.double().cpu() - g_ref.double().cpu()).pow(2).mean().sqrt())
+    dec = m_ref.double().cpu().flatten().abs() > 10 * (1 - BETA1) * sigma + 1e-30
+    n = int(dec.sum())
+    if n == 0:
+        return 1.0, 0.0, 0.0, nrel(p_hip, p_ref)
+    agree = float((torch.sign(d_hip[dec]) == torch.sign(d_ref[dec])).double().mean())
+    err = float((d_hip[dec] - d_ref[dec]).norm() / max(float(d_ref[dec].norm()), 1e-30))
+    return agree, err, n / d_ref.numel(), nrel(p_hip, p_ref)
+
+
+@pytest.mark.parametrize("R_", [32, 64])
+def test_update_teacher_forced_vs_golden_inputs(golden, R_, report):
+    """Two iterations on the reference's golden inputs.  Before each, the fp64 oracle is loaded with
+    the HIP state (G, D, both Adam states); it then runs the same iteration with the G half on the
+    HIP discriminator after Adam(D).  Asserted: gradients <= 1e-3 (norm-relative; they share the
+    pre-update state), every decided element's update direction agrees, and the decided elements'
+    updates agree to 1e-3."""
+    g = golden(R_)
+    m = _model()
+    skip_g, skip_d = O.cancelled_biases()
+    G, D = m.generator, m.discriminator
+    for it in range(2):
+        lr = float(g[f"it{it}_lr"][0])
+        for opt in (m.optimizer_generator, m.optimizer_discriminator):
+            for grp in opt.param_groups:
+                grp["lr"] = lr
+        x, y = torch.from_numpy(g[f"x{it}"]), torch.from_numpy(g[f"y{it}"])
+        g0 = {k: v.detach().clone() for k, v in G.named_parameters()}
+        d0 = {k: v.detach().clone() for k, v in D.named_parameters()}
+        st = O.PairedStepOracle(dtype=torch.float64, lr=lr)
+        st.load_state(g0, d0, m.optimizer_generator.state_dict() if it else None,
+                      m.optimizer_discriminator.state_dict() if it else None)
+        m.step_fn(x.to(DEV), y.to(DEV))
+        torch.cuda.synchronize()
+        rec = {}
+        st.step(x, y, record=rec, d_after={k: v.detach().cpu() for k, v in D.named_parameters()})
+        rows, bad = [], []
+        for net, mod, P0, grads, skip, opt_ref in (("G", G, g0, rec["g_grads"], skip_g, st.opt_g),
+                                                   ("D", D, d0, rec["d_grads"], skip_d, st.opt_d)):
+            params_ref = st.G if net == "G" else rec["d_after_own"]
+            order = list(st.G if net == "G" else st.D)
+            for idx, (k, p) in enumerate(mod.named_parameters()):
+                if k in skip:
+                    continue
+                ge = nrel(p.grad, grads[k])
+                m_ref = opt_ref.state[opt_ref.param_groups[0]["params"][order.index(k)]]["exp_avg"]
+                agree, uerr, frac, perr = _update_agreement(P0[k], p, params_ref[k], p.grad, grads[k], m_ref)
+                rows.append((net, k, ge, agree, uerr, frac, perr))
+                if ge > NTOL or agree < 1.0 or uerr > NTOL:
+                    bad.append(rows[-1])
+        report("update_teacher_forced", R=R_, it=it,
+               worst_grad=max(rows, key=lambda r: r[2])[1:3], min_agree=min(r[3] for r in rows),
+               worst_update=max(rows, key=lambda r: r[4])[1:5:3], min_decided=min(r[5] for r in rows),
+               worst_param_rel=max(rows, key=lambda r: r[6])[1:7:5], bad=bad)
+        assert not bad, bad
+
+
+# ---------------------------------------------------------------------------------------------- topography
+
+@pytest.mark.parametrize("c_in,topo", [(3, None), (4, "dem"), (6, "map")])
+def test_topography_variants_step(c_in, topo, report):
+    """The reference's other input stacks (models/model.py:78: None -> 3, dem/flow/river -> 4, map -> 6
+    generator channels; the paired D takes c_in + 3): seed-47 init bit-identical to the oracle's, P1
+    losses of one fused step, and P2 gradients under the smooth loss vs fp64 at 32x32."""
+    Rr = 32
+    m = _model(topography=topo)
+    assert m.generator.conv1.weight.shape[1] == c_in and m.discriminator.model[0].weight.shape[1] == c_in + 3
+    Gp, Dp = O.init_params(c_in=c_in)
+    for k, v in m.generator.named_parameters():
+        assert torch.equal(v.detach().cpu(), Gp[k]), k
+    x, y = _inputs(2, c=c_in, res=Rr, seed=c_in)
+    Gd = {k: v.double().requires_grad_(True) for k, v in Gp.items()}
+    Dd = {k: v.double().requires_grad_(True) for k, v in Dp.items()}
+    fake_r, _ = O.generator_forward(Gd, x.double())
+    pr = O.discriminator_forward(Dd, torch.cat((x.double(), fake_r), 1))
+    (F.mse_loss(pr, torch.ones_like(pr)) + 100 * F.mse_loss(fake_r, y.double())).backward()
+    xd, yd = x.to(DEV), y.to(DEV)
+    fake = m.generator(xd)
+    pred = m.discriminator(torch.cat((xd, fake), 1))
+    (F.mse_loss(pred, torch.ones_like(pred)) + 100 * F.mse_loss(fake, yd)).backward()
+    skip_g, skip_d = O.cancelled_biases()
+    eg = [(k, nrel(p.grad, Gd[k].grad)) for k, p in m.generator.named_parameters() if k not in skip_g]
+    ed = [(k, nrel(p.grad, Dd[k].grad)) for k, p in m.discriminator.named_parameters() if k not in skip_d]
+    for p in list(m.generator.parameters()) + list(m.discriminator.parameters()):
+        p.grad = None
+    ref = np.array(O.PairedStepOracle(c_in=c_in).step(x, y))
+    ref[3] *= 100
+    losses = m.step_fn(xd, yd).cpu().numpy().astype(np.float64)
+    lrel = np.abs(losses - ref) / np.abs(ref)
+    report("topography_variant", c_in=c_in, worst_G=_worst(eg), worst_D=_worst(ed), loss_rel=lrel.tolist())
+    assert _worst(eg)[1] < 1e-4 and _worst(ed)[1] < 1e-4, (_worst(eg), _worst(ed))
+    assert lrel[[0, 1, 3]].max() < KTOL, lrel
+
+
+# ---------------------------------------------------------------------------------------------- cycle @ 512
+
+@pytest.mark.parametrize("model", ["attentiongan", "cyclegan"])
+def test_cycle_p1_losses_512(model, report):
+    """BASELINE configs[3]/[4] resolution: the eight iteration-0 losses of CycleStep at 512x512,
+    batch 1 (all evaluated before any parameter update: the D losses use pre-update D weights and the
+    synthetic images of the pre-update generators) vs the fp32 oracle's forwards (models/model.py:685-737)."""
+    from floodgan.model import Model
+    g = torch.Generator().manual_seed(31)
+    x = torch.rand((1, 9, R, R), generator=g) * 2 - 1
+    y = torch.rand((1, 3, R, R), generator=g) * 2 - 1
+    P = OC.init_cycle_params(model=model)
+    gen = OC.cyclegan_generator_forward if model == "cyclegan" else (lambda p, t: O.generator_forward(p, t)[0])
+    D = O.discriminator_forward
+    cond = x[:, 3:]
+    with torch.no_grad():
+        post_real = torch.cat((y, cond), 1)
+        sp = torch.cat((gen(P["pre_to_post"], x), cond), 1)
+        spre = torch.cat((gen(P["post_to_pre"], post_real), cond), 1)
+        rp = gen(P["pre_to_post"], spre)
+        rq = gen(P["post_to_pre"], sp)
+
+        def mse(p, t):
+            return float(F.mse_loss(p, torch.full_like(p, t)))
+        ref = np.array([mse(D(P["post_d"], sp), 1), mse(D(P["pre_d"], spre), 1), 10 * float(F.l1_loss(rq, x[:, :3])),
+                        10 * float(F.l1_loss(rp, y)), mse(D(P["pre_d"], x), 1), mse(D(P["post_d"], post_real), 1),
+                        mse(D(P["pre_d"], spre), 0), mse(D(P["post_d"], sp), 0)])
+    m = Model(model=model, num_epochs=2, topography="all")
+    losses = m.cycle_step_fn(x.to(DEV), y.to(DEV)).cpu().numpy().astype(np.float64)
+    lrel = np.abs(losses - ref) / np.abs(ref)
+    report("cycle_p1_512", model=model, loss_rel=lrel.tolist())
+    assert lrel.max() < KTOL, lrel
+
+
+@pytest.mark.parametrize("model", ["attentiongan", "cyclegan"])
+def test_cycle_generator_input_gradient_512(model, report):
+    """The cycle path's generator input gradient and weight gradients at 512x512 (smooth loss) vs fp64."""
+    from floodgan.model import Model
+    g = torch.Generator().manual_seed(41)
+    x = torch.rand((1, 9, R, R), generator=g) * 2 - 1
+    y = torch.rand((1, 3, R, R), generator=g) * 2 - 1
+    P = OC.init_cycle_params(model=model)
+    Gd = {k: v.double().requires_grad_(True) for k, v in P["pre_to_post"].items()}
+    xr = x.double().requires_grad_(True)
+    out_r = OC.cyclegan_generator_forward(Gd, xr) if model == "cyclegan" else O.generator_forward(Gd, xr)[0]
+    F.mse_loss(out_r, y.double()).backward()
+    m = Model(model=model, num_epochs=2, topography="all")
+    xd = x.to(DEV).requires_grad_(True)
+    F.mse_loss(m.pre_to_post_generator(xd), y.to(DEV)).backward()
+    skip = OC.cyclegan_cancelled_biases() if model == "cyclegan" else O.cancelled_biases()[0]
+    eg = _worst([(k, nrel(p.grad, Gd[k].grad)) for k, p in m.pre_to_post_generator.named_parameters()
+                 if k not in skip])
+    e_x = nrel(xd.grad, xr.grad)
+    report("cycle_input_grad_512", model=model, input_grad=e_x, worst_G=eg)
+    assert e_x < 1e-4 and eg[1] < 1e-4, (e_x, eg)
+
+
+# ---------------------------------------------------------------------------------------------- kernels
+
+@pytest.mark.parametrize("cap", [2, 3, 7])
+@pytest.mark.parametrize("cfg,case", [(4, (256, 256, 3, 1, 1, "reflect", 20)), (6, (256, 128, 3, 1, 1, "reflect", 19)),
+                                      (9, (128, 64, 3, 1, 1, "constant", 21)), (1, (128, 256, 4, 2, 1, "constant", 22))])
+def test_conv_f3_tile_stream(cfg, case, cap):
+    """conv_fwd_f3 with at most `cap` persistent workgroups: every workgroup streams many tiles back to
+    back (next tile's k-stages issued during the current tile's last stages and epilogue, setup_issue()
+    mid-stream, ragged last tiles) -- the path the bench's 512x512 batch-8 resblock convs take."""
+    from floodgan import _lib as L, ops, plans as PL
+    from floodgan.plans import Buf
+    cin, cout, k, s, p, mode, H = case
+    prev = L.get_conv_math()
+    L.set_conv_math("f16x3")
+    try:
+        L.set_f3_tile(cfg)
+        L.load().fg_set_f3_persistent(cap)
+        torch.manual_seed(cap + cfg)
+        x = torch.randn(3, cin, H, H, dtype=torch.float64)
+        w = torch.randn(cout, cin, k, k, dtype=torch.float64) * 0.05
+        b = torch.randn(cout, dtype=torch.float64)
+        xin = F.pad(x, (p,) * 4, mode=mode) if p else x
+        y = F.conv2d(xin, w, b, stride=s)
+        X = buf_from(x, p, mode)
+        wd = w.float().to(DEV)
+        mm = PL.wmap_conv_fwd(wd.shape, X.c)
+        Ho = PL.out_size(H, k, s, p)
+        Y = Buf.empty(3, Ho, Ho, cout, 0, DEV)
+        ops.conv([PL.conv_problem(X, p, k, s, ops.pack_weight(wd, mm), mm, Y, bias=b.float().to(DEV))])
+        torch.cuda.synchronize()
+        assert nrel(nchw(Y), y) < KTOL
+        # a 4-problem launch (ConvTranspose2d phases) crossing problem boundaries mid-stream
+        if cin >= 128 and s == 1:
+            wt = torch.randn(cin, cout // 2, 3, 3, dtype=torch.float64) * 0.05
+            yt = F.conv_transpose2d(x, wt, None, stride=2, padding=1, output_padding=1)
+            XT = buf_from(x, 1, "constant")
+            wtd = wt.float().to(DEV)
+            maps = PL.phase_maps(wtd.shape, 3, 1, XT.c)
+            YT = Buf.empty(3, 2 * H, 2 * H, cout // 2, 0, DEV)
+            ops.conv(PL.phase_problems(XT, wtd.shape, 3, 1, YT, [ops.pack_weight(wtd, q) for q, _, _ in maps], maps))
+            torch.cuda.synchronize()
+            assert nrel(nchw(YT), yt) < KTOL
+    finally:
+        L.set_f3_tile(-1)
+        L.load().fg_set_f3_persistent(1)
+        L.set_conv_math(prev)
+
+
+def _log_uniform(shape, lo=-12, hi=0, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    mag = 10 ** (torch.rand(shape, generator=g, dtype=torch.float64) * (hi - lo) + lo)
+    sign = torch.where(torch.rand(shape, generator=g) < 0.5, -1.0, 1.0).double()
+    return mag * sign
+
+
+@pytest.mark.parametrize("case", ["log_uniform", "sample_disparity"])
+def test_f16x3_dynamic_range(case, report):
+    """f16x3 (per-tensor power-of-two scale, two fp16 pieces) on operands with a heavy dynamic range
+    vs fp64 and vs the exact-fp32 MFMA path: 'log_uniform' -- activations and gradients log-uniform
+    over 1e-12..1 within one tensor; 'sample_disparity' -- one image of the batch 1e-5 x smaller than
+    the other (its elements sit 2^-17 below the tensor's scale)."""
+    from floodgan import _lib as L, ops, plans as PL
+    from floodgan.plans import Buf
+    cin, cout, H = 256, 256, 12
+    if case == "log_uniform":
+        x = _log_uniform((2, cin, H, H), seed=1)
+        gy = _log_uniform((2, cout, H, H), seed=2)
+    else:
+        torch.manual_seed(3)
+        x = torch.randn(2, cin, H, H, dtype=torch.float64)
+        x[1] *= 1e-5
+        gy = torch.randn(2, cout, H, H, dtype=torch.float64)
+        gy[0] *= 1e-5
+    torch.manual_seed(4)
+    w = torch.randn(cout, cin, 3, 3, dtype=torch.float64) * 0.05
+    y_ref = F.conv2d(F.pad(x, (1,) * 4, mode="reflect"), w)
+    gw_ref = torch.nn.grad.conv2d_weight(F.pad(x, (1,) * 4, mode="reflect"), w.shape, gy)
+    prev = L.get_conv_math()
+    res = {}
+    try:
+        for math in ("fp32", "f16x3"):
+            L.set_conv_math(math)
+            X = buf_from(x, 1, "reflect")
+            wd = w.float().to(DEV)
+            mm = PL.wmap_conv_fwd(wd.shape, X.c)
+            Y = Buf.empty(2, H, H, cout, 0, DEV)
+            ops.conv([PL.conv_problem(X, 1, 3, 1, ops.pack_weight(wd, mm), mm, Y)])
+            GY = buf_from(gy, 0, "constant")
+            dw = torch.empty(wd.shape, dtype=torch.float32, device=DEV)
+            ops.wgrad(PL.wgrad_conv(GY, X, 1, 3, 1, cout), PL.wmap_wgrad(wd.shape, True, X.c, 3), dw)
+            torch.cuda.synchronize()
+            yo = nchw(Y)
+            res[math] = dict(fwd=nrel(yo, y_ref), fwd_per_image=[nrel(yo[i], y_ref[i]) for i in range(2)],
+                             wgrad=nrel(dw, gw_ref))
+    finally:
+        L.set_conv_math(prev)
+    report("f16x3_dynamic_range", case=case, **res)
+    f3, f32 = res["f16x3"], res["fp32"]
+    assert f3["fwd"] < KTOL and f3["wgrad"] < KTOL, res
+    # per image: no worse than 1e-5, or than 4x the exact-fp32 path where that is itself above it
+    for a, b in zip(f3["fwd_per_image"], f32["fwd_per_image"]):
+        assert a < max(KTOL, 4 * b), res
