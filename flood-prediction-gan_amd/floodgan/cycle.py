@@ -79,6 +79,10 @@ class CycleStep:
         self.dflat = FlatGrads(dnamed, db)
         self.pre_pool, self.post_pool = ImagePool(rng=pool_rng), ImagePool(rng=pool_rng)
         self.last = {}
+        # test instrumentation: when True, each call stores every network pass's activation decisions
+        # in self.decisions, keyed like the oracle's networks, each list in that network's call order
+        self.record_decisions = False
+        self.decisions = None
 
     @staticmethod
     def _grads(params):
@@ -109,12 +113,18 @@ class CycleStep:
         ops.l1(rq, x[:, :3], 10.0 * inv, losses[2:3], g_rq)
         g_rp = torch.empty_like(g_rq)
         ops.l1(rp, y, 10.0 * inv, losses[3:4], g_rp)
+        rec = None
+        if self.record_decisions:
+            rec = {"pre_to_post": [X.gen_act_decisions(S_a), X.gen_act_decisions(S_c)],
+                   "post_to_pre": [X.gen_act_decisions(S_b), X.gen_act_decisions(S_d)], "pre_d": [], "post_d": []}
         preds = []
-        for params, img, slot in ((self.dpost, sp, 0), (self.dpre, spre, 1)):
+        for params, img, slot, net in ((self.dpost, sp, 0, "post_d"), (self.dpre, spre, 1, "pre_d")):
             pred, dS = X.disc_forward(params, X.disc_pack([(img, cond)], C), save=True)
             g_pred = torch.empty_like(pred)
             ops.mse_const(pred, 1.0, inv, losses[slot:slot + 1], g_pred)
             preds.append((params, dS, g_pred))
+            if rec is not None:
+                rec[net].append(X.disc_act_decisions(dS))
         # ---- generator backward: second round first; its input gradient, plus the frozen
         # discriminator's, is d/d(first-round output).  A generator's gradient buckets are complete
         # (and start their all-reduce) in its last backward of the iteration.
@@ -142,6 +152,8 @@ class CycleStep:
             for params, grads, a, b, target, slot, tag in ((self.g1, g1g, y, cond, y, 8, "g1"),
                                                            (self.g2, g2g, x, None, x[:, :3], 9, "g2")):
                 out, _, S_i = X.gen_forward(params, a, x_extra=b)
+                if rec is not None:
+                    rec["pre_to_post" if tag == "g1" else "post_to_pre"].append(X.gen_act_decisions(S_i))
                 g_i = torch.empty_like(g_rq)
                 ops.l1(out, target, 5.0 * inv, losses[slot:slot + 1], g_i)
                 X.gen_backward(params, S_i, g_i, grads_into=grads, accumulate=True, ready=ready(self.gflat, tag))
@@ -155,6 +167,8 @@ class CycleStep:
         for params, real, real_extra, syn, syn_extra, slots, tag in (
                 (self.dpre, x, None, spre_b, cq, (4, 6), "dpre"), (self.dpost, y, cond, sp_b, cp, (5, 7), "dpost")):
             pred, dS = X.disc_forward(params, X.disc_pack([(real, real_extra), (syn, syn_extra)], C), save=True)
+            if rec is not None:
+                rec[tag[1:] + "_d"] += [X.disc_act_decisions(dS, 0, N), X.disc_act_decisions(dS, N)]
             g_pred = torch.empty_like(pred)
             ops.mse_const(pred[:N], 1.0, 0.5 * inv, losses[slots[0]:slots[0] + 1], g_pred[:N])
             ops.mse_const(pred[N:], 0.0, 0.5 * inv, losses[slots[1]:slots[1] + 1], g_pred[N:])
@@ -163,6 +177,7 @@ class CycleStep:
             del dS
         self.dflat.finish()
         self.opt_d.step()
+        self.decisions = rec
         self.last = dict(synthetic_post=sp, synthetic_pre=spre, mask_pre_to_post=mask_p, mask_post_to_pre=mask_q,
                          recreated_post=rp, recreated_pre=rq)
         n = 10 if self.identity else 8

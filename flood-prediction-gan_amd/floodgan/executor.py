@@ -340,6 +340,29 @@ def gen_backward(P, S, g_out, grads_into=None, ready=None, input_grad=None, accu
     return G.out
 
 
+def _decided(B, lo=0, hi=None):
+    """activation decisions of an activation-output Buf (output > 0 <=> input > 0 for ReLU and
+    LeakyReLU): NCHW bool on the host"""
+    return (B.interior()[lo:hi] > 0).permute(0, 3, 1, 2).contiguous().cpu()
+
+
+def gen_act_decisions(S):
+    """The generator's ReLU decisions in a saved forward, keyed by the oracle's layer names (test
+    instrumentation: oracle ActDecisions teacher-forces them to compare gradients at full size)."""
+    out = {"conv1": _decided(S["a1"]), "conv2": _decided(S["a2"]), "conv3": _decided(S["blocks"][0]["h"])}
+    for i, b in enumerate(S["blocks"]):
+        out[f"block{i}"] = _decided(b["rb"])
+    for tag, hd in S["heads"].items():
+        out[f"deconv1_{tag}"], out[f"deconv2_{tag}"] = _decided(hd["ad1"]), _decided(hd["ad2"])
+    return out
+
+
+def disc_act_decisions(S, lo=0, hi=None):
+    """The discriminator's LeakyReLU decisions for images lo..hi of a saved forward (test instrumentation)"""
+    return {"model.0": _decided(S["e0"], lo, hi), "model.2": _decided(S["a1"], lo, hi),
+            "model.5": _decided(S["a2"], lo, hi), "model.8": _decided(S["a3"], lo, hi)}
+
+
 # ======================================================================================
 # discriminator
 # ======================================================================================

@@ -42,6 +42,10 @@ class PairedStep:
         self.group = group
         self.last_mask = None
         self.last_output = None
+        # test instrumentation: when True, each call stores the activation decisions of its three
+        # networks' passes in self.decisions ({"G": [...], "D": [fake, real, G-step]}, oracle order)
+        self.record_decisions = False
+        self.decisions = None
 
     def __call__(self, x, y):
         ws, _ = world()
@@ -60,6 +64,8 @@ class PairedStep:
         g_pred = torch.empty_like(pred)
         ops.mse_const(pred[:N], 0.0, 0.5 * inv, losses[1:2], g_pred[:N])
         ops.mse_const(pred[N:], 1.0, 0.5 * inv, losses[0:1], g_pred[N:])
+        rec = {"G": [X.gen_act_decisions(gS)], "D": [X.disc_act_decisions(dS, 0, N), X.disc_act_decisions(dS, N)]} \
+            if self.record_decisions else None
         self.dflat.begin(self.group)
         X.disc_backward(self.dp, dS, g_pred, param_grads=True, grads_into=self._grads(self.dp),
                         ready=self.dflat.ready)
@@ -75,6 +81,9 @@ class PairedStep:
         ops.l1(fake, y, 100.0 * inv, losses[3:4], g_fake)
         X.disc_backward(self.dp, dS, g_pred, param_grads=False, input_grad=g_fake, input_grad_channels=(C, 3),
                         input_grad_accumulate=True)
+        if rec is not None:
+            rec["D"].append(X.disc_act_decisions(dS))
+            self.decisions = rec
         del dS, dinp
         self.gflat.begin(self.group)
         X.gen_backward(self.gp, gS, g_fake, grads_into=self._grads(self.gp), ready=self.gflat.ready)

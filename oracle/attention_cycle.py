@@ -27,7 +27,7 @@ from collections import OrderedDict
 import torch
 import torch.nn.functional as F
 
-from .paired_attention import (_construct, _initialise, discriminator_forward, discriminator_layout,
+from .paired_attention import (_act, _construct, _forced, _initialise, discriminator_forward, discriminator_layout,
                                generator_forward, generator_layout)
 
 NETS = ("pre_to_post", "post_to_pre", "pre_d", "post_d")
@@ -51,23 +51,24 @@ def _in(x):
     return F.instance_norm(x, eps=1e-5)
 
 
-def cyclegan_generator_forward(P, x):
-    """models/model_architectures.py:95-120 (CycleGANBlock.forward :132-134)."""
+def cyclegan_generator_forward(P, x, forced=None):
+    """models/model_architectures.py:95-120 (CycleGANBlock.forward :132-134).  forced: teacher-forced
+    ReLU decisions keyed by the executor's layer names (conv1..3, block<i>, deconv1/2_content)."""
     def conv(name, h, stride=1, padding=0):
         return F.conv2d(h, P[name + ".weight"], P[name + ".bias"], stride=stride, padding=padding)
 
     def convT(name, h):
         return F.conv_transpose2d(h, P[name + ".weight"], P[name + ".bias"], stride=2, padding=1, output_padding=1)
 
-    h = F.relu(_in(conv("model.1", F.pad(x, (3, 3, 3, 3), mode="reflect"))))
-    h = F.relu(_in(conv("model.4", h, 2, 1)))
-    h = F.relu(_in(conv("model.7", h, 2, 1)))
+    h = _act(_in(conv("model.1", F.pad(x, (3, 3, 3, 3), mode="reflect"))), 0, "conv1", forced)
+    h = _act(_in(conv("model.4", h, 2, 1)), 0, "conv2", forced)
+    h = _act(_in(conv("model.7", h, 2, 1)), 0, "conv3", forced)
     for i in range(9):
         pre = f"model.{10 + i}.conv_block."
-        r = F.relu(_in(conv(pre + "1", F.pad(h, (1, 1, 1, 1), mode="reflect"))))
+        r = _act(_in(conv(pre + "1", F.pad(h, (1, 1, 1, 1), mode="reflect"))), 0, f"block{i}", forced)
         h = h + _in(conv(pre + "5", F.pad(r, (1, 1, 1, 1), mode="reflect")))
-    h = F.relu(_in(convT("model.19", h)))
-    h = F.relu(_in(convT("model.22", h)))
+    h = _act(_in(convT("model.19", h)), 0, "deconv1_content", forced)
+    h = _act(_in(convT("model.22", h)), 0, "deconv2_content", forced)
     return torch.tanh(conv("model.26", F.pad(h, (3, 3, 3, 3), mode="reflect")))
 
 
@@ -125,16 +126,21 @@ class CycleStepOracle:
                 g["lr"] = lr
 
     def _g(self, name, x):
+        f = _forced(self._dec, name)
         if self.model == "cyclegan":
-            return cyclegan_generator_forward(self.P[name], x)
-        return generator_forward(self.P[name], x)[0]
+            return cyclegan_generator_forward(self.P[name], x, f)
+        return generator_forward(self.P[name], x, f)[0]
 
     def _d(self, name, x):
-        return discriminator_forward(self.P[name], x)
+        return discriminator_forward(self.P[name], x, _forced(self._dec, name))
 
-    def step(self, input_stack, output_image, record=None):
+    _dec = None
+
+    def step(self, input_stack, output_image, record=None, decisions=None):
         """One iteration; returns the losses in the reference's `losses` dict order
-        (models/model.py:189-199, appended at :741-752)."""
+        (models/model.py:189-199, appended at :741-752).  decisions (tests only): ActDecisions keyed
+        by network name (NETS), each queue in that network's call order."""
+        self._dec = decisions
         real_pre = input_stack.to(self.dtype)
         conditions = real_pre[:, 3:].detach().clone()
         real_post = torch.cat((output_image.to(self.dtype), conditions), 1)
@@ -185,6 +191,7 @@ class CycleStepOracle:
             record["d_grads"] = {n: OrderedDict((k, v.grad.detach().clone()) for k, v in self.P[n].items())
                                  for n in ("pre_d", "post_d")}
         self.opt_d.step()
+        self._dec = None
         out = [g_post, g_pre, cyc_pre, cyc_post, d_pre_real, d_post_real, d_pre_syn, d_post_syn]
         if self.identity:
             out += [id_post, id_pre]

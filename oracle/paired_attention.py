@@ -21,6 +21,7 @@ tests/golden/make_golden.py produced by running the reference's own, unmodified
 Parameters are held in a plain ordered dict `name -> tensor` whose keys, shapes and order
 are exactly the reference modules' `state_dict()` keys.
 """
+import copy
 import math
 from collections import OrderedDict
 
@@ -104,6 +105,53 @@ def _in(x):
     return F.instance_norm(x, eps=EPS_IN)
 
 
+class ActDecisions:
+    """Teacher-forced activation decisions (tests only).  A ReLU / LeakyReLU whose input sits within
+    rounding of 0 can be decided differently by any two fp32 evaluations, and one such flip moves
+    the gradients of a whole network by ~1/sqrt(pixels x channels) of their norm.
+    To compare gradients at full size, the oracle can take the implementation's decisions:
+    `masks` = {network: [ {layer: bool tensor NCHW}, ... one per call of that network in call
+    order ]}.  Each forced layer logs (network, layer, disagreements, max |pre-activation| / rms
+    of the layer over the disagreements): the caller asserts that every disagreement is at the kink."""
+
+    def __init__(self, masks):
+        self.queues = {k: list(v) for k, v in masks.items()}
+        self.log = []
+
+    def take(self, net):
+        q = self.queues.get(net)
+        return (q.pop(0), net) if q else None
+
+    def worst(self):
+        """largest normalized |pre-activation| at which a decision differed (0 if none)"""
+        return max([w for _, _, n, w in self.log if n] or [0.0])
+
+
+def _act(h, slope, name, forced):
+    """ReLU (slope 0) / LeakyReLU(slope), or the teacher-forced decision of `forced` = (masks, net, log)"""
+    if forced is None or name not in forced[0]:
+        return F.relu(h) if slope == 0 else F.leaky_relu(h, slope)
+    masks, net, log = forced
+    # contiguous NCHW: a channels-last-strided mask makes torch.where's output channels-last, and
+    # that memory format propagating through the fp64 CPU graph changed its backward (forward
+    # bit-identical, weight gradients off by O(1): tests/test_oracle_decisions_cpu.py guards this)
+    m = masks[name].to(h.device).contiguous()
+    hd = h.detach()
+    dis = (hd > 0) != m
+    n = int(dis.sum())
+    rms = float(hd.pow(2).mean().sqrt()) or 1.0
+    log.append((net, name, n, float(hd[dis].abs().max()) / rms if n else 0.0))
+    return torch.where(m, h, h * slope)
+
+
+def _forced(decisions, net):
+    """(masks, net, log) for the next call of `net`, or None"""
+    if decisions is None:
+        return None
+    t = decisions.take(net)
+    return None if t is None else (t[0], t[1], decisions.log)
+
+
 def _conv(P, name, x, stride=1, padding=0):
     return F.conv2d(x, P[name + ".weight"], P[name + ".bias"], stride=stride, padding=padding)
 
@@ -114,26 +162,27 @@ def _convT(P, name, x):
                               output_padding=1)
 
 
-def resnet_block(P, i, x):
+def resnet_block(P, i, x, forced=None):
     """models/model_architectures.py:412-418."""
     pre = f"resnet_blocks.{i}."
-    h = F.relu(_in(_conv(P, pre + "conv1", F.pad(x, (1, 1, 1, 1), mode="reflect"))))
+    h = _act(_in(_conv(P, pre + "conv1", F.pad(x, (1, 1, 1, 1), mode="reflect"))), 0, f"block{i}", forced)
     h = _in(_conv(P, pre + "conv2", F.pad(h, (1, 1, 1, 1), mode="reflect")))
     return x + h
 
 
-def generator_forward(P, x):
-    """models/model_architectures.py:339-400. Returns (output [N,3,H,W], mask [N,H,W])."""
-    h = F.relu(_in(_conv(P, "conv1", F.pad(x, (3, 3, 3, 3), mode="reflect"))))
-    h = F.relu(_in(_conv(P, "conv2", h, stride=2, padding=1)))
-    h = F.relu(_in(_conv(P, "conv3", h, stride=2, padding=1)))
+def generator_forward(P, x, forced=None):
+    """models/model_architectures.py:339-400. Returns (output [N,3,H,W], mask [N,H,W]).
+    forced: teacher-forced ReLU decisions (ActDecisions / _forced), tests only."""
+    h = _act(_in(_conv(P, "conv1", F.pad(x, (3, 3, 3, 3), mode="reflect"))), 0, "conv1", forced)
+    h = _act(_in(_conv(P, "conv2", h, stride=2, padding=1)), 0, "conv2", forced)
+    h = _act(_in(_conv(P, "conv3", h, stride=2, padding=1)), 0, "conv3", forced)
     for i in range(9):
-        h = resnet_block(P, i, h)
-    c = F.relu(_in(_convT(P, "deconv1_content", h)))
-    c = F.relu(_in(_convT(P, "deconv2_content", c)))
+        h = resnet_block(P, i, h, forced)
+    c = _act(_in(_convT(P, "deconv1_content", h)), 0, "deconv1_content", forced)
+    c = _act(_in(_convT(P, "deconv2_content", c)), 0, "deconv2_content", forced)
     content = torch.tanh(_conv(P, "deconv3_content", F.pad(c, (3, 3, 3, 3), mode="reflect")))
-    a = F.relu(_in(_convT(P, "deconv1_attention", h)))
-    a = F.relu(_in(_convT(P, "deconv2_attention", a)))
+    a = _act(_in(_convT(P, "deconv1_attention", h)), 0, "deconv1_attention", forced)
+    a = _act(_in(_convT(P, "deconv2_attention", a)), 0, "deconv2_attention", forced)
     att = torch.softmax(_conv(P, "deconv3_attention", a), dim=1)
     # composite: sum_{i<9} content[3i:3i+3] * att[i]  +  input[:, :3] * att[9]   (:371-399)
     # (summed left to right in the reference's order: output1 + ... + output9 + output10)
@@ -144,12 +193,12 @@ def generator_forward(P, x):
     return out, att[:, 9]
 
 
-def discriminator_forward(P, x):
+def discriminator_forward(P, x, forced=None):
     """models/model_architectures.py:424-441 (LeakyReLU 0.2 after every conv but the last)."""
-    h = F.leaky_relu(_conv(P, "model.0", x, 2, 1), 0.2)
-    h = F.leaky_relu(_in(_conv(P, "model.2", h, 2, 1)), 0.2)
-    h = F.leaky_relu(_in(_conv(P, "model.5", h, 2, 1)), 0.2)
-    h = F.leaky_relu(_in(_conv(P, "model.8", h, 1, 1)), 0.2)
+    h = _act(_conv(P, "model.0", x, 2, 1), 0.2, "model.0", forced)
+    h = _act(_in(_conv(P, "model.2", h, 2, 1)), 0.2, "model.2", forced)
+    h = _act(_in(_conv(P, "model.5", h, 2, 1)), 0.2, "model.5", forced)
+    h = _act(_in(_conv(P, "model.8", h, 1, 1)), 0.2, "model.8", forced)
     return _conv(P, "model.11", h, 1, 1)
 
 
@@ -188,27 +237,31 @@ class PairedStepOracle:
             for P, src in ((self.G, G), (self.D, D)):
                 for k, v in P.items():
                     v.copy_(src[k].detach().to(v.device, v.dtype))
+        # deep copies: a state_dict holds the optimiser's LIVE tensors (its CPU 'step' counter is
+        # shared and would keep counting with the implementation's own steps)
         if opt_g_state is not None:
-            self.opt_g.load_state_dict(opt_g_state)
+            self.opt_g.load_state_dict(copy.deepcopy(opt_g_state))
         if opt_d_state is not None:
-            self.opt_d.load_state_dict(opt_d_state)
+            self.opt_d.load_state_dict(copy.deepcopy(opt_d_state))
 
-    def step(self, x, y, record=None, d_after=None):
+    def step(self, x, y, record=None, d_after=None, decisions=None):
         """One iteration of models/model.py:615-646. Returns the four losses (D real,
         D synthetic, G synthetic, raw L1 before x100) as floats.
         d_after (teacher forcing, tests only): discriminator parameters to continue the G step
         with instead of this oracle's own Adam(D) result, so that the G half is compared on the
-        same D as the implementation under test."""
+        same D as the implementation under test.
+        decisions (tests only): ActDecisions with networks "G" (one call) and "D" (three calls:
+        synthetic and real of the D step, synthetic of the G step)."""
         x, y = x.to(self.dtype), y.to(self.dtype)
-        fake, mask = generator_forward(self.G, x)
+        fake, mask = generator_forward(self.G, x, _forced(decisions, "G"))
         cat_real = torch.cat((x, y), 1)
         cat_fake = torch.cat((x, fake), 1)
         for p in self.D.values():
             p.requires_grad_(True)
         self.opt_d.zero_grad()
-        pred_fake = discriminator_forward(self.D, cat_fake.detach())
+        pred_fake = discriminator_forward(self.D, cat_fake.detach(), _forced(decisions, "D"))
         l_d_fake = F.mse_loss(pred_fake, torch.zeros_like(pred_fake))
-        pred_real = discriminator_forward(self.D, cat_real)
+        pred_real = discriminator_forward(self.D, cat_real, _forced(decisions, "D"))
         l_d_real = F.mse_loss(pred_real, torch.ones_like(pred_real))
         l_d = (l_d_fake + l_d_real) * 0.5
         l_d.backward()
@@ -224,7 +277,7 @@ class PairedStepOracle:
         for p in self.D.values():
             p.requires_grad_(False)
         self.opt_g.zero_grad()
-        pred = discriminator_forward(self.D, cat_fake)
+        pred = discriminator_forward(self.D, cat_fake, _forced(decisions, "D"))
         l_g = F.mse_loss(pred, torch.ones_like(pred))
         l1 = F.l1_loss(fake, y)
         (l_g + l1 * 100).backward()

@@ -30,6 +30,12 @@ def nets(m, kind):
                                        "post_discriminator")}
 
 
+def grads(m, kind):
+    """the (all-reduced) gradients the last iteration's optimiser steps used"""
+    return {f"{net}/{k}": p.grad.detach().cpu().clone() for net, mod in nets(m, kind).items()
+            for k, p in mod.named_parameters()}
+
+
 def make_model(kind):
     from floodgan.model import Model
     name = {"paired": "PairedAttention", "attentiongan": "AttentionGAN", "cyclegan": "CycleGAN"}[kind]
@@ -44,6 +50,9 @@ def run(m, kind, x, y, iters):
 def main():
     out, kind, n, res, iters = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5])
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    if os.environ.get("FLOODGAN_CONV_MATH"):
+        from floodgan import _lib
+        _lib.load()             # applies FLOODGAN_CONV_MATH
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{os.environ['MASTER_PORT']}", rank=rank,
                             world_size=world)
     from floodgan.parallel import broadcast_params, shard_batch
@@ -56,10 +65,12 @@ def main():
         import random
         for pool in (m.cycle_step_fn.pre_pool, m.cycle_step_fn.post_pool):
             pool.rng = random.Random(5)
-    losses = run(m, kind, xs, ys, iters)
+    losses = run(m, kind, xs, ys, 1)
+    grads0 = grads(m, kind)
+    losses += run(m, kind, xs, ys, iters - 1)
     torch.cuda.synchronize()
     state = {f"{net}/{k}": v.detach().cpu() for net, mod in nets(m, kind).items() for k, v in mod.state_dict().items()}
-    torch.save({"losses": torch.stack(losses), "state": state}, f"{out}.rank{rank}")
+    torch.save({"losses": torch.stack(losses), "state": state, "grads0": grads0}, f"{out}.rank{rank}")
     dist.barrier()
     dist.destroy_process_group()
 

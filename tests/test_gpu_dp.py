@@ -7,7 +7,14 @@ losses (equal shards, mean losses), and the parameters after two iterations agre
 
 What this pins: the 1/world pre-scaling folded into the loss gradients (model.py PairedStep,
 cycle.py CycleStep), the bucket layout and the ready() order of the executors' backward, and the
-asynchronous all-reduces racing the remaining backward kernels."""
+asynchronous all-reduces racing the remaining backward kernels.
+
+Both sides run the exact-fp32 conv math (FLOODGAN_CONV_MATH=fp32): every output element's
+accumulation order is then independent of the batch it sits in, so each rank's per-sample forward is
+bit-identical to the single process's and the only difference left is the order in which the
+all-reduce adds the two shards' gradient partial sums.  (Under f16x3 the per-tensor operand scale of a
+half batch can differ from the whole batch's by a power of two: rounding-level differences that flip
+ReLU kinks -- the same chaos the single-device tests handle by teacher-forcing decisions.)"""
 import os
 import socket
 import subprocess
@@ -46,7 +53,7 @@ def test_two_rank_step_equals_single_rank(kind, n, res, tmp_path, report):
     out = str(tmp_path / "dp")
     port = _free_port()
     env = dict(os.environ, WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
-               OMP_NUM_THREADS="2")
+               OMP_NUM_THREADS="2", FLOODGAN_CONV_MATH="fp32")
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dp_worker.py"), out, kind, str(n), str(res),
                                str(iters)], env=dict(env, RANK=str(r), LOCAL_RANK=str(r)))
              for r in range(2)]
@@ -59,13 +66,21 @@ def test_two_rank_step_equals_single_rank(kind, n, res, tmp_path, report):
     assert rcs == [0, 0], rcs
     ranks = [torch.load(f"{out}.rank{r}", weights_only=True) for r in range(2)]
     # single process, whole batch
-    m = W.make_model(kind)
-    if kind != "paired":
-        import random
-        for pool in (m.cycle_step_fn.pre_pool, m.cycle_step_fn.post_pool):
-            pool.rng = random.Random(5)
-    x, y = W.global_batch(kind, n, res)
-    single = torch.stack(W.run(m, kind, x, y, iters)).double()
+    from floodgan import _lib as L
+    prev = L.get_conv_math()
+    L.set_conv_math("fp32")
+    try:
+        m = W.make_model(kind)
+        if kind != "paired":
+            import random
+            for pool in (m.cycle_step_fn.pre_pool, m.cycle_step_fn.post_pool):
+                pool.rng = random.Random(5)
+        x, y = W.global_batch(kind, n, res)
+        single = W.run(m, kind, x, y, 1)
+        grads0 = W.grads(m, kind)
+        single = torch.stack(single + W.run(m, kind, x, y, iters - 1)).double()
+    finally:
+        L.set_conv_math(prev)
     mean = (ranks[0]["losses"].double() + ranks[1]["losses"].double()) / 2
     lrel = ((mean - single).abs() / single.abs()).numpy()
     if kind == "paired":
@@ -74,6 +89,14 @@ def test_two_rank_step_equals_single_rank(kind, n, res, tmp_path, report):
         skip = {k: (O.cancelled_biases()[0] if "generator" in k else O.cancelled_biases()[1])
                 for k in W.nets(m, kind)}
     worst, same = ("", 0.0), True
+    # the all-reduced iteration-0 gradients equal the whole-batch gradients up to summation order;
+    # the paired G step already sees Adam(D), whose elements with rounding-level gradients (undecided
+    # directions) may move differently: 1e-4 there, 1e-5 for every gradient of pre-update state
+    errs = [(k, nrel(ranks[0]["grads0"][k], v)) for k, v in grads0.items()
+            if k.split("/", 1)[1] not in skip[k.split("/", 1)[0]]]
+    post = [e for e in errs if kind == "paired" and e[0].startswith("generator/")]
+    gworst = max([e for e in errs if e not in post], key=lambda t: t[1])
+    gworst_post = max(post, key=lambda t: t[1]) if post else ("", 0.0)
     for net, mod in W.nets(m, kind).items():
         for k, v in mod.state_dict().items():
             a, b = ranks[0]["state"][f"{net}/{k}"], ranks[1]["state"][f"{net}/{k}"]
@@ -84,11 +107,13 @@ def test_two_rank_step_equals_single_rank(kind, n, res, tmp_path, report):
             if e > worst[1]:
                 worst = (f"{net}/{k}", e)
     report("dp_two_rank_vs_single", kind=kind, n=n, res=res, loss_rel=lrel.tolist(), worst_param=worst,
-           replicas_identical=bool(same))
+           worst_grad_it0=gworst, worst_grad_it0_after_adam_d=gworst_post, replicas_identical=bool(same))
     assert same
+    assert gworst[1] < 1e-5 and gworst_post[1] < 1e-4, (gworst, gworst_post)
     # iteration 0: the losses evaluated before any update agree to rounding (in the paired step the
     # G loss [2] already sees Adam(D): P3 like everything after an update)
     pre = [0, 1, 3] if kind == "paired" else list(range(lrel.shape[1]))
     assert lrel[0][pre].max() < 1e-5, lrel
-    # after updates: within the P3 bound of the single-device parity tests
+    # after updates: the iteration-0 gradients agree to summation order (above), so only elements whose
+    # gradient is at rounding level can take a different Adam direction -- the P3 bound
     assert lrel.max() < 1e-3 and worst[1] < 1e-3, (lrel, worst)
