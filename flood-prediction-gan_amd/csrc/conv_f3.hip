@@ -289,6 +289,15 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
     auto compute = [&](int buf, const f32x4 (&va)[TM][2]) {
         const char* sbuf = smem + buf * STAGE;
         f16x8 ah[TM], al[TM];
+#ifdef FG_F3_DIAG
+        if ((alt_order >> 6) & 1) {                      // diag bit 2: no split (A bits reinterpreted)
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm) {
+                ah[tm] = __builtin_bit_cast(f16x8, va[tm][0]);
+                al[tm] = __builtin_bit_cast(f16x8, va[tm][1]);
+            }
+        } else
+#endif
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm) {
             const float v[8] = {va[tm][0][0], va[tm][0][1], va[tm][0][2], va[tm][0][3],

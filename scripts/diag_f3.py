@@ -27,11 +27,12 @@ def main():
         prob = mk(True)
         res = {}
         for _ in range(3):
-            for mode in (0, 1, 2):
+            for mode in (0, 1, 2, 4, 5):
                 os.environ["FG_F3_DIAG"] = str(mode)
                 res.setdefault(mode, []).append(time_it(lambda: ops.conv([prob])))
         os.environ["FG_F3_DIAG"] = "0"
-        for mode, tag in ((0, "full"), (1, "compute only"), (2, "data movement only")):
+        for mode, tag in ((0, "full"), (1, "compute only"), (2, "data movement only"), (4, "no A split"),
+                          (5, "compute only, no A split")):
             ms = min(res[mode])
             print(f"{name:36s} {tag:20s} {ms:8.3f} ms {flops / ms / 1e9:7.1f} TFLOP/s", flush=True)
 

@@ -188,8 +188,13 @@ def _update_agreement(p0, p_hip, p_ref, g_hip, g_ref, m_ref):
     the decided elements, fraction decided, norm-relative error of the whole updated tensor)"""
     d_hip = (p_hip.double().cpu() - p0.double().cpu()).flatten()
     d_ref = (p_ref.double().cpu() - p0.double().cpu()).flatten()
-    sigma = float((g_hip.double().cpu() - g_ref.double().cpu()).pow(2).mean().sqrt())
-    dec = m_ref.double().cpu().flatten().abs() > 10 * (1 - BETA1) * sigma + 1e-30
+    dg = (g_hip.double().cpu() - g_ref.double().cpu()).flatten()
+    sigma = float(dg.pow(2).mean().sqrt())
+    # m_new = beta1*m_old + (1 - beta1)*g with m_old shared, so the direction of an element's update can
+    # only differ if (1 - beta1)*|dg_e| >= |m_e|: decided = |m| above 10x that (and 10x the tensor's rms)
+    dec = m_ref.double().cpu().flatten().abs() > 10 * (1 - BETA1) * torch.clamp(dg.abs(), min=sigma) + 1e-30
+    # and an update the fp32 parameter can hold: |dp| below ~2 ulp of p rounds away in the HIP state
+    dec &= d_ref.abs() > p0.double().cpu().flatten().abs() * 2.0 ** -22
     n = int(dec.sum())
     if n == 0:
         return 1.0, 0.0, 0.0, nrel(p_hip, p_ref)
