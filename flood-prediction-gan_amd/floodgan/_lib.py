@@ -64,6 +64,19 @@ class fg_adam_tensor(C.Structure):
                 ("exp_avg_sq", C.c_void_p), ("numel", C.c_longlong), ("absmax", C.c_void_p)]
 
 
+FG_TILE_MAX_CH = 16
+
+
+class fg_tile_batch(C.Structure):
+    _fields_ = [("src", C.c_void_p), ("tile_stride", C.c_longlong),
+                ("n", C.c_int), ("h_in", C.c_int), ("w_in", C.c_int), ("c_src", C.c_int),
+                ("flip", C.c_void_p), ("c_out", C.c_int), ("chan", C.c_int * FG_TILE_MAX_CH),
+                ("crop", C.c_void_p), ("row_lo", C.c_void_p), ("rows", C.c_int), ("out_h", C.c_int), ("out_w", C.c_int),
+                ("x_idx0", C.c_void_p), ("x_w", C.c_void_p), ("x_taps", C.c_int),
+                ("y_idx0", C.c_void_p), ("y_w", C.c_void_p), ("y_taps", C.c_int),
+                ("tmp", C.c_void_p), ("dst", fg_wview)]
+
+
 # (name, argtypes) of every exported symbol; tests check the library exports all of them
 SIGNATURES = {
     "fg_last_error": [],
@@ -116,6 +129,9 @@ SIGNATURES = {
               C.c_int, C.c_void_p, C.c_void_p],
     "fg_adam_step": [C.POINTER(fg_adam_tensor), C.c_int, C.c_double, C.c_double, C.c_double, C.c_double,
                      C.c_longlong, C.c_void_p],
+    "fg_tiff_probe": [C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)],
+    "fg_tiff_read": [C.c_char_p, C.c_void_p, C.c_longlong],
+    "fg_tile_transform": [C.POINTER(fg_tile_batch), C.c_void_p],
 }
 RESTYPES = {"fg_last_error": C.c_char_p, "fg_in_workspace_doubles": C.c_longlong,
             "fg_channel_sum_workspace_doubles": C.c_longlong}

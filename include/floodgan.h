@@ -343,6 +343,48 @@ typedef struct fg_adam_tensor {
 int fg_adam_step(const fg_adam_tensor* tensors, int count, double lr, double beta1,
                  double beta2, double eps, long long step, hipStream_t stream);
 
+/* ---------------------------------------------------------------------------------------- */
+/* tile data path                                                    */
+/* ---------------------------------------------------------------------------------------- */
+/* Host-side baseline TIFF decode, replacing tifffile.imread (models/data.py:64-68) for the files
+ * tifffile.imsave(..., planarconfig="contig") writes (pre_processing/data_pre_processing.py:377-418):
+ * uncompressed chunky strips, either byte order, uint8 / uint16 / float32 / float64 samples.
+ * fg_tiff_probe: image size, samples per pixel, sample code (100*SampleFormat + bits).
+ * fg_tiff_read: the samples as float32 HWC into HOST memory `dst` (capacity in floats) -- the
+ * loader decodes straight into a pinned staging slot.  Both are synchronous host calls. */
+int fg_tiff_probe(const char* path, int* height, int* width, int* channels, int* sample_code);
+int fg_tiff_read(const char* path, float* dst, long long capacity);
+
+enum { FG_TILE_MAX_CH = 16 };
+/* A batch of staged raw tiles -> model tensors: np.fliplr (models/data.py:63-65), topography
+ * channel selection, Resize(resize, BICUBIC, antialias=True), quadrant crop and Normalize(0.5, 0.5)
+ * (models/utils.py:30-61), over only the crop window of the resized image.  The resize is given as
+ * separable tap tables over the RESIZED image's columns / rows (x_idx0[i] = first source index of
+ * output index i, x_w[i*x_taps + k] its weights; identity tables when no resize). */
+typedef struct fg_tile_batch {
+    const float* src;          /* device: n raw tiles, HWC fp32, h_in x w_in x c_src each            */
+    long long tile_stride;     /* floats from one raw tile to the next                              */
+    int n, h_in, w_in, c_src;
+    const int* flip;           /* device, per tile: 1 = mirror columns (np.fliplr); NULL = none      */
+    int c_out;
+    int chan[FG_TILE_MAX_CH];  /* output channel o <- source channel chan[o]                         */
+    const int* crop;           /* device, per tile: (row0, col0) of the window in the resized image;
+                                  NULL = (0, 0)                                                      */
+    const int* row_lo;         /* device, per tile: first source row the window's row taps read
+                                  (required with crop)                                              */
+    int rows;                  /* source rows per tile the horizontal pass produces, from row_lo     */
+    int out_h, out_w;          /* window size                                                        */
+    const int* x_idx0;
+    const float* x_w;
+    int x_taps;
+    const int* y_idx0;
+    const float* y_w;
+    int y_taps;
+    float* tmp;                /* device workspace: n * rows * out_w * c_out floats                  */
+    fg_wview dst;              /* output [n, c_out, out_h, out_w], any strides                       */
+} fg_tile_batch;
+int fg_tile_transform(const fg_tile_batch* batch, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

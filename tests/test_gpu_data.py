@@ -1,0 +1,142 @@
+"""Tile data path on the GPU: libfloodgan's batch transform and the staged
+TileLoader against the reference's per-item pipeline restated with torch CPU ops -- np.fliplr of the
+decoded HWC tile (models/data.py:63-65), topography channel selection, torchvision Resize(resize,
+BICUBIC, antialias=True) = F.interpolate(mode="bicubic", antialias=True) on the CHW tensor, quadrant
+crop and Normalize(0.5, 0.5) (models/utils.py:30-61).  Tolerance 1e-5 (max abs, values in [-1, 1])."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from tiff_util import write_tiff
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+TOL = 1e-5
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+
+
+def reference_item(x_hwc, y_hwc, flip, topography, resize, crop, crop_index):
+    from floodgan.data import TOPOGRAPHY_SOURCE_CHANNELS, crop_window
+    if flip:
+        x_hwc, y_hwc = np.fliplr(x_hwc).copy(), np.fliplr(y_hwc).copy()
+    x = torch.from_numpy(x_hwc.transpose(2, 0, 1).copy())[TOPOGRAPHY_SOURCE_CHANNELS[topography]]
+    y = torch.from_numpy(y_hwc.transpose(2, 0, 1).copy())
+    if resize:
+        size = (resize, resize) if x.shape[1] == x.shape[2] else None
+        x = F.interpolate(x[None], size=size, mode="bicubic", antialias=True, align_corners=False)[0]
+        y = F.interpolate(y[None], size=size, mode="bicubic", antialias=True, align_corners=False)[0]
+    r0, c0, rs, cs = crop_window(x.shape[1], x.shape[2], crop, crop_index)
+    x, y = x[:, r0:r0 + rs, c0:c0 + cs], y[:, r0:r0 + rs, c0:c0 + cs]
+    return (x - 0.5) / 0.5, (y - 0.5) / 0.5
+
+
+@pytest.mark.parametrize("h,resize,crop", [(96, 64, 4), (40, 64, None), (64, None, 4), (128, 40, 4), (64, 64, None)])
+def test_transform_batch_vs_reference(h, resize, crop):
+    from floodgan.data import TOPOGRAPHY_SOURCE_CHANNELS, crop_window, resized_size, transform_batch
+    rng = np.random.default_rng(h)
+    n = 3
+    xs = rng.random((n, h, h, 9)).astype(np.float32)
+    ys = rng.random((n, h, h, 3)).astype(np.float32)
+    flips, crops = [0, 1, 0], [0, 3, 1]
+    rh, rw = resized_size(h, h, resize)
+    _, _, oh, ow = crop_window(rh, rw, crop, 0)
+    for topo in ("all", "map", None):
+        chan = TOPOGRAPHY_SOURCE_CHANNELS[topo]
+        xo = torch.empty((n, len(chan), oh, ow), device=DEV, memory_format=torch.channels_last)
+        yo = torch.empty((n, 3, oh, ow), device=DEV)
+        f = torch.tensor(flips, dtype=torch.int32, device=DEV)
+        transform_batch(torch.from_numpy(xs).to(DEV), f, crops, chan, resize, crop, xo)
+        transform_batch(torch.from_numpy(ys).to(DEV), f, crops, [0, 1, 2], resize, crop, yo)
+        torch.cuda.synchronize()
+        for k in range(n):
+            rx, ry = reference_item(xs[k], ys[k], flips[k], topo, resize, crop, crops[k])
+            assert float((xo[k].cpu() - rx).abs().max()) < TOL, (topo, k)
+            assert float((yo[k].cpu() - ry).abs().max()) < TOL, (topo, k)
+
+
+def _dataset_dir(root, n_img=7, h=64):
+    """a synthetic dataset in the reference's layout: dataset_input/<image>_<DEM>.tif (9-ch float32),
+    dataset_output/<image>.tif (3-ch float32), metadata/dataset_split.csv"""
+    rng = np.random.default_rng(11)
+    os.makedirs(os.path.join(root, "dataset_input"))
+    os.makedirs(os.path.join(root, "dataset_output"))
+    os.makedirs(os.path.join(root, "metadata"))
+    rows = ["image,best_DEM,same_DEM,version,split,disaster,country"]
+    arrays = {}
+    for i in range(n_img):
+        name = f"hurricane-harvey_{i:08d}"
+        x = rng.random((h, h, 9)).astype(np.float32)
+        y = rng.random((h, h, 3)).astype(np.float32)
+        write_tiff(os.path.join(root, "dataset_input", f"{name}_10m.tif"), x, rows_per_strip=16)
+        write_tiff(os.path.join(root, "dataset_output", f"{name}.tif"), y)
+        arrays[name] = (x, y)
+        rows.append(f"{name},10m,10m,original,train,hurricane-harvey,usa")
+        if i % 3 == 0:
+            rows.append(f"{name},10m,10m,flipped,train,hurricane-harvey,usa")
+    with open(os.path.join(root, "metadata", "dataset_split.csv"), "w") as f:
+        f.write("\n".join(rows) + "\n")
+    return arrays
+
+
+@pytest.mark.parametrize("crop,resize,topo", [(4, 48, "map"), (None, None, "all")])
+def test_tile_loader_vs_reference_items(tmp_path, crop, resize, topo):
+    """The staged loader: the item order of DataLoader(shuffle=True) under the same global seed, every
+    batch equal to the reference's per-item pipeline, names with the crop suffix (models/utils.py:56),
+    and data-parallel sharding of each global batch (rank order)."""
+    from floodgan.data import create_flood_dataset
+    from torch.utils.data import BatchSampler, RandomSampler
+    root = str(tmp_path)
+    arrays = _dataset_dir(root)
+    csv = os.path.join(root, "metadata", "dataset_split.csv")
+    train, _, _ = create_flood_dataset("hurricane-harvey", "same", root, topo, resize=resize, crop=crop, batch_size=3,
+                                       csv_path=csv, prefetch=2)
+    ds = train.ds
+    torch.manual_seed(5)
+    order = [i for b in BatchSampler(RandomSampler(ds), 3, False) for i in b]
+    torch.manual_seed(5)
+    seen = []
+    for xb, yb, names in train:
+        assert xb.is_contiguous(memory_format=torch.channels_last)
+        for k, name in enumerate(names):
+            idx = order[len(seen)]
+            _, _, flip, ci, want = ds.item(idx)
+            assert name == want
+            x, y = arrays[want[:len("hurricane-harvey_00000000")]]
+            rx, ry = reference_item(x, y, flip, topo, resize, crop, ci)
+            assert float((xb[k].cpu() - rx).abs().max()) < TOL and float((yb[k].cpu() - ry).abs().max()) < TOL
+            seen.append(idx)
+    assert seen == order and len(seen) == len(ds)
+    # two ranks: each global batch of 2 x 2 items is split in rank order, the short tail dropped
+    shards = []
+    for rank in range(2):
+        tr, _, _ = create_flood_dataset("hurricane-harvey", "same", root, topo, resize=resize, crop=crop, batch_size=2,
+                                        csv_path=csv, rank=rank, world=2)
+        torch.manual_seed(9)
+        shards.append([n for _, _, names in tr for n in names])
+    torch.manual_seed(9)
+    glob = [b for b in BatchSampler(RandomSampler(ds), 4, True)]
+    assert shards[0] == [ds.item(i)[4] for b in glob for i in b[:2]]
+    assert shards[1] == [ds.item(i)[4] for b in glob for i in b[2:]]
+
+
+def test_cycle_training_through_the_loader(tmp_path):
+    """BASELINE configs[4]'s pipeline in miniature: AttentionGAN train_cycle fed by the staged loader
+    with crop=4 (models/model.py:151-156 -> :660-758)."""
+    from floodgan.data import create_flood_dataset
+    from floodgan.model import Model
+    root = str(tmp_path)
+    _dataset_dir(root, n_img=3, h=64)
+    train, _, _ = create_flood_dataset("hurricane-harvey", "same", root, "all", resize=64, crop=4, batch_size=4,
+                                       csv_path=os.path.join(root, "metadata", "dataset_split.csv"))
+    m = Model(model="AttentionGAN", num_epochs=1, topography="all", train_loader=train)
+    m.train_cycle()
+    vals = [v[-1] for v in m.all_losses.values()]
+    assert len(vals) == 8 and all(np.isfinite(vals))
