@@ -138,6 +138,12 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--workload", choices=["paired", "attentiongan", "cyclegan"], default="paired")
+    ap.add_argument("--data", choices=["resident", "tiles"], default="resident",
+                    help="tiles: feed the step through the staged tile pipeline (floodgan.data.TileLoader) from "
+                         "synthetic TIFF tiles on disk, --res = Resize size, --crop quadrants (BASELINE configs[4])")
+    ap.add_argument("--crop", type=int, default=None)
+    ap.add_argument("--tile", type=int, default=1024, help="raw tile edge for --data tiles (xBD tiles are 1024)")
+    ap.add_argument("--tiles", type=int, default=8, help="distinct synthetic tiles for --data tiles")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -154,6 +160,10 @@ def main():
 
     B, R = args.batch, args.res
     cycle = args.workload != "paired"
+    loader = None
+    if args.data == "tiles":
+        loader, tmpdir = tile_loader(args, B, rank, world, dev)
+        R = R // int(round((args.crop or 1) ** 0.5))       # the model sees the crop windows
     m = Model(model={"paired": "PairedAttention", "attentiongan": "AttentionGAN", "cyclegan": "CycleGAN"}[args.workload],
               num_epochs=2, topography="all", device=dev)
     nets = ([m.pre_to_post_generator, m.post_to_pre_generator, m.pre_discriminator, m.post_discriminator] if cycle
@@ -161,13 +171,30 @@ def main():
     if world > 1:
         for net in nets:
             broadcast_params(net)
-    step = m.cycle_step_fn if cycle else m.step_fn
-    g = torch.Generator().manual_seed(1234 + rank)
-    x = (torch.rand((B, 9, R, R), generator=g) * 2 - 1).to(dev)
-    y = (torch.rand((B, 3, R, R), generator=g) * 2 - 1).to(dev)
+    step_fn = m.cycle_step_fn if cycle else m.step_fn
+    if loader is None:
+        g = torch.Generator().manual_seed(1234 + rank)
+        x = (torch.rand((B, 9, R, R), generator=g) * 2 - 1).to(dev)
+        y = (torch.rand((B, 3, R, R), generator=g) * 2 - 1).to(dev)
+
+        def step():
+            return step_fn(x, y)
+    else:
+        def batches():
+            epoch = 0
+            while True:
+                torch.manual_seed(epoch)                 # models/model.py:609 / :676
+                for xb, yb, _ in loader:
+                    yield xb, yb
+                epoch += 1
+        it = batches()
+
+        def step():
+            xb, yb = next(it)
+            return step_fn(xb, yb)
 
     for _ in range(args.warmup):
-        step(x, y).cpu()
+        step().cpu()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -176,7 +203,7 @@ def main():
     t0 = time.perf_counter()
     with timer:
         for _ in range(args.steps):
-            losses = step(x, y).cpu()       # the reference logs the four losses every iteration
+            losses = step().cpu()           # the reference logs the losses every iteration
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -211,7 +238,10 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic U[-1,1) tiles resident in HBM, seed-47 weights (models/model.py:80)",
+            "data": ("synthetic U[-1,1) tiles resident in HBM, seed-47 weights (models/model.py:80)" if loader is None
+                     else f"synthetic {args.tile}x{args.tile} TIFF tiles ({args.tiles} distinct, 9-ch float32 inputs + "
+                          f"3-ch targets) decoded, staged (pinned ring + copy stream) and transformed (Resize {args.res}, "
+                          f"crop={args.crop}, fliplr versions) by floodgan.data.TileLoader inside the timed region"),
             "config": {"workload": (f"PairedAttention paired train step, {R}x{R}, topography=all "
                                     f"(9-ch G input, 12-ch D input), batch {B}/GPU" if not cycle else
                                     f"{m.model} train_cycle step (2 G + 2 D, recreated images, Adam x2), {R}x{R}, "
@@ -245,8 +275,42 @@ def main():
             out["cpu_baseline"] = cpu_baseline(R, threads, steps=1 if cycle else 3, workload=args.workload,
                                                batches=(1,) if cycle else (1, 8))
         print(json.dumps(out), flush=True)
+    if loader is not None:
+        import shutil
+        shutil.rmtree(tmpdir, ignore_errors=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def tile_loader(args, B, rank, world, dev):
+    """A synthetic dataset in the reference's on-disk layout (dataset_input/*.tif 9-ch float32,
+    dataset_output/*.tif 3-ch float32, metadata/dataset_split.csv; every third tile also listed as its
+    'flipped' version) and the staged train loader over it (models/data.py:11-44 -> floodgan.data)."""
+    import tempfile
+
+    import numpy as np
+    from floodgan.data import create_flood_dataset, write_tile
+    root = tempfile.mkdtemp(prefix=f"floodgan_tiles_r{rank}_", dir="/tmp")
+    for d in ("dataset_input", "dataset_output", "metadata"):
+        os.makedirs(os.path.join(root, d))
+    rng = np.random.default_rng(1234 + rank)
+    rows = ["image,best_DEM,same_DEM,version,split,disaster,country"]
+    for i in range(args.tiles):
+        name = f"hurricane-harvey_{i:08d}"
+        write_tile(os.path.join(root, "dataset_input", f"{name}_10m.tif"),
+                   rng.random((args.tile, args.tile, 9), dtype=np.float32))
+        write_tile(os.path.join(root, "dataset_output", f"{name}.tif"),
+                   rng.random((args.tile, args.tile, 3), dtype=np.float32))
+        rows.append(f"{name},10m,10m,original,train,hurricane-harvey,usa")
+        if i % 3 == 0:
+            rows.append(f"{name},10m,10m,flipped,train,hurricane-harvey,usa")
+    with open(os.path.join(root, "metadata", "dataset_split.csv"), "w") as f:
+        f.write("\n".join(rows) + "\n")
+    train, _, _ = create_flood_dataset("hurricane-harvey", "same", root, "all", resize=args.res, crop=args.crop,
+                                       batch_size=B, csv_path=os.path.join(root, "metadata", "dataset_split.csv"),
+                                       device=dev, rank=rank, world=world)
+    train.drop_last = True        # fixed batch shape in the timed region
+    return train, root
 
 
 if __name__ == "__main__":
