@@ -129,11 +129,20 @@ SIGNATURES = {
               C.c_int, C.c_void_p, C.c_void_p],
     "fg_adam_step": [C.POINTER(fg_adam_tensor), C.c_int, C.c_double, C.c_double, C.c_double, C.c_double,
                      C.c_longlong, C.c_void_p],
+    "fg_bn_workspace_doubles": [C.c_int, C.c_int],
+    "fg_bn_stats": [fg_view, C.c_int, C.c_float, C.c_float, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                    C.c_void_p, C.c_void_p, C.c_void_p],
+    "fg_bn_eval_stats": [C.c_int, C.c_void_p, C.c_void_p, C.c_float, C.c_void_p, C.c_void_p, C.c_void_p],
+    "fg_bn_apply": [fg_view, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_float, C.c_int,
+                    fg_view, C.c_void_p, C.c_int, fg_view, C.c_void_p, C.c_void_p],
+    "fg_bn_bwd": [fg_view, C.c_int, fg_view, C.c_int, fg_view, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                  C.c_void_p, C.c_float, fg_view, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p],
+    "fg_maxpool2": [fg_view, fg_view, C.c_void_p],
     "fg_tiff_probe": [C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)],
     "fg_tiff_read": [C.c_char_p, C.c_void_p, C.c_longlong],
     "fg_tile_transform": [C.POINTER(fg_tile_batch), C.c_void_p],
 }
-RESTYPES = {"fg_last_error": C.c_char_p, "fg_in_workspace_doubles": C.c_longlong,
+RESTYPES = {"fg_last_error": C.c_char_p, "fg_in_workspace_doubles": C.c_longlong, "fg_bn_workspace_doubles": C.c_longlong,
             "fg_channel_sum_workspace_doubles": C.c_longlong}
 
 _lib = None

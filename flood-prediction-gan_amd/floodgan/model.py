@@ -18,9 +18,11 @@ from torch.optim import lr_scheduler
 
 from . import executor as X
 from . import ops
+from . import pix2pix as P2P
 from .cycle import IDENTITY_KEYS, LOSS_KEYS, CycleStep
 from .model_architectures import (AttentionGANDiscriminator, AttentionGANGenerator, CycleGANDiscriminator,
-                                  CycleGANGenerator, PairedAttentionDiscriminator, PairedAttentionGenerator)
+                                  CycleGANGenerator, PairedAttentionDiscriminator, PairedAttentionGenerator,
+                                  Pix2PixDiscriminator, Pix2PixGenerator)
 from .optim import FusedAdam
 from .parallel import FlatGrads, world
 
@@ -98,6 +100,74 @@ class PairedStep:
         return {k: p.grad for k, p in params.items()}
 
 
+class Pix2PixStep(PairedStep):
+    """The same iteration (models/model.py:611-651) for Pix2Pix: BatchNorm in training mode, so the D
+    step's D(fake) and D(real) -- separate calls in the reference -- run as one 2N pass with two
+    BatchNorm groups (per-half statistics, two running-stat updates in order), and the G step's D call
+    updates the discriminator's running statistics a third time.  The generator's Dropout masks are
+    drawn from torch's CPU generator in the reference's order (floodgan.pix2pix.draw_dropout_masks)."""
+
+    def __init__(self, generator, discriminator, opt_g, opt_d, group=None):
+        self.G, self.D = generator, discriminator
+        self.opt_g, self.opt_d = opt_g, opt_d
+        self.gp, self.dp = generator.param_dict(), discriminator.param_dict()
+        self.gb, self.db = generator.buffer_dict(), discriminator.buffer_dict()
+        self.gflat = FlatGrads(self.gp, P2P.gen_bucket_names())
+        self.dflat = FlatGrads(self.dp, P2P.disc_bucket_names())
+        self.group = group
+        self.last_mask = None
+        self.last_output = None
+        self.record_decisions = False
+        self.decisions = None
+        self.masks = None        # test hook: dropout masks to use instead of drawing
+        self.last_masks = None
+
+    def __call__(self, x, y):
+        ws, _ = world()
+        inv = 1.0 / ws
+        N, C, H, W = x.shape
+        dev = x.device
+        losses = torch.empty(4, dtype=torch.float32, device=dev)
+        self.gflat.attach()
+        self.dflat.attach()
+        masks = self.masks if self.masks is not None else P2P.draw_dropout_masks(N, H, W)
+        self.last_masks = masks
+        fake, gS = P2P.gen_forward(self.gp, self.gb, x, masks=masks, training=True, save=True)
+        dinp = X.disc_pack([(x, fake), (x, y)], C + 3)
+        pred, dS = P2P.disc_forward(self.dp, self.db, dinp, groups=2, training=True, save=True)
+        g_pred = torch.empty_like(pred)
+        ops.mse_const(pred[:N], 0.0, 0.5 * inv, losses[1:2], g_pred[:N])
+        ops.mse_const(pred[N:], 1.0, 0.5 * inv, losses[0:1], g_pred[N:])
+        rec = {"G": [P2P.gen_act_decisions(gS)], "D": [P2P.disc_act_decisions(dS, 0, N),
+                                                       P2P.disc_act_decisions(dS, N)]} \
+            if self.record_decisions else None
+        self.dflat.begin(self.group)
+        P2P.disc_backward(self.dp, dS, g_pred, param_grads=True, grads_into=self._grads(self.dp),
+                          ready=self.dflat.ready)
+        del dS, dinp
+        self.dflat.finish()
+        self.opt_d.step()
+        dinp = X.disc_pack([(x, fake)], C + 3)
+        pred, dS = P2P.disc_forward(self.dp, self.db, dinp, groups=1, training=True, save=True)
+        g_pred = torch.empty_like(pred)
+        ops.mse_const(pred, 1.0, inv, losses[2:3], g_pred)
+        g_fake = torch.empty(N, 3, H, W, dtype=torch.float32, device=dev)
+        ops.l1(fake, y, 100.0 * inv, losses[3:4], g_fake)
+        P2P.disc_backward(self.dp, dS, g_pred, param_grads=False, input_grad=g_fake, input_grad_channels=(C, 3),
+                          input_grad_accumulate=True)
+        if rec is not None:
+            rec["D"].append(P2P.disc_act_decisions(dS))
+            self.decisions = rec
+        del dS, dinp
+        self.gflat.begin(self.group)
+        P2P.gen_backward(self.gp, gS, g_fake, grads_into=self._grads(self.gp), ready=self.gflat.ready)
+        del gS
+        self.gflat.finish()
+        self.opt_g.step()
+        self.last_output = fake
+        return losses * torch.tensor([1.0, 1.0, 1.0, 100.0], device=dev)
+
+
 class Model:
     """The reference's Model (models/model.py:26-160) with identical construction semantics (seed,
     initialise_weights, Adam(2e-4, (0.5, 0.999)), LambdaLR) for "PairedAttention" (train_paired,
@@ -113,9 +183,8 @@ class Model:
             saved = torch.load(pretrained_model_path, map_location="cpu", weights_only=True)
             model = saved["model"]
         self.model = model.lower()
-        if self.model not in ("pairedattention", "attentiongan", "cyclegan"):
-            raise NotImplementedError("floodgan implements the PairedAttention (paired), AttentionGAN and CycleGAN "
-                                      f"(cycle) training paths; '{model}' is out of scope (SURVEY.md §2)")
+        if self.model not in ("pairedattention", "pix2pix", "attentiongan", "cyclegan"):
+            raise NotImplementedError("Model must be one of: Pix2Pix, CycleGAN, AttentionGAN or PairedAttention")
         if saved is not None:
             self.num_epochs, self.topography = saved["num_epochs"], saved["topography"]
             self.add_identity_loss = saved["add_identity_loss"]
@@ -127,18 +196,18 @@ class Model:
         self.dataset_subset, self.dataset_dem, self.resize, self.crop = dataset_subset, dataset_dem, resize, crop
         self.training_model, self.seed, self.device = training_model, seed, device
         self.model_is_cycle = self.model in ("attentiongan", "cyclegan")
-        self.model_is_attention = self.model != "cyclegan"
+        self.model_is_attention = self.model in ("pairedattention", "attentiongan")     # models/model.py:219-229
 
         input_channels = TOPOGRAPHY_CHANNELS[self.topography]
         torch.manual_seed(self.seed)
         if self.model_is_cycle:                                   # models/model.py:96-100, :108-115
             self._init_cycle(input_channels, device)
         else:
-            self.generator = PairedAttentionGenerator(input_channels=input_channels).apply(
-                self.initialise_weights).to(device)
+            gcls, dcls = ((Pix2PixGenerator, Pix2PixDiscriminator) if self.model == "pix2pix"
+                          else (PairedAttentionGenerator, PairedAttentionDiscriminator))
+            self.generator = gcls(input_channels=input_channels).apply(self.initialise_weights).to(device)
         if self.training_model and not self.model_is_cycle:
-            self.discriminator = PairedAttentionDiscriminator(input_channels=input_channels).apply(
-                self.initialise_weights).to(device)
+            self.discriminator = dcls(input_channels=input_channels).apply(self.initialise_weights).to(device)
             self.optimizer_discriminator = FusedAdam(self.discriminator.parameters(), lr=0.0002, betas=(0.5, 0.999))
             self.optimizer_generator = FusedAdam(self.generator.parameters(), lr=0.0002, betas=(0.5, 0.999))
         if self.training_model:
@@ -218,8 +287,8 @@ class Model:
     @property
     def step_fn(self):
         if self._step is None:
-            self._step = PairedStep(self.generator, self.discriminator, self.optimizer_generator,
-                                    self.optimizer_discriminator)
+            cls = Pix2PixStep if self.model == "pix2pix" else PairedStep
+            self._step = cls(self.generator, self.discriminator, self.optimizer_generator, self.optimizer_discriminator)
         return self._step
 
     def train_paired(self):
@@ -283,7 +352,8 @@ class Model:
             print(f"Epoch {epoch} ({time.time() - epoch_start_time:.2f} seconds) | "
                   + " | ".join(f"{k} = {v[-1]:.2f}" for k, v in self.all_losses.items()))
         if self.save_model_interval != 0 and epoch % self.save_model_interval == 0:
-            name = {"attentiongan": "AttentionGAN", "cyclegan": "CycleGAN"}.get(self.model, "PairedAttention")
+            name = {"attentiongan": "AttentionGAN", "cyclegan": "CycleGAN", "pix2pix": "Pix2Pix"}.get(self.model,
+                                                                                               "PairedAttention")
             torch.save(self.checkpoint(epoch), f"{self.data_path}/models/{name}_epoch{epoch}.pth.tar")
 
     def checkpoint(self, epoch):

@@ -286,3 +286,153 @@ class CycleGANBlock(nn.Module):
 
 class CycleGANDiscriminator(AttentionGANDiscriminator):
     """models/model_architectures.py:136-157 -- the same PatchGAN over input_channels."""
+
+
+# ------------------------------------------------------------------------------------------
+# Pix2Pix (paired path): U-Net-256 generator with BatchNorm / Dropout, BatchNorm PatchGAN
+# ------------------------------------------------------------------------------------------
+
+from . import pix2pix as P2P  # noqa: E402
+
+PIX2PIX_GEN_KEYS = tuple(P2P.gen_state_keys())
+PIX2PIX_DISC_KEYS = tuple(P2P.DISC_KEYS)
+
+
+class _Pix2PixGeneratorFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, buffers, training, masks, x, *params):
+        P = dict(zip(PIX2PIX_GEN_KEYS, params))
+        out, S = P2P.gen_forward(P, buffers, x, masks=masks, training=training,
+                                 save=any(ctx.needs_input_grad))
+        ctx.P, ctx.S, ctx.training = P, S, training
+        ctx.save_for_backward(x, *params)
+        return out
+
+    @staticmethod
+    def backward(ctx, g_out):
+        _ = ctx.saved_tensors          # version check of the input and the parameters
+        if not ctx.training:
+            raise RuntimeError("floodgan: the Pix2Pix generator's backward is implemented for training-mode "
+                               "BatchNorm (the reference trains and evaluates in training mode)")
+        if ctx.needs_input_grad[3]:
+            raise RuntimeError("floodgan: the Pix2Pix generator does not provide an input gradient (no caller of "
+                               "the reference needs one)")
+        grads = P2P.gen_backward(ctx.P, ctx.S, g_out)
+        ctx.S = None
+        return (None, None, None, None) + tuple(grads[k] if need else None
+                                                for k, need in zip(PIX2PIX_GEN_KEYS, ctx.needs_input_grad[4:]))
+
+
+class _Pix2PixDiscriminatorFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, buffers, training, x, *params):
+        P = dict(zip(PIX2PIX_DISC_KEYS, params))
+        buf = X.disc_pack([(x, None)], x.shape[1])
+        pred, S = P2P.disc_forward(P, buffers, buf, 1, training, save=any(ctx.needs_input_grad))
+        ctx.P, ctx.S, ctx.xshape, ctx.training = P, S, tuple(x.shape), training
+        ctx.save_for_backward(*params)
+        return pred
+
+    @staticmethod
+    def backward(ctx, g_pred):
+        _ = ctx.saved_tensors
+        if not ctx.training:
+            raise RuntimeError("floodgan: the Pix2Pix discriminator's backward is implemented for training-mode "
+                               "BatchNorm")
+        need_params = any(ctx.needs_input_grad[3:])
+        gx = None
+        if ctx.needs_input_grad[2]:
+            N, C, H, W = ctx.xshape
+            gx = torch.empty(N, C, H, W, dtype=torch.float32, device=g_pred.device)
+        grads = P2P.disc_backward(ctx.P, ctx.S, g_pred.contiguous(), param_grads=need_params, input_grad=gx,
+                                  input_grad_channels=(0, ctx.xshape[1]))
+        ctx.S = None
+        return (None, None, gx) + tuple(grads.get(k) if need else None
+                                        for k, need in zip(PIX2PIX_DISC_KEYS, ctx.needs_input_grad[3:]))
+
+
+class Pix2PixBlock(nn.Module):
+    """models/model_architectures.py:24-62 -- the same modules in the same construction order (RNG
+    parity) and nn.Sequential layout (state_dict keys).  Executed by its Pix2PixGenerator's fused node."""
+
+    def __init__(self, outer_nc, inner_nc, input_nc, submodule, outermost, innermost, use_dropout):
+        super().__init__()
+        self.outermost = outermost
+        if input_nc is None:
+            input_nc = outer_nc
+        downconv = nn.Conv2d(input_nc, inner_nc, kernel_size=4, stride=2, padding=1, bias=False)
+        downrelu = nn.LeakyReLU(0.2, True)
+        uprelu = nn.ReLU(True)
+        downnorm = nn.BatchNorm2d(inner_nc)
+        upnorm = nn.BatchNorm2d(outer_nc)
+        if outermost:
+            upconv = nn.ConvTranspose2d(inner_nc * 2, outer_nc, kernel_size=4, stride=2, padding=1)
+            model = [downconv, submodule, uprelu, upconv, nn.Tanh()]
+        elif innermost:
+            upconv = nn.ConvTranspose2d(inner_nc, outer_nc, kernel_size=4, stride=2, padding=1, bias=False)
+            model = [downrelu, downconv, uprelu, upconv, upnorm]
+        else:
+            upconv = nn.ConvTranspose2d(inner_nc * 2, outer_nc, kernel_size=4, stride=2, padding=1, bias=False)
+            model = [downrelu, downconv, downnorm, submodule, uprelu, upconv, upnorm]
+            if use_dropout:
+                model.append(nn.Dropout(0.5))
+        self.model = nn.Sequential(*model)
+
+    def forward(self, x):
+        raise RuntimeError("floodgan: a Pix2PixBlock runs inside its Pix2PixGenerator's fused node; call the "
+                           "generator")
+
+
+class Pix2PixGenerator(nn.Module):
+    """models/model_architectures.py:9-22 -- U-Net-256: eight Pix2PixBlocks, innermost first.  The
+    whole network is one autograd node on floodgan.pix2pix; BatchNorm running statistics are updated
+    in place, Dropout masks come from torch's CPU generator in the reference's order."""
+
+    def __init__(self, input_channels):
+        super().__init__()
+        unet_block = Pix2PixBlock(512, 512, None, None, False, True, False)
+        for _ in range(3):
+            unet_block = Pix2PixBlock(512, 512, None, unet_block, False, False, True)
+        unet_block = Pix2PixBlock(256, 512, None, unet_block, False, False, False)
+        unet_block = Pix2PixBlock(128, 256, None, unet_block, False, False, False)
+        unet_block = Pix2PixBlock(64, 128, None, unet_block, False, False, False)
+        self.model = Pix2PixBlock(3, 64, input_channels, unet_block, True, False, False)
+
+    def param_dict(self):
+        sd = dict(self.named_parameters())
+        return {k: sd[k] for k in PIX2PIX_GEN_KEYS}
+
+    def buffer_dict(self):
+        return dict(self.named_buffers())
+
+    def forward(self, input):
+        masks = P2P.draw_dropout_masks(input.shape[0], input.shape[2], input.shape[3]) if self.training else None
+        return _Pix2PixGeneratorFn.apply(self.buffer_dict(), self.training, masks, input,
+                                         *self.param_dict().values())
+
+
+class Pix2PixDiscriminator(nn.Module):
+    """models/model_architectures.py:64-85 -- PatchGAN over input_channels + 3 with BatchNorm."""
+
+    def __init__(self, input_channels):
+        super().__init__()
+        sequence = [nn.Conv2d(input_channels + 3, 64, kernel_size=4, stride=2, padding=1), nn.LeakyReLU(0.2, True)]
+        nf_mult = 1
+        for n in range(1, 3):
+            nf_prev, nf_mult = nf_mult, min(2 ** n, 8)
+            sequence += [nn.Conv2d(64 * nf_prev, 64 * nf_mult, kernel_size=4, stride=2, padding=1, bias=False),
+                         nn.BatchNorm2d(64 * nf_mult), nn.LeakyReLU(0.2, True)]
+        sequence += [nn.Conv2d(64 * nf_mult, 512, kernel_size=4, stride=1, padding=1, bias=False),
+                     nn.BatchNorm2d(512), nn.LeakyReLU(0.2, True)]
+        sequence += [nn.Conv2d(512, 1, kernel_size=4, stride=1, padding=1)]
+        self.model = nn.Sequential(*sequence)
+
+    def param_dict(self):
+        sd = dict(self.named_parameters())
+        return {k: sd[k] for k in PIX2PIX_DISC_KEYS}
+
+    def buffer_dict(self):
+        return dict(self.named_buffers())
+
+    def forward(self, x):
+        return _Pix2PixDiscriminatorFn.apply(self.buffer_dict(), self.training, x, *self.param_dict().values())

@@ -7,7 +7,7 @@ import ctypes as C
 import torch
 
 from . import _lib as L
-from .plans import Buf, f3_wgrad_eligible, packed_numel, slab_numel, wgrad_splits
+from .plans import Buf, Slice, f3_wgrad_eligible, packed_numel, slab_numel, wgrad_splits
 
 EPS = 1e-5
 
@@ -17,7 +17,7 @@ def _lib():
 
 
 def _dev(t):
-    return t.t.device if isinstance(t, Buf) else t.device
+    return t.t.device if isinstance(t, (Buf, Slice)) else t.device
 
 
 def _addr(ref):
@@ -30,6 +30,9 @@ def _addr(ref):
 def view(B):
     if B is None:
         return L.fg_view(None, 0, 0, 0, 0, 0)
+    if isinstance(B, Slice):
+        b = B.buf
+        return L.fg_view(b.t.data_ptr() + 4 * B.c0, b.n, b.h, b.w, b.c, b.pad)
     return L.fg_view(B.t.data_ptr(), B.n, B.h, B.w, B.c, B.pad)
 
 
@@ -83,7 +86,7 @@ _SLOTS = _SlotPool()
 
 
 def _tensor(obj):
-    return obj.t if isinstance(obj, Buf) else obj
+    return obj.t if isinstance(obj, (Buf, Slice)) else obj
 
 
 def _wrote(*objs):
@@ -454,6 +457,75 @@ def channel_sum(src, c_valid, out, accumulate=False):
     work = torch.empty(_lib().fg_channel_sum_workspace_doubles(src.c), dtype=torch.float64, device=src.t.device)
     L.check(_lib().fg_channel_sum(view(src), c_valid, L.ptr(out), int(accumulate), L.ptr(work), L.stream_handle()),
             "channel_sum")
+
+
+# ------------------------------------------------------------------ batch norm
+
+BN_MOMENTUM = 0.1
+
+
+def _bn_work(n, c, dev):
+    return torch.empty(int(_lib().fg_bn_workspace_doubles(n, c)), dtype=torch.float64, device=dev)
+
+
+def _dst_slot(dst, slot):
+    """absmax slot a producer raises for dst: the caller's (a buffer several producers write in
+    channel slices shares one slot, taken once with _amax_out(buffer)), else a fresh one for a whole
+    Buf; a Slice without a slot only invalidates its buffer's caches"""
+    if dst is None:
+        return None
+    if slot is not None:
+        return slot
+    if isinstance(dst, Slice):
+        _wrote(dst)
+        return None
+    return _amax_out(dst)
+
+
+def bn_stats(src, groups=1, running=None, eps=EPS, momentum=BN_MOMENTUM):
+    """nn.BatchNorm2d(train) statistics of src's interior, per group of src.n / groups images ->
+    (mean, invstd) [groups * C]; running = (running_mean, running_var[, num_batches_tracked]) updated
+    once per group"""
+    dev = src.t.device
+    mean = torch.empty(groups * src.c, dtype=torch.float32, device=dev)
+    invstd = torch.empty_like(mean)
+    rm, rv, nbt = (tuple(running) + (None,))[:3] if running is not None else (None, None, None)
+    L.check(_lib().fg_bn_stats(view(src), groups, C.c_float(eps), C.c_float(momentum), L.ptr(mean), L.ptr(invstd),
+                               L.ptr(rm), L.ptr(rv), L.ptr(nbt), L.ptr(_bn_work(src.n, src.c, dev)),
+                               L.stream_handle()), "bn_stats")
+    return mean, invstd
+
+
+def bn_eval_stats(running_mean, running_var, eps=EPS):
+    """module.eval(): (running_mean, 1 / sqrt(running_var + eps))"""
+    mean, invstd = torch.empty_like(running_mean), torch.empty_like(running_var)
+    L.check(_lib().fg_bn_eval_stats(running_mean.numel(), L.ptr(running_mean), L.ptr(running_var), C.c_float(eps),
+                                    L.ptr(mean), L.ptr(invstd), L.stream_handle()), "bn_eval_stats")
+    return mean, invstd
+
+
+def bn_apply(src, groups, mean, invstd, gamma, beta, mask, act0, dst0, act1=0, dst1=None, slots=(None, None)):
+    """dst0 = act0(BN(src) * mask / 0.5), dst1 = act1(same) (interiors; Buf or Slice destinations);
+    mean None = no normalisation; mask None = no dropout"""
+    s0, s1 = _dst_slot(dst0, slots[0]), _dst_slot(dst1, slots[1])
+    L.check(_lib().fg_bn_apply(view(src), groups, L.ptr(mean), L.ptr(invstd), L.ptr(gamma), L.ptr(beta),
+                               L.ptr(mask), C.c_float(2.0), act0, view(dst0), L.ptr(s0), act1, view(dst1),
+                               L.ptr(s1), L.stream_handle()), "bn_apply")
+
+
+def bn_bwd(gA, actA, gB, actB, src, groups, mean, invstd, gamma, beta, mask, dst, gamma_grad=None, beta_grad=None,
+           accumulate=False):
+    """dst = dL/dsrc of bn_apply, the incoming gradient being gA * actA'(u) (+ gB * actB'(u))"""
+    slot = _dst_slot(dst, None)
+    L.check(_lib().fg_bn_bwd(view(gA), actA, view(gB), actB, view(src), groups, L.ptr(mean), L.ptr(invstd),
+                             L.ptr(gamma), L.ptr(beta), L.ptr(mask), C.c_float(2.0), view(dst), L.ptr(gamma_grad),
+                             L.ptr(beta_grad), int(accumulate), L.ptr(_bn_work(src.n, src.c, src.t.device)),
+                             L.ptr(slot), L.stream_handle()), "bn_bwd")
+
+
+def maxpool2(src, dst):
+    _wrote(dst)
+    L.check(_lib().fg_maxpool2(view(src), view(dst), L.stream_handle()), "maxpool2")
 
 
 # ------------------------------------------------------------------ tail / losses / adam

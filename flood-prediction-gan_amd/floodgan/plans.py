@@ -82,6 +82,25 @@ class Buf:
         return f"Buf(n={self.n}, h={self.h}, w={self.w}, c={self.c}, pad={self.pad})"
 
 
+class Slice:
+    """Channels [c0, c0 + c) of a Buf: the U-Net's torch.cat([skip, up], 1) halves are slices of one
+    buffer (models/model_architectures.py:62).  A kernel given a slice view walks the channel count of
+    its source operand with the wider buffer's pixel stride."""
+
+    __slots__ = ("buf", "c0", "c")
+
+    def __init__(self, buf, c0, c):
+        assert 0 <= c0 and c0 + c <= buf.c and c0 % 4 == 0
+        self.buf, self.c0, self.c = buf, c0, c
+
+    @property
+    def t(self):
+        return self.buf.t
+
+    def interior(self):
+        return self.buf.interior()[..., self.c0:self.c0 + self.c]
+
+
 def out_size(h, k, s, p):
     return (h + 2 * p - k) // s + 1
 

@@ -344,6 +344,40 @@ int fg_adam_step(const fg_adam_tensor* tensors, int count, double lr, double bet
                  double beta2, double eps, long long step, hipStream_t stream);
 
 /* ---------------------------------------------------------------------------------------- */
+/* batch norm (nn.BatchNorm2d, training mode) -- Pix2Pix U-Net / PatchGAN and the segmentation */
+/* U-Net (models/model_architectures.py:9-85, :508-587)             */
+/* ---------------------------------------------------------------------------------------- */
+/* Images of src split into `groups` equal consecutive batches, each one separate BatchNorm call
+ * (statistics over its images x H x W per channel; the running statistics, when given, are
+ * updated once per group in group order with torch's momentum rule and unbiased variance).
+ * mean / invstd: [groups * C].  num_batches_tracked (optional, the module's int64 buffer) is raised
+ * by `groups`.  work >= fg_bn_workspace_doubles(n, c). */
+long long fg_bn_workspace_doubles(int n, int c);
+int fg_bn_stats(fg_view src, int groups, float eps, float momentum, float* mean, float* invstd,
+                float* running_mean, float* running_var, long long* num_batches_tracked, double* work,
+                hipStream_t stream);
+/* Eval-mode statistics (module.eval()): mean = running_mean, invstd = 1 / sqrt(running_var + eps). */
+int fg_bn_eval_stats(int c, const float* running_mean, const float* running_var, float eps, float* mean,
+                     float* invstd, hipStream_t stream);
+/* y = (x - mean) * invstd * gamma + beta (no normalisation when mean is NULL, no affine when gamma
+ * is NULL), then y *= drop_mask * drop_scale (nn.Dropout with a caller-drawn NCHW 0/1 mask, optional),
+ * dst0 = act0(y) and optionally dst1 = act1(y): interiors only; a destination may be a channel
+ * slice of a wider buffer (ptr offset, c_alloc = the wider buffer's channels). */
+int fg_bn_apply(fg_view src, int groups, const float* mean, const float* invstd, const float* gamma,
+                const float* beta, const float* drop_mask, float drop_scale, int act0, fg_view dst0,
+                float* absmax0, int act1, fg_view dst1, float* absmax1, hipStream_t stream);
+/* Backward of fg_bn_apply: the incoming gradient of the normalised, dropped-out value u is
+ * gA * actA'(u) (+ gB * actB'(u) when gB.ptr), times the dropout mask * scale; dst = dL/dx through the
+ * batch statistics of each group (identity when mean is NULL); gamma_grad / beta_grad (written, or
+ * added to when accumulate) summed over the groups. */
+int fg_bn_bwd(fg_view gA, int actA, fg_view gB, int actB, fg_view src, int groups, const float* mean,
+              const float* invstd, const float* gamma, const float* beta, const float* drop_mask,
+              float drop_scale, fg_view dst, float* gamma_grad, float* beta_grad, int accumulate,
+              double* work, float* absmax, hipStream_t stream);
+/* nn.MaxPool2d(2) over NHWC interiors (floor output size). */
+int fg_maxpool2(fg_view src, fg_view dst, hipStream_t stream);
+
+/* ---------------------------------------------------------------------------------------- */
 /* tile data path                                                    */
 /* ---------------------------------------------------------------------------------------- */
 /* Host-side baseline TIFF decode, replacing tifffile.imread (models/data.py:64-68) for the files

@@ -20,7 +20,9 @@ run() {   # name limit cmd...
   return 0
 }
 if [ "${TESTS:-1}" = 1 ]; then
-  run tests ${TEST_LIMIT:-1200} python -u -m pytest tests -m gpu -v -rf --timeout 300 --timeout-method thread "$@"
+  # pytest selection: the arguments, else the whole GPU suite
+  SEL=("$@"); [ ${#SEL[@]} -eq 0 ] && SEL=(tests)
+  run tests ${TEST_LIMIT:-1200} python -u -m pytest -m gpu -v -rf --timeout 300 --timeout-method thread "${SEL[@]}"
 fi
 if [ "${SMOKE:-1}" = 1 ]; then run smoke 300 python -u __graft_entry__.py smoke; fi
 if [ "${BENCH:-1}" = 1 ]; then run bench 600 python -u bench.py --steps ${STEPS:-20} --warmup 5 ${BENCH_ARGS}; fi

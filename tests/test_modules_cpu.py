@@ -67,10 +67,38 @@ def test_fused_adam_state_format_matches_torch_adam():
         FusedAdam([p], weight_decay=0.1)
 
 
-def test_model_rejects_out_of_scope_models():
+def test_model_rejects_unknown_models():
     from floodgan.model import Model
     with pytest.raises(NotImplementedError):
-        Model(model="Pix2Pix", device="cpu")
+        Model(model="UNet", device="cpu")
+    m = Model(model="Pix2Pix", device="cpu")
+    assert not m.model_is_cycle and not m.model_is_attention
+
+
+def test_pix2pix_modules_match_reference_init_and_layout():
+    """Pix2Pix drop-ins: torch.manual_seed(47) + construction + initialise_weights reproduces the
+    reference's state_dict (parameters and BatchNorm buffers, same keys in the same order) bit for bit
+    (tests/golden/pix2pix_step_256.npz from the reference's own Model)."""
+    from floodgan import pix2pix as P2P
+    from floodgan.model import Model
+    gold = np.load(os.path.join(ROOT, "tests", "golden", "pix2pix_step_256.npz"))
+    m = Model(model="Pix2Pix", device="cpu")
+    for prefix, mod in (("init_G", m.generator), ("init_D", m.discriminator)):
+        keys = [k for k in (f.replace("__", ".") for f in gold.files) if k.startswith(prefix + "/")]
+        assert [prefix + "/" + k for k in mod.state_dict()] == keys
+        for name, t in mod.state_dict().items():
+            ref = gold[f"{prefix}/{name}".replace(".", "__")]
+            t = t.double().flatten()
+            n8 = min(8, t.numel())
+            assert np.array_equal(t[:n8].numpy(), ref[2:2 + n8]), name
+            assert abs(t.sum().item() - ref[0]) <= 1e-9 * max(1.0, abs(ref[1])), name
+    # the executor's parameter inventory / bucket layout cover every parameter exactly once
+    assert list(m.generator.param_dict()) == [k for k, _ in m.generator.named_parameters()]
+    assert sorted(k for b in P2P.gen_bucket_names() for k in b) == sorted(m.generator.param_dict())
+    assert sorted(k for b in P2P.disc_bucket_names() for k in b) == sorted(m.discriminator.param_dict())
+    assert sum(p.numel() for p in m.generator.parameters()) == 54420099     # U-Net-256 with 9 input channels
+    with pytest.raises(RuntimeError, match="HIP device"):
+        m.generator(torch.randn(1, 9, 256, 256))
 
 
 def test_lambda_rule_matches_reference():
