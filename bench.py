@@ -12,7 +12,8 @@ batch already resident in HBM.  Prints ONE JSON line (rank 0).
 --workload attentiongan | cyclegan times the cycle path instead (SURVEY.md §8(f) row 1,
 BASELINE.json configs[3]/[4]): one iteration of models/model.py:677-752 (two generators, the
 recreated images through the other generator, two discriminators, both Adam steps, the eight
-logged losses read back).  The default (paired) is the headline line.
+logged losses read back).  --workload pix2pix times the same paired iteration on the Pix2Pix U-Net-256
++ BatchNorm PatchGAN.  The default (paired) is the headline line.
 """
 import argparse
 import json
@@ -63,6 +64,38 @@ def step_roofline(img_s_per_gpu, res, peak_conv):
                      "math's MFMA roof (f16x3: 2500/3 TFLOP/s) and the exact-fp32 MFMA roof 157.3 TFLOP/s"}
 
 
+def p2p_conv_layers(res, c_in=9):
+    """(name, n_out, k_eff, out_pixels, network, needs_dgrad) of every Pix2Pix conv at res x res:
+    k_eff = input channels x taps per output (a ConvTranspose2d 4x4 s2 output pixel sees 2x2 taps)"""
+    lv = [(c_in, 64, 3), (64, 128, 64), (128, 256, 128), (256, 512, 256)] + [(512, 512, 512)] * 4
+    out = []
+    for k in range(1, 9):
+        i, inner, outer = lv[k - 1]
+        out.append((f"down{k}", inner, i * 16, (res >> k) ** 2, "G", k > 1))
+        cin_up = inner if k == 8 else 2 * inner
+        out.append((f"up{k}", outer, cin_up * 4, (res >> (k - 1)) ** 2, "G", True))
+    h = [res // 2, res // 4, res // 8, res // 8 - 1, res // 8 - 2]
+    for name, n, kk, hw in (("model.0", 64, 12 * 16, h[0]), ("model.2", 128, 64 * 16, h[1]),
+                            ("model.5", 256, 128 * 16, h[2]), ("model.8", 512, 256 * 16, h[3]),
+                            ("model.11", 1, 512 * 16, h[4])):
+        out.append((name, n, kk, hw * hw, "D", name != "model.0"))
+    return out
+
+
+def p2p_step_gflop_per_img(res):
+    """MAC-count FLOPs of one Pix2Pix training iteration per image (models/model.py:615-646): G forward,
+    weight + input gradients; D forward + weight/input gradients on 2N images (D step), forward + input
+    gradient on N (G step; model.0's input gradient for the 3 image channels only)"""
+    tot = 0.0
+    for name, n, kk, px, net, dgrad in p2p_conv_layers(res):
+        f = 2.0 * px * n * kk
+        if net == "G":
+            tot += f * (3 if dgrad else 2)
+        else:
+            tot += 2 * f * (3 if dgrad else 2) + f * 2 + (0 if dgrad else f * 3 / 12)
+    return tot / 1e9
+
+
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "round1", "r1l_pmc_resblock_fwd.json")
 
 
@@ -105,9 +138,11 @@ def cpu_baseline(res, threads, steps=3, workload="paired", batches=(1, 8)):
     bounded sample: `steps` timed iterations at each batch size (1 warm-up iteration at batch 1)."""
     from oracle import attention_cycle as OC  # the checker / CPU baseline only
     from oracle import paired_attention as O
+    from oracle import pix2pix as OP
 
     torch.set_num_threads(threads)
-    st = O.PairedStepOracle() if workload == "paired" else OC.CycleStepOracle(model=workload)
+    st = (O.PairedStepOracle() if workload == "paired" else OP.Pix2PixStepOracle() if workload == "pix2pix"
+          else OC.CycleStepOracle(model=workload))
     rates = {}
     for bs in batches:
         g = torch.Generator().manual_seed(4321)
@@ -137,7 +172,7 @@ def main():
     ap.add_argument("--res", type=int, default=512)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
-    ap.add_argument("--workload", choices=["paired", "attentiongan", "cyclegan"], default="paired")
+    ap.add_argument("--workload", choices=["paired", "pix2pix", "attentiongan", "cyclegan"], default="paired")
     ap.add_argument("--data", choices=["resident", "tiles"], default="resident",
                     help="tiles: feed the step through the staged tile pipeline (floodgan.data.TileLoader) from "
                          "synthetic TIFF tiles on disk, --res = Resize size, --crop quadrants (BASELINE configs[4])")
@@ -159,13 +194,14 @@ def main():
     from floodgan.parallel import broadcast_params
 
     B, R = args.batch, args.res
-    cycle = args.workload != "paired"
+    cycle = args.workload in ("attentiongan", "cyclegan")
+    p2p = args.workload == "pix2pix"
     loader = None
     if args.data == "tiles":
         loader, tmpdir = tile_loader(args, B, rank, world, dev)
         R = R // int(round((args.crop or 1) ** 0.5))       # the model sees the crop windows
-    m = Model(model={"paired": "PairedAttention", "attentiongan": "AttentionGAN", "cyclegan": "CycleGAN"}[args.workload],
-              num_epochs=2, topography="all", device=dev)
+    m = Model(model={"paired": "PairedAttention", "pix2pix": "Pix2Pix", "attentiongan": "AttentionGAN",
+                     "cyclegan": "CycleGAN"}[args.workload], num_epochs=2, topography="all", device=dev)
     nets = ([m.pre_to_post_generator, m.post_to_pre_generator, m.pre_discriminator, m.post_discriminator] if cycle
             else [m.generator, m.discriminator])
     if world > 1:
@@ -198,7 +234,8 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    timer = ops.KernelTimer(["resblock_conv_fwd"])
+    tag = "p2p_d_model8_fwd" if p2p else "resblock_conv_fwd"
+    timer = ops.KernelTimer([tag])
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     with timer:
@@ -218,16 +255,23 @@ def main():
     nprod = {"f16x3": 3, "fwd_f16x3": 3, "bf16x6": 6, "fwd_x6": 6}.get(math)
     peak = BF16_MFMA_PEAK_TFLOPS / nprod if nprod else FP32_MFMA_PEAK_TFLOPS
     fwd_x6 = nprod is not None
-    durs = timer.durations_ms()["resblock_conv_fwd"]
+    durs = timer.durations_ms()[tag]
     avg_ms = sum(durs) / max(len(durs), 1)
-    flops = resblock_conv_flops(B, R)
+    if p2p:
+        # the discriminator's model.8 conv (256 -> 512, 4x4 s1): per step one 2B-image launch (D step) and
+        # one B-image launch (G step) -> average B * 1.5 images per launch
+        hw = R // 8 - 1
+        flops = 2.0 * (1.5 * B) * hw * hw * 512 * (256 * 16)
+    else:
+        flops = resblock_conv_flops(B, R)
     achieved = flops / (avg_ms * 1e-3) / 1e12
 
     if rank == 0:
         img_s = world * B * args.steps / elapsed
         out = {
-            "metric": ("GAN training images/sec (512x512, PairedAttention)" if not cycle else
-                       f"GAN training images/sec ({R}x{R}, {m.model} cycle)"),
+            "metric": ("GAN training images/sec (512x512, PairedAttention)" if not (cycle or p2p) else
+                       f"GAN training images/sec ({R}x{R}, {m.model} cycle)" if cycle else
+                       f"GAN training images/sec ({R}x{R}, Pix2Pix)"),
             "value": round(img_s, 3),
             "unit": "img/s",
             "n_gpus": world,
@@ -243,7 +287,9 @@ def main():
                           f"3-ch targets) decoded, staged (pinned ring + copy stream) and transformed (Resize {args.res}, "
                           f"crop={args.crop}, fliplr versions) by floodgan.data.TileLoader inside the timed region"),
             "config": {"workload": (f"PairedAttention paired train step, {R}x{R}, topography=all "
-                                    f"(9-ch G input, 12-ch D input), batch {B}/GPU" if not cycle else
+                                    f"(9-ch G input, 12-ch D input), batch {B}/GPU" if not (cycle or p2p) else
+                                    f"Pix2Pix paired train step (U-Net-256 G with BatchNorm + Dropout, BatchNorm "
+                                    f"PatchGAN), {R}x{R}, topography=all, batch {B}/GPU" if p2p else
                                     f"{m.model} train_cycle step (2 G + 2 D, recreated images, Adam x2), {R}x{R}, "
                                     f"topography=all (9-ch G and D inputs), batch {B}/GPU"),
                        "global_batch": world * B, "per_gpu_batch": B, "resolution": R,
@@ -253,27 +299,37 @@ def main():
                          "kernel": ("conv_fwd_f3_kernel<256,256,32,256,2> (LDS-DMA ring, 8 waves, 16x16x32 f16 MFMA)"
                                     if nprod == 3 else
                                     f"conv_fwd_x6_kernel<MathBF16x6,128,256,64,64>" if fwd_x6 else
-                                    "conv_fwd_kernel<128,128,64,64>") + " resblock 3x3 256->256 @128x128",
+                                    "conv_fwd_kernel<128,128,64,64>") + (
+                                        f" Pix2Pix D model.8 4x4 s1 256->512 @{R // 8 - 1}x{R // 8 - 1}" if p2p else
+                                        " resblock 3x3 256->256 @128x128"),
                          "achieved": round(achieved, 2), "peak": round(peak, 2), "unit": "TFLOP/s",
                          "peak_basis": (f"16-bit dense MFMA 2500 TFLOP/s / {nprod} split products per fp32 MAC"
                                         if fwd_x6 else "fp32 MFMA dense peak"),
                          "frac": round(achieved / peak, 4),
-                         "traffic": pmc_traffic("conv_fwd_f3_kernel<256,256,32,256,2>" if nprod == 3 else None),
+                         "traffic": (None if p2p else
+                                     pmc_traffic("conv_fwd_f3_kernel<256,256,32,256,2>" if nprod == 3 else None)),
                          "avg_launch_ms": round(avg_ms, 4), "launches": len(durs),
                          "flop_per_launch": flops},
             "step_tflops": (None if cycle else
-                            round(STEP_GFLOP_PER_IMG_512 * (R / 512) ** 2 * world * B * args.steps / elapsed / 1e3, 2)),
-            "step_roofline": (None if cycle else step_roofline(img_s / world, R, peak)),
+                            round((p2p_step_gflop_per_img(R) if p2p else STEP_GFLOP_PER_IMG_512 * (R / 512) ** 2)
+                                  * world * B * args.steps / elapsed / 1e3, 2)),
+            "step_roofline": (None if cycle or p2p else step_roofline(img_s / world, R, peak)),
             "losses_last_step": [round(float(v), 5) for v in losses],
         }
         tr = out["roofline"]["traffic"]
+        if p2p:
+            gf = p2p_step_gflop_per_img(R)
+            out["step_roofline"] = {"gflop_per_img": round(gf, 2),
+                                    "ceiling_conv_math_img_s": round(peak * 1e3 / gf, 1),
+                                    "frac_conv_math": round(img_s / world / (peak * 1e3 / gf), 4),
+                                    "basis": "bench.p2p_step_gflop_per_img: MAC FLOPs of every conv of the step"}
         if tr:
             tr["over_algorithmic"] = round(tr["bytes_per_launch"] / resblock_conv_bytes(B, R), 3)
             tr["algorithmic_bytes"] = resblock_conv_bytes(B, R)
         if world == 1 and not args.no_cpu_baseline:
             threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", 0)) or len(os.sched_getaffinity(0))
-            out["cpu_baseline"] = cpu_baseline(R, threads, steps=1 if cycle else 3, workload=args.workload,
-                                               batches=(1,) if cycle else (1, 8))
+            out["cpu_baseline"] = cpu_baseline(R, threads, steps=1 if cycle or p2p else 3, workload=args.workload,
+                                               batches=(1,) if cycle or p2p else (1, 8))
         print(json.dumps(out), flush=True)
     if loader is not None:
         import shutil

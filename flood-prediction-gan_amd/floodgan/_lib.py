@@ -133,10 +133,12 @@ SIGNATURES = {
     "fg_bn_stats": [fg_view, C.c_int, C.c_float, C.c_float, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                     C.c_void_p, C.c_void_p, C.c_void_p],
     "fg_bn_eval_stats": [C.c_int, C.c_void_p, C.c_void_p, C.c_float, C.c_void_p, C.c_void_p, C.c_void_p],
-    "fg_bn_apply": [fg_view, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_float, C.c_int,
-                    fg_view, C.c_void_p, C.c_int, fg_view, C.c_void_p, C.c_void_p],
+    "fg_bn_apply": [fg_view, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_float,
+                    C.c_ulonglong, C.c_int, fg_view, C.c_void_p, C.c_int, fg_view, C.c_void_p, C.c_void_p],
     "fg_bn_bwd": [fg_view, C.c_int, fg_view, C.c_int, fg_view, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
-                  C.c_void_p, C.c_float, fg_view, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p],
+                  C.c_void_p, C.c_float, C.c_ulonglong, fg_view, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p,
+                  C.c_void_p, C.c_void_p],
+    "fg_dropout_mask": [C.c_ulonglong, C.c_float, C.c_longlong, C.c_void_p, C.c_void_p],
     "fg_maxpool2": [fg_view, fg_view, C.c_void_p],
     "fg_tiff_probe": [C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)],
     "fg_tiff_read": [C.c_char_p, C.c_void_p, C.c_longlong],

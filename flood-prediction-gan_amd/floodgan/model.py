@@ -130,7 +130,7 @@ class Pix2PixStep(PairedStep):
         losses = torch.empty(4, dtype=torch.float32, device=dev)
         self.gflat.attach()
         self.dflat.attach()
-        masks = self.masks if self.masks is not None else P2P.draw_dropout_masks(N, H, W)
+        masks = self.masks if self.masks is not None else P2P.draw_dropout(N, H, W, self.G.dropout_rng)
         self.last_masks = masks
         fake, gS = P2P.gen_forward(self.gp, self.gb, x, masks=masks, training=True, save=True)
         dinp = X.disc_pack([(x, fake), (x, y)], C + 3)

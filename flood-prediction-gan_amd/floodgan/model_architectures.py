@@ -386,7 +386,10 @@ class Pix2PixBlock(nn.Module):
 class Pix2PixGenerator(nn.Module):
     """models/model_architectures.py:9-22 -- U-Net-256: eight Pix2PixBlocks, innermost first.  The
     whole network is one autograd node on floodgan.pix2pix; BatchNorm running statistics are updated
-    in place, Dropout masks come from torch's CPU generator in the reference's order."""
+    in place.  dropout_rng: "device" (default; hashed keep decisions seeded from torch's CPU generator)
+    or "host" (masks drawn exactly as the reference's CPU path draws them; see floodgan.pix2pix)."""
+
+    dropout_rng = "device"
 
     def __init__(self, input_channels):
         super().__init__()
@@ -406,7 +409,8 @@ class Pix2PixGenerator(nn.Module):
         return dict(self.named_buffers())
 
     def forward(self, input):
-        masks = P2P.draw_dropout_masks(input.shape[0], input.shape[2], input.shape[3]) if self.training else None
+        masks = (P2P.draw_dropout(input.shape[0], input.shape[2], input.shape[3], self.dropout_rng) if self.training
+                 else None)
         return _Pix2PixGeneratorFn.apply(self.buffer_dict(), self.training, masks, input,
                                          *self.param_dict().values())
 

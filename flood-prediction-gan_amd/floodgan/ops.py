@@ -504,23 +504,46 @@ def bn_eval_stats(running_mean, running_var, eps=EPS):
     return mean, invstd
 
 
-def bn_apply(src, groups, mean, invstd, gamma, beta, mask, act0, dst0, act1=0, dst1=None, slots=(None, None)):
-    """dst0 = act0(BN(src) * mask / 0.5), dst1 = act1(same) (interiors; Buf or Slice destinations);
-    mean None = no normalisation; mask None = no dropout"""
+DROP_SCALE = 2.0      # nn.Dropout(0.5): kept elements x 1 / (1 - p)
+
+
+def _drop_args(drop):
+    """drop: None, a 0/1 NCHW mask tensor, or an int seed (device-hashed keep decisions)"""
+    if drop is None:
+        return C.c_void_p(0), 0
+    if isinstance(drop, int):
+        assert drop > 0
+        return C.c_void_p(0), drop
+    return L.ptr(drop), 0
+
+
+def bn_apply(src, groups, mean, invstd, gamma, beta, drop, act0, dst0, act1=0, dst1=None, slots=(None, None)):
+    """dst0 = act0(BN(src) * keep * 2), dst1 = act1(same) (interiors; Buf or Slice destinations);
+    mean None = no normalisation; drop: None, a 0/1 mask tensor or a seed (see _drop_args)"""
     s0, s1 = _dst_slot(dst0, slots[0]), _dst_slot(dst1, slots[1])
-    L.check(_lib().fg_bn_apply(view(src), groups, L.ptr(mean), L.ptr(invstd), L.ptr(gamma), L.ptr(beta),
-                               L.ptr(mask), C.c_float(2.0), act0, view(dst0), L.ptr(s0), act1, view(dst1),
-                               L.ptr(s1), L.stream_handle()), "bn_apply")
+    mask, seed = _drop_args(drop)
+    L.check(_lib().fg_bn_apply(view(src), groups, L.ptr(mean), L.ptr(invstd), L.ptr(gamma), L.ptr(beta), mask,
+                               C.c_float(DROP_SCALE), seed, act0, view(dst0), L.ptr(s0), act1, view(dst1), L.ptr(s1),
+                               L.stream_handle()), "bn_apply")
 
 
-def bn_bwd(gA, actA, gB, actB, src, groups, mean, invstd, gamma, beta, mask, dst, gamma_grad=None, beta_grad=None,
+def bn_bwd(gA, actA, gB, actB, src, groups, mean, invstd, gamma, beta, drop, dst, gamma_grad=None, beta_grad=None,
            accumulate=False):
     """dst = dL/dsrc of bn_apply, the incoming gradient being gA * actA'(u) (+ gB * actB'(u))"""
     slot = _dst_slot(dst, None)
+    mask, seed = _drop_args(drop)
     L.check(_lib().fg_bn_bwd(view(gA), actA, view(gB), actB, view(src), groups, L.ptr(mean), L.ptr(invstd),
-                             L.ptr(gamma), L.ptr(beta), L.ptr(mask), C.c_float(2.0), view(dst), L.ptr(gamma_grad),
-                             L.ptr(beta_grad), int(accumulate), L.ptr(_bn_work(src.n, src.c, src.t.device)),
-                             L.ptr(slot), L.stream_handle()), "bn_bwd")
+                             L.ptr(gamma), L.ptr(beta), mask, C.c_float(DROP_SCALE), seed, view(dst),
+                             L.ptr(gamma_grad), L.ptr(beta_grad), int(accumulate),
+                             L.ptr(_bn_work(src.n, src.c, src.t.device)), L.ptr(slot), L.stream_handle()), "bn_bwd")
+
+
+def dropout_mask(seed, shape, device):
+    """the 0/1 keep decisions bn_apply makes for `seed` over a tensor of NCHW `shape` (float32, device)"""
+    out = torch.empty(shape, dtype=torch.float32, device=device)
+    L.check(_lib().fg_dropout_mask(seed, C.c_float(1.0 / DROP_SCALE), out.numel(), L.ptr(out), L.stream_handle()),
+            "dropout_mask")
+    return out
 
 
 def maxpool2(src, dst):

@@ -16,9 +16,15 @@ border is the next conv's padding:
 The up convs (ConvTranspose2d 4x4 s2 p1) run as four sub-pixel phase GEMMs; the outermost one adds
 its bias and feeds the tanh head.  BatchNorm (training mode: batch statistics, running statistics
 updated in place on the module buffers; eval mode: running statistics) is one statistics pass and
-one apply pass that also writes the activated copies.  Dropout(0.5) of levels 5-7 multiplies by a
-0/1 mask the caller draws with torch's CPU generator in the reference's order (innermost first:
-levels 7, 6, 5) -- the same draws as the reference's CPU path, so a seeded run reproduces it.
+one apply pass that also writes the activated copies.  Dropout(0.5) of levels 5-7 is fused into the
+BatchNorm apply / backward passes, its keep decisions either
+  "device" (default): a counter-based hash of (seed, element) evaluated in the apply pass and
+             recomputed in the backward -- no mask is drawn, stored or copied; one 62-bit seed per
+             generator call comes from torch's CPU generator, so torch.manual_seed fixes the masks; or
+  "host":    0/1 masks drawn with torch's CPU generator exactly as the reference's CPU path draws them
+             (F.dropout: empty_like(x).bernoulli_(0.5), innermost level first: 7, 6, 5) and copied to
+             the device -- a seeded run then reproduces the reference's CPU run (the parity mode; a
+             512x512 batch of 8 costs ~0.1 s of host time per call).
 
 The discriminator's D(fake) and D(real) of the D step are separate BatchNorm calls in the
 reference (:624-628): one 2N-image pass with groups=2 (statistics per half, the running statistics
@@ -102,14 +108,44 @@ def disc_bucket_names():
             ["model.0.weight", "model.0.bias"]]
 
 
+def _mix64(z):
+    z = (z + 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+    return z ^ (z >> 31)
+
+
+def dropout_shapes(n, h, w):
+    """{level: NCHW shape of the tensor its Dropout applies to} at input h x w"""
+    return {k: (n, 512, h >> (k - 1), w >> (k - 1)) for k in DROPOUT_LEVELS}
+
+
+def draw_dropout(n, h, w, mode="device"):
+    """One generator call's Dropout decisions: {level: host 0/1 mask} ("host") or {level: seed} ("device")"""
+    if mode == "host":
+        return draw_dropout_masks(n, h, w)
+    if mode != "device":
+        raise ValueError(f"dropout mode must be 'device' or 'host' (got {mode!r})")
+    base = int(torch.randint(1, 2 ** 62, (1,)).item())
+    return {k: (_mix64(base + k) & 0x7FFFFFFFFFFFFFFF) or 1 for k in DROPOUT_LEVELS}
+
+
+def dropout_masks(drop, n, h, w, device="cuda"):
+    """{level: 0/1 mask} of a draw_dropout result (seeds materialised on the device; tests / inspection)"""
+    out = {}
+    for k, shape in dropout_shapes(n, h, w).items():
+        d = drop[k]
+        out[k] = ops.dropout_mask(d, shape, device) if isinstance(d, int) else d
+    return out
+
+
 def draw_dropout_masks(n, h, w):
     """The Dropout masks of one generator call at input h x w, from torch's (CPU) global generator in
     the reference's CPU order: F.dropout draws empty_like(x).bernoulli_(1 - p) per call, levels 7, 6, 5.
     Returns {level: float32 0/1 mask [n, 512, h_k, w_k]} on the host."""
     masks = {}
-    for k in DROPOUT_LEVELS:
-        s = 2 ** (k - 1)                   # level k's up output = its input size
-        masks[k] = torch.empty((n, 512, h // s, w // s), dtype=torch.float32).bernoulli_(1 - DROP_P)
+    for k, shape in dropout_shapes(n, h, w).items():      # level k's up output = its input size
+        masks[k] = torch.empty(shape, dtype=torch.float32).bernoulli_(1 - DROP_P)
     return masks
 
 
@@ -117,11 +153,12 @@ def draw_dropout_masks(n, h, w):
 # generator
 # ======================================================================================
 
-def _conv_nb(P, name, X_, pad, k, stride, Y, act=FG_ACT_NONE):
+def _conv_nb(P, name, X_, pad, k, stride, Y, act=FG_ACT_NONE, tag=None):
     """conv whose module may have no bias (bias=False in the reference)"""
     w = P[name + ".weight"]
     m = PL.wmap_conv_fwd(w.shape, X_.c)
-    ops.conv([PL.conv_problem(X_, pad, k, stride, ops.pack_weight(w, m), m, Y, bias=P.get(name + ".bias"), act=act)])
+    ops.conv([PL.conv_problem(X_, pad, k, stride, ops.pack_weight(w, m), m, Y, bias=P.get(name + ".bias"), act=act)],
+             tag=tag)
 
 
 def _convT4(P, name, X_, Y):
@@ -151,15 +188,15 @@ def check_input_size(H, W):
 
 def gen_forward(P, B, x, masks=None, training=True, save=True):
     """x: [N, C, H, W] fp32 on the device (any strides); P: parameters, B: BatchNorm buffers (updated
-    in place in training mode), masks: {level: host 0/1 mask} (training mode; drawn here when None).
-    Returns (out [N, 3, H, W], saved)."""
+    in place in training mode), masks: a draw_dropout result (training mode; drawn here, device mode,
+    when None).  Returns (out [N, 3, H, W], saved)."""
     require_device(x, "generator input")
     N, Cin, H, W = x.shape
     check_input_size(H, W)
     dev = x.device
     if training and masks is None:
-        masks = draw_dropout_masks(N, H, W)
-    dmask = {k: m.to(dev, non_blocking=False) for k, m in masks.items()} if training else {}
+        masks = draw_dropout(N, H, W)
+    dmask = {k: (m if isinstance(m, int) else m.to(dev)) for k, m in masks.items()} if training else {}
     ch = level_channels(Cin)
     S = dict(x=x, N=N, H=H, W=W, training=training, lv={})
     X0 = Buf.empty(N, H, W, PL.rup(Cin, 4), 1, dev)
@@ -322,7 +359,7 @@ def disc_forward(P, B, inp, groups=1, training=True, save=True):
         norm = DISC_NORMS[conv]
         hh, ww = PL.out_size(prev.h, 4, stride, 1), PL.out_size(prev.w, 4, stride, 1)
         e = Buf.empty(N, hh, ww, c, 0, dev)
-        _conv_nb(P, conv, prev, 1, 4, stride, e)
+        _conv_nb(P, conv, prev, 1, 4, stride, e, tag="p2p_d_model8_fwd" if conv == "model.8" else None)
         mean, invstd = _stats(B, norm, e, groups, training)
         a = Buf.zeros(N, hh, ww, c, 1, dev)
         ops.bn_apply(e, groups, mean, invstd, P[norm + ".weight"], P[norm + ".bias"], None, FG_ACT_LRELU, a)

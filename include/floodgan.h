@@ -360,20 +360,26 @@ int fg_bn_stats(fg_view src, int groups, float eps, float momentum, float* mean,
 int fg_bn_eval_stats(int c, const float* running_mean, const float* running_var, float eps, float* mean,
                      float* invstd, hipStream_t stream);
 /* y = (x - mean) * invstd * gamma + beta (no normalisation when mean is NULL, no affine when gamma
- * is NULL), then y *= drop_mask * drop_scale (nn.Dropout with a caller-drawn NCHW 0/1 mask, optional),
- * dst0 = act0(y) and optionally dst1 = act1(y): interiors only; a destination may be a channel
- * slice of a wider buffer (ptr offset, c_alloc = the wider buffer's channels). */
+ * is NULL), then nn.Dropout: y *= keep(n, c, y, x) * drop_scale (drop_scale = 1 / (1 - p)), with keep
+ * read from a caller-drawn NCHW 0/1 drop_mask or -- drop_mask NULL, drop_seed != 0 -- decided on the
+ * device by a counter-based hash of (drop_seed, NCHW element index) with probability 1 / drop_scale
+ * (fg_dropout_mask materialises the same decisions); dst0 = act0(y) and optionally dst1 = act1(y):
+ * interiors only; a destination may be a channel slice of a wider buffer (ptr offset, c_alloc = the
+ * wider buffer's channels). */
 int fg_bn_apply(fg_view src, int groups, const float* mean, const float* invstd, const float* gamma,
-                const float* beta, const float* drop_mask, float drop_scale, int act0, fg_view dst0,
-                float* absmax0, int act1, fg_view dst1, float* absmax1, hipStream_t stream);
+                const float* beta, const float* drop_mask, float drop_scale, unsigned long long drop_seed, int act0,
+                fg_view dst0, float* absmax0, int act1, fg_view dst1, float* absmax1, hipStream_t stream);
 /* Backward of fg_bn_apply: the incoming gradient of the normalised, dropped-out value u is
- * gA * actA'(u) (+ gB * actB'(u) when gB.ptr), times the dropout mask * scale; dst = dL/dx through the
- * batch statistics of each group (identity when mean is NULL); gamma_grad / beta_grad (written, or
- * added to when accumulate) summed over the groups. */
+ * gA * actA'(u) (+ gB * actB'(u) when gB.ptr), times the dropout keep * scale (the same mask or seed as
+ * the forward); dst = dL/dx through the batch statistics of each group (identity when mean is NULL);
+ * gamma_grad / beta_grad (written, or added to when accumulate) summed over the groups. */
 int fg_bn_bwd(fg_view gA, int actA, fg_view gB, int actB, fg_view src, int groups, const float* mean,
               const float* invstd, const float* gamma, const float* beta, const float* drop_mask,
-              float drop_scale, fg_view dst, float* gamma_grad, float* beta_grad, int accumulate,
-              double* work, float* absmax, hipStream_t stream);
+              float drop_scale, unsigned long long drop_seed, fg_view dst, float* gamma_grad, float* beta_grad,
+              int accumulate, double* work, float* absmax, hipStream_t stream);
+/* The 0/1 keep decisions of fg_bn_apply's hashed dropout for elements 0 .. total-1 (NCHW order of the
+ * tensor the dropout applies to) into dst as floats (tests / host inspection). */
+int fg_dropout_mask(unsigned long long seed, float keep, long long total, float* dst, hipStream_t stream);
 /* nn.MaxPool2d(2) over NHWC interiors (floor output size). */
 int fg_maxpool2(fg_view src, fg_view dst, hipStream_t stream);
 

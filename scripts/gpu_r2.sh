@@ -31,6 +31,6 @@ if [ "${PROF:-0}" = 1 ]; then
   mkdir -p "$P"
   cd /tmp
   run prof 600 rocprofv3 --kernel-trace --stats -d "$P" -o prof --output-format csv -- \
-      python3 "$REPO/bench.py" --steps ${PSTEPS:-4} --warmup 2 --no-cpu-baseline
+      python3 "$REPO/bench.py" --steps ${PSTEPS:-4} --warmup 2 --no-cpu-baseline ${BENCH_ARGS}
 fi
 echo "session done"

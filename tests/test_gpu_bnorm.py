@@ -29,7 +29,7 @@ def _ref_fwd(x, groups, gamma, beta, rm, rv, mask):
 
 
 CASES = [(2, 64, 8, 8, 1, False), (4, 128, 16, 12, 2, True), (2, 512, 1, 1, 1, False), (2, 512, 2, 2, 1, True),
-         (6, 256, 4, 4, 3, False), (1, 64, 64, 64, 1, True)]
+         (6, 256, 4, 4, 3, False), (1, 64, 64, 64, 1, True), (8, 64, 64, 64, 2, True)]
 
 
 @pytest.mark.parametrize("n,c,h,w,groups,drop", CASES)
@@ -127,3 +127,37 @@ def test_maxpool2(h, w):
     ops.maxpool2(buf_from(x, 1, "constant"), dst)
     torch.cuda.synchronize()
     assert torch.equal(nchw(dst).double(), F.max_pool2d(x.float(), 2).double())
+
+
+def test_hashed_dropout_equals_its_mask():
+    """Device dropout (keep decisions hashed from (seed, NCHW index), recomputed in the backward) gives
+    exactly the result of the same decisions passed as a mask; the decisions are Bernoulli(0.5):
+    the kept fraction and its independence across seeds / neighbouring elements."""
+    from floodgan import _lib as L
+    from floodgan import ops
+    from floodgan.plans import Buf
+
+    g = torch.Generator().manual_seed(11)
+    n, c, h, w = 2, 512, 16, 16
+    x = torch.randn(n, c, h, w, generator=g, dtype=torch.float64)
+    gA = torch.randn(n, c, h, w, generator=g, dtype=torch.float64)
+    gamma, beta = torch.ones(c, device=DEV), torch.zeros(c, device=DEV)
+    src = buf_from(x, 0, "constant")
+    seed = 0x1234_5678_9ABC
+    mask = ops.dropout_mask(seed, (n, c, h, w), DEV)
+    outs = []
+    for drop in (seed, mask):
+        mean, invstd = ops.bn_stats(src, 1)
+        d = Buf.zeros(n, h, w, c, 1, DEV)
+        ops.bn_apply(src, 1, mean, invstd, gamma, beta, drop, L.FG_ACT_RELU, d)
+        gd = Buf.zeros(n, h, w, c, 1, DEV)
+        ops.bn_bwd(buf_from(gA, 0, "constant"), L.FG_ACT_RELU, None, 0, src, 1, mean, invstd, gamma, beta, drop, gd)
+        torch.cuda.synchronize()
+        outs.append((nchw(d), nchw(gd)))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    m = mask.cpu().double()
+    assert set(m.unique().tolist()) == {0.0, 1.0}
+    assert abs(float(m.mean()) - 0.5) < 0.005                                # 262144 draws: sd 0.001
+    m2 = ops.dropout_mask(seed + 1, (n, c, h, w), DEV).cpu().double()
+    assert abs(float(((m - 0.5) * (m2 - 0.5)).mean())) < 0.005              # seeds independent
+    assert abs(float(((m[..., 1:] - 0.5) * (m[..., :-1] - 0.5)).mean())) < 0.005   # neighbours independent

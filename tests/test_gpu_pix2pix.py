@@ -80,6 +80,7 @@ def test_p1_forward_and_running_stats(report):
 def test_update_teacher_forced(report):
     """Two fused iterations at 256x256, batch 2 (the golden inputs), each checked against the fp64
     oracle continuing from the HIP state with the HIP masks and decisions."""
+    from floodgan import pix2pix as P2P
     m = _model()
     G, D = m.generator, m.discriminator
     step = m.step_fn
@@ -98,7 +99,8 @@ def test_update_teacher_forced(report):
         torch.cuda.synchronize()
         rec = {}
         dec = O.ActDecisions(step.decisions)
-        st.step(x, y, record=rec, masks=dict(step.last_masks), decisions=dec,
+        masks = {k: v.cpu() for k, v in P2P.dropout_masks(step.last_masks, 2, R, R).items()}
+        st.step(x, y, record=rec, masks=masks, decisions=dec,
                 d_after={k: v.detach().cpu() for k, v in D.named_parameters()})
         rows, bad = [], []
         for net, mod, P0, grads, opt_ref in (("G", G, g0, rec["g_grads"], st.opt_g), ("D", D, d0, rec["d_grads"],
@@ -164,12 +166,13 @@ def test_train_paired_vs_reference_golden(report):
             return iter([(x, y, ["synthetic"] * 2)])
 
     m = _model(train_loader=_Loader())
+    m.generator.dropout_rng = "host"          # the reference's CPU draws, mask for mask
     orig = m.save_results
 
     def _record(epoch, losses, t0):
         with torch.no_grad(), torch.random.fork_rng(devices=[]):
             torch.manual_seed(99)
-            g = copy.deepcopy(m.generator)(x0)
+            g = copy.deepcopy(m.generator)(x0)           # the copy keeps dropout_rng = "host"
             d = copy.deepcopy(m.discriminator)(torch.cat((x0, y0), 1))
         recorded.append(([losses[k][-1] for k in ("losses_discriminator_real", "losses_discriminator_synthetic",
                                                   "losses_generator_synthetic", "l1_losses_generator_synthetic")],
