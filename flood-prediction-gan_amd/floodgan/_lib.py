@@ -139,12 +139,22 @@ SIGNATURES = {
                   C.c_void_p, C.c_float, C.c_ulonglong, fg_view, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p,
                   C.c_void_p, C.c_void_p],
     "fg_dropout_mask": [C.c_ulonglong, C.c_float, C.c_longlong, C.c_void_p, C.c_void_p],
+    "fg_unit_image": [fg_sview, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, fg_view, C.c_void_p],
+    "fg_ssim_workspace_doubles": [C.c_int, C.c_int, C.c_int, C.c_int],
+    "fg_ssim": [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_float, C.c_float,
+                C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p],
+    "fg_avg_pool2": [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p],
+    "fg_msssim_combine": [C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p],
+    "fg_sq_err_workspace_doubles": [],
+    "fg_sq_err_sum": [C.c_void_p, C.c_void_p, C.c_longlong, C.c_void_p, C.c_void_p, C.c_void_p],
+    "fg_mask_confusion": [fg_view, fg_view, C.c_void_p, C.c_void_p],
     "fg_maxpool2": [fg_view, fg_view, C.c_void_p],
     "fg_tiff_probe": [C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)],
     "fg_tiff_read": [C.c_char_p, C.c_void_p, C.c_longlong],
     "fg_tile_transform": [C.POINTER(fg_tile_batch), C.c_void_p],
 }
 RESTYPES = {"fg_last_error": C.c_char_p, "fg_in_workspace_doubles": C.c_longlong, "fg_bn_workspace_doubles": C.c_longlong,
+            "fg_ssim_workspace_doubles": C.c_longlong, "fg_sq_err_workspace_doubles": C.c_longlong,
             "fg_channel_sum_workspace_doubles": C.c_longlong}
 
 _lib = None

@@ -176,7 +176,8 @@ class Model:
     def __init__(self, model="PairedAttention", dataset_subset="all", dataset_dem="best", data_path=None,
                  num_epochs=1, topography="all", resize=256, crop=None, save_model_interval=0,
                  save_images_interval=0, verbose=False, load_pretrained_model=False, pretrained_model_path=None,
-                 add_identity_loss=False, training_model=True, seed=47, device="cuda", train_loader=None):
+                 add_identity_loss=False, training_model=True, seed=47, device="cuda", train_loader=None,
+                 val_loader=None, test_loader=None):
         saved = None
         if load_pretrained_model:
             # models/model.py:52-57: the checkpoint, not the `model` argument, names the architecture
@@ -237,7 +238,7 @@ class Model:
         self.current_epoch = self.starting_epoch
         # The tile pipeline (tifffile decode, resize, crop; models/data.py) is outside this
         # build's scope: assign any iterable of (input [N,C,H,W], target [N,3,H,W], names).
-        self.train_loader = train_loader
+        self.train_loader, self.val_loader, self.test_loader = train_loader, val_loader, test_loader
         self._step = None
 
     def _cycle_nets(self):
@@ -342,6 +343,29 @@ class Model:
             self.scheduler_generator.step()
             self.scheduler_discriminator.step()
             self.save_results(epoch, losses, t0)
+
+    def calculate_metrics(self, use_test_data=False, seg_model_path=None, seg_model=None):
+        """models/model.py:363-422 on the device (floodgan.evaluate): the generator (pre_to_post for the
+        cycle models) over the validation / test loader, PSNR / SSIM / MS-SSIM of its [0, 1] outputs,
+        the segmentation U-Net's flood masks of output and target and their binary metrics.  Returns
+        the one-row DataFrame the reference prints (and writes it under data_path/metrics/ when set)."""
+        import pandas as pd
+
+        from .evaluate import calculate_metrics, segmentation_model
+        loader = self.test_loader if use_test_data else self.val_loader
+        if loader is None:
+            raise RuntimeError("assign Model.val_loader / Model.test_loader first (floodgan.data.create_flood_dataset)")
+        seg = seg_model if seg_model is not None else segmentation_model(seg_model_path, self.device)
+        gen = self.pre_to_post_generator if self.model_is_cycle else self.generator
+        res = calculate_metrics(gen, loader, seg, self.topography, self.device)
+        df = pd.DataFrame([res])
+        if self.verbose:
+            print(df)
+        if self.data_path:
+            import os
+            os.makedirs(f"{self.data_path}/metrics", exist_ok=True)
+            df.to_csv(f"{self.data_path}/metrics/{self.model}_metrics_epoch{self.current_epoch - 1}.csv", index=False)
+        return df
 
     def save_results(self, epoch, losses, epoch_start_time):
         """models/model.py:322-358 (loss bookkeeping + checkpoint; plots are out of scope)."""

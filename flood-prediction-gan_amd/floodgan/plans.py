@@ -97,8 +97,21 @@ class Slice:
     def t(self):
         return self.buf.t
 
+    n = property(lambda self: self.buf.n)
+    h = property(lambda self: self.buf.h)
+    w = property(lambda self: self.buf.w)
+
     def interior(self):
         return self.buf.interior()[..., self.c0:self.c0 + self.c]
+
+
+def _ydesc(Y):
+    """(storage object, element offset of image 0 pixel (py, px) fn, s_img, s_row, pixel stride) of a conv
+    output Buf or Slice (a slice is written with its buffer's strides, channels shifted by c0)"""
+    if isinstance(Y, Slice):
+        b = Y.buf
+        return b, (lambda y, x: b.off(y, x) + Y.c0), b.s_img, b.s_row, b.c, Y.c
+    return Y, Y.off, Y.s_img, Y.s_row, Y.c, Y.c
 
 
 def out_size(h, k, s, p):
@@ -183,8 +196,9 @@ def conv_problem(X, pad_used, k, stride, wp, wmap, Y, bias=None, act=0, accumula
                 m_img=X.n, m_a=Ho, m_b=Wo, kh=k, j_valid=k * X.c, jp=wmap["jp"],
                 n_out=wmap["n_out"], ldw=k * wmap["jp"], act=act, accumulate=accumulate)
     if y_nchw is None:
-        assert (Y.h, Y.w, Y.n) == (Ho, Wo, X.n) and Y.c >= wmap["n_out"], (Y, Ho, Wo)
-        prob.update(y=(Y, Y.off(0, 0)), syn=Y.s_img, sya=Y.s_row, syb=Y.c, syc=1)
+        obj, off, s_img, s_row, pix, cw = _ydesc(Y)
+        assert (Y.h, Y.w, Y.n) == (Ho, Wo, X.n) and cw >= wmap["n_out"], (Y, Ho, Wo)
+        prob.update(y=(obj, off(0, 0)), syn=s_img, sya=s_row, syb=pix, syc=1)
     else:
         t, Cc, Hh, Ww = y_nchw
         assert (Hh, Ww) == (Ho, Wo)
@@ -212,7 +226,8 @@ def phase_problems(S, shape, k, p, Y, wp_list, maps, bias=None, act=0, accumulat
                     m_img=S.n, m_a=ma, m_b=mb, kh=m["kh"], j_valid=m["kw"] * S.c, jp=m["jp"],
                     n_out=m["n_out"], ldw=m["kh"] * m["jp"], act=act, accumulate=accumulate)
         if y_nchw is None:
-            prob.update(y=(Y, Y.off(py, px)), syn=Y.s_img, sya=2 * Y.s_row, syb=2 * Y.c, syc=1)
+            obj, off, s_img, s_row, pix, _ = _ydesc(Y)
+            prob.update(y=(obj, off(py, px)), syn=s_img, sya=2 * s_row, syb=2 * pix, syc=1)
         else:
             t = y_nchw[0]
             prob.update(y=(t, py * Wo + px), syn=Cc * Ho * Wo, sya=2 * Wo, syb=2, syc=Ho * Wo)

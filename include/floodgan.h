@@ -384,6 +384,31 @@ int fg_dropout_mask(unsigned long long seed, float keep, long long total, float*
 int fg_maxpool2(fg_view src, fg_view dst, hipStream_t stream);
 
 /* ---------------------------------------------------------------------------------------- */
+/* evaluation metrics (models/model.py:363-422, models/group.py:114-221) */
+/* ---------------------------------------------------------------------------------------- */
+/* torch.clamp((src + 1) * 0.5, 0, 1) of an [n, c, h, w] (strided) generator output into dst (contiguous
+ * NCHW, optional) and into buf's interior channels 0..c-1 (NHWC, optional: the segmentation U-Net's input). */
+int fg_unit_image(fg_sview src, int n, int c, int h, int w, float* dst, fg_view buf, hipStream_t stream);
+/* SSIM of two contiguous NCHW [n, c, h, w] images in [0, 1] (torchmetrics 1.2.0 _ssim_update: gaussian
+ * 11x11 window gauss11 (normalised 1-D taps), constants c1 = (0.01 dr)^2, c2 = (0.03 dr)^2; the mean runs
+ * over channels and the (h-10) x (w-10) windows inside the image): ssim[i], cs[i] (each optional) = per
+ * image means of the SSIM and contrast-sensitivity maps.  work >= fg_ssim_workspace_doubles(). */
+long long fg_ssim_workspace_doubles(int n, int c, int h, int w);
+int fg_ssim(const float* a, const float* b, int n, int c, int h, int w, const float* gauss11, float c1, float c2,
+            double* ssim, double* cs, double* work, hipStream_t stream);
+/* F.avg_pool2d(x, 2) over `planes` contiguous h x w planes (floor). */
+int fg_avg_pool2(const float* src, int planes, int h, int w, float* dst, hipStream_t stream);
+/* MS-SSIM per image: prod_s relu(m_s)^betas[s], m = cs[s * n + i] for s < scales-1, ssim_last[i] last. */
+int fg_msssim_combine(int n, int scales, const double* cs, const double* ssim_last, const double* betas,
+                      double* out, hipStream_t stream);
+/* out[0] = sum (a - b)^2 over `total` floats (PSNR); work >= fg_sq_err_workspace_doubles(). */
+long long fg_sq_err_workspace_doubles(void);
+int fg_sq_err_sum(const float* a, const float* b, long long total, double* out, double* work, hipStream_t stream);
+/* counts[0..3] += true positives, false positives, true negatives, false negatives of the flood masks
+ * (sigmoid(logit) > 0.5, channel 0 of each view) of pred vs true segmentation logits. */
+int fg_mask_confusion(fg_view pred_logits, fg_view true_logits, unsigned long long* counts, hipStream_t stream);
+
+/* ---------------------------------------------------------------------------------------- */
 /* tile data path                                                    */
 /* ---------------------------------------------------------------------------------------- */
 /* Host-side baseline TIFF decode, replacing tifffile.imread (models/data.py:64-68) for the files
