@@ -8,6 +8,8 @@ autograd-facing drop-in modules (floodgan.model_architectures) and the fused tra
 Reference: models/model_architectures.py:339-400 (generator forward), :412-418 (resnet
 block), :424-441 (discriminator); backward = autograd of those graphs.
 """
+import os
+
 import torch
 
 from . import ops
@@ -39,14 +41,41 @@ def disc_bucket_names():
     return [[f"{layer}.{k}" for k in ("weight", "bias")] for layer in reversed(DISC_LAYERS)]
 
 
+# Off by default: measured at the bs-8 512^2 step (profiles/round2/r2m_*), the side-stream weight gradients
+# do run concurrently with the input-gradient chain, but every kernel then slows by the same factor (the
+# pipelined convs already hold every CU): 57.3 ms per step vs 56.6 on one stream.
+SIDE_STREAM = os.environ.get("FLOODGAN_SIDE_STREAM", "0") == "1"
+_SIDE_STREAMS = {}
+
+
+def _side_stream(device):
+    key = torch.device(device).index
+    if key not in _SIDE_STREAMS:
+        _SIDE_STREAMS[key] = torch.cuda.Stream(device=device)
+    return _SIDE_STREAMS[key]
+
+
 class _Grads:
     """Destination of parameter gradients: either fresh tensors (autograd path) or
-    preallocated .grad tensors (fused step)."""
+    preallocated .grad tensors (fused step).
 
-    def __init__(self, params, into=None, accumulate=False):
+    The weight gradients are off the backward's critical path -- nothing but the optimiser step
+    reads them -- so they run on a second HIP stream (side), overlapping the chain of input
+    gradients and norm backward passes that each next layer waits on.  A side launch waits for the
+    main stream's work so far; its operand buffers are recorded on the side stream (the caching
+    allocator then cannot hand their memory to a main-stream allocation while the side kernels still
+    read it) and their cached operand scales / split copies are computed on the main stream first
+    (a cache filled on the side stream could be read by a later main-stream kernel before it is
+    written).  join() makes the main stream wait for every side launch; ready() starts a gradient
+    bucket's all-reduce from the side stream, after both streams' writes to it."""
+
+    def __init__(self, params, into=None, accumulate=False, device=None):
         self.params, self.into = params, into
         self.acc = accumulate       # raise existing gradients (a network used several times per step)
         self.out = {}
+        self.side = _side_stream(device) if SIDE_STREAM and device is not None and torch.device(device).type == "cuda" \
+            else None
+        self.main = torch.cuda.current_stream(device) if self.side is not None else None
 
     def get(self, name):
         if name not in self.out:
@@ -56,6 +85,36 @@ class _Grads:
             else:
                 self.out[name] = torch.empty_like(p)
         return self.out[name]
+
+    def off_path(self, fn, bufs, names=(), prepare=None):
+        """run fn() (weight-gradient launches reading the Bufs `bufs`, writing the gradients `names`)
+        on the side stream; prepare() fills their operand caches on the main stream first"""
+        for n in names:
+            self.get(n)                                   # allocated on the main stream
+        if self.side is None:
+            return fn()
+        if prepare is not None:
+            prepare()
+        self.side.wait_stream(self.main)
+        with torch.cuda.stream(self.side):
+            fn()
+        for b in bufs:
+            b.t.record_stream(self.side)
+
+    def wgrad(self, prob, wmap, name, bufs):
+        self.off_path(lambda: ops.wgrad(prob, wmap, self.get(name), accumulate=self.acc), bufs, (name,),
+                      prepare=lambda: ops.prepare_wgrad(prob))
+
+    def ready(self, ready, name):
+        if self.side is None:
+            return ready(name)
+        self.side.wait_stream(self.main)
+        with torch.cuda.stream(self.side):
+            ready(name)
+
+    def join(self):
+        if self.side is not None:
+            self.main.wait_stream(self.side)
 
 
 # ======================================================================================
@@ -165,7 +224,8 @@ def _block_fwd(P, pre, h, out_mode):
 
 
 def _block_bwd(P, pre, b, g_h, G):
-    """Backward of _block_fwd: g_h = dL/d(block output) (compact) -> dL/d(block input)."""
+    """Backward of _block_fwd: g_h = dL/d(block output) (compact) -> dL/d(block input).  The caller
+    joins G's side stream."""
     N, Hh, Ww, Cc = g_h.n, g_h.h, g_h.w, g_h.c
     dev = g_h.t.device
     g_cb2 = Buf.empty(N, Hh, Ww, Cc, 2, dev)          # zero border 2: full correlation of a 3x3
@@ -203,8 +263,9 @@ def block_backward_nchw(S, g, need_input=True):
     N, Cc, Hh, Ww = g.shape
     gb = Buf.empty(N, Hh, Ww, Cc, 0, g.device)
     ops.pack_input(g, Cc, None, 0, gb, 0, N, FG_PAD_ZERO)
-    G = _Grads(S["P"])
+    G = _Grads(S["P"], device=g.device)
     g_new = _block_bwd(S["P"], "", S["b"], gb, G)
+    G.join()
     grads = {"w1": G.out["conv1.weight"], "b1": G.out["conv1.bias"],
              "w2": G.out["conv2.weight"], "b2": G.out["conv2.bias"]}
     return (_to_nchw(g_new) if need_input else None), grads
@@ -212,8 +273,8 @@ def block_backward_nchw(S, g, need_input=True):
 
 def _wgrad_conv(P, G, name, gy, X, pad, k, stride):
     w = P[name + ".weight"]
-    ops.wgrad(PL.wgrad_conv(gy, X, pad, k, stride, w.shape[0]), PL.wmap_wgrad(w.shape, True, X.c, k),
-              G.get(name + ".weight"), accumulate=G.acc)
+    G.wgrad(PL.wgrad_conv(gy, X, pad, k, stride, w.shape[0]), PL.wmap_wgrad(w.shape, True, X.c, k), name + ".weight",
+            (gy, X))
 
 
 def _dgrad_s1(P, name, gyp, pad_used, k, Y):
@@ -255,9 +316,9 @@ def gen_backward(P, S, g_out, grads_into=None, ready=None, input_grad=None, accu
     accumulate: add into grads_into instead of overwriting (a generator applied several times in
     one cycle iteration)."""
     ready = ready or (lambda name: None)
-    G = _Grads(P, grads_into, accumulate)
-    assert not accumulate or grads_into is not None
     x = S["x"]
+    G = _Grads(P, grads_into, accumulate, device=x.device)
+    assert not accumulate or grads_into is not None
     N, _, H, W = x.shape
     Cin = S["X0"].c            # input channels, including a fused x_extra
     dev = x.device
@@ -296,8 +357,8 @@ def gen_backward(P, S, g_out, grads_into=None, ready=None, input_grad=None, accu
                    G.get(f"deconv2_{tag}.bias"), G.acc)
         name = f"deconv2_{tag}"
         w = P[name + ".weight"]
-        ops.wgrad(PL.wgrad_convT(hd["ad1"], g_d2, 3, 1, w.shape[0]), PL.wmap_wgrad(w.shape, True, g_d2.c, 3),
-                  G.get(name + ".weight"), accumulate=G.acc)
+        G.wgrad(PL.wgrad_convT(hd["ad1"], g_d2, 3, 1, w.shape[0]), PL.wmap_wgrad(w.shape, True, g_d2.c, 3),
+                name + ".weight", (hd["ad1"], g_d2))
         g_ad1 = Buf.empty(N, H // 2, W // 2, 128, 0, dev)
         m = PL.wmap_convT_dgrad(w.shape, g_d2.c)
         ops.conv([PL.conv_problem(g_d2, 1, 3, 2, ops.pack_weight(w, m), m, g_ad1)])
@@ -306,15 +367,15 @@ def gen_backward(P, S, g_out, grads_into=None, ready=None, input_grad=None, accu
                    G.acc)
         name = f"deconv1_{tag}"
         w = P[name + ".weight"]
-        ops.wgrad(PL.wgrad_convT(S["h"], g_d1, 3, 1, w.shape[0]), PL.wmap_wgrad(w.shape, True, g_d1.c, 3),
-                  G.get(name + ".weight"), accumulate=G.acc)
+        G.wgrad(PL.wgrad_convT(S["h"], g_d1, 3, 1, w.shape[0]), PL.wmap_wgrad(w.shape, True, g_d1.c, 3),
+                name + ".weight", (S["h"], g_d1))
         m = PL.wmap_convT_dgrad(w.shape, g_d1.c)
         ops.conv([PL.conv_problem(g_d1, 1, 3, 2, ops.pack_weight(w, m), m, g_h, accumulate=idx)])
-    ready("deconv1_content")
+    G.ready(ready, "deconv1_content")
     # ---- resnet blocks in reverse: out = h + IN(conv2(pad(relu(IN(conv1(pad(h)))))))
     for i in reversed(range(N_BLOCKS)):
         g_h = _block_bwd(P, f"resnet_blocks.{i}.", S["blocks"][i], g_h, G)
-        ready(_blk(i, 1))
+        G.ready(ready, _blk(i, 1))
     # ---- encoder
     g_c3 = Buf.empty(N, H // 4, W // 4, 256, 1, dev)
     ops.in_bwd(g_h, 0, None, S["c3"], S["m3"], S["r3"], FG_ACT_RELU, g_c3, G.get("conv3.bias"), G.acc)
@@ -330,13 +391,14 @@ def gen_backward(P, S, g_out, grads_into=None, ready=None, input_grad=None, accu
     g_c1 = Buf.empty(N, H, W, 64, 0 if input_grad is None else 6, dev)
     ops.in_bwd(g_a1, 0, None, S["c1"], S["m1"], S["r1"], FG_ACT_RELU, g_c1, G.get("conv1.bias"), G.acc)
     _wgrad_conv(P, G, "conv1", g_c1, S["X0"], 3, 7, 1)
-    ready("conv1")
+    G.ready(ready, "conv1")
     if input_grad is not None:
         # gradient of the reflect-padded input (9 -> 12 channels: aligned rows), then the pad's
         # adjoint into NCHW, accumulated onto the tail's x[:, :3] term
         g_x0 = Buf.empty(N, H + 6, W + 6, PL.rup(Cin, 4), 0, dev)
         _dgrad_s1(P, "conv1", g_c1, 6, 7, g_x0)
         ops.unfold_nchw(g_x0, 3, Cin, input_grad, acc_channels=3 if attention else 0)
+    G.join()
     return G.out
 
 
@@ -420,19 +482,20 @@ def disc_backward(P, S, g_pred, param_grads=True, grads_into=None, input_grad=No
     receive dL/d(input channels input_grad_channels=(start, count)), written or accumulated.  ready(layer name), when
     given, is called as each layer's gradients are complete (parallel.FlatGrads buckets)."""
     ready = (ready if param_grads and ready is not None else (lambda name: None))
-    G = _Grads(P, grads_into)
     inp = S["inp"]
     N = inp.n
     dev = inp.t.device
+    G = _Grads(P, grads_into, device=dev)
     a3 = S["a3"]
     h5, w5 = g_pred.shape[2], g_pred.shape[3]
     g11 = Buf.empty(N, h5, w5, 1, 3, dev)              # zero border 3: the n1 weight-gradient kernel's reach
     ops.pack_input(g_pred, 1, None, 0, g11, 0, N, FG_PAD_ZERO)
     if param_grads:
         w11 = P["model.11.weight"]
-        ops.conv_n1_wgrad(a3, g11, PL.wmap_wgrad(w11.shape, True, a3.c, 4), G.get("model.11.weight"))
+        G.off_path(lambda: ops.conv_n1_wgrad(a3, g11, PL.wmap_wgrad(w11.shape, True, a3.c, 4),
+                                             G.get("model.11.weight")), (a3, g11), ("model.11.weight",))   # fp32
         ops.channel_sum(g11, 1, G.get("model.11.bias"))
-        ready("model.11")
+        G.ready(ready, "model.11")
     g_a3 = Buf.empty(N, a3.h, a3.w, 512, 0, dev)
     _dgrad_s1(P, "model.11", g11, 2, 4, g_a3)
     # model.8 (k4 s1 p1) + IN + LReLU
@@ -442,7 +505,7 @@ def disc_backward(P, S, g_pred, param_grads=True, grads_into=None, input_grad=No
     a2 = S["a2"]
     if param_grads:
         _wgrad_conv(P, G, "model.8", g_e3, a2, 1, 4, 1)
-        ready("model.8")
+        G.ready(ready, "model.8")
     g_a2 = Buf.empty(N, a2.h, a2.w, 256, 0, dev)
     _dgrad_s1(P, "model.8", g_e3, 2, 4, g_a2)
     # model.5 (k4 s2 p1)
@@ -452,7 +515,7 @@ def disc_backward(P, S, g_pred, param_grads=True, grads_into=None, input_grad=No
     a1 = S["a1"]
     if param_grads:
         _wgrad_conv(P, G, "model.5", g_e2, a1, 1, 4, 2)
-        ready("model.5")
+        G.ready(ready, "model.5")
     g_a1 = Buf.empty(N, a1.h, a1.w, 128, 0, dev)
     _dgrad_s2(P, "model.5", g_e2, 4, Y=g_a1)
     # model.2
@@ -462,7 +525,7 @@ def disc_backward(P, S, g_pred, param_grads=True, grads_into=None, input_grad=No
     e0 = S["e0"]
     if param_grads:
         _wgrad_conv(P, G, "model.2", g_e1, e0, 1, 4, 2)
-        ready("model.2")
+        G.ready(ready, "model.2")
     g_e0 = Buf.empty(N, e0.h, e0.w, 64, 1, dev)
     _dgrad_s2(P, "model.2", g_e1, 4, Y=g_e0)
     ops.zero_border(g_e0)
@@ -470,11 +533,12 @@ def disc_backward(P, S, g_pred, param_grads=True, grads_into=None, input_grad=No
     if param_grads:
         _wgrad_conv(P, G, "model.0", g_e0, inp, 1, 4, 2)
         ops.channel_sum(g_e0, 64, G.get("model.0.bias"))
-        ready("model.0")
+        G.ready(ready, "model.0")
     if input_grad is not None:
         c0, cn = input_grad_channels
         # input_grad: contiguous [N, Ctot, H, W]; D-input channels c0 .. c0+cn land in its channels 0 .. cn
         assert input_grad.is_contiguous() and input_grad.shape[1] >= cn
         _dgrad_s2(P, "model.0", g_e0, 4, y_nchw=(input_grad.view(-1), input_grad.shape[1], inp.h, inp.w), n_base=c0,
                   n_out=cn, accumulate=int(input_grad_accumulate))
+    G.join()
     return G.out

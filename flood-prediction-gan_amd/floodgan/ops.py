@@ -340,6 +340,19 @@ _WG_FIELDS = ("spn", "spa", "spb", "sxn", "sxa", "sxb", "sxr", "m_img", "m_a", "
               "splits", "m_chunk")
 
 
+def prepare_wgrad(prob):
+    """fill the operand caches a wgrad(prob) launch reads (f16x3 scale slots; the window kernel's split
+    copies) on the current stream, ahead of running wgrad on another stream"""
+    if not L.wgrad_f16x3():
+        return
+    if USE_WIN and wgrad_win_eligible(prob):
+        split_pixels(prob["p"][0])
+        split_pixels(prob["x"][0])
+    else:
+        absmax(prob["p"][0])
+        absmax(prob["x"][0])
+
+
 def wgrad(prob, wmap, dw, accumulate=False):
     """weight gradient into the PyTorch-layout tensor dw (overwritten, or += if accumulate)"""
     dev = _dev(prob["p"][0])

@@ -254,9 +254,9 @@ def gen_backward(P, S, g_out, grads_into=None, ready=None, accumulate=False):
     """Explicit backward of gen_forward (training-mode BatchNorm: through the batch statistics).
     g_out: [N, 3, H, W] (any strides).  Returns {parameter name: gradient}."""
     ready = ready or (lambda name: None)
-    G = X._Grads(P, grads_into, accumulate)
     N, H, W = S["N"], S["H"], S["W"]
     dev = g_out.device
+    G = X._Grads(P, grads_into, accumulate, device=dev)
     ch = level_channels(S["x"].shape[1])
     lv = S["lv"]
     # ---- tanh head + outermost up conv (bias)
@@ -264,10 +264,10 @@ def gen_backward(P, S, g_out, grads_into=None, ready=None, accumulate=False):
     g_logits = Buf.empty(N, H, W, 4, 1, dev)
     ops.tanh_head_bwd(S["logits"], 3, g_out, g_logits)
     w = P[nm["up"] + ".weight"]
-    ops.wgrad(PL.wgrad_convT(lv[1]["cat"], g_logits, 4, 1, w.shape[0]), PL.wmap_wgrad(w.shape, True, g_logits.c, 4),
-              G.get(nm["up"] + ".weight"), accumulate=G.acc)
+    G.wgrad(PL.wgrad_convT(lv[1]["cat"], g_logits, 4, 1, w.shape[0]), PL.wmap_wgrad(w.shape, True, g_logits.c, 4),
+            nm["up"] + ".weight", (lv[1]["cat"], g_logits))
     ops.channel_sum(g_logits, 3, G.get(nm["up"] + ".bias"), G.acc)
-    ready(nm["up"])
+    G.ready(ready, nm["up"])
     g_cat = {}
     g_cat[1] = Buf.empty(N, H >> 1, W >> 1, w.shape[0], 0, dev)
     m = PL.wmap_convT_dgrad(w.shape, g_logits.c)
@@ -286,9 +286,9 @@ def gen_backward(P, S, g_out, grads_into=None, ready=None, accumulate=False):
         ops.zero_border(g_u)
         xin = L["r"] if k == N_LEVELS else L["cat"]
         w = P[nm["up"] + ".weight"]
-        ops.wgrad(PL.wgrad_convT(xin, g_u, 4, 1, w.shape[0]), PL.wmap_wgrad(w.shape, True, g_u.c, 4),
-                  G.get(nm["up"] + ".weight"), accumulate=G.acc)
-        ready(nm["up"])
+        G.wgrad(PL.wgrad_convT(xin, g_u, 4, 1, w.shape[0]), PL.wmap_wgrad(w.shape, True, g_u.c, 4),
+                nm["up"] + ".weight", (xin, g_u))
+        G.ready(ready, nm["up"])
         g_x = Buf.empty(N, xin.h, xin.w, xin.c, 0, dev)
         m = PL.wmap_convT_dgrad(w.shape, g_u.c)
         ops.conv([PL.conv_problem(g_u, 1, 4, 2, ops.pack_weight(w, m), m, g_x)])
@@ -311,7 +311,7 @@ def gen_backward(P, S, g_out, grads_into=None, ready=None, accumulate=False):
                        G.get(nm["downnorm"] + ".weight"), G.get(nm["downnorm"] + ".bias"), G.acc)
             ops.zero_border(g_c)
         X._wgrad_conv(P, G, nm["down"], g_c, L["a"], 1, 4, 2)
-        ready(nm["down"])
+        G.ready(ready, nm["down"])
         a = L["a"]
         g_a = Buf.empty(N, a.h, a.w, a.c, 0, dev)
         X._dgrad_s2(P, nm["down"], g_c, 4, Y=g_a)
@@ -320,7 +320,8 @@ def gen_backward(P, S, g_out, grads_into=None, ready=None, accumulate=False):
     g_d1 = Buf.empty(N, L["c"].h, L["c"].w, 64, 0, dev)
     ops.bn_bwd(g_a, FG_ACT_LRELU, Slice(g_cat[1], 0, 64), FG_ACT_RELU, L["c"], 1, None, None, None, None, None, g_d1)
     X._wgrad_conv(P, G, nm["down"], g_d1, L["a"], 1, 4, 2)
-    ready(nm["down"])
+    G.ready(ready, nm["down"])
+    G.join()
     return G.out
 
 
@@ -375,19 +376,20 @@ def disc_backward(P, S, g_pred, param_grads=True, grads_into=None, input_grad=No
                   input_grad_accumulate=False, ready=None):
     """Explicit backward of disc_forward (see executor.disc_backward for the arguments)."""
     ready = (ready if param_grads and ready is not None else (lambda name: None))
-    G = X._Grads(P, grads_into)
     inp, groups = S["inp"], S["groups"]
     N = inp.n
     dev = inp.t.device
+    G = X._Grads(P, grads_into, device=dev)
     a3 = S["model.8"]["a"]
     h5, w5 = g_pred.shape[2], g_pred.shape[3]
     g11 = Buf.empty(N, h5, w5, 1, 3, dev)
     ops.pack_input(g_pred, 1, None, 0, g11, 0, N, FG_PAD_ZERO)
     if param_grads:
         w11 = P["model.11.weight"]
-        ops.conv_n1_wgrad(a3, g11, PL.wmap_wgrad(w11.shape, True, a3.c, 4), G.get("model.11.weight"))
+        G.off_path(lambda: ops.conv_n1_wgrad(a3, g11, PL.wmap_wgrad(w11.shape, True, a3.c, 4),
+                                             G.get("model.11.weight")), (a3, g11), ("model.11.weight",))
         ops.channel_sum(g11, 1, G.get("model.11.bias"))
-        ready("model.11")
+        G.ready(ready, "model.11")
     g_a = Buf.empty(N, a3.h, a3.w, 512, 0, dev)
     X._dgrad_s1(P, "model.11", g11, 2, 4, g_a)
     for conv, stride in (("model.8", 1), ("model.5", 2), ("model.2", 2)):
@@ -401,7 +403,7 @@ def disc_backward(P, S, g_pred, param_grads=True, grads_into=None, input_grad=No
         ops.zero_border(g_e)
         if param_grads:
             X._wgrad_conv(P, G, conv, g_e, L["x"], 1, 4, stride)
-            ready(conv)
+            G.ready(ready, conv)
         xprev = L["x"]
         g_a = Buf.empty(N, xprev.h, xprev.w, xprev.c, 1 if conv == "model.2" else 0, dev)
         if stride == 1:
@@ -415,12 +417,13 @@ def disc_backward(P, S, g_pred, param_grads=True, grads_into=None, input_grad=No
     if param_grads:
         X._wgrad_conv(P, G, "model.0", g_e0, inp, 1, 4, 2)
         ops.channel_sum(g_e0, 64, G.get("model.0.bias"))
-        ready("model.0")
+        G.ready(ready, "model.0")
     if input_grad is not None:
         c0, cn = input_grad_channels
         assert input_grad.is_contiguous() and input_grad.shape[1] >= cn
         X._dgrad_s2(P, "model.0", g_e0, 4, y_nchw=(input_grad.view(-1), input_grad.shape[1], inp.h, inp.w),
                     n_base=c0, n_out=cn, accumulate=int(input_grad_accumulate))
+    G.join()
     return G.out
 
 

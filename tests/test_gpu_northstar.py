@@ -449,3 +449,25 @@ def test_f16x3_dynamic_range(case, report):
     # per image: no worse than 1e-5, or than 4x the exact-fp32 path where that is itself above it
     for a, b in zip(f3["fwd_per_image"], f32["fwd_per_image"]):
         assert a < max(KTOL, 4 * b), res
+
+
+def test_side_stream_weight_gradients_identical():
+    """FLOODGAN_SIDE_STREAM's schedule (weight gradients on a second stream) changes nothing but the
+    order of independent launches: two fused steps give bit-identical losses and parameters."""
+    from floodgan import executor as X
+    x, y = _inputs(2, res=64, seed=3)
+    out = []
+    prev = X.SIDE_STREAM
+    try:
+        for side in (False, True):
+            X.SIDE_STREAM = side
+            m = _model()
+            ls = [m.step_fn(x.to(DEV), y.to(DEV)).cpu() for _ in range(2)]
+            torch.cuda.synchronize()
+            out.append((torch.stack(ls), [p.detach().cpu().clone() for p in m.generator.parameters()],
+                        [p.detach().cpu().clone() for p in m.discriminator.parameters()]))
+    finally:
+        X.SIDE_STREAM = prev
+    assert torch.equal(out[0][0], out[1][0])
+    assert all(torch.equal(a, b) for a, b in zip(out[0][1], out[1][1]))
+    assert all(torch.equal(a, b) for a, b in zip(out[0][2], out[1][2]))
