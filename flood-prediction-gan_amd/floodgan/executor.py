@@ -231,16 +231,36 @@ def _block_bwd(P, pre, b, g_h, G):
     g_cb2 = Buf.empty(N, Hh, Ww, Cc, 2, dev)          # zero border 2: full correlation of a 3x3
     ops.in_bwd(g_h, 0, None, b["cb2"], b["mb2"], b["rb2"], FG_ACT_NONE, g_cb2, G.get(pre + "conv2.bias"), G.acc)
     _wgrad_conv(P, G, pre + "conv2", g_cb2, b["rb"], 1, 3, 1)
-    g_rbp = Buf.empty(N, Hh + 2, Ww + 2, Cc, 0, dev)  # gradient w.r.t. the reflect-padded relu output
-    _dgrad_s1(P, pre + "conv2", g_cb2, 2, 3, g_rbp)
+    g_rbp = _dgrad_s1_padded(P, pre + "conv2", g_cb2)  # gradient w.r.t. the reflect-padded relu output
     g_cb1 = Buf.empty(N, Hh, Ww, Cc, 2, dev)
     ops.in_bwd(g_rbp, 1, None, b["cb1"], b["mb1"], b["rb1"], FG_ACT_RELU, g_cb1, G.get(pre + "conv1.bias"), G.acc)
     _wgrad_conv(P, G, pre + "conv1", g_cb1, b["h"], 1, 3, 1)
-    g_hp = Buf.empty(N, Hh + 2, Ww + 2, Cc, 0, dev)
-    _dgrad_s1(P, pre + "conv1", g_cb1, 2, 3, g_hp)
+    g_hp = _dgrad_s1_padded(P, pre + "conv1", g_cb1)
     g_new = Buf.empty(N, Hh, Ww, Cc, 0, dev)
     ops.fold_add(g_hp, 1, g_h, g_new)                 # reflect-pad adjoint + residual path
     return g_new
+
+
+def _dgrad_s1_padded(P, name, gy):
+    """Input gradient of a 3x3 stride-1 conv that read a reflect-padded (1) input: the gradient over the
+    whole (H+2) x (W+2) padded domain, as an unpadded Buf of that extent (the layout in_bwd / fold_add
+    fold).  Computed as the H x W interior -- an output grid of H-px rows, which the pipelined kernel's
+    256-row tiles split evenly (the (H+2)-px grid at bs 8, 128^2 gives 529 tiles for 256 resident
+    workgroups: 3 rounds instead of 2, +38 %) -- plus the four one-pixel edge strips in a second launch."""
+    N, Hh, Ww, Cc = gy.n, gy.h, gy.w, gy.c
+    assert gy.pad >= 2
+    w = P[name + ".weight"]
+    m = PL.wmap_conv_dgrad_s1(w.shape, gy.c)
+    wp = ops.pack_weight(w, m)
+    out = Buf.empty(N, Hh, Ww, Cc, 1, gy.t.device)     # interior = padded rows / cols 1..H
+    ops.conv([PL.conv_problem(gy, 1, 3, 1, wp, m, out)])
+    # padded-domain position p reads gy rows p-2 .. p (relative to gy's interior); out's interior origin
+    # is padded position 1
+    ops.conv([PL.window_problem(gy, -2, -2, 1, Ww + 2, 3, wp, m, out, -1, -1),         # padded row 0
+              PL.window_problem(gy, Hh - 1, -2, 1, Ww + 2, 3, wp, m, out, Hh, -1),     # padded row H+1
+              PL.window_problem(gy, -1, -2, Hh, 1, 3, wp, m, out, 0, -1),              # padded column 0
+              PL.window_problem(gy, -1, Ww - 1, Hh, 1, 3, wp, m, out, 0, Ww)])         # padded column W+1
+    return out.padded()
 
 
 def _to_nchw(B):

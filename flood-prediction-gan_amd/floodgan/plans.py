@@ -206,6 +206,20 @@ def conv_problem(X, pad_used, k, stride, wp, wmap, Y, bias=None, act=0, accumula
     return prob
 
 
+def window_problem(X, y0, x0, rows, cols, k, wp, wmap, Y, oy0, ox0):
+    """Stride-1 conv over a rectangular window of output positions: output (oy0 + i, ox0 + j) of Y
+    (coordinates relative to Y's interior origin, the border included) = sum over taps (r, s) of
+    X(y0 + i + r, x0 + j + s) (relative to X's interior origin; must stay inside X's padded extent)"""
+    assert -X.pad <= y0 and y0 + rows - 1 + k - 1 <= X.h - 1 + X.pad
+    assert -X.pad <= x0 and x0 + cols - 1 + k - 1 <= X.w - 1 + X.pad
+    assert -Y.pad <= oy0 and oy0 + rows <= Y.h + Y.pad and -Y.pad <= ox0 and ox0 + cols <= Y.w + Y.pad
+    assert wmap["kh"] == k and wmap["kw"] == k and wmap["c"] == X.c and Y.c >= wmap["n_out"]
+    return dict(x=(X, X.off(y0, x0)), w=(wp, 0), bias=None, sxn=X.s_img, sxa=X.s_row, sxb=X.c, sxr=X.s_row,
+                m_img=X.n, m_a=rows, m_b=cols, kh=k, j_valid=k * X.c, jp=wmap["jp"], n_out=wmap["n_out"],
+                ldw=k * wmap["jp"], act=0, accumulate=0, y=(Y, Y.off(oy0, ox0)), syn=Y.s_img, sya=Y.s_row, syb=Y.c,
+                syc=1)
+
+
 def phase_problems(S, shape, k, p, Y, wp_list, maps, bias=None, act=0, accumulate=0, y_nchw=None, n_out=None):
     """The four output phases of a stride-2 transposed op reading S (zero border >= 1):
     a ConvTranspose2d(k, 2, p, output_padding) forward, or a stride-2 conv's input gradient.
