@@ -246,7 +246,9 @@ def _dgrad_s1_padded(P, name, gy):
     whole (H+2) x (W+2) padded domain, as an unpadded Buf of that extent (the layout in_bwd / fold_add
     fold).  Computed as the H x W interior -- an output grid of H-px rows, which the pipelined kernel's
     256-row tiles split evenly (the (H+2)-px grid at bs 8, 128^2 gives 529 tiles for 256 resident
-    workgroups: 3 rounds instead of 2, +38 %) -- plus the four one-pixel edge strips in a second launch."""
+    workgroups: 3 rounds instead of 2, +38 %, profiles/round2/r2n_diag_dgrad.log) -- plus the four
+    one-pixel edge strips in a second launch.  gy's zero border leaves one kernel row (row strips) or
+    column (column strips) there: K = 3 x C instead of 9 x C."""
     N, Hh, Ww, Cc = gy.n, gy.h, gy.w, gy.c
     assert gy.pad >= 2
     w = P[name + ".weight"]
@@ -254,12 +256,15 @@ def _dgrad_s1_padded(P, name, gy):
     wp = ops.pack_weight(w, m)
     out = Buf.empty(N, Hh, Ww, Cc, 1, gy.t.device)     # interior = padded rows / cols 1..H
     ops.conv([PL.conv_problem(gy, 1, 3, 1, wp, m, out)])
-    # padded-domain position p reads gy rows p-2 .. p (relative to gy's interior); out's interior origin
-    # is padded position 1
-    ops.conv([PL.window_problem(gy, -2, -2, 1, Ww + 2, 3, wp, m, out, -1, -1),         # padded row 0
-              PL.window_problem(gy, Hh - 1, -2, 1, Ww + 2, 3, wp, m, out, Hh, -1),     # padded row H+1
-              PL.window_problem(gy, -1, -2, Hh, 1, 3, wp, m, out, 0, -1),              # padded column 0
-              PL.window_problem(gy, -1, Ww - 1, Hh, 1, 3, wp, m, out, 0, Ww)])         # padded column W+1
+    # padded-domain position p reads gy rows / cols p-2 .. p (relative to gy's interior; rows -2, -1 and
+    # H, H+1 are zero); out's interior origin is padded position 1.  Row strips: one row of the full
+    # pack (gather row r at pack row r); column strips: packs of their single kernel column.
+    strips = [PL.window_problem(gy, 0, -2, 1, Ww + 2, 1, 3, wp, m, out, -1, -1, w_row0=2),          # row 0
+              PL.window_problem(gy, Hh - 1, -2, 1, Ww + 2, 1, 3, wp, m, out, Hh, -1, w_row0=0)]     # row H+1
+    for col, x0, ox in ((2, 0, -1), (0, Ww - 1, Ww)):                                               # columns 0, W+1
+        ms = PL.wmap_conv_dgrad_s1_taps(w.shape, gy.c, (0, 1, 2), (col,))
+        strips.append(PL.window_problem(gy, -1, x0, Hh, 1, 3, 1, ops.pack_weight(w, ms), ms, out, 0, ox))
+    ops.conv(strips)
     return out.padded()
 
 

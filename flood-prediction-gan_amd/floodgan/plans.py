@@ -206,18 +206,34 @@ def conv_problem(X, pad_used, k, stride, wp, wmap, Y, bias=None, act=0, accumula
     return prob
 
 
-def window_problem(X, y0, x0, rows, cols, k, wp, wmap, Y, oy0, ox0):
+def window_problem(X, y0, x0, rows, cols, kh, kw, wp, wmap, Y, oy0, ox0, w_row0=0):
     """Stride-1 conv over a rectangular window of output positions: output (oy0 + i, ox0 + j) of Y
-    (coordinates relative to Y's interior origin, the border included) = sum over taps (r, s) of
-    X(y0 + i + r, x0 + j + s) (relative to X's interior origin; must stay inside X's padded extent)"""
-    assert -X.pad <= y0 and y0 + rows - 1 + k - 1 <= X.h - 1 + X.pad
-    assert -X.pad <= x0 and x0 + cols - 1 + k - 1 <= X.w - 1 + X.pad
+    (coordinates relative to Y's interior origin, the border included) = sum over taps (r < kh, s < kw)
+    of X(y0 + i + r, x0 + j + s) (relative to X's interior origin; inside X's padded extent) with the
+    packed weights of wmap (its rtab / stab say which kernel rows / columns the taps are).  w_row0 > 0:
+    the taps are rows w_row0 .. w_row0 + kh - 1 of a pack with wmap["kh"] rows (a sub-range of a full
+    kernel's pack, no pack of its own)"""
+    assert -X.pad <= y0 and y0 + rows - 1 + kh - 1 <= X.h - 1 + X.pad
+    assert -X.pad <= x0 and x0 + cols - 1 + kw - 1 <= X.w - 1 + X.pad
     assert -Y.pad <= oy0 and oy0 + rows <= Y.h + Y.pad and -Y.pad <= ox0 and ox0 + cols <= Y.w + Y.pad
-    assert wmap["kh"] == k and wmap["kw"] == k and wmap["c"] == X.c and Y.c >= wmap["n_out"]
-    return dict(x=(X, X.off(y0, x0)), w=(wp, 0), bias=None, sxn=X.s_img, sxa=X.s_row, sxb=X.c, sxr=X.s_row,
-                m_img=X.n, m_a=rows, m_b=cols, kh=k, j_valid=k * X.c, jp=wmap["jp"], n_out=wmap["n_out"],
-                ldw=k * wmap["jp"], act=0, accumulate=0, y=(Y, Y.off(oy0, ox0)), syn=Y.s_img, sya=Y.s_row, syb=Y.c,
-                syc=1)
+    assert w_row0 + kh <= wmap["kh"] and wmap["kw"] == kw and wmap["c"] == X.c and Y.c >= wmap["n_out"]
+    # weight-row offset in the 4-byte units of the problem's w reference: fp32 packs hold 1 float per k, the
+    # f16x3 pre-split packs 2 fp16 (h, l), the bf16x6 packs 3 bf16 (h, m, l)
+    units = {torch.float32: 1, torch.float16: 1, torch.bfloat16: 1.5}[wp.dtype] * w_row0 * wmap["jp"]
+    assert units == int(units)
+    return dict(x=(X, X.off(y0, x0)), w=(wp, int(units)), bias=None, sxn=X.s_img, sxa=X.s_row, sxb=X.c,
+                sxr=X.s_row, m_img=X.n, m_a=rows, m_b=cols, kh=kh, j_valid=kw * X.c, jp=wmap["jp"],
+                n_out=wmap["n_out"], ldw=wmap["kh"] * wmap["jp"], act=0, accumulate=0, y=(Y, Y.off(oy0, ox0)),
+                syn=Y.s_img, sya=Y.s_row, syb=Y.c, syc=1)
+
+
+def wmap_conv_dgrad_s1_taps(shape, c_alloc_gy, rows, cols):
+    """wmap_conv_dgrad_s1 restricted to the gather taps `rows` x `cols` (indices into the full 0..k-1
+    correlation): the edge strips of a padded-domain input gradient, where the zero border of the
+    output gradient leaves a single kernel row or column"""
+    O, I, kh, kw = shape
+    return _wmap(I, len(rows), len(cols), c_alloc_gy, O, 0, shape, [kh - 1 - r for r in rows],
+                 [kw - 1 - s for s in cols])
 
 
 def phase_problems(S, shape, k, p, Y, wp_list, maps, bias=None, act=0, accumulate=0, y_nchw=None, n_out=None):
