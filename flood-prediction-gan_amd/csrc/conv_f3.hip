@@ -582,7 +582,10 @@ int launch_fwd_f3(const ConvBatch& b, int nprob, int max_n, hipStream_t stream, 
             p.m_img * p.m_a * p.m_b < 1)
             return 0;
     }
-    int cfg = g_f3_tile >= 0 ? g_f3_tile : (max_n > 128 ? 4 : max_n > 64 ? 6 : max_n > 32 ? 9 : -1);
+    // N <= 64: the 256-row tile (cfg 7) beats the 128-row one by 4-13 % on the step's N=64 convs (content
+    // input gradient 1.67 vs 1.92 ms, deconv2 / conv2-dgrad phases 0.626 vs 0.653 ms at bs 8 512^2:
+    // profiles/round2/r2r_diag_n64.log)
+    int cfg = g_f3_tile >= 0 ? g_f3_tile : (max_n > 128 ? 4 : max_n > 64 ? 6 : max_n > 32 ? 7 : -1);
     switch (cfg) {
         case 0: *rc = launch_cfg<128, 256, 32, 128>(b, nprob, stream); return 1;
         case 1: *rc = launch_cfg<256, 128, 64, 64>(b, nprob, stream); return 1;

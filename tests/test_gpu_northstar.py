@@ -351,7 +351,8 @@ def test_cycle_generator_input_gradient_512(model, report):
 
 @pytest.mark.parametrize("cap", [2, 3, 7])
 @pytest.mark.parametrize("cfg,case", [(4, (256, 256, 3, 1, 1, "reflect", 20)), (6, (256, 128, 3, 1, 1, "reflect", 19)),
-                                      (9, (128, 64, 3, 1, 1, "constant", 21)), (1, (128, 256, 4, 2, 1, "constant", 22))])
+                                      (9, (128, 64, 3, 1, 1, "constant", 21)), (7, (128, 64, 3, 1, 1, "constant", 21)),
+                                      (7, (32, 64, 7, 1, 3, "constant", 23)), (1, (128, 256, 4, 2, 1, "constant", 22))])
 def test_conv_f3_tile_stream(cfg, case, cap):
     """conv_fwd_f3 with at most `cap` persistent workgroups: every workgroup streams many tiles back to
     back (next tile's k-stages issued during the current tile's last stages and epilogue, setup_issue()
