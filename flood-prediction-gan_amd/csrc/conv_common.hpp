@@ -65,6 +65,7 @@ __device__ __forceinline__ int swz_pixel(int x) {
 // Pipelined f16x3 forward kernel (conv_f3.hip).  Returns 1 if it took the batch (launched or
 // failed: *rc holds the launch status), 0 if the batch does not fit its constraints.
 int launch_fwd_f3(const ConvBatch& b, int nprob, int max_n, hipStream_t stream, int* rc);
+bool f3_stats_ok(const fg_conv_problem* probs, int nprob, int max_n);
 
 // Pipelined f16x3 weight-gradient kernel (conv_wgrad_f3.hip), same contract.
 int launch_wgrad_f3(const fg_wgrad_problem& p, hipStream_t stream, int* rc);

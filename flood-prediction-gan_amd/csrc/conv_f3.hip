@@ -98,7 +98,7 @@ __device__ __forceinline__ void wait_vmcnt() {
 // the B fragments double-buffered in 2-block groups, pinned (group g+1 is read while group g's
 // products run; group 0 is read together with A, ahead of the DMA issue); 3 = as 1, with the
 // next stage's LDS-DMA pieces spread between the column groups instead of one burst.
-template <int BM, int BN, int WM, int WN, int NS, int SCH>
+template <int BM, int BN, int WM, int WN, int NS, int SCH, bool STATS = false>
 __global__ void __launch_bounds__((BM / WM) * (BN / WN) * 64, 1)
 conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
     constexpr int NWN = BN / WN;
@@ -431,6 +431,61 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
             bias_v[tn] = P.bias ? P.bias[min(ncol[tn], P.n_out - 1)] : 0.f;
         }
         const bool full_n = cg.n0 + BN <= P.n_out;
+        if (STATS && P.in_stats) {
+            // InstanceNorm partials of this wave's 32-row block (WM = 32: tm x g x reg), per column: two
+            // passes (mean, then M2) over the raw accumulators, each reduced over the 4 lanes of the column
+            // (g); out_scale (a power of 2) and the bias are applied to the results.  Columns go in groups of
+            // SG so that a group's cross-lane exchanges are in flight together
+            const int rb0 = cg.m0 + wm * WM;
+            if (rb0 < M) {
+                constexpr int SG = TN < 4 ? TN : 4;
+                const float sc = out_scale;
+                float* const dst0 = P.in_stats + (size_t)(rb0 / WM) * P.n_out * 2;
+#pragma unroll
+                for (int t0 = 0; t0 < TN; t0 += SG) {
+                    float sm[SG], sq[SG];
+#pragma unroll
+                    for (int u = 0; u < SG; ++u) {
+                        f32x2 s2 = f32x2{acc[0][t0 + u][0], acc[0][t0 + u][1]} +
+                                   f32x2{acc[0][t0 + u][2], acc[0][t0 + u][3]};
+#pragma unroll
+                        for (int tm = 1; tm < TM; ++tm)
+                            s2 += f32x2{acc[tm][t0 + u][0], acc[tm][t0 + u][1]} +
+                                  f32x2{acc[tm][t0 + u][2], acc[tm][t0 + u][3]};
+                        sm[u] = s2[0] + s2[1];
+                    }
+#pragma unroll
+                    for (int u = 0; u < SG; ++u) sm[u] += __shfl_xor(sm[u], 16);
+#pragma unroll
+                    for (int u = 0; u < SG; ++u) sm[u] += __shfl_xor(sm[u], 32);
+#pragma unroll
+                    for (int u = 0; u < SG; ++u) {
+                        const float mu = sm[u] * (1.f / (TM * 16));
+                        sm[u] = mu;
+                        const f32x2 m2 = {mu, mu};
+                        f32x2 q2;
+#pragma unroll
+                        for (int tm = 0; tm < TM; ++tm) {
+                            const f32x2 d0 = f32x2{acc[tm][t0 + u][0], acc[tm][t0 + u][1]} - m2;
+                            const f32x2 d1 = f32x2{acc[tm][t0 + u][2], acc[tm][t0 + u][3]} - m2;
+                            q2 = tm ? q2 + d0 * d0 + d1 * d1 : d0 * d0 + d1 * d1;
+                        }
+                        sq[u] = q2[0] + q2[1];
+                    }
+#pragma unroll
+                    for (int u = 0; u < SG; ++u) sq[u] += __shfl_xor(sq[u], 16);
+#pragma unroll
+                    for (int u = 0; u < SG; ++u) sq[u] += __shfl_xor(sq[u], 32);
+                    if (g == 0) {
+#pragma unroll
+                        for (int u = 0; u < SG; ++u)
+                            if (ncol[t0 + u] < P.n_out)
+                                *reinterpret_cast<f32x2*>(dst0 + ncol[t0 + u] * 2) =
+                                    f32x2{sm[u] * sc + bias_v[t0 + u], sq[u] * (sc * sc)};
+                    }
+                }
+            }
+        }
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm) {
 #pragma unroll
@@ -546,6 +601,18 @@ int launch_cfg(const ConvBatch& in, int nprob, hipStream_t stream) {
     const char* dg = getenv("FG_F3_DIAG");
     const int g_f3_alt = ::g_f3_alt | ((dg ? atoi(dg) : 0) << 4);
 #endif
+    bool stats = false;
+    for (int i = 0; i < nprob; ++i) stats |= b.p[i].in_stats != nullptr;
+    // the epilogue-statistics variant is its own instantiation (WM = 32 configs, default order), so that
+    // the launches without statistics keep the plain epilogue's code
+    if constexpr (WM == 32) {
+        if (stats) {
+            hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 3, true>), dim3(grid), dim3(NT), 0, stream, b,
+                               total, g_f3_alt);
+            return fg::launched("conv_fwd_f3");
+        }
+    }
+    if (stats) return fg::fail(FG_ERR_INVALID, "conv_fwd_f3: epilogue statistics need a WM = 32 tile");
     if (sched == 5)
         hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 5>), dim3(grid), dim3(NT), 0, stream, b, total,
                            g_f3_alt);
@@ -573,19 +640,40 @@ int g_f3_tile = -1;   // tuning hook (fg_set_f3_tile): -2 disables the kernel, >
 
 namespace fgc {
 
-int launch_fwd_f3(const ConvBatch& b, int nprob, int max_n, hipStream_t stream, int* rc) {
-    if (g_f3_tile == -2) return 0;
+int f3_config(int max_n) {
+    return g_f3_tile >= 0 ? g_f3_tile : (max_n > 128 ? 4 : max_n > 64 ? 6 : max_n > 32 ? 7 : -1);
+}
+
+bool f3_takes(const fg_conv_problem* probs, int nprob, int max_n) {
+    if (g_f3_tile == -2 || f3_config(max_n) < 0) return false;
     for (int i = 0; i < nprob; ++i) {
-        const fg_conv_problem& p = b.p[i];
+        const fg_conv_problem& p = probs[i];
         // no K padding (every staged k is a real tap: padded j would gather past the row run)
         if (p.w_split != 2 || p.jp % 32 || p.j_valid != p.jp || p.ldw != p.kh * p.jp || !p.x_absmax || !p.w_absmax ||
             p.m_img * p.m_a * p.m_b < 1)
-            return 0;
+            return false;
     }
+    return true;
+}
+
+// the epilogue statistics need whole 32-row wave blocks inside one image (WM = 32 in every config)
+bool f3_stats_ok(const fg_conv_problem* probs, int nprob, int max_n) {
+    if (!f3_takes(probs, nprob, max_n)) return false;
+    const int cfg = f3_config(max_n);
+    if (!(cfg == 0 || cfg == 3 || cfg == 4 || cfg == 6 || cfg == 7 || cfg == 9)) return false;   // WM = 32 configs
+    for (int i = 0; i < nprob; ++i) {
+        const fg_conv_problem& p = probs[i];
+        if ((p.m_a * p.m_b) % 32 || p.act != 0 || p.accumulate) return false;
+    }
+    return true;
+}
+
+int launch_fwd_f3(const ConvBatch& b, int nprob, int max_n, hipStream_t stream, int* rc) {
+    if (!f3_takes(b.p, nprob, max_n)) return 0;
     // N <= 64: the 256-row tile (cfg 7) beats the 128-row one by 4-13 % on the step's N=64 convs (content
     // input gradient 1.67 vs 1.92 ms, deconv2 / conv2-dgrad phases 0.626 vs 0.653 ms at bs 8 512^2:
     // profiles/round2/r2r_diag_n64.log)
-    int cfg = g_f3_tile >= 0 ? g_f3_tile : (max_n > 128 ? 4 : max_n > 64 ? 6 : max_n > 32 ? 7 : -1);
+    const int cfg = f3_config(max_n);
     switch (cfg) {
         case 0: *rc = launch_cfg<128, 256, 32, 128>(b, nprob, stream); return 1;
         case 1: *rc = launch_cfg<256, 128, 64, 64>(b, nprob, stream); return 1;

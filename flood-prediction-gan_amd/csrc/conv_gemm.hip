@@ -1260,6 +1260,10 @@ FG_API int fg_conv_fwd(const fg_conv_problem* probs, int nprob, hipStream_t stre
     }
     const bool f16 = (g_conv_math & FG_MATH_FWD_F16X3) != 0;
     const bool x6 = f16 || (g_conv_math & FG_MATH_FWD_X6) != 0;   // a split-math kernel
+    bool stats = false;
+    for (int i = 0; i < nprob; ++i) stats |= probs[i].in_stats != nullptr;
+    if (stats && !(f16 && vec && ws == 2 && g_fwd_tile < 0 && fgc::f3_stats_ok(probs, nprob, max_n)))
+        return fg::fail(FG_ERR_INVALID, "fg_conv_fwd: in_stats needs the pipelined f16x3 kernel (see fg_conv_stats_ok)");
     if ((ws == 1 && (!x6 || f16)) || (ws == 2 && !f16))
         return fg::fail(FG_ERR_INVALID, "fg_conv_fwd: pre-split weights (w_split=%d) do not match the conv math %d",
                         ws, g_conv_math);
@@ -1279,6 +1283,7 @@ FG_API int fg_conv_fwd(const fg_conv_problem* probs, int nprob, hipStream_t stre
             if (ext > kLim) fits = false;
         }
         if (!fits) {
+            if (stats) return fg::fail(FG_ERR_INVALID, "fg_conv_fwd: in_stats with an operand beyond 2 GiB");
             for (int i = 0; i < nprob; ++i) {
                 fg_conv_problem q = probs[i];
                 const long long tail = (long long)(q.m_a - 1) * q.sxa + (long long)(q.m_b - 1) * q.sxb +
@@ -1324,6 +1329,18 @@ FG_API int fg_conv_fwd(const fg_conv_problem* probs, int nprob, hipStream_t stre
     if (BN == 128) return launch_fwd<128, 128, 64, 64>(b, total, vec, stream);
     if (BN == 64) return launch_fwd<256, 64, 64, 64>(b, total, vec, stream);
     return launch_fwd<256, 32, 64, 32>(b, total, vec, stream);
+}
+
+FG_API int fg_conv_stats_ok(const fg_conv_problem* probs, int nprob) {
+    if (!probs || nprob < 1 || nprob > 4) return 0;
+    if (!(g_conv_math & FG_MATH_FWD_F16X3) || g_fwd_tile >= 0) return 0;
+    int max_n = 0;
+    for (int i = 0; i < nprob; ++i) {
+        const fg_conv_problem& p = probs[i];
+        if (p.w_split != 2 || !aligned16(p.x) || (p.sxn | p.sxa | p.sxb | p.sxr) % 4 || p.j_valid % 4) return 0;
+        max_n = std::max(max_n, p.n_out);
+    }
+    return fgc::f3_stats_ok(probs, nprob, max_n) ? 1 : 0;
 }
 
 FG_API int fg_set_wgrad_tile(int cfg) {

@@ -466,7 +466,92 @@ __global__ void channel_sum_finalize(int c_valid, int chunks, const double* __re
 
 bool ok_view(const fg_view& v) { return v.ptr && v.n > 0 && v.h > 0 && v.w > 0 && v.c_alloc > 0 && v.pad >= 0; }
 
+// per-(image, channel) statistics from the pipelined conv kernel's epilogue partials: (mean, M2) of
+// every 32-row block, merged in fp64 (S1 = sum 32 mean_i, S2 = sum M2_i + 32 mean_i^2) in two levels:
+// in_partials_reduce -- block = 64 channels x 4 row slices over one of `splits` ranges of an image's blocks
+// (coalesced 512-B rows of f32x2), fp64 partial sums into work; in_partials_finalize -- sums the splits.
+constexpr int kPartialSplitsMax = 64;
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__global__ void in_partials_reduce(const float* __restrict__ part, int nprob, int n_img, int rb_per_img, int c,
+                                   int splits, double* __restrict__ work) {
+    const int img = blockIdx.x, sp = blockIdx.z, cl = threadIdx.x % 64, sl = threadIdx.x / 64;
+    const int ch = blockIdx.y * 64 + cl;
+    const size_t prob_stride = (size_t)n_img * rb_per_img * c * 2;
+    const int K = nprob * rb_per_img;
+    const int lo = (int)((long long)K * sp / splits), hi = (int)((long long)K * (sp + 1) / splits);
+    double s1 = 0, s2 = 0;
+    if (ch < c)
+        for (int k = lo + sl; k < hi; k += 4) {
+            const int pr = k / rb_per_img, rb = img * rb_per_img + (k - pr * rb_per_img);
+            const f32x2 q = *reinterpret_cast<const f32x2*>(part + pr * prob_stride + ((size_t)rb * c + ch) * 2);
+            const double m = q[0];
+            s1 += 32.0 * m;
+            s2 += (double)q[1] + 32.0 * m * m;
+        }
+    __shared__ double red[256][2];
+    red[threadIdx.x][0] = s1;
+    red[threadIdx.x][1] = s2;
+    __syncthreads();
+    if (sl == 0 && ch < c) {
+        for (int q = 1; q < 4; ++q) {
+            s1 += red[q * 64 + cl][0];
+            s2 += red[q * 64 + cl][1];
+        }
+        double* w = work + (((size_t)img * splits + sp) * c + ch) * 2;
+        w[0] = s1;
+        w[1] = s2;
+    }
+}
+
+__global__ void in_partials_finalize(const double* __restrict__ work, int nprob, int rb_per_img, int c, int splits,
+                                     float eps, float* __restrict__ mean, float* __restrict__ rstd) {
+    const int img = blockIdx.x, cl = threadIdx.x % 64, sl = threadIdx.x / 64;
+    const int ch = blockIdx.y * 64 + cl;
+    double s1 = 0, s2 = 0;
+    if (ch < c)
+        for (int sp = sl; sp < splits; sp += 4) {
+            const double* w = work + (((size_t)img * splits + sp) * c + ch) * 2;
+            s1 += w[0];
+            s2 += w[1];
+        }
+    __shared__ double red[256][2];
+    red[threadIdx.x][0] = s1;
+    red[threadIdx.x][1] = s2;
+    __syncthreads();
+    if (sl == 0 && ch < c) {
+        for (int q = 1; q < 4; ++q) {
+            s1 += red[q * 64 + cl][0];
+            s2 += red[q * 64 + cl][1];
+        }
+        const double n = 32.0 * nprob * rb_per_img;
+        const double mu = s1 / n;
+        double var = s2 / n - mu * mu;
+        if (var < 0) var = 0;
+        mean[img * c + ch] = (float)mu;
+        rstd[img * c + ch] = (float)(1.0 / sqrt(var + (double)eps));
+    }
+}
+
 }  // namespace
+
+FG_API long long fg_in_partials_workspace_doubles(int n_img, int c) {
+    return (long long)n_img * kPartialSplitsMax * c * 2;
+}
+
+FG_API int fg_in_stats_partials(const float* partials, int nprob, int n_img, int rb_per_img, int c, float eps,
+                                float* mean, float* rstd, double* work, hipStream_t stream) {
+    if (!partials || !mean || !rstd || !work || nprob < 1 || nprob > 4 || n_img < 1 || rb_per_img < 1 || c < 1)
+        return fg::fail(FG_ERR_INVALID, "fg_in_stats_partials: bad args");
+    const int cg = (c + 63) / 64, K = nprob * rb_per_img;
+    // ~1024 blocks over the chip, each thread at least ~4 of the image's 32-row blocks
+    const int splits = std::max(1, std::min({kPartialSplitsMax, (1024 + n_img * cg - 1) / (n_img * cg), K / 16}));
+    hipLaunchKernelGGL(in_partials_reduce, dim3(n_img, cg, splits), dim3(256), 0, stream, partials, nprob, n_img,
+                       rb_per_img, c, splits, work);
+    hipLaunchKernelGGL(in_partials_finalize, dim3(n_img, cg), dim3(256), 0, stream, work, nprob, rb_per_img, c, splits,
+                       eps, mean, rstd);
+    return fg::launched("in_stats_partials");
+}
 
 FG_API long long fg_in_workspace_doubles(int n, int c) { return (long long)n * c * (MAX_CHUNKS * 3 + 2) + 64; }
 // layout: [stats n*c*MAX_CHUNKS*3][coef n*c*2 floats = n*c doubles][bias partials n*c]

@@ -40,7 +40,8 @@ class fg_conv_problem(C.Structure):
                 ("m_img", C.c_int), ("m_a", C.c_int), ("m_b", C.c_int),
                 ("kh", C.c_int), ("j_valid", C.c_int), ("jp", C.c_int),
                 ("n_out", C.c_int), ("ldw", C.c_int), ("act", C.c_int), ("accumulate", C.c_int),
-                ("w_split", C.c_int), ("x_absmax", C.c_void_p), ("w_absmax", C.c_void_p), ("jc", C.c_int)]
+                ("w_split", C.c_int), ("x_absmax", C.c_void_p), ("w_absmax", C.c_void_p), ("jc", C.c_int),
+                ("in_stats", C.c_void_p)]
 
 
 class fg_wgrad_problem(C.Structure):
@@ -83,6 +84,7 @@ SIGNATURES = {
     "fg_version": [],
     "fg_device_ok": [],
     "fg_conv_fwd": [C.POINTER(fg_conv_problem), C.c_int, C.c_void_p],
+    "fg_conv_stats_ok": [C.POINTER(fg_conv_problem), C.c_int],
     "fg_set_conv_math": [C.c_int],
     "fg_get_conv_math": [],
     "fg_set_fwd_tile": [C.c_int],
@@ -113,6 +115,9 @@ SIGNATURES = {
     "fg_unfold_nchw": [fg_view, C.c_int, C.c_int, fg_wview, C.c_int, C.c_int, C.c_int, C.c_void_p],
     "fg_in_workspace_doubles": [C.c_int, C.c_int],
     "fg_in_stats": [fg_view, C.c_float, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p],
+    "fg_in_stats_partials": [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_float, C.c_void_p, C.c_void_p,
+                             C.c_void_p, C.c_void_p],
+    "fg_in_partials_workspace_doubles": [C.c_int, C.c_int],
     "fg_in_apply": [fg_view, C.c_void_p, C.c_void_p, C.c_int, fg_view, fg_view, C.c_int, C.c_void_p, C.c_void_p],
     "fg_in_bwd": [fg_view, C.c_int, fg_view, fg_view, C.c_void_p, C.c_void_p, C.c_int, fg_view, C.c_void_p,
                   C.c_int, C.c_void_p, C.c_void_p, C.c_void_p],
@@ -155,7 +160,8 @@ SIGNATURES = {
 }
 RESTYPES = {"fg_last_error": C.c_char_p, "fg_in_workspace_doubles": C.c_longlong, "fg_bn_workspace_doubles": C.c_longlong,
             "fg_ssim_workspace_doubles": C.c_longlong, "fg_sq_err_workspace_doubles": C.c_longlong,
-            "fg_channel_sum_workspace_doubles": C.c_longlong}
+            "fg_channel_sum_workspace_doubles": C.c_longlong,
+            "fg_in_partials_workspace_doubles": C.c_longlong}
 
 _lib = None
 

@@ -121,22 +121,25 @@ class _Grads:
 # generator
 # ======================================================================================
 
-def _conv_fwd(P, name, X, pad, k, stride, Y, act=FG_ACT_NONE, tag=None):
+def _conv_fwd(P, name, X, pad, k, stride, Y, act=FG_ACT_NONE, tag=None, in_stats=False):
+    """returns the InstanceNorm statistics of Y from the conv's epilogue when in_stats and available"""
     w = P[name + ".weight"]
     m = PL.wmap_conv_fwd(w.shape, X.c)
-    ops.conv([PL.conv_problem(X, pad, k, stride, ops.pack_weight(w, m), m, Y, bias=P[name + ".bias"], act=act)],
-             tag=tag)
+    return ops.conv([PL.conv_problem(X, pad, k, stride, ops.pack_weight(w, m), m, Y, bias=P[name + ".bias"],
+                                     act=act)], tag=tag, in_stats=in_stats)
 
 
 def _convT_fwd(P, name, X, Y):
     w = P[name + ".weight"]
     maps = PL.phase_maps(w.shape, 3, 1, X.c)
     wps = [ops.pack_weight(w, m) for m, _, _ in maps]
-    ops.conv(PL.phase_problems(X, w.shape, 3, 1, Y, wps, maps, bias=P[name + ".bias"]))
+    return ops.conv(PL.phase_problems(X, w.shape, 3, 1, Y, wps, maps, bias=P[name + ".bias"]), in_stats=True)
 
 
-def _norm(c, act, pad, mode, residual=None):
-    mean, rstd = ops.in_stats(c)
+def _norm(c, act, pad, mode, residual=None, stats=None):
+    """InstanceNorm + activation of conv output c; stats = (mean, rstd) from the conv's epilogue, or
+    computed here"""
+    mean, rstd = stats if stats is not None else ops.in_stats(c)
     out = Buf.empty(c.n, c.h, c.w, c.c, pad, c.t.device)
     ops.in_apply(c, mean, rstd, act, residual, out, mode)
     return mean, rstd, out
@@ -168,14 +171,14 @@ def gen_forward(P, x, save=True, x_extra=None):
     X0 = Buf.empty(N, H, W, Cin + Ce, 3, dev)
     ops.pack_input(x, Cin, x_extra, Ce, X0, 0, N, FG_PAD_REFLECT)             # F.pad(input, 3, reflect)
     c1 = Buf.empty(N, H, W, 64, 0, dev)
-    _conv_fwd(P, "conv1", X0, 3, 7, 1, c1)
-    m1, r1, a1 = _norm(c1, FG_ACT_RELU, 1, FG_PAD_ZERO)
+    st = _conv_fwd(P, "conv1", X0, 3, 7, 1, c1, in_stats=True)
+    m1, r1, a1 = _norm(c1, FG_ACT_RELU, 1, FG_PAD_ZERO, stats=st)
     c2 = Buf.empty(N, H // 2, W // 2, 128, 0, dev)
-    _conv_fwd(P, "conv2", a1, 1, 3, 2, c2)
-    m2, r2, a2 = _norm(c2, FG_ACT_RELU, 1, FG_PAD_ZERO)
+    st = _conv_fwd(P, "conv2", a1, 1, 3, 2, c2, in_stats=True)
+    m2, r2, a2 = _norm(c2, FG_ACT_RELU, 1, FG_PAD_ZERO, stats=st)
     c3 = Buf.empty(N, H // 4, W // 4, 256, 0, dev)
-    _conv_fwd(P, "conv3", a2, 1, 3, 2, c3)
-    m3, r3, h = _norm(c3, FG_ACT_RELU, 1, FG_PAD_REFLECT)
+    st = _conv_fwd(P, "conv3", a2, 1, 3, 2, c3, in_stats=True)
+    m3, r3, h = _norm(c3, FG_ACT_RELU, 1, FG_PAD_REFLECT, stats=st)
     S.update(x=x, X0=X0, c1=c1, m1=m1, r1=r1, a1=a1, c2=c2, m2=m2, r2=r2, a2=a2, c3=c3, m3=m3, r3=r3)
     blocks = []
     for i in range(N_BLOCKS):
@@ -188,11 +191,11 @@ def gen_forward(P, x, save=True, x_extra=None):
     attention = has_attention(P)
     for tag, pad2, mode2 in (("content", 3, FG_PAD_REFLECT), ("attention", 0, FG_PAD_ZERO))[:1 + attention]:
         d1 = Buf.empty(N, H // 2, W // 2, 128, 0, dev)
-        _convT_fwd(P, f"deconv1_{tag}", h, d1)
-        md1, rd1, ad1 = _norm(d1, FG_ACT_RELU, 1, FG_PAD_ZERO)
+        st = _convT_fwd(P, f"deconv1_{tag}", h, d1)
+        md1, rd1, ad1 = _norm(d1, FG_ACT_RELU, 1, FG_PAD_ZERO, stats=st)
         d2 = Buf.empty(N, H, W, 64, 0, dev)
-        _convT_fwd(P, f"deconv2_{tag}", ad1, d2)
-        md2, rd2, ad2 = _norm(d2, FG_ACT_RELU, pad2, mode2)
+        st = _convT_fwd(P, f"deconv2_{tag}", ad1, d2)
+        md2, rd2, ad2 = _norm(d2, FG_ACT_RELU, pad2, mode2, stats=st)
         heads[tag] = dict(d1=d1, md1=md1, rd1=rd1, ad1=ad1, d2=d2, md2=md2, rd2=rd2, ad2=ad2)
     cl = Buf.empty(N, H, W, CONTENT_ALLOC, 0, dev)
     _conv_fwd(P, "deconv3_content", heads["content"]["ad2"], 3, 7, 1, cl)
@@ -215,11 +218,11 @@ def _block_fwd(P, pre, h, out_mode):
     N, Hh, Ww, Cc = h.n, h.h, h.w, h.c
     dev = h.t.device
     cb1 = Buf.empty(N, Hh, Ww, Cc, 0, dev)
-    _conv_fwd(P, pre + "conv1", h, 1, 3, 1, cb1, tag="resblock_conv_fwd")
-    mb1, rb1, rb = _norm(cb1, FG_ACT_RELU, 1, FG_PAD_REFLECT)
+    st = _conv_fwd(P, pre + "conv1", h, 1, 3, 1, cb1, tag="resblock_conv_fwd", in_stats=True)
+    mb1, rb1, rb = _norm(cb1, FG_ACT_RELU, 1, FG_PAD_REFLECT, stats=st)
     cb2 = Buf.empty(N, Hh, Ww, Cc, 0, dev)
-    _conv_fwd(P, pre + "conv2", rb, 1, 3, 1, cb2, tag="resblock_conv_fwd")
-    mb2, rb2, hn = _norm(cb2, FG_ACT_NONE, 1, out_mode, residual=h)
+    st = _conv_fwd(P, pre + "conv2", rb, 1, 3, 1, cb2, tag="resblock_conv_fwd", in_stats=True)
+    mb2, rb2, hn = _norm(cb2, FG_ACT_NONE, 1, out_mode, residual=h, stats=st)
     return hn, dict(h=h, cb1=cb1, mb1=mb1, rb1=rb1, rb=rb, cb2=cb2, mb2=mb2, rb2=rb2)
 
 
@@ -482,16 +485,16 @@ def disc_forward(P, inp, save=True):
     ops.zero_border(e0)
     h2, w2 = PL.out_size(h1, 4, 2, 1), PL.out_size(w1, 4, 2, 1)
     e1 = Buf.empty(N, h2, w2, 128, 0, dev)
-    _conv_fwd(P, "model.2", e0, 1, 4, 2, e1)
-    m1, r1, a1 = _norm(e1, FG_ACT_LRELU, 1, FG_PAD_ZERO)
+    st = _conv_fwd(P, "model.2", e0, 1, 4, 2, e1, in_stats=True)
+    m1, r1, a1 = _norm(e1, FG_ACT_LRELU, 1, FG_PAD_ZERO, stats=st)
     h3, w3 = PL.out_size(h2, 4, 2, 1), PL.out_size(w2, 4, 2, 1)
     e2 = Buf.empty(N, h3, w3, 256, 0, dev)
-    _conv_fwd(P, "model.5", a1, 1, 4, 2, e2)
-    m2, r2, a2 = _norm(e2, FG_ACT_LRELU, 1, FG_PAD_ZERO)
+    st = _conv_fwd(P, "model.5", a1, 1, 4, 2, e2, in_stats=True)
+    m2, r2, a2 = _norm(e2, FG_ACT_LRELU, 1, FG_PAD_ZERO, stats=st)
     h4, w4 = PL.out_size(h3, 4, 1, 1), PL.out_size(w3, 4, 1, 1)
     e3 = Buf.empty(N, h4, w4, 512, 0, dev)
-    _conv_fwd(P, "model.8", a2, 1, 4, 1, e3)
-    m3, r3, a3 = _norm(e3, FG_ACT_LRELU, 1, FG_PAD_ZERO)
+    st = _conv_fwd(P, "model.8", a2, 1, 4, 1, e3, in_stats=True)
+    m3, r3, a3 = _norm(e3, FG_ACT_LRELU, 1, FG_PAD_ZERO, stats=st)
     h5, w5 = PL.out_size(h4, 4, 1, 1), PL.out_size(w4, 4, 1, 1)
     pred = torch.empty(N, 1, h5, w5, dtype=torch.float32, device=dev)
     ops.conv_n1_fwd(a3, P["model.11.weight"], P["model.11.bias"], pred)      # GEMV-shaped: fp32 FMA kernel

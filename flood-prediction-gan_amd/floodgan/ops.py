@@ -3,6 +3,7 @@
 Every function here launches HIP kernels from libfloodgan.so; nothing falls back to ATen.
 """
 import ctypes as C
+import os
 
 import torch
 
@@ -202,22 +203,30 @@ _TIMER = None
 USE_WIN = True   # route eligible single convs to the row-strip kernel (fg_conv_win)
 
 
-def conv(probs, tag=None):
+# InstanceNorm statistics from the pipelined kernel's epilogue where it runs (FLOODGAN_FUSED_IN_STATS=0: off)
+FUSED_IN_STATS = os.environ.get("FLOODGAN_FUSED_IN_STATS", "1") != "0"
+
+
+def conv(probs, tag=None, in_stats=False):
     """Launch 1-4 fg_conv_problem dicts (plans.conv_problem / phase_problems) in one kernel
-    (the row-strip window kernel for a lone eligible 7x7 conv, see win_eligible)."""
+    (the row-strip window kernel for a lone eligible 7x7 conv, see win_eligible).  in_stats=True:
+    the problems all write one output Buf (the 4 phases of a transposed conv, or a single conv) that an
+    InstanceNorm reads next; when the pipelined kernel takes them, its epilogue also emits the norm's
+    statistics partials and conv returns (mean, rstd) per (image, channel), else None."""
     if USE_WIN and len(probs) == 1 and win_eligible(probs[0]):
         return conv_win(probs[0], tag)
     if _TIMER is not None and tag in _TIMER.tags:
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
-        _conv(probs)
+        stats = _conv(probs, in_stats)
         e.record()
         _TIMER.events[tag].append((s, e))
     else:
-        _conv(probs)
+        stats = _conv(probs, in_stats)
+    return None if stats is None else _merge_stats(len(probs), *stats)
 
 
-def _conv(probs):
+def _conv(probs, in_stats=False):
     arr = (L.fg_conv_problem * len(probs))()
     f16 = L.fwd_f16x3()
     keep = {}
@@ -243,8 +252,41 @@ def _conv(probs):
                                              L.stream_handle()), "absmax")
                 wa = keep[("w", id(wt))]
             s.w_absmax = wa.data_ptr()
+    stats = _stats_partials(probs, arr) if (in_stats and FUSED_IN_STATS) else None
     L.check(_lib().fg_conv_fwd(arr, len(probs), L.stream_handle()), "conv_fwd")
     _wrote(*[p["y"][0] for p in probs])
+    return stats
+
+
+def _merge_stats(nprob, buf, n_img, rb, c):
+    """(mean, rstd) per (image, channel) from the epilogue partials of one conv launch"""
+    mean = torch.empty(n_img * c, dtype=torch.float32, device=buf.device)
+    rstd = torch.empty_like(mean)
+    work = torch.empty(int(_lib().fg_in_partials_workspace_doubles(n_img, c)), dtype=torch.float64,
+                       device=buf.device)
+    L.check(_lib().fg_in_stats_partials(L.ptr(buf), nprob, n_img, rb, c, C.c_float(EPS), L.ptr(mean),
+                                        L.ptr(rstd), L.ptr(work), L.stream_handle()), "in_stats_partials")
+    return mean, rstd
+
+
+def _stats_partials(probs, arr):
+    """attach epilogue-statistics buffers to the problem structs when the pipelined kernel takes them:
+    (buffer, images, 32-row blocks per image and problem, channels) or None"""
+    Y = probs[0]["y"][0]
+    if not isinstance(Y, Buf) or any(p["y"][0] is not Y for p in probs):
+        return None
+    rows = {p["m_a"] * p["m_b"] for p in probs}
+    c = probs[0]["n_out"]
+    if len(rows) != 1 or c != Y.c or any(p["n_out"] != c or p["m_img"] != Y.n for p in probs):
+        return None
+    r = rows.pop()
+    if r % 32 or not _lib().fg_conv_stats_ok(arr, len(probs)):
+        return None
+    rb = r // 32
+    buf = torch.empty(len(probs) * Y.n * rb * c * 2, dtype=torch.float32, device=Y.t.device)
+    for i in range(len(probs)):
+        arr[i].in_stats = buf.data_ptr() + 4 * i * Y.n * rb * c * 2
+    return buf, Y.n, rb, c
 
 
 def split_pixels(X):

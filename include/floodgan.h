@@ -96,6 +96,11 @@ typedef struct fg_conv_problem {
     int jc;               /* channels per pixel of the j run (j = s*jc + ch), or 0 if unknown: lets the
                              pipelined kernel walk the taps of one channel chunk back to back (the
                              gathered input rows are re-read while still in L2)                  */
+    float* in_stats;      /* optional: InstanceNorm statistics partials of the output, computed in the
+                             pipelined kernel's epilogue (see fg_conv_stats_ok): for every block of 32
+                             consecutive rows rb = m / 32 and column n < n_out, (mean, M2) of the 32
+                             stored values at in_stats[(rb * n_out + n) * 2] -- combined per image by
+                             fg_in_stats_partials                                                   */
 } fg_conv_problem;
 
 /*
@@ -141,6 +146,11 @@ int fg_device_ok(void);   /* 0 if a gfx950 device is current, else an error code
 /* ---------------------------------------------------------------------------------------- */
 /* Up to 4 problems in one launch (the four output phases of a stride-2 transposed conv). */
 int fg_conv_fwd(const fg_conv_problem* probs, int nprob, hipStream_t stream);
+
+/* 1 if fg_conv_fwd would run these problems on the pipelined f16x3 kernel with in_stats partials
+ * (f16x3 math, pre-split weights, N > 32, rows per image a multiple of 32, no activation, no
+ * accumulate); fg_conv_fwd fails on problems with in_stats that it cannot honour. */
+int fg_conv_stats_ok(const fg_conv_problem* probs, int nprob);
 
 /* Select the convolution arithmetic (FG_MATH_*) for subsequent launches (process-wide). */
 int fg_set_conv_math(int mode);
@@ -264,6 +274,15 @@ int fg_unfold_nchw(fg_view gpad, int fold_pad, int c, fg_wview dst, int h, int w
 /* ---------------------------------------------------------------------------------------- */
 /* instance norm (nn.InstanceNorm2d, affine=False, eps 1e-5) fused with activation           */
 /* ---------------------------------------------------------------------------------------- */
+/* Per-(n,c) mean and 1/sqrt(var+eps) from a conv's epilogue partials (fg_conv_problem.in_stats):
+ * `partials` holds nprob consecutive problems' [rows / 32][c][2] blocks, every problem with n_img images
+ * of rb_per_img 32-row blocks each (the 4 phases of a transposed conv: one image's statistics span all
+ * four).  Replaces fg_in_stats for outputs of the pipelined kernel. */
+int fg_in_stats_partials(const float* partials, int nprob, int n_img, int rb_per_img, int c, float eps, float* mean,
+                         float* rstd, double* work, hipStream_t stream);
+/* work doubles fg_in_stats_partials needs */
+long long fg_in_partials_workspace_doubles(int n_img, int c);
+
 /* Per-(n,c) mean and 1/sqrt(var+eps) of src's interior; work >= fg_in_workspace_doubles(). */
 long long fg_in_workspace_doubles(int n, int c);
 int fg_in_stats(fg_view src, float eps, float* mean, float* rstd, double* work,

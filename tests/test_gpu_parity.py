@@ -397,6 +397,71 @@ def test_instnorm_fwd_bwd(act, fold, residual, C, gadd):
     assert abs(float(bias_g.sum())) < 1e-3
 
 
+FUSED_CASES = [("resblock 3x3 s1 256->256", 256, 256, 3, 1, 1, 32, False, 0.0),
+               ("resblock, large mean", 256, 256, 3, 1, 1, 32, False, 40.0),
+               ("conv2 3x3 s2 64->128", 64, 128, 3, 2, 1, 64, False, 0.0),
+               ("disc 4x4 s2 128->256", 128, 256, 4, 2, 1, 64, False, 0.0),
+               ("deconv1 convT 256->128 (4 phases)", 256, 128, 3, 2, 1, 16, True, 0.0),
+               ("deconv2 convT 128->64 (4 phases)", 128, 64, 3, 2, 1, 32, True, 0.0)]
+
+
+@pytest.mark.parametrize("conv_math", ["f16x3"], indirect=True)
+@pytest.mark.parametrize("case", FUSED_CASES, ids=[c[0] for c in FUSED_CASES])
+def test_fused_in_stats(case, conv_math):
+    """InstanceNorm statistics from the pipelined conv kernel's epilogue (per-32-row (mean, M2) partials
+    merged in fp64) agree with the standalone fg_in_stats pass over the same conv output within 1e-5, and
+    the epilogue leaves the conv output bit-identical"""
+    from floodgan import ops, plans as PL
+    from floodgan.plans import Buf
+    _, ci, co, k, s, p, H, transposed, shift = case
+    torch.manual_seed(11)
+    N = 2
+    x = torch.randn(N, ci, H, H)
+    X = buf_from(x, p if not transposed else 1, "reflect" if (k == 3 and s == 1) else "constant")
+    if transposed:
+        w = torch.randn(ci, co, k, k) * 0.05
+        maps = PL.phase_maps(w.shape, 3, 1, ci)
+        wps = [ops.pack_weight(w.to(DEV), m) for m, _, _ in maps]
+        Ho = 2 * H
+        mk = lambda Y: PL.phase_problems(X, w.shape, 3, 1, Y, wps, maps, bias=b)  # noqa: E731
+    else:
+        w = torch.randn(co, ci, k, k) * 0.05
+        m = PL.wmap_conv_fwd(w.shape, ci)
+        wp = ops.pack_weight(w.to(DEV), m)
+        Ho = PL.out_size(H, k, s, p)
+        mk = lambda Y: [PL.conv_problem(X, p, k, s, wp, m, Y, bias=b)]  # noqa: E731
+    b = (torch.randn(co) * 0.1 + shift).to(DEV)
+    Y0 = Buf.empty(N, Ho, Ho, co, 0, DEV)
+    assert ops.conv(mk(Y0)) is None
+    Y1 = Buf.empty(N, Ho, Ho, co, 0, DEV)
+    st = ops.conv(mk(Y1), in_stats=True)
+    assert st is not None, "the pipelined kernel should take this conv with epilogue statistics"
+    mean_ref, rstd_ref = ops.in_stats(Y1)
+    torch.cuda.synchronize()
+    assert torch.equal(Y0.interior(), Y1.interior())
+    assert nrel(st[0], mean_ref) < KTOL
+    assert nrel(st[1], rstd_ref) < KTOL
+    # and against fp64 statistics of the output itself
+    y = Y1.interior().double().cpu()
+    mu = y.mean(dim=(1, 2))
+    var = y.var(dim=(1, 2), unbiased=False)
+    assert nrel(st[0].view(N, co), mu) < KTOL
+    assert nrel(st[1].view(N, co), (var + 1e-5).rsqrt()) < KTOL
+
+
+def test_fused_in_stats_declined():
+    """a conv the epilogue statistics cannot cover (output rows per image not a multiple of 32, e.g. the
+    discriminator's 4x4 stride-1 conv) returns None and the caller computes the statistics itself"""
+    from floodgan import ops, plans as PL
+    from floodgan.plans import Buf
+    torch.manual_seed(12)
+    X = buf_from(torch.randn(2, 256, 16, 16), 1, "constant")
+    w = torch.randn(512, 256, 4, 4, device=DEV) * 0.05
+    m = PL.wmap_conv_fwd(w.shape, 256)
+    Y = Buf.empty(2, 15, 15, 512, 0, DEV)
+    assert ops.conv([PL.conv_problem(X, 1, 4, 1, ops.pack_weight(w, m), m, Y)], in_stats=True) is None
+
+
 # ------------------------------------------------------------------ tail, losses, adam
 
 def test_tail():
