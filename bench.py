@@ -42,10 +42,11 @@ def resblock_conv_flops(batch, res):
 
 
 def resblock_conv_bytes(batch, res):
-    """algorithmic HBM bytes of one resblock conv launch: the reflect-padded input read once, the
-    pre-split fp16 (h, l) weights, the output written once"""
+    """algorithmic HBM bytes of one resblock forward conv launch: the reflect-padded input read once, the
+    pre-split fp16 (h, l) weights, the output written once, and the InstanceNorm statistics partials of
+    the epilogue ((mean, M2) per 32 output rows and channel)"""
     hw = res // 4
-    return 4.0 * batch * ((hw + 2) ** 2 * 256 + hw * hw * 256) + 2 * 2 * 256 * 2304
+    return 4.0 * batch * ((hw + 2) ** 2 * 256 + hw * hw * 256 + hw * hw // 32 * 256 * 2) + 2 * 2 * 256 * 2304
 
 
 def step_roofline(img_s_per_gpu, res, peak_conv):
@@ -96,7 +97,7 @@ def p2p_step_gflop_per_img(res):
     return tot / 1e9
 
 
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "round1", "r1l_pmc_resblock_fwd.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "round2", "r2_pmc_resblock_fwd.json")
 
 
 def pmc_traffic(kernel_tag):
@@ -296,7 +297,8 @@ def main():
                        "parallelism": f"dp{world}"},
             "conv_math": math,
             "roofline": {"bound": "mfma",
-                         "kernel": ("conv_fwd_f3_kernel<256,256,32,256,2> (LDS-DMA ring, 8 waves, 16x16x32 f16 MFMA)"
+                         "kernel": ("conv_fwd_f3_kernel<256,256,32,256,2> (LDS-DMA ring, 8 waves, 16x16x32 f16 MFMA, "
+                                    "InstanceNorm statistics epilogue)"
                                     if nprod == 3 else
                                     f"conv_fwd_x6_kernel<MathBF16x6,128,256,64,64>" if fwd_x6 else
                                     "conv_fwd_kernel<128,128,64,64>") + (

@@ -1,5 +1,6 @@
 """Run one conv-engine launch shape repeatedly (for rocprofv3 counter passes).
-  python scripts/conv_one.py [fwd|wgrad] [reps]  -- resblock 3x3 256->256 @128, bs 8"""
+  python scripts/conv_one.py [fwd|fwd_stats|wgrad] [reps]  -- resblock 3x3 256->256 @128, bs 8
+  (fwd_stats: with the InstanceNorm statistics epilogue, as the step's resblock forward runs)"""
 import os
 import sys
 
@@ -24,9 +25,9 @@ def main():
     m = PL.wmap_conv_fwd(w.shape, C)
     Y = Buf.empty(N, H, H, C, 0, dev)
     Y.t.uniform_(-1, 1)
-    if kind == "fwd":
+    if kind in ("fwd", "fwd_stats"):
         prob = PL.conv_problem(X, 1, k, 1, ops.pack_weight(w, m), m, Y, bias=torch.zeros(C, device=dev))
-        fn = lambda: ops.conv([prob])  # noqa: E731
+        fn = lambda: ops.conv([prob], in_stats=kind == "fwd_stats")  # noqa: E731
     else:
         wprob = PL.wgrad_conv(Y, X, 1, k, 1, C)
         dw = torch.empty_like(w)
