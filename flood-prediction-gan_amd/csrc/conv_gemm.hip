@@ -1108,6 +1108,40 @@ __global__ void pack_weight_f16_kernel(const float* __restrict__ w, fg_weight_ma
     }
 }
 
+// a batch of f16x3 repacks: the jobs' units (row, 8-k slot) are dealt to blocks job by job (blk[j] ..
+// blk[j+1]); a block's job index is uniform, its units are grid-strided over the job's blocks
+struct PackBatch {
+    fg_pack_job job[FG_PACK_BATCH_MAX];
+    int blk[FG_PACK_BATCH_MAX + 1];
+    int n;
+};
+static_assert(sizeof(PackBatch) <= 4096, "kernel argument size");
+
+__global__ void pack_weight_f16_batch_kernel(const PackBatch b) {
+    int j = 0;
+    while (j + 1 < b.n && (int)blockIdx.x >= b.blk[j + 1]) ++j;
+    const fg_pack_job& J = b.job[j];
+    const fg_weight_map& map = J.map;
+    const int QS = map.kh * map.jp / 8;
+    const long long total = (long long)map.n_out * QS;
+    const float sc = pow2_scale(J.w_absmax);
+    f16x8* wps = reinterpret_cast<f16x8*>(J.dst);
+    const int nb = b.blk[j + 1] - b.blk[j];
+    for (long long idx = (blockIdx.x - b.blk[j]) * (long long)blockDim.x + threadIdx.x; idx < total;
+         idx += (long long)nb * blockDim.x) {
+        const int n = (int)(idx / QS);
+        const int k0 = (int)(idx - (long long)n * QS) * 8;
+        const int kr = k0 / map.jp, j0 = k0 - (k0 / map.jp) * map.jp;
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = packed_w(J.w, map, n, kr, j0 + e);
+        f16x8 pc[2];
+        MathF16x3::split(v, sc, pc);
+        wps[idx * 2] = pc[0];
+        wps[idx * 2 + 1] = pc[1];
+    }
+}
+
 // max |x| as the bit pattern of a non-negative float (uint order = float order; NaN sorts high)
 __global__ void absmax_kernel(const float* __restrict__ x, long long n, unsigned* __restrict__ out) {
     unsigned m = 0;
@@ -1434,6 +1468,30 @@ FG_API int fg_pack_weight_f16(const float* w, const fg_weight_map* map, const fl
     hipLaunchKernelGGL(pack_weight_f16_kernel, dim3(fg::blocks_for(total, 256, 8192)), dim3(256), 0, stream, w, *map,
                        w_absmax, reinterpret_cast<f16x8*>(wps));
     return fg::launched("pack_weight_f16");
+}
+
+FG_API int fg_pack_weight_f16_batch(const fg_pack_job* jobs, int njobs, hipStream_t stream) {
+    if (!jobs || njobs < 0 || njobs > FG_PACK_BATCH_MAX)
+        return fg::fail(FG_ERR_INVALID, "fg_pack_weight_f16_batch: %d jobs (at most %d)", njobs, FG_PACK_BATCH_MAX);
+    if (njobs == 0) return 0;
+    PackBatch b;
+    b.n = njobs;
+    int blocks = 0;
+    for (int j = 0; j < njobs; ++j) {
+        const fg_pack_job& J = jobs[j];
+        const fg_weight_map& m = J.map;
+        if (!J.w || !J.dst || !J.w_absmax || !aligned16(J.dst))
+            return fg::fail(FG_ERR_INVALID, "fg_pack_weight_f16_batch: job %d null/unaligned", j);
+        if (m.kh > 8 || m.kw > 8 || m.jp % BK || m.jp < m.kw * m.c || m.c < 1 || m.n_out < 1)
+            return fg::fail(FG_ERR_INVALID, "fg_pack_weight_f16_batch: job %d bad map kh=%d kw=%d c=%d jp=%d", j,
+                            m.kh, m.kw, m.c, m.jp);
+        b.job[j] = J;
+        b.blk[j] = blocks;
+        blocks += (int)fg::blocks_for((long long)m.n_out * m.kh * m.jp / 8, 256, 512);
+    }
+    b.blk[njobs] = blocks;
+    hipLaunchKernelGGL(pack_weight_f16_batch_kernel, dim3(blocks), dim3(256), 0, stream, b);
+    return fg::launched("pack_weight_f16_batch");
 }
 
 FG_API int fg_absmax(const float* x, long long n, float* out, hipStream_t stream) {

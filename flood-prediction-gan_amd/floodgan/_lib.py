@@ -60,6 +60,13 @@ class fg_weight_map(C.Structure):
                 ("n_base", C.c_int), ("rtab", C.c_int * 8), ("stab", C.c_int * 8)]
 
 
+class fg_pack_job(C.Structure):
+    _fields_ = [("w", C.c_void_p), ("w_absmax", C.c_void_p), ("dst", C.c_void_p), ("map", fg_weight_map)]
+
+
+FG_PACK_BATCH_MAX = 24
+
+
 class fg_adam_tensor(C.Structure):
     _fields_ = [("param", C.c_void_p), ("grad", C.c_void_p), ("exp_avg", C.c_void_p),
                 ("exp_avg_sq", C.c_void_p), ("numel", C.c_longlong), ("absmax", C.c_void_p)]
@@ -99,6 +106,7 @@ SIGNATURES = {
     "fg_pack_weight": [C.c_void_p, C.POINTER(fg_weight_map), C.c_void_p, C.c_void_p],
     "fg_pack_weight_split": [C.c_void_p, C.POINTER(fg_weight_map), C.c_void_p, C.c_void_p],
     "fg_pack_weight_f16": [C.c_void_p, C.POINTER(fg_weight_map), C.c_void_p, C.c_void_p, C.c_void_p],
+    "fg_pack_weight_f16_batch": [C.c_void_p, C.c_int, C.c_void_p],
     "fg_absmax": [C.c_void_p, C.c_longlong, C.c_void_p, C.c_void_p],
     "fg_conv_n1_fwd": [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
                        C.c_int, C.c_void_p],

@@ -143,6 +143,33 @@ def _weight_absmax(w):
     return slot
 
 
+# Pack cache (f16x3): each parameter keeps its packed layouts (one per weight map) with the absmax slot
+# they were scaled by; a pack is current while that slot is the parameter's current one (a torch write
+# moves the version counter, an adam_step installs a new slot AND re-packs every cached layout of the
+# parameters it updated in batched launches), so a training step packs nothing itself.
+# FLOODGAN_PACK_CACHE=0: pack at every use.
+PACK_CACHE = os.environ.get("FLOODGAN_PACK_CACHE", "1") != "0"
+
+
+def _repack(params):
+    """re-pack every cached f16x3 layout of `params` with their current absmax slots (after an update)"""
+    jobs = []
+    for p in params:
+        packs = p.__dict__.get("_fg_packs")
+        if not packs:
+            continue
+        slot = _weight_absmax(p)
+        for wp in packs.values():
+            j = L.fg_pack_job()
+            j.w, j.w_absmax, j.dst, j.map = p.data_ptr(), slot.data_ptr(), wp.data_ptr(), wp._fg_map
+            jobs.append(j)
+            wp.absmax = slot
+    for i in range(0, len(jobs), L.FG_PACK_BATCH_MAX):
+        part = jobs[i:i + L.FG_PACK_BATCH_MAX]
+        arr = (L.fg_pack_job * len(part))(*part)
+        L.check(_lib().fg_pack_weight_f16_batch(arr, len(part), L.stream_handle()), "pack_weight_f16_batch")
+
+
 def pack_weight(w, m, split=None):
     """Packed weight for the conv engine: fp32 [n][kh*jp]; or, by default under a split forward
     math, the pre-split layout -- bf16 h/m/l pieces (bf16x6, fg_pack_weight_split) or scaled fp16
@@ -157,10 +184,17 @@ def pack_weight(w, m, split=None):
         split = "f16x3" if L.fwd_f16x3() else "bf16x6"
     if split == "f16x3":
         amax = _weight_absmax(w)
+        packs = w.__dict__.setdefault("_fg_packs", {}) if PACK_CACHE else None
+        key = bytes(s)
+        if packs is not None and key in packs and packs[key].absmax is amax:
+            return packs[key]          # packed from the current values (re-packed by the last adam_step)
         wp = torch.empty(2 * packed_numel(m), dtype=torch.float16, device=w.device)
         L.check(_lib().fg_pack_weight_f16(L.ptr(w), C.byref(s), L.ptr(amax), L.ptr(wp), L.stream_handle()),
                 "pack_weight_f16")
         wp.absmax = amax
+        if packs is not None:
+            wp._fg_map = s
+            packs[key] = wp
         return wp
     if split == "bf16x6":
         wp = torch.empty(3 * packed_numel(m), dtype=torch.bfloat16, device=w.device)
@@ -669,3 +703,5 @@ def adam_step(entries, lr, beta1, beta2, eps, step):
         # the kernel wrote p through a raw pointer: torch's version counter did not move, so a
         # later in-place torch write (another optimizer, load_state_dict) still invalidates this
         p._fg_amax, p._fg_amax_ver = slot, p._version
+    if slots and slots[0] is not None and PACK_CACHE:
+        _repack([e[0] for e in entries])

@@ -207,6 +207,20 @@ int fg_pack_weight_split(const float* w, const fg_weight_map* map, void* wps, hi
 int fg_pack_weight_f16(const float* w, const fg_weight_map* map, const float* w_absmax, void* wps,
                        hipStream_t stream);
 
+/* One weight repack of a batch (fg_pack_weight_f16_batch): w through map into the f16x3 layout at dst,
+ * scaled by the w_absmax slot -- the arguments of one fg_pack_weight_f16 call. */
+typedef struct fg_pack_job {
+    const float* w;
+    const float* w_absmax;
+    void* dst;
+    fg_weight_map map;
+} fg_pack_job;
+
+/* Up to FG_PACK_BATCH_MAX fg_pack_weight_f16 repacks in one launch (the pack cache refreshing every
+ * packed layout of the parameters an optimizer step just updated). */
+#define FG_PACK_BATCH_MAX 24
+int fg_pack_weight_f16_batch(const fg_pack_job* jobs, int njobs, hipStream_t stream);
+
 /* Pre-split operand for fg_conv_win: the npix NHWC pixels of c (32 or 64) fp32 channels at src,
  * scaled by the power of two of the absmax slot (as fg_pack_weight_f16) and split into fp16
  * pieces h, l; pixel p (padded-row column x = p % wp) becomes 2c fp16 whose 16-byte chunk k
