@@ -345,9 +345,12 @@ def win_eligible(prob):
     X, off = prob["x"]
     if not L.fwd_f16x3() or not isinstance(X, Buf) or X.c not in (32, 64):
         return False
+    # C = 32 is the content head's input gradient (27(32) -> 64): its split copy is the one the content
+    # weight gradient already made, and the strip form beats the pipelined kernel's per-tap re-gather
+    # (1.58 vs 1.67 ms at bs 8, profiles/round2/r2v_content_dgrad_win.log)
     return (prob["kh"] == 7 and prob["j_valid"] == 7 * X.c and prob["jp"] == prob["j_valid"]
             and prob["sxb"] == X.c and prob["sxa"] == prob["sxr"] == X.s_row and off == 0
-            and prob["n_out"] <= 32 and X.c == 64 and prob["m_b"] >= 256
+            and prob["n_out"] <= (32 if X.c == 64 else 64) and prob["m_b"] >= 256
             and prob["w"][0].dtype == torch.float16)
 
 
