@@ -644,12 +644,29 @@ int f3_config(int max_n) {
     return g_f3_tile >= 0 ? g_f3_tile : (max_n > 128 ? 4 : max_n > 64 ? 6 : max_n > 32 ? 7 : -1);
 }
 
+// tiles a batch makes on a BM x BN tile
+long long batch_tiles(const fg_conv_problem* p, int nprob, int bm, int bn) {
+    long long t = 0;
+    for (int i = 0; i < nprob; ++i)
+        t += ((long long)p[i].m_img * p[i].m_a * p[i].m_b + bm - 1) / bm * ((p[i].n_out + bn - 1) / bn);
+    return t;
+}
+
+// the automatic choice's exception: a batch that gives fewer than half the CUs a 256-row tile
+bool small_batch_cfg9(const fg_conv_problem* p, int nprob, int max_n) {
+    const int cfg = f3_config(max_n);
+    if (g_f3_tile >= 0 || cfg < 0 || cfg == 9) return false;
+    const int bn = cfg == 4 ? 256 : cfg == 6 ? 128 : 64;     // cfgs 4 / 6 / 7: 256-row tiles
+    return batch_tiles(p, nprob, 256, bn) < fg::num_cus() / 2;
+}
+
 bool f3_takes(const fg_conv_problem* probs, int nprob, int max_n) {
     if (g_f3_tile == -2 || f3_config(max_n) < 0) return false;
     for (int i = 0; i < nprob; ++i) {
         const fg_conv_problem& p = probs[i];
-        // no K padding (every staged k is a real tap: padded j would gather past the row run)
-        if (p.w_split != 2 || p.jp % 32 || p.j_valid != p.jp || p.ldw != p.kh * p.jp || !p.x_absmax || !p.w_absmax ||
+        // no K padding (every staged k is a real tap: padded j would gather past the row run); ldw may exceed
+        // kh * jp (a kernel-row range of a larger pack: the resblock input gradient's row strips)
+        if (p.w_split != 2 || p.jp % 32 || p.j_valid != p.jp || p.ldw < p.kh * p.jp || !p.x_absmax || !p.w_absmax ||
             p.m_img * p.m_a * p.m_b < 1)
             return false;
     }
@@ -668,12 +685,18 @@ bool f3_stats_ok(const fg_conv_problem* probs, int nprob, int max_n) {
     return true;
 }
 
+
 int launch_fwd_f3(const ConvBatch& b, int nprob, int max_n, hipStream_t stream, int* rc) {
     if (!f3_takes(b.p, nprob, max_n)) return 0;
     // N <= 64: the 256-row tile (cfg 7) beats the 128-row one by 4-13 % on the step's N=64 convs (content
     // input gradient 1.67 vs 1.92 ms, deconv2 / conv2-dgrad phases 0.626 vs 0.653 ms at bs 8 512^2:
     // profiles/round2/r2r_diag_n64.log)
-    const int cfg = f3_config(max_n);
+    int cfg = f3_config(max_n);
+    // a batch too small to give half the CUs a tile (the resblock input gradient's edge strips: 18 tiles of
+    // 256 x 256) runs on 128 x 64 tiles instead: a workgroup's time is its tile's K walk, so 8x smaller tiles
+    // on 8x more CUs finish sooner (strips 58 us on the x6 kernel, 75 us on cfg 4, 33 us on cfg 9:
+    // profiles/round2/r2aa_strips.log).  cfg 9 has 32-row wave blocks, so statistics launches take it too.
+    if (small_batch_cfg9(b.p, nprob, max_n)) cfg = 9;
     switch (cfg) {
         case 0: *rc = launch_cfg<128, 256, 32, 128>(b, nprob, stream); return 1;
         case 1: *rc = launch_cfg<256, 128, 64, 64>(b, nprob, stream); return 1;
