@@ -652,12 +652,24 @@ long long batch_tiles(const fg_conv_problem* p, int nprob, int bm, int bn) {
     return t;
 }
 
-// the automatic choice's exception: a batch that gives fewer than half the CUs a 256-row tile
-bool small_batch_cfg9(const fg_conv_problem* p, int nprob, int max_n) {
-    const int cfg = f3_config(max_n);
-    if (g_f3_tile >= 0 || cfg < 0 || cfg == 9) return false;
-    const int bn = cfg == 4 ? 256 : cfg == 6 ? 128 : 64;     // cfgs 4 / 6 / 7: 256-row tiles
-    return batch_tiles(p, nprob, 256, bn) < fg::num_cus() / 2;
+// the automatic choice for a batch that leaves at least half the CUs without a tile: narrower 256-row tiles
+// (cfg 4 -> 6 -> 7) while that is so, then 128 x 64 (cfg 9).  A workgroup's time is its tile's K walk, so a
+// launch with idle CUs finishes sooner on more, smaller tiles: D model.8's input gradient in the G step (bs 8,
+// 128 tiles) 496 -> 354 us and model.5's forward 145 -> 103 us on cfg 6, the resblock input gradient's edge
+// strips (18 tiles) 75 -> 33 us on cfg 9 (profiles/round2/r2ac_underfill.log, r2aa_strips.log).  A nearly full
+// wave stays (D model.8's forward, 250 tiles: 322 us on cfg 4, 367 on cfg 6).  All have 32-row wave blocks.
+int g_f3_fill = 1;    // fg_set_f3_fill: 0 = keep the tile f3_config picks by N (A/B hook)
+
+int auto_cfg(const fg_conv_problem* p, int nprob, int max_n) {
+    int cfg = f3_config(max_n);
+    if (g_f3_tile >= 0 || cfg < 0 || !g_f3_fill) return cfg;
+    const int cus = fg::num_cus();
+    while (cfg == 4 || cfg == 6 || cfg == 7) {
+        const int bn = cfg == 4 ? 256 : cfg == 6 ? 128 : 64;
+        if (2 * batch_tiles(p, nprob, 256, bn) > cus) return cfg;
+        cfg = cfg == 4 ? 6 : cfg == 6 ? 7 : 9;
+    }
+    return cfg;
 }
 
 bool f3_takes(const fg_conv_problem* probs, int nprob, int max_n) {
@@ -676,7 +688,7 @@ bool f3_takes(const fg_conv_problem* probs, int nprob, int max_n) {
 // the epilogue statistics need whole 32-row wave blocks inside one image (WM = 32 in every config)
 bool f3_stats_ok(const fg_conv_problem* probs, int nprob, int max_n) {
     if (!f3_takes(probs, nprob, max_n)) return false;
-    const int cfg = f3_config(max_n);
+    const int cfg = auto_cfg(probs, nprob, max_n);
     if (!(cfg == 0 || cfg == 3 || cfg == 4 || cfg == 6 || cfg == 7 || cfg == 9)) return false;   // WM = 32 configs
     for (int i = 0; i < nprob; ++i) {
         const fg_conv_problem& p = probs[i];
@@ -691,12 +703,7 @@ int launch_fwd_f3(const ConvBatch& b, int nprob, int max_n, hipStream_t stream, 
     // N <= 64: the 256-row tile (cfg 7) beats the 128-row one by 4-13 % on the step's N=64 convs (content
     // input gradient 1.67 vs 1.92 ms, deconv2 / conv2-dgrad phases 0.626 vs 0.653 ms at bs 8 512^2:
     // profiles/round2/r2r_diag_n64.log)
-    int cfg = f3_config(max_n);
-    // a batch too small to give half the CUs a tile (the resblock input gradient's edge strips: 18 tiles of
-    // 256 x 256) runs on 128 x 64 tiles instead: a workgroup's time is its tile's K walk, so 8x smaller tiles
-    // on 8x more CUs finish sooner (strips 58 us on the x6 kernel, 75 us on cfg 4, 33 us on cfg 9:
-    // profiles/round2/r2aa_strips.log).  cfg 9 has 32-row wave blocks, so statistics launches take it too.
-    if (small_batch_cfg9(b.p, nprob, max_n)) cfg = 9;
+    const int cfg = auto_cfg(b.p, nprob, max_n);
     switch (cfg) {
         case 0: *rc = launch_cfg<128, 256, 32, 128>(b, nprob, stream); return 1;
         case 1: *rc = launch_cfg<256, 128, 64, 64>(b, nprob, stream); return 1;
@@ -735,5 +742,11 @@ FG_API int fg_set_f3_sched(int sched) {
 FG_API int fg_set_f3_order(int alt) {
     if (alt < 0 || alt > 7) return fg::fail(FG_ERR_INVALID, "fg_set_f3_order: %d", alt);
     g_f3_alt = alt;
+    return 0;
+}
+
+FG_API int fg_set_f3_fill(int on) {
+    if (on < 0 || on > 1) return fg::fail(FG_ERR_INVALID, "fg_set_f3_fill: %d", on);
+    fgc::g_f3_fill = on;
     return 0;
 }

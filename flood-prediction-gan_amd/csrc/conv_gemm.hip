@@ -1045,6 +1045,41 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ slabs, int splits,
     }
 }
 
+// the same reduction for small weights split many ways (the 1x1 attention head: 640 elements x 512 slabs ran
+// as 3 blocks of sequential 512-term sums, 41 us): block = 64 elements x 16 split lanes, each lane a strided
+// fp64 sum, the 16 lanes combined in LDS in a fixed order (deterministic)
+__global__ void __launch_bounds__(1024) wgrad_reduce_wide_kernel(const float* __restrict__ slabs, int splits,
+                                                                  fg_weight_map map, float* __restrict__ dw,
+                                                                  int accumulate) {
+    const int J = map.kw * map.c;
+    const long long K = (long long)map.kh * J;
+    const long long total = (long long)map.n_out * K;
+    const int e = threadIdx.x & 63, q = threadIdx.x >> 6;
+    const long long idx = (long long)blockIdx.x * 64 + e;
+    double acc = 0.0;
+    if (idx < total)
+        for (int sp = q; sp < splits; sp += 16) acc += slabs[(size_t)sp * total + idx];
+    __shared__ double red[16][64];
+    red[q][e] = acc;
+    __syncthreads();
+    if (q != 0 || idx >= total) return;
+    double sum = 0.0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) sum += red[i][e];
+    const int a = (int)(idx / K);
+    const int k = (int)(idx - (long long)a * K);
+    const int kr = k / J, j = k - (k / J) * J;
+    const int ks = j / map.c, ch = j - (j / map.c) * map.c;
+    if (ch >= map.c_valid) return;
+    const int r = map.rtab[kr], c2 = map.stab[ks];
+    const int n = a + map.n_base;
+    const size_t dst = map.dim0_is_n ? (((size_t)n * map.d1 + ch) * map.KH + r) * map.KW + c2
+                                     : (((size_t)ch * map.d1 + n) * map.KH + r) * map.KW + c2;
+    float v = (float)sum;
+    if (accumulate) v += dw[dst];
+    dw[dst] = v;
+}
+
 __device__ __forceinline__ float packed_w(const float* __restrict__ w, const fg_weight_map& map, int n, int kr, int j) {
     if (j >= map.kw * map.c) return 0.f;
     const int ks = j / map.c, ch = j - (j / map.c) * map.c;
@@ -1430,6 +1465,12 @@ FG_API int fg_wgrad_reduce(const float* slabs, int splits, const fg_weight_map* 
     if (map->kh > 8 || map->kw > 8 || map->c < 1 || map->n_out < 1)
         return fg::fail(FG_ERR_INVALID, "fg_wgrad_reduce: bad map");
     const long long total = (long long)map->n_out * map->kh * map->kw * map->c;
+    if (total <= 256 * 1024 && splits >= 32 && total * 4 < (long long)splits * 1024) {
+        // few elements, many slabs: parallel over the splits too
+        hipLaunchKernelGGL(wgrad_reduce_wide_kernel, dim3((unsigned)((total + 63) / 64)), dim3(1024), 0, stream, slabs,
+                           splits, *map, dw, accumulate);
+        return fg::launched("wgrad_reduce_wide");
+    }
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(fg::blocks_for(total, 256, 8192)), dim3(256), 0, stream, slabs,
                        splits, *map, dw, accumulate);
     return fg::launched("wgrad_reduce");

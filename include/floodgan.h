@@ -179,6 +179,9 @@ int fg_set_f3_sched(int sched);
  * 0 = one workgroup per tile; n >= 2 = at most n resident workgroups (test hook: every workgroup then
  * streams many tiles back to back even at small problem sizes). */
 int fg_set_f3_persistent(int on);
+/* A/B hook: 1 (default) = a pipelined-kernel launch that would leave at least half the CUs without a tile
+ * runs on narrower / shorter tiles (conv_f3.hip auto_cfg); 0 = the tile chosen by output channels only. */
+int fg_set_f3_fill(int on);
 /* A/B hook of the pipelined f16x3 weight-gradient kernel (conv_wgrad_f3.hip, n_a >= 128): 0 off,
  * 1 = staging as one burst per stage, 3 = staging slots interleaved with the MFMA groups,
  * 2 (default) = the measured choice per tile (interleaved for 128-row tiles). */

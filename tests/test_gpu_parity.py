@@ -72,7 +72,9 @@ def _fold_cpu(gpad, p):
 
 CONV_CASES = [(9, 64, 7, 1, 3, "reflect", 24), (64, 128, 3, 2, 1, "constant", 20), (256, 256, 3, 1, 1, "reflect", 12),
               (64, 27, 7, 1, 3, "reflect", 16), (64, 10, 1, 1, 0, "constant", 16), (12, 64, 4, 2, 1, "constant", 32),
-              (128, 256, 4, 2, 1, "constant", 16), (256, 512, 4, 1, 1, "constant", 9), (512, 1, 4, 1, 1, "constant", 9)]
+              (128, 256, 4, 2, 1, "constant", 16), (256, 512, 4, 1, 1, "constant", 9), (512, 1, 4, 1, 1, "constant", 9),
+              # 1x1 head at 96^2: the weight gradient splits >= 32 ways over 640 elements (split-parallel reduce)
+              (64, 10, 1, 1, 0, "constant", 96)]
 
 
 @pytest.mark.parametrize("conv_math", MATHS, indirect=True)
