@@ -118,6 +118,10 @@ SIGNATURES = {
     "fg_conv_win": [C.POINTER(fg_conv_problem), C.c_void_p, C.c_longlong, C.c_void_p],
     "fg_conv_wgrad_win": [C.POINTER(fg_wgrad_problem), C.c_void_p, C.c_longlong, C.c_int, C.c_int, C.c_void_p,
                           C.c_longlong, C.c_int, C.c_void_p],
+    "fg_conv1x1_fwd": [fg_view, C.c_void_p, C.c_void_p, C.c_int, fg_view, C.c_void_p],
+    "fg_conv1x1_dgrad": [fg_view, C.c_void_p, C.c_int, fg_view, C.c_void_p],
+    "fg_conv1x1_wgrad": [fg_view, fg_view, C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p],
+    "fg_conv1x1_wgrad_workspace_floats": [C.c_int],
     "fg_pack_input": [fg_sview, C.c_int, fg_sview, C.c_int, fg_view, C.c_int, C.c_int, C.c_int, C.c_void_p],
     "fg_zero_border": [fg_view, C.c_void_p],
     "fg_fold_add": [fg_view, C.c_int, fg_view, fg_view, C.c_void_p],
@@ -170,7 +174,7 @@ SIGNATURES = {
 RESTYPES = {"fg_last_error": C.c_char_p, "fg_in_workspace_doubles": C.c_longlong, "fg_bn_workspace_doubles": C.c_longlong,
             "fg_ssim_workspace_doubles": C.c_longlong, "fg_sq_err_workspace_doubles": C.c_longlong,
             "fg_channel_sum_workspace_doubles": C.c_longlong,
-            "fg_in_partials_workspace_doubles": C.c_longlong}
+            "fg_in_partials_workspace_doubles": C.c_longlong, "fg_conv1x1_wgrad_workspace_floats": C.c_longlong}
 
 _lib = None
 

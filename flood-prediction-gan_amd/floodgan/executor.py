@@ -19,6 +19,10 @@ from .plans import Buf
 
 N_BLOCKS = 9
 CONTENT_ALLOC = 32   # 27 content channels, padded for aligned NHWC rows
+N_ATT = 10           # attention logits (deconv3_attention's output channels)
+# the attention head's 1x1 conv and its gradients as fp32 FMA kernels (csrc/head1x1.hip); FLOODGAN_HEAD_1X1=0:
+# the implicit-GEMM engine
+HEAD_1X1 = os.environ.get("FLOODGAN_HEAD_1X1", "1") != "0"
 ATT_ALLOC = 16       # 10 attention channels
 
 
@@ -205,7 +209,12 @@ def gen_forward(P, x, save=True, x_extra=None):
         S.update(heads=heads, cl=cl)
         return out, None, (S if save else None)
     al = Buf.empty(N, H, W, ATT_ALLOC, 0, dev)
-    _conv_fwd(P, "deconv3_attention", heads["attention"]["ad2"], 0, 1, 1, al)
+    if HEAD_1X1:
+        # 1x1 64 -> 10: a per-pixel matrix-vector product, fp32 FMA over LDS-staged tiles (csrc/head1x1.hip)
+        ops.conv1x1_fwd(heads["attention"]["ad2"], P["deconv3_attention.weight"], P["deconv3_attention.bias"],
+                        N_ATT, al)
+    else:
+        _conv_fwd(P, "deconv3_attention", heads["attention"]["ad2"], 0, 1, 1, al)
     mask = torch.empty(N, H, W, dtype=torch.float32, device=dev)
     ops.tail_fwd(cl, al, x, out, mask)
     S.update(heads=heads, cl=cl, al=al)
@@ -372,10 +381,16 @@ def gen_backward(P, S, g_out, grads_into=None, ready=None, input_grad=None, accu
     heads = [("content", hc, g_ad2c, 3)]
     if attention:
         # ---- deconv3_attention: 1x1
-        _wgrad_conv(P, G, "deconv3_attention", gal, ha["ad2"], 0, 1, 1)
-        ops.channel_sum(gal, 10, G.get("deconv3_attention.bias"), G.acc)
         g_ad2a = Buf.empty(N, H, W, 64, 0, dev)
-        _dgrad_s1(P, "deconv3_attention", gal, 0, 1, g_ad2a)
+        if HEAD_1X1:
+            names = ("deconv3_attention.weight", "deconv3_attention.bias")
+            G.off_path(lambda: ops.conv1x1_wgrad(gal, ha["ad2"], N_ATT, G.get(names[0]), G.get(names[1]), G.acc),
+                       (gal, ha["ad2"]), names)
+            ops.conv1x1_dgrad(gal, P["deconv3_attention.weight"], N_ATT, g_ad2a)
+        else:
+            _wgrad_conv(P, G, "deconv3_attention", gal, ha["ad2"], 0, 1, 1)
+            ops.channel_sum(gal, 10, G.get("deconv3_attention.bias"), G.acc)
+            _dgrad_s1(P, "deconv3_attention", gal, 0, 1, g_ad2a)
         heads.append(("attention", ha, g_ad2a, 0))
     # ---- deconv2 / deconv1 of both heads
     g_h = Buf.empty(N, H // 4, W // 4, 256, 0, dev)

@@ -488,6 +488,24 @@ def pack_input(a, ca, b, cb, dst, img0, nimg, pad_mode):
             "pack_input")
 
 
+def conv1x1_fwd(X, w, b, n_out, Y):
+    """the attention head's 1x1 conv (fp32 FMA, fg_conv1x1_fwd): Y[..., :n_out] = w X + b, Y's other
+    channels 0"""
+    _wrote(Y)
+    L.check(_lib().fg_conv1x1_fwd(view(X), L.ptr(w), L.ptr(b), n_out, view(Y), L.stream_handle()), "conv1x1_fwd")
+
+
+def conv1x1_dgrad(GY, w, n_out, GX):
+    _wrote(GX)
+    L.check(_lib().fg_conv1x1_dgrad(view(GY), L.ptr(w), n_out, view(GX), L.stream_handle()), "conv1x1_dgrad")
+
+
+def conv1x1_wgrad(GY, X, n_out, dw, db, accumulate=False):
+    work = torch.empty(int(_lib().fg_conv1x1_wgrad_workspace_floats(n_out)), dtype=torch.float32, device=dw.device)
+    L.check(_lib().fg_conv1x1_wgrad(view(GY), view(X), n_out, L.ptr(dw), L.ptr(db), int(accumulate), L.ptr(work),
+                                    L.stream_handle()), "conv1x1_wgrad")
+
+
 def zero_border(B):
     _wrote(B)
     L.check(_lib().fg_zero_border(view(B), L.stream_handle()), "zero_border")

@@ -247,6 +247,19 @@ int fg_conv_win(const fg_conv_problem* prob, const void* x_split, long long x_pi
 int fg_conv_wgrad_win(const fg_wgrad_problem* prob, const void* p_split, long long p_pix0, int p_col0,
                       int wp_p, const void* x_split, long long x_pix0, int wp_x, hipStream_t stream);
 
+/* The attention head's 1x1 conv (Conv2d(64, n_out <= 16, 1), models/model_architectures.py:334) in fp32
+ * FMA over LDS-staged 64-pixel tiles: y (4 <= c_alloc <= 16; channels >= n_out written as 0) = w x + b over
+ * x's interior (c_alloc 64); replaces fg_conv_fwd on that layer (a matrix-vector product per pixel). */
+int fg_conv1x1_fwd(fg_view x, const float* w, const float* bias, int n_out, fg_view y, hipStream_t stream);
+/* Its input gradient: gx (c_alloc 64) = w^T gy over the interior. */
+int fg_conv1x1_dgrad(fg_view gy, const float* w, int n_out, fg_view gx, hipStream_t stream);
+/* Its weight and bias gradients (PyTorch layouts, written or, with accumulate, raised; db optional):
+ * per-block partial sums in `work` (fg_conv1x1_wgrad_workspace_floats(n_out) floats), reduced in fp64
+ * in a fixed order. */
+long long fg_conv1x1_wgrad_workspace_floats(int n_out);
+int fg_conv1x1_wgrad(fg_view gy, fg_view x, int n_out, float* dw, float* db, int accumulate, float* work,
+                     hipStream_t stream);
+
 /* The discriminator's last conv (Conv2d(512, 1, 4, 1, 1), models/model_architectures.py:437) in fp32:
  * y[n][oy][ox] = bias[0] + sum_{c,r,s} x(n, oy+r, ox+s, c) * w[c*16 + r*4 + s] over the 1-padded NHWC
  * input x (nimg images of hp x wp padded pixels, c = 512), y NCHW [nimg, 1, ho, wo], ho = hp-3. */

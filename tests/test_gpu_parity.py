@@ -324,6 +324,43 @@ def test_conv_window(case):
         L.set_conv_math(prev)
 
 
+@pytest.mark.parametrize("N,H,W,n_out,xpad", [(2, 20, 37, 10, 0), (3, 9, 64, 10, 1), (1, 5, 7, 16, 0), (2, 96, 96, 3, 0)])
+def test_conv1x1_head(N, H, W, n_out, xpad):
+    """the attention head's 1x1 conv in fp32 FMA (fg_conv1x1_*): forward (pad channels written as 0), input
+    gradient, weight + bias gradients (written and accumulated) against fp64, ragged last tiles"""
+    from floodgan import ops
+    from floodgan.plans import Buf
+    torch.manual_seed(21)
+    x = torch.randn(N, 64, H, W, dtype=torch.float64)
+    w = (torch.randn(n_out, 64, 1, 1, dtype=torch.float64) * 0.1).requires_grad_(True)
+    b = torch.randn(n_out, dtype=torch.float64, requires_grad=True)
+    xr = x.clone().requires_grad_(True)
+    y = F.conv2d(xr, w, b)
+    gy = torch.randn_like(y)
+    gx_ref, gw_ref, gb_ref = torch.autograd.grad(y, (xr, w, b), gy)
+    X = buf_from(x, xpad, "constant")
+    wd, bd = w.detach().float().to(DEV), b.detach().float().to(DEV)
+    Y = Buf.empty(N, H, W, 16, 0, DEV)
+    Y.t.fill_(float("nan"))
+    ops.conv1x1_fwd(X, wd, bd, n_out, Y)
+    torch.cuda.synchronize()
+    assert nrel(nchw(Y, n_out), y) < KTOL
+    if n_out < 16:
+        assert float(Y.nhwc()[..., n_out:].abs().max()) == 0.0
+    GY = buf_from(gy, 0, "constant", c_alloc=16)
+    GX = Buf.empty(N, H, W, 64, 0, DEV)
+    ops.conv1x1_dgrad(GY, wd, n_out, GX)
+    dw = torch.full(w.shape, 3.0, device=DEV)
+    db = torch.full((n_out,), -2.0, device=DEV)
+    ops.conv1x1_wgrad(GY, X, n_out, dw, db)
+    torch.cuda.synchronize()
+    assert nrel(nchw(GX), gx_ref) < KTOL
+    assert nrel(dw, gw_ref) < KTOL and nrel(db, gb_ref) < KTOL
+    ops.conv1x1_wgrad(GY, X, n_out, dw, db, accumulate=True)
+    torch.cuda.synchronize()
+    assert nrel(dw, 2 * gw_ref) < KTOL and nrel(db, 2 * gb_ref) < KTOL
+
+
 def test_disc_head_n1():
     """model.11 (Conv2d(512, 1, 4, 1, 1)): the fp32 FMA forward and weight-gradient kernels vs fp64"""
     from floodgan import ops, plans as PL
