@@ -37,6 +37,7 @@ __device__ __forceinline__ int swz_wrow(int n) {         // weight image row n
 template <int N>
 __device__ __forceinline__ void vm_wait() {
     if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
     else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else static_assert(N < 0, "add the vmcnt immediate");
@@ -65,6 +66,8 @@ __global__ void split_pixels_kernel(const float* __restrict__ src, long long npi
     }
 }
 
+int g_win_waves = 8;   // FLOODGAN_WIN_WAVES overrides (A/B)
+
 struct WinArgs {
     fg_conv_problem P;
     const char* xs;     // split input at the problem's x origin (pixel (0,0) of image 0's padded grid)
@@ -72,9 +75,9 @@ struct WinArgs {
     int tiles_per_img;
 };
 
-template <int C, int KW, int TN>
-__global__ void __launch_bounds__(256, 1) conv_win_kernel(const WinArgs args) {
-    constexpr int BM = 256, NW = 4, WM = 64, TM = WM / 16;
+template <int C, int KW, int TN, int NW = 4>
+__global__ void __launch_bounds__(NW * 64, 1) conv_win_kernel(const WinArgs args) {
+    constexpr int BM = 256, WM = BM / NW, TM = WM / 16;
     constexpr int PB = 4 * C;                                   // strip bytes per pixel (h | l)
     constexpr int NR = TN * 16;                                 // weight rows staged
     constexpr int STRIP_PIX = BM + 2 * (KW - 1);
@@ -257,9 +260,16 @@ __global__ void __launch_bounds__(256, 1) conv_win_kernel(const WinArgs args) {
     }
 }
 
+// waves per workgroup: 4 (one per SIMD, 64 rows each) or 8 (two per SIMD, 32 rows each: a partner wave's
+// MFMAs cover each wave's fragment-read latency); FLOODGAN_WIN_WAVES selects (A/B)
 template <int C, int KW, int TN>
 int launch_win(const WinArgs& a, int tiles, hipStream_t stream) {
-    hipLaunchKernelGGL((conv_win_kernel<C, KW, TN>), dim3(tiles), dim3(256), 0, stream, a);
+    const char* e = getenv("FLOODGAN_WIN_WAVES");
+    const int nw = e ? atoi(e) : g_win_waves;
+    if (nw == 8)
+        hipLaunchKernelGGL((conv_win_kernel<C, KW, TN, 8>), dim3(tiles), dim3(512), 0, stream, a);
+    else
+        hipLaunchKernelGGL((conv_win_kernel<C, KW, TN, 4>), dim3(tiles), dim3(256), 0, stream, a);
     return fg::launched("conv_win");
 }
 

@@ -1,0 +1,51 @@
+"""A/B (GPU) of the row-strip window kernel's workgroup shape (FLOODGAN_WIN_WAVES 4 or 8 waves) on the content
+head's forward (7x7 64 -> 27 at 512^2) and input gradient (7x7 27(32) -> 64 over 518^2), bs 8; outputs compared.
+  python scripts/diag_win_waves.py"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "flood-prediction-gan_amd"))
+sys.path.insert(0, os.path.join(ROOT, "scripts"))
+
+import torch  # noqa: E402
+
+from bench_conv import time_it  # noqa: E402
+from floodgan import _lib as L, ops, plans as PL  # noqa: E402
+from floodgan.plans import Buf  # noqa: E402
+
+
+def main():
+    L.load()
+    L.set_conv_math("f16x3")
+    N = 8
+    torch.manual_seed(0)
+    ad2 = Buf.empty(N, 512, 512, 64, 3, "cuda")
+    ad2.t.uniform_(-1, 1)
+    w = torch.randn(27, 64, 7, 7, device="cuda") * 0.02
+    m = PL.wmap_conv_fwd(w.shape, 64)
+    cl = Buf.empty(N, 512, 512, 32, 0, "cuda")
+    fwd = PL.conv_problem(ad2, 3, 7, 1, ops.pack_weight(w, m), m, cl)
+    gcl = Buf.zeros(N, 512, 512, 32, 6, "cuda")
+    gcl.interior()[..., :27].uniform_(-1, 1)
+    md = PL.wmap_conv_dgrad_s1(w.shape, 32)
+    Y = Buf.empty(N, 518, 518, 64, 0, "cuda")
+    dgr = PL.conv_problem(gcl, 6, 7, 1, ops.pack_weight(w, md), md, Y)
+    for name, prob, out, flops in (("content fwd 7x7 64->27 @512", fwd, cl, 2.0 * N * 512 * 512 * 27 * 64 * 49),
+                                   ("content dgrad 7x7 27->64 @518", dgr, Y, 2.0 * N * 518 * 518 * 64 * 27 * 49)):
+        res = {}
+        for nw in ("4", "8", "4", "8"):
+            os.environ["FLOODGAN_WIN_WAVES"] = nw
+            ops.conv_win(prob)
+            torch.cuda.synchronize()
+            res[nw] = out.t.clone()
+            ms = min(time_it(lambda: ops.conv_win(prob)) for _ in range(3))
+            d = float((res[nw] - res["4"]).norm() / res["4"].norm())
+            print(f"{name:32s} waves {nw} {ms * 1e3:8.1f} us {flops / ms / 1e9:7.1f} TFLOP/s  rel diff vs 4 {d:.1e}",
+                  flush=True)
+    os.environ.pop("FLOODGAN_WIN_WAVES")
+
+
+if __name__ == "__main__":
+    main()
