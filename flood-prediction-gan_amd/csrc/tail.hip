@@ -69,8 +69,21 @@ __global__ void tail_fwd_kernel(fg_view cl, fg_view al, fg_sview x, float* __res
     }
 }
 
-__global__ void tail_bwd_kernel(fg_view cl, fg_view al, fg_sview x, fg_sview gout, fg_view gc, fg_view ga,
-                                fg_wview gx) {
+// fold a thread's max |v| bits into shard blockIdx % FG_AMAX_SHARDS of an absmax slot (256-thread blocks)
+__device__ __forceinline__ void flush_amax(unsigned m, unsigned* out, unsigned* red) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, off));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicMax(out + (blockIdx.x & (FG_AMAX_SHARDS - 1)), max(max(red[0], red[1]), max(red[2], red[3])));
+    __syncthreads();
+}
+
+__device__ __forceinline__ unsigned abits(float v) { return __float_as_uint(v) & 0x7fffffffu; }
+
+__global__ void __launch_bounds__(256) tail_bwd_kernel(fg_view cl, fg_view al, fg_sview x, fg_sview gout, fg_view gc,
+                                                       fg_view ga, fg_wview gx, unsigned* amax_c, unsigned* amax_a) {
+    unsigned mc = 0, ma = 0;                      // max |g_content|, |g_att| written by this thread
     // iterate over gc's padded extent so its zero border is written too
     const int H = cl.h, W = cl.w;
     const int hp = H + 2 * gc.pad, wp = W + 2 * gc.pad;
@@ -109,6 +122,8 @@ __global__ void tail_bwd_kernel(fg_view cl, fg_view al, fg_sview x, fg_sview gou
 #pragma unroll
         for (int i = NCONT; i < 32; ++i) go[i] = 0.f;
 #pragma unroll
+        for (int i = 0; i < NCONT; ++i) mc = max(mc, abits(go[i]));
+#pragma unroll
         for (int q = 0; q < 8; ++q)
             *reinterpret_cast<f32x4*>(gcp + 4 * q) = f32x4{go[4 * q], go[4 * q + 1], go[4 * q + 2], go[4 * q + 3]};
         for (int i = 32; i < gc.c_alloc; i += 4) *reinterpret_cast<f32x4*>(gcp + i) = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -127,10 +142,15 @@ __global__ void tail_bwd_kernel(fg_view cl, fg_view al, fg_sview x, fg_sview gou
 #pragma unroll
         for (int i = NATT; i < 16; ++i) ao[i] = 0.f;
 #pragma unroll
+        for (int i = 0; i < NATT; ++i) ma = max(ma, abits(ao[i]));
+#pragma unroll
         for (int q = 0; q < 4; ++q)
             *reinterpret_cast<f32x4*>(gap + 4 * q) = f32x4{ao[4 * q], ao[4 * q + 1], ao[4 * q + 2], ao[4 * q + 3]};
         for (int i = 16; i < ga.c_alloc; i += 4) *reinterpret_cast<f32x4*>(gap + i) = f32x4{0.f, 0.f, 0.f, 0.f};
     }
+    __shared__ unsigned red[4];
+    if (amax_c) flush_amax(mc, amax_c, red);
+    if (amax_a) flush_amax(ma, amax_a, red);
 }
 
 // CycleGAN head (models/model_architectures.py:115-117: conv 7x7 64->3 then nn.Tanh): one thread
@@ -195,7 +215,7 @@ FG_API int fg_tail_fwd(fg_view content_logits, fg_view att_logits, fg_sview x, f
 }
 
 FG_API int fg_tail_bwd(fg_view content_logits, fg_view att_logits, fg_sview x, fg_sview g_out, fg_view g_content,
-                       fg_view g_att, fg_wview g_x, hipStream_t stream) {
+                       fg_view g_att, fg_wview g_x, float* absmax_content, float* absmax_att, hipStream_t stream) {
     if (!content_logits.ptr || !att_logits.ptr || !x.ptr || !g_out.ptr || !g_content.ptr || !g_att.ptr ||
         content_logits.c_alloc < 28 || content_logits.c_alloc % 4 || att_logits.c_alloc < 12 ||
         att_logits.c_alloc % 4 || g_content.c_alloc < 32 || g_content.c_alloc % 4 || g_att.c_alloc < 16 ||
@@ -206,7 +226,8 @@ FG_API int fg_tail_bwd(fg_view content_logits, fg_view att_logits, fg_sview x, f
     const long long total = (long long)content_logits.n * (content_logits.h + 2 * g_content.pad) *
                             (content_logits.w + 2 * g_content.pad);
     hipLaunchKernelGGL(tail_bwd_kernel, dim3(fg::blocks_for(total, 256, 16384)), dim3(256), 0, stream,
-                       content_logits, att_logits, x, g_out, g_content, g_att, g_x);
+                       content_logits, att_logits, x, g_out, g_content, g_att, g_x,
+                       reinterpret_cast<unsigned*>(absmax_content), reinterpret_cast<unsigned*>(absmax_att));
     return fg::launched("tail_bwd");
 }
 

@@ -138,7 +138,8 @@ SIGNATURES = {
     "fg_channel_sum": [fg_view, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p],
     "fg_channel_sum_workspace_doubles": [C.c_int],
     "fg_tail_fwd": [fg_view, fg_view, fg_sview, C.c_void_p, C.c_void_p, C.c_void_p],
-    "fg_tail_bwd": [fg_view, fg_view, fg_sview, fg_sview, fg_view, fg_view, fg_wview, C.c_void_p],
+    "fg_tail_bwd": [fg_view, fg_view, fg_sview, fg_sview, fg_view, fg_view, fg_wview, C.c_void_p, C.c_void_p,
+                    C.c_void_p],
     "fg_tanh_head_fwd": [fg_view, C.c_int, fg_wview, C.c_void_p],
     "fg_tanh_head_bwd": [fg_view, C.c_int, fg_sview, fg_view, C.c_void_p],
     "fg_mse_const": [C.c_void_p, C.c_longlong, C.c_float, C.c_float, C.c_void_p, C.c_void_p, C.c_void_p,

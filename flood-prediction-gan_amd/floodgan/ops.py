@@ -670,9 +670,9 @@ def tail_fwd(cl, al, x, out, mask):
 
 def tail_bwd(cl, al, x, g_out, gc, ga, gx=None):
     """gx (optional [N, C, H, W] tensor): channels 0..2 receive the background term's input gradient"""
-    _wrote(gc, ga, gx)
+    _wrote(gx)
     L.check(_lib().fg_tail_bwd(view(cl), view(al), sview(x), sview(g_out), view(gc), view(ga), sview(gx),
-                               L.stream_handle()), "tail_bwd")
+                               L.ptr(_amax_out(gc)), L.ptr(_amax_out(ga)), L.stream_handle()), "tail_bwd")
 
 
 def tanh_head_fwd(logits, c, out):

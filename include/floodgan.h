@@ -353,9 +353,12 @@ int fg_tail_fwd(fg_view content_logits, fg_view att_logits, fg_sview x, float* o
  * g_att: dst view (10 used).  g_x (optional, NULL ptr = skip): channels 0..2 of a strided
  * [N,C,H,W] tensor receive the direct gradient w.r.t. input[:, :3] of the background term
  * `input[:, :3] * attention10` (models/model_architectures.py:393, :251) -- the input
- * gradient that the cycle path (models/model.py:677-706) back-propagates into G. */
+ * gradient that the cycle path (models/model.py:677-706) back-propagates into G.  absmax_content /
+ * absmax_att (optional absmax slots, initialised by the caller) are raised to bound |g_content| / |g_att|:
+ * the f16x3 scale sources of the convs reading them, with no separate pass. */
 int fg_tail_bwd(fg_view content_logits, fg_view att_logits, fg_sview x, fg_sview g_out,
-                fg_view g_content, fg_view g_att, fg_wview g_x, hipStream_t stream);
+                fg_view g_content, fg_view g_att, fg_wview g_x, float* absmax_content, float* absmax_att,
+                hipStream_t stream);
 
 /* CycleGAN generator head (models/model_architectures.py:115-117, conv 7x7 64->3 + nn.Tanh):
  * out (strided [N,c,H,W]) = tanh(logits[..., :c]). */

@@ -531,6 +531,12 @@ def test_tail():
     torch.cuda.synchronize()
     assert nrel(nchw(GC, 27), gcl_ref) < KTOL and nrel(nchw(GA, 10), gal_ref) < KTOL
     assert float(GC.nhwc()[..., 27:].abs().max()) == 0.0 and float(GC.nhwc()[:, :6].abs().max()) == 0.0
+    # the kernel raised both outputs' absmax slots (the f16x3 scale sources of the convs reading them)
+    from floodgan import _lib as L
+    if L.fwd_f16x3():
+        assert float(GC.t._fg_amax.max()) == float(GC.t.abs().max())
+        assert float(GA.t._fg_amax.max()) == float(GA.t.abs().max())
+        assert ops.absmax(GC) is GC.t._fg_amax          # cached: no separate pass
 
 
 def test_losses_and_adam():
