@@ -322,7 +322,8 @@ __global__ void in_bwd_apply_kernel(fg_view g, int fp, fg_view gadd, fg_view src
 }
 
 // float4 form: block = interior row (n, yy), threads over (x, channel quad) of the row
-__global__ void __launch_bounds__(256) act_bwd4_kernel(fg_view g, fg_view y, int act) {
+__global__ void __launch_bounds__(256) act_bwd4_kernel(fg_view g, fg_view y, int act, unsigned* __restrict__ amax) {
+    unsigned am = 0;
     const int C = g.c_alloc, C4 = C / 4, W4 = g.w * C4;
     const int n = blockIdx.x / g.h, yy = blockIdx.x - (blockIdx.x / g.h) * g.h;
     float* grow = g.ptr + fg::vidx(g, n, yy, 0);
@@ -333,11 +334,14 @@ __global__ void __launch_bounds__(256) act_bwd4_kernel(fg_view g, fg_view y, int
         const f32x4 yv = ld4(yrow + (size_t)x * C + c);
 #pragma unroll
         for (int e = 0; e < 4; ++e) gv[e] *= fg::act_grad(yv[e], act);
+        am = max(am, absbits4(gv));
         *reinterpret_cast<f32x4*>(grow + (size_t)x * C + c) = gv;
     }
+    if (amax) absmax_flush(am, amax);
 }
 
-__global__ void act_bwd_kernel(fg_view g, fg_view y, int act) {
+__global__ void act_bwd_kernel(fg_view g, fg_view y, int act, unsigned* __restrict__ amax) {
+    unsigned am = 0;
     const int C = g.c_alloc;
     const long long total = (long long)g.n * g.h * g.w * C;
     for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
@@ -349,8 +353,11 @@ __global__ void act_bwd_kernel(fg_view g, fg_view y, int act) {
         const int yy = (int)(pix % g.h);
         const int n = (int)(pix / g.h);
         const float yv = y.ptr[fg::vidx(y, n, yy, x) + c];
-        g.ptr[fg::vidx(g, n, yy, x) + c] *= fg::act_grad(yv, act);
+        const float v = g.ptr[fg::vidx(g, n, yy, x) + c] * fg::act_grad(yv, act);
+        am = max(am, __float_as_uint(v) & 0x7fffffffu);
+        g.ptr[fg::vidx(g, n, yy, x) + c] = v;
     }
+    if (amax) absmax_flush(am, amax);
 }
 
 __global__ void channel_sum_kernel(fg_view src, int c_valid, int chunks, double* __restrict__ work) {
@@ -620,15 +627,16 @@ FG_API int fg_in_bwd(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, cons
     return fg::launched("in_bwd_apply");
 }
 
-FG_API int fg_act_bwd(fg_view g, fg_view y, int act, hipStream_t stream) {
+FG_API int fg_act_bwd(fg_view g, fg_view y, int act, float* absmax, hipStream_t stream) {
+    unsigned* am = reinterpret_cast<unsigned*>(absmax);
     if (!ok_view(g) || !ok_view(y) || g.c_alloc != y.c_alloc || g.h != y.h || g.w != y.w || g.n != y.n)
         return fg::fail(FG_ERR_INVALID, "fg_act_bwd: bad args");
     if (g.c_alloc % 4 == 0) {
-        hipLaunchKernelGGL(act_bwd4_kernel, dim3(g.n * g.h), dim3(256), 0, stream, g, y, act);
+        hipLaunchKernelGGL(act_bwd4_kernel, dim3(g.n * g.h), dim3(256), 0, stream, g, y, act, am);
         return fg::launched("act_bwd4");
     }
     const long long total = (long long)g.n * g.h * g.w * g.c_alloc;
-    hipLaunchKernelGGL(act_bwd_kernel, dim3(fg::blocks_for(total, 256, 16384)), dim3(256), 0, stream, g, y, act);
+    hipLaunchKernelGGL(act_bwd_kernel, dim3(fg::blocks_for(total, 256, 16384)), dim3(256), 0, stream, g, y, act, am);
     return fg::launched("act_bwd");
 }
 

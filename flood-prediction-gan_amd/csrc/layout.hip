@@ -5,8 +5,20 @@
 
 namespace {
 
+// fold this thread's max |v| bits into shard blockIdx % FG_AMAX_SHARDS of an absmax slot (256-thread
+// blocks; every thread of the block must call it)
+__device__ __forceinline__ void flush_amax(unsigned m, unsigned* out, int bid) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, off));
+    __shared__ unsigned red[4];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicMax(out + (bid & (FG_AMAX_SHARDS - 1)), max(max(red[0], red[1]), max(red[2], red[3])));
+}
+
 __global__ void pack_input_kernel(fg_sview a, int ca, fg_sview b, int cb, fg_view dst, int img0, int nimg,
-                                  int pad_mode) {
+                                  int pad_mode, unsigned* amax) {
+    unsigned am = 0;
     const int hp = dst.h + 2 * dst.pad, wp = dst.w + 2 * dst.pad, C = dst.c_alloc;
     const long long total = (long long)nimg * hp * wp * C;
     for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
@@ -28,18 +40,21 @@ __global__ void pack_input_kernel(fg_sview a, int ca, fg_sview b, int cb, fg_vie
             else if (c < ca + cb)
                 v = b.ptr[n * b.sn + (c - ca) * b.sc + y * b.sy + x * b.sx];
         }
+        am = max(am, __float_as_uint(v) & 0x7fffffffu);
         dst.ptr[(((size_t)(img0 + n) * hp + yp) * wp + xp) * C + c] = v;
     }
+    if (amax) flush_amax(am, amax, blockIdx.x);
 }
 
 // the same packing, one thread per destination pixel for narrow buffers (C <= 16: the generator and
 // discriminator inputs): per-pixel reflect indices once, NCHW reads coalesced over x, float4 stores when C % 4 == 0
 // (the element-per-thread form above spent 71-112 us per 75-100 MB pack on index arithmetic)
 __global__ void __launch_bounds__(256) pack_input_pix_kernel(fg_sview a, int ca, fg_sview b, int cb, fg_view dst,
-                                                             int img0, int pad_mode) {
+                                                             int img0, int pad_mode, unsigned* amax) {
     const int hp = dst.h + 2 * dst.pad, wp = dst.w + 2 * dst.pad, C = dst.c_alloc;
     const int xp = blockIdx.x * 256 + threadIdx.x, yp = blockIdx.y, n = blockIdx.z;
-    if (xp >= wp) return;
+    unsigned am = 0;
+    if (xp < wp) {
     int y = yp - dst.pad, x = xp - dst.pad;
     const bool inside = y >= 0 && y < dst.h && x >= 0 && x < dst.w;
     float v[16];
@@ -60,6 +75,8 @@ __global__ void __launch_bounds__(256) pack_input_pix_kernel(fg_sview a, int ca,
         }
     }
     float* o = dst.ptr + (((size_t)(img0 + n) * hp + yp) * wp + xp) * C;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) am = max(am, __float_as_uint(v[c]) & 0x7fffffffu);
     if ((C & 3) == 0) {
 #pragma unroll
         for (int q = 0; q < 4; ++q)
@@ -69,6 +86,8 @@ __global__ void __launch_bounds__(256) pack_input_pix_kernel(fg_sview a, int ca,
         for (int c = 0; c < 16; ++c)
             if (c < C) o[c] = v[c];
     }
+    }
+    if (amax) flush_amax(am, amax, blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z));
 }
 
 __global__ void zero_border_kernel(fg_view dst) {
@@ -160,7 +179,8 @@ __global__ void unfold_nchw_kernel(fg_view g, int fp, int c, fg_wview dst, int h
 }  // namespace
 
 FG_API int fg_pack_input(fg_sview a, int ca, fg_sview b, int cb, fg_view dst, int img0, int nimg, int pad_mode,
-                         hipStream_t stream) {
+                         float* absmax, hipStream_t stream) {
+    unsigned* am = reinterpret_cast<unsigned*>(absmax);
     if (!a.ptr || !dst.ptr || ca < 0 || cb < 0 || (cb > 0 && !b.ptr) || ca + cb > dst.c_alloc || img0 < 0 ||
         nimg < 0 || img0 + nimg > dst.n)
         return fg::fail(FG_ERR_INVALID, "fg_pack_input: bad args");
@@ -171,11 +191,11 @@ FG_API int fg_pack_input(fg_sview a, int ca, fg_sview b, int cb, fg_view dst, in
     if (dst.c_alloc <= 16 && ((uintptr_t)dst.ptr & 15) == 0 && nimg <= 65535 && dst.h + 2 * dst.pad <= 65535) {
         const int wp = dst.w + 2 * dst.pad;
         hipLaunchKernelGGL(pack_input_pix_kernel, dim3((wp + 255) / 256, dst.h + 2 * dst.pad, nimg), dim3(256), 0,
-                           stream, a, ca, b, cb, dst, img0, pad_mode);
+                           stream, a, ca, b, cb, dst, img0, pad_mode, am);
         return fg::launched("pack_input_pix");
     }
     hipLaunchKernelGGL(pack_input_kernel, dim3(fg::blocks_for(total, 256, 16384)), dim3(256), 0, stream, a, ca, b,
-                       cb, dst, img0, nimg, pad_mode);
+                       cb, dst, img0, nimg, pad_mode, am);
     return fg::launched("pack_input");
 }
 

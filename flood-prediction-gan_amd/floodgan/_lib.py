@@ -122,7 +122,7 @@ SIGNATURES = {
     "fg_conv1x1_dgrad": [fg_view, C.c_void_p, C.c_int, fg_view, C.c_void_p],
     "fg_conv1x1_wgrad": [fg_view, fg_view, C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p],
     "fg_conv1x1_wgrad_workspace_floats": [C.c_int],
-    "fg_pack_input": [fg_sview, C.c_int, fg_sview, C.c_int, fg_view, C.c_int, C.c_int, C.c_int, C.c_void_p],
+    "fg_pack_input": [fg_sview, C.c_int, fg_sview, C.c_int, fg_view, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p],
     "fg_zero_border": [fg_view, C.c_void_p],
     "fg_fold_add": [fg_view, C.c_int, fg_view, fg_view, C.c_void_p],
     "fg_unfold_nchw": [fg_view, C.c_int, C.c_int, fg_wview, C.c_int, C.c_int, C.c_int, C.c_void_p],
@@ -134,7 +134,7 @@ SIGNATURES = {
     "fg_in_apply": [fg_view, C.c_void_p, C.c_void_p, C.c_int, fg_view, fg_view, C.c_int, C.c_void_p, C.c_void_p],
     "fg_in_bwd": [fg_view, C.c_int, fg_view, fg_view, C.c_void_p, C.c_void_p, C.c_int, fg_view, C.c_void_p,
                   C.c_int, C.c_void_p, C.c_void_p, C.c_void_p],
-    "fg_act_bwd": [fg_view, fg_view, C.c_int, C.c_void_p],
+    "fg_act_bwd": [fg_view, fg_view, C.c_int, C.c_void_p, C.c_void_p],
     "fg_channel_sum": [fg_view, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p],
     "fg_channel_sum_workspace_doubles": [C.c_int],
     "fg_tail_fwd": [fg_view, fg_view, fg_sview, C.c_void_p, C.c_void_p, C.c_void_p],

@@ -479,11 +479,12 @@ def disc_pack(pairs, c_in_total):
     N = sum(a.shape[0] for a, _ in pairs)
     H, W = a0.shape[2], a0.shape[3]
     buf = Buf.empty(N, H, W, c_in_total, 1, a0.device)
+    slot = ops.amax_slot(buf) if len(pairs) > 1 else None      # the parts raise one shared absmax slot
     img0 = 0
     for a, b in pairs:
         require_device(a, "discriminator input")
         cb = 0 if b is None else b.shape[1]
-        ops.pack_input(a, a.shape[1], b, cb, buf, img0, a.shape[0], FG_PAD_ZERO)
+        ops.pack_input(a, a.shape[1], b, cb, buf, img0, a.shape[0], FG_PAD_ZERO, amax=slot)
         img0 += a.shape[0]
     return buf
 
@@ -572,7 +573,7 @@ def disc_backward(P, S, g_pred, param_grads=True, grads_into=None, input_grad=No
     g_e0 = Buf.empty(N, e0.h, e0.w, 64, 1, dev)
     _dgrad_s2(P, "model.2", g_e1, 4, Y=g_e0)
     ops.zero_border(g_e0)
-    ops.act_bwd(Buf(g_e0.t, N, e0.h, e0.w, 64, 1), e0, FG_ACT_LRELU)      # through LeakyReLU of model.1
+    ops.act_bwd(Buf(g_e0.t, N, e0.h, e0.w, 64, 1), e0, FG_ACT_LRELU, border_zero=True)   # LeakyReLU of model.1
     if param_grads:
         _wgrad_conv(P, G, "model.0", g_e0, inp, 1, 4, 2)
         ops.channel_sum(g_e0, 64, G.get("model.0.bias"))

@@ -482,10 +482,27 @@ def conv_n1_wgrad(X, G, wmap, dw):
 
 # ------------------------------------------------------------------ layout
 
-def pack_input(a, ca, b, cb, dst, img0, nimg, pad_mode):
-    _wrote(dst)
-    L.check(_lib().fg_pack_input(sview(a), ca, sview(b), cb, view(dst), img0, nimg, pad_mode, L.stream_handle()),
-            "pack_input")
+def pack_input(a, ca, b, cb, dst, img0, nimg, pad_mode, amax=None):
+    """F.pad + torch.cat into the NHWC Buf dst (fg_pack_input).  The kernel raises dst's absmax slot: a pack
+    of all of dst's images takes a fresh one; packs that fill dst in parts pass the slot they share
+    (amax_slot(dst), taken before the first part)."""
+    if amax is None:
+        full = img0 == 0 and nimg == dst.n
+        slot = _amax_out(dst) if full else None
+        if slot is None:
+            _wrote(dst)
+    else:
+        slot = amax
+        t = _tensor(dst)
+        if getattr(t, "_fg_split", None) is not None:
+            t._fg_split = None
+    L.check(_lib().fg_pack_input(sview(a), ca, sview(b), cb, view(dst), img0, nimg, pad_mode, L.ptr(slot),
+                                 L.stream_handle()), "pack_input")
+
+
+def amax_slot(dst):
+    """a fresh absmax slot recorded on dst, for producers that write dst in several launches"""
+    return _amax_out(dst)
 
 
 def conv1x1_fwd(X, w, b, n_out, Y):
@@ -552,15 +569,20 @@ def in_bwd(gsrc, fold_pad, gadd, src, mean, rstd, act, dst, bias_grad=None, bias
                              L.ptr(_amax_out(dst)), L.stream_handle()), "in_bwd")
 
 
-def act_bwd(g, y, act):
+def act_bwd(g, y, act, border_zero=False):
     # in place g *= act'(y) with act' in {0, 0.2, 1}: |g| cannot grow, so a cached absmax slot still
-    # bounds it and is kept; a cached pre-split copy no longer matches the contents and is dropped
+    # bounds it and is kept; a cached pre-split copy no longer matches the contents and is dropped.  Without a
+    # cached slot, border_zero=True (g's border holds zeros) lets the kernel raise a fresh one over the interior.
     t = _tensor(g)
     slot, ver = getattr(t, "_fg_amax", None), getattr(t, "_fg_amax_ver", None)
+    valid = slot is not None and ver == t._version
     _wrote(g)
-    if slot is not None:
+    raise_slot = None
+    if valid:
         t._fg_amax, t._fg_amax_ver = slot, ver
-    L.check(_lib().fg_act_bwd(view(g), view(y), act, L.stream_handle()), "act_bwd")
+    elif border_zero:
+        raise_slot = _amax_out(g)
+    L.check(_lib().fg_act_bwd(view(g), view(y), act, L.ptr(raise_slot), L.stream_handle()), "act_bwd")
 
 
 def channel_sum(src, c_valid, out, accumulate=False):

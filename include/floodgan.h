@@ -282,9 +282,10 @@ int fg_absmax(const float* x, long long n, float* out, hipStream_t stream);
 /* ---------------------------------------------------------------------------------------- */
 /* dst(img0+n, y, x, ch) = ch < ca ? a(n,ch,y,x) : ch < ca+cb ? b(n,ch-ca,y,x) : 0, for the full
  * padded extent of dst (border filled by `pad_mode`).  Replaces F.pad(reflect) at
- * models/model_architectures.py:341 and torch.cat at models/model.py:616-617. */
+ * models/model_architectures.py:341 and torch.cat at models/model.py:616-617.  absmax (optional absmax slot,
+ * initialised by the caller; several packs into one dst may share it) is raised to max |written values|. */
 int fg_pack_input(fg_sview a, int ca, fg_sview b, int cb, fg_view dst, int img0, int nimg,
-                  int pad_mode, hipStream_t stream);
+                  int pad_mode, float* absmax, hipStream_t stream);
 
 /* Fill the border of dst with zeros (interior untouched). */
 int fg_zero_border(fg_view dst, hipStream_t stream);
@@ -334,8 +335,10 @@ int fg_in_bwd(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, const float
               const float* rstd, int act, fg_view dst, float* bias_grad, int bias_accumulate, double* work,
               float* absmax, hipStream_t stream);
 
-/* g *= act'(y) in place over the interior (y = saved activation output). */
-int fg_act_bwd(fg_view g, fg_view y, int act, hipStream_t stream);
+/* g *= act'(y) in place over the interior (y = saved activation output).  absmax (optional absmax slot,
+ * initialised by the caller) is raised to max |g| over the interior -- a bound for the whole buffer when its
+ * border is zero. */
+int fg_act_bwd(fg_view g, fg_view y, int act, float* absmax, hipStream_t stream);
 
 /* out[c] (+)= sum over n,y,x of src(n,y,x,c) for c < c_valid.  Bias gradients.  `work` holds
  * fg_channel_sum_workspace_doubles(src.c_alloc) doubles. */

@@ -895,3 +895,30 @@ def test_act_bwd(C, act):
     slope = 0.0 if act == 1 else 0.2
     ref = g.float().double() * torch.where(y.float() > 0, torch.ones_like(y), torch.full_like(y, slope))
     assert nrel(nchw(gb), ref) < 1e-6
+    # border_zero: the kernel raises a fresh absmax slot of g (f16x3)
+    from floodgan import _lib as L
+    if L.fwd_f16x3():
+        g2 = buf_from(g, 1, "constant")
+        ops.act_bwd(g2, yb, act, border_zero=True)
+        torch.cuda.synchronize()
+        assert float(g2.t._fg_amax.max()) == float(g2.t.abs().max())
+
+
+def test_pack_input_absmax_slots():
+    """fg_pack_input raises dst's absmax slot: a full pack a fresh slot, a discriminator input packed in two
+    parts one shared slot over both (executor.disc_pack), equal to the packed buffer's max |value|"""
+    from floodgan import _lib as L, executor as X, ops
+    from floodgan.plans import Buf
+    if not L.fwd_f16x3():
+        pytest.skip("absmax slots are kept under the f16x3 math")
+    torch.manual_seed(9)
+    x = (torch.randn(2, 9, 24, 24) * 3).to(DEV)
+    y = (torch.randn(2, 3, 24, 24) * 7).to(DEV)
+    X0 = Buf.empty(2, 24, 24, 9, 3, DEV)
+    ops.pack_input(x, 9, None, 0, X0, 0, 2, 1)
+    torch.cuda.synchronize()
+    assert float(X0.t._fg_amax.max()) == float(X0.t.abs().max()) == float(x.abs().max())
+    buf = X.disc_pack([(x, y), (x, -2 * y)], 12)
+    torch.cuda.synchronize()
+    assert float(buf.t._fg_amax.max()) == float(buf.t.abs().max())
+    assert ops.absmax(buf) is buf.t._fg_amax
