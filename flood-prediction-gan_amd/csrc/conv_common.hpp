@@ -11,12 +11,16 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 namespace fgc {
 
 // Up to four fg_conv_problems sharing one launch (the four output phases of a stride-2
-// transposed conv); blocks [blk_start[i], blk_start[i+1]) belong to problem i.
+// transposed conv); blocks [blk_start[i], blk_start[i+1]) belong to problem i -- or, with
+// interleave set (problems of equal tile counts, set by the pipelined kernel's launcher), tile t
+// belongs to problem t % count as its local tile t / count, so that the phases reading the same
+// input rows run side by side and share them in L2 instead of streaming the input once per phase.
 struct ConvBatch {
     fg_conv_problem p[4];
     int count;
     int ntiles_n[4];
     int blk_start[5];
+    int interleave;
 };
 
 __device__ __forceinline__ void decomp(int m, int mb, int mab, int& img, int& a, int& b) {

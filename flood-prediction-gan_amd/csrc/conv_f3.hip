@@ -129,9 +129,17 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
     };
     auto geo = [&](int t) {
         Geo q;
-        q.pi = 0;
-        while (q.pi + 1 < batch.count && t >= batch.blk_start[q.pi + 1]) ++q.pi;
-        const int local = t - batch.blk_start[q.pi];
+        int local;
+        if (batch.interleave) {
+            // the count consecutive tiles of one local index are the count problems, rotated by the round
+            // t / G so that every workgroup takes each problem in turn (the phases differ in K)
+            q.pi = (t % batch.count + t / G) % batch.count;
+            local = t / batch.count;
+        } else {
+            q.pi = 0;
+            while (q.pi + 1 < batch.count && t >= batch.blk_start[q.pi + 1]) ++q.pi;
+            local = t - batch.blk_start[q.pi];
+        }
         const int ntn = batch.ntiles_n[q.pi];
         q.mt = local / ntn;
         q.m0 = q.mt * BM;
@@ -573,6 +581,7 @@ int g_f3_persist = 1; // fg_set_f3_persistent: 1 resident workgroups loop over t
                       // tile, n >= 2 at most n workgroups (test hook: forces the tile-crossing stream
                       // -- setup_issue() mid-stream, next tile's stages in flight over an epilogue --
                       // at small sizes)
+int g_f3_interleave = 1;  // fg_set_f3_interleave: 0 = problem-major tile order (A/B hook)
 int g_f3_sched = -1;  // fg_set_f3_sched: per-stage instruction order (kernel template SCH), -1 auto
 
 template <int BM, int BN, int WM, int WN, int NS = 3>
@@ -590,10 +599,18 @@ int launch_cfg(const ConvBatch& in, int nprob, hipStream_t stream) {
     b.blk_start[nprob] = total;
     b.blk_start[4] = total;
     if (total == 0) return 0;
+    // phase-interleaved tile order when every problem has the same tile count (the 4 phases of an even-sized
+    // transposed conv / stride-2 input gradient): the phases gather the same input rows at the same time
     // persistent: as many workgroups as fit at once (LDS-limited), each looping over tiles
     constexpr int LDS = NS * (BM * 128 + 2 * BN * 64);
     const int per_cu = (160 * 1024) / LDS;
     const int grid = g_f3_persist ? std::min(total, g_f3_persist > 1 ? g_f3_persist : fg::num_cus() * per_cu) : total;
+    b.interleave = 0;
+    if (nprob > 1 && g_f3_interleave && grid % nprob == 0) {
+        bool eq = true;
+        for (int i = 1; i < nprob; ++i) eq &= b.blk_start[i + 1] - b.blk_start[i] == b.blk_start[1];
+        b.interleave = eq ? 1 : 0;
+    }
     const int sched = g_f3_sched >= 0 ? g_f3_sched : 3;
 #ifdef FG_F3_DIAG
     // timing-only diagnostic build (outputs are wrong): FG_F3_DIAG=1 compute without data movement,
@@ -742,6 +759,12 @@ FG_API int fg_set_f3_sched(int sched) {
 FG_API int fg_set_f3_order(int alt) {
     if (alt < 0 || alt > 7) return fg::fail(FG_ERR_INVALID, "fg_set_f3_order: %d", alt);
     g_f3_alt = alt;
+    return 0;
+}
+
+FG_API int fg_set_f3_interleave(int on) {
+    if (on < 0 || on > 1) return fg::fail(FG_ERR_INVALID, "fg_set_f3_interleave: %d", on);
+    g_f3_interleave = on;
     return 0;
 }
 

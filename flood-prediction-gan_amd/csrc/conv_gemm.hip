@@ -1306,6 +1306,7 @@ FG_API int fg_conv_fwd(const fg_conv_problem* probs, int nprob, hipStream_t stre
     if (!probs || nprob < 1 || nprob > 4) return fg::fail(FG_ERR_INVALID, "fg_conv_fwd: nprob=%d", nprob);
     ConvBatch b;
     b.count = nprob;
+    b.interleave = 0;
     int max_n = 0;
     bool vec = true;
     const int ws = probs[0].w_split;

@@ -81,8 +81,9 @@ __device__ __forceinline__ void flush_amax(unsigned m, unsigned* out, unsigned* 
 
 __device__ __forceinline__ unsigned abits(float v) { return __float_as_uint(v) & 0x7fffffffu; }
 
-__global__ void __launch_bounds__(256) tail_bwd_kernel(fg_view cl, fg_view al, fg_sview x, fg_sview gout, fg_view gc,
-                                                       fg_view ga, fg_wview gx, unsigned* amax_c, unsigned* amax_a) {
+__global__ void __launch_bounds__(256) tail_bwd_kernel(fg_view cl, fg_view al, fg_sview x, fg_sview gout, fg_sview gmask,
+                                                       fg_view gc, fg_view ga, fg_wview gx, unsigned* amax_c,
+                                                       unsigned* amax_a) {
     unsigned mc = 0, ma = 0;                      // max |g_content|, |g_att| written by this thread
     // iterate over gc's padded extent so its zero border is written too
     const int H = cl.h, W = cl.w;
@@ -128,6 +129,8 @@ __global__ void __launch_bounds__(256) tail_bwd_kernel(fg_view cl, fg_view al, f
             *reinterpret_cast<f32x4*>(gcp + 4 * q) = f32x4{go[4 * q], go[4 * q + 1], go[4 * q + 2], go[4 * q + 3]};
         for (int i = 32; i < gc.c_alloc; i += 4) *reinterpret_cast<f32x4*>(gcp + i) = f32x4{0.f, 0.f, 0.f, 0.f};
         gatt[9] = g[0] * xin[0] + g[1] * xin[1] + g[2] * xin[2];
+        // a loss on last_attention_mask = attention10 (models/model_architectures.py:396) adds its gradient here
+        if (gmask.ptr) gatt[9] += gmask.ptr[n * gmask.sn + yy * gmask.sy + xx * gmask.sx];
         if (gx.ptr) {  // d(output10)/d(input[:, :3]) = attention10 (models/model_architectures.py:393, :251)
 #pragma unroll
             for (int c = 0; c < 3; ++c) gx.ptr[n * gx.sn + c * gx.sc + yy * gx.sy + xx * gx.sx] = g[c] * v.a[9];
@@ -214,8 +217,9 @@ FG_API int fg_tail_fwd(fg_view content_logits, fg_view att_logits, fg_sview x, f
     return fg::launched("tail_fwd");
 }
 
-FG_API int fg_tail_bwd(fg_view content_logits, fg_view att_logits, fg_sview x, fg_sview g_out, fg_view g_content,
-                       fg_view g_att, fg_wview g_x, float* absmax_content, float* absmax_att, hipStream_t stream) {
+FG_API int fg_tail_bwd(fg_view content_logits, fg_view att_logits, fg_sview x, fg_sview g_out, fg_sview g_mask,
+                       fg_view g_content, fg_view g_att, fg_wview g_x, float* absmax_content, float* absmax_att,
+                       hipStream_t stream) {
     if (!content_logits.ptr || !att_logits.ptr || !x.ptr || !g_out.ptr || !g_content.ptr || !g_att.ptr ||
         content_logits.c_alloc < 28 || content_logits.c_alloc % 4 || att_logits.c_alloc < 12 ||
         att_logits.c_alloc % 4 || g_content.c_alloc < 32 || g_content.c_alloc % 4 || g_att.c_alloc < 16 ||
@@ -226,7 +230,7 @@ FG_API int fg_tail_bwd(fg_view content_logits, fg_view att_logits, fg_sview x, f
     const long long total = (long long)content_logits.n * (content_logits.h + 2 * g_content.pad) *
                             (content_logits.w + 2 * g_content.pad);
     hipLaunchKernelGGL(tail_bwd_kernel, dim3(fg::blocks_for(total, 256, 16384)), dim3(256), 0, stream,
-                       content_logits, att_logits, x, g_out, g_content, g_att, g_x,
+                       content_logits, att_logits, x, g_out, g_mask, g_content, g_att, g_x,
                        reinterpret_cast<unsigned*>(absmax_content), reinterpret_cast<unsigned*>(absmax_att));
     return fg::launched("tail_bwd");
 }

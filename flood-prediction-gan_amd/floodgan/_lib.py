@@ -101,6 +101,7 @@ SIGNATURES = {
     "fg_set_f3_sched": [C.c_int],
     "fg_set_f3_persistent": [C.c_int],
     "fg_set_f3_fill": [C.c_int],
+    "fg_set_f3_interleave": [C.c_int],
     "fg_set_wgrad_f3": [C.c_int],
     "fg_conv_wgrad": [C.POINTER(fg_wgrad_problem), C.c_void_p],
     "fg_wgrad_reduce": [C.c_void_p, C.c_int, C.POINTER(fg_weight_map), C.c_void_p, C.c_int, C.c_void_p],
@@ -138,7 +139,7 @@ SIGNATURES = {
     "fg_channel_sum": [fg_view, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p],
     "fg_channel_sum_workspace_doubles": [C.c_int],
     "fg_tail_fwd": [fg_view, fg_view, fg_sview, C.c_void_p, C.c_void_p, C.c_void_p],
-    "fg_tail_bwd": [fg_view, fg_view, fg_sview, fg_sview, fg_view, fg_view, fg_wview, C.c_void_p, C.c_void_p,
+    "fg_tail_bwd": [fg_view, fg_view, fg_sview, fg_sview, fg_sview, fg_view, fg_view, fg_wview, C.c_void_p, C.c_void_p,
                     C.c_void_p],
     "fg_tanh_head_fwd": [fg_view, C.c_int, fg_wview, C.c_void_p],
     "fg_tanh_head_bwd": [fg_view, C.c_int, fg_sview, fg_view, C.c_void_p],

@@ -46,24 +46,26 @@ def _gen_setup(ctx, inputs, output):
 
 
 @torch.library.custom_op("floodgan::paired_attention_generator_backward", mutates_args=(), device_types="cuda")
-def paired_attention_generator_backward(x: torch.Tensor, params: List[torch.Tensor],
-                                        g_out: torch.Tensor) -> Tuple[torch.Tensor, List[torch.Tensor]]:
-    """(dL/dx, [dL/dparam]) of the generator at (x, params) for dL/dout = g_out (re-runs the forward)"""
+def paired_attention_generator_backward(x: torch.Tensor, params: List[torch.Tensor], g_out: torch.Tensor,
+                                        g_mask: torch.Tensor) -> Tuple[torch.Tensor, List[torch.Tensor]]:
+    """(dL/dx, [dL/dparam]) of the generator at (x, params) for dL/dout = g_out and dL/dmask = g_mask
+    (re-runs the forward)"""
     P = dict(zip(GEN_KEYS, params))
     _, _, S = X.gen_forward(P, x, save=True)
     gx = torch.empty(x.shape, dtype=torch.float32, device=x.device)
-    grads = X.gen_backward(P, S, g_out.contiguous(), input_grad=gx)
+    grads = X.gen_backward(P, S, g_out.contiguous(), input_grad=gx, g_mask=g_mask)
     return gx, [grads[k] for k in GEN_KEYS]
 
 
 @paired_attention_generator_backward.register_fake
-def _(x, params, g_out):
+def _(x, params, g_out, g_mask):
     return torch.empty_like(x), [torch.empty_like(p) for p in params]
 
 
 def _gen_backward(ctx, g_out, g_mask):
     x, *params = ctx.saved_tensors
-    return torch.ops.floodgan.paired_attention_generator_backward(x, params, g_out)
+    # autograd materialises the gradient of an unused output as zeros: the mask's term is then a no-op add
+    return torch.ops.floodgan.paired_attention_generator_backward(x, params, g_out, g_mask)
 
 
 paired_attention_generator.register_autograd(_gen_backward, setup_context=_gen_setup)

@@ -4,7 +4,7 @@ device-side transform of the reference's dataset (models/data.py:11-146, models/
   determine_flood_dataset   models/data.py:83-146 (metadata/dataset_split.csv -> file lists)
   read_tile                 tifffile.imread (models/data.py:64-68): libfloodgan's host TIFF decoder
   FloodDataset              models/data.py:46-81: (input [C,R,R], target [3,R,R], name) per item
-  TileLoader                the DataLoader of models/data.py:28-42 (shuffle via torch's RandomSampler,
+  TileLoader                the DataLoader of models/data.py:28-42 (the index order of a real DataLoader,
                             so the order under torch.manual_seed(epoch) is the reference's), but
                             batches come out on the device: decode into a pinned-host ring, H2D on
                             a copy stream, then one HIP transform per batch (fg_tile_transform:
@@ -24,7 +24,7 @@ import threading
 
 import numpy as np
 import torch
-from torch.utils.data import BatchSampler, RandomSampler, SequentialSampler
+from torch.utils.data import DataLoader
 
 from . import _lib as L
 
@@ -353,8 +353,8 @@ class TileLoader:
     stream waits for that copy and runs the transform, so decode + PCIe of batch i+1 overlap the
     training step on batch i.  Yields (input [B,C,R,R], target [B,3,R,R], names), channels-last.
 
-    Order: torch.utils.data's RandomSampler / BatchSampler (seeded from the global torch RNG when the
-    iteration starts, exactly like DataLoader(shuffle=True)).  Data parallelism: each global batch of
+    Order: that of torch.utils.data.DataLoader(shuffle=True) over the item indices (the same draws from
+    the global torch RNG when the iteration starts as the reference's loader).  Data parallelism: each global batch of
     batch_size * world items is split in rank order (every rank gets batch_size items; the last, short
     global batch is dropped when world > 1 so the shards stay equal)."""
 
@@ -376,8 +376,12 @@ class TileLoader:
         return n
 
     def _batches(self):
-        sampler = RandomSampler(self.ds) if self.shuffle else SequentialSampler(self.ds)
-        for b in BatchSampler(sampler, self.bs * self.world, self.drop_last):
+        # the index order of an actual DataLoader(shuffle=True) over the items: its iterator draws the
+        # base seed from the global generator BEFORE RandomSampler draws its own, so a bare RandomSampler
+        # would visit the items in another order than the reference's loader (models/data.py:28-42)
+        order = DataLoader(range(len(self.ds)), batch_size=self.bs * self.world, shuffle=self.shuffle,
+                           drop_last=self.drop_last, collate_fn=list)
+        for b in order:
             shard = b[self.rank * self.bs:(self.rank + 1) * self.bs] if self.world > 1 else b
             if shard:
                 yield shard

@@ -173,7 +173,9 @@ def calculate_metrics(generator, loader, seg_model, topography="all", device="cu
 
 def compare_metrics(generators, loader, seg_model, compare="model", device="cuda"):
     """ModelsGroup.compare_metrics (models/group.py:114-221): {generator name: {metric: value}} plus the
-    per-disaster mask metrics {generator name: {disaster: {metric: value}}}.  compare="topography": the
+    per-disaster metrics {generator name: {disaster: {metric: value}}} -- the mask metrics over that
+    disaster's pixels and the batch means of PSNR / SSIM / MS-SSIM (LPIPS NaN) over its batches, as the
+    reference's grouped table (group.py:211-221).  compare="topography": the
     generators are keyed by topography ("All", "DEM", "Flow accumulation", "Distance to rivers", "Map",
     "None") and see the matching channels of one 9-channel input (models/group.py:83-94)."""
     topo_keys = {"All": "all", "DEM": "dem", "Flow accumulation": "flow", "Distance to rivers": "river", "Map": "map",
@@ -182,10 +184,12 @@ def compare_metrics(generators, loader, seg_model, compare="model", device="cuda
     conf = {g: MaskConfusion(device) for g in generators}
     grouped = {}
     per = {g: {k: [] for k in ("PSNR", "SSIM", "MS-SSIM", "Inference")} for g in generators}
+    disasters = []
     for input_stack, ground_truth, names in loader:
         x = input_stack.to(device)
         y = ground_truth.to(device)
         disaster = names[0].split("_")[0]
+        disasters.append(disaster)
         for g, gen in generators.items():
             xi = extract_input_topography(x, topo_keys[g]) if compare == "topography" else x
             key = (g, disaster)
@@ -204,7 +208,11 @@ def compare_metrics(generators, loader, seg_model, compare="model", device="cuda
         out[g] = {k: res[k] for k in METRIC_NAMES + ["Inference"]}
     by_disaster = {}
     for (g, d), c in grouped.items():
-        by_disaster.setdefault(g, {})[d] = c.compute()
+        vals = {k: float(np.mean([v for v, dd in zip(per[g][k], disasters) if dd == d]))
+                for k in ("PSNR", "SSIM", "MS-SSIM")}
+        vals["LPIPS"] = float("nan")
+        vals.update(c.compute())
+        by_disaster.setdefault(g, {})[d] = vals
     return out, by_disaster
 
 

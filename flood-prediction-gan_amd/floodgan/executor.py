@@ -344,14 +344,15 @@ def gen_bucket_names(P=None):
     return out
 
 
-def gen_backward(P, S, g_out, grads_into=None, ready=None, input_grad=None, accumulate=False):
+def gen_backward(P, S, g_out, grads_into=None, ready=None, input_grad=None, accumulate=False, g_mask=None):
     """Explicit backward of gen_forward.  g_out: [N,3,H,W] (any strides).  Returns
     {param name: grad} (written into grads_into[name] when given).  ready(layer name), when
     given, is called as soon as a gradient bucket (G_BUCKETS) is complete.  input_grad (optional
     [N,C,H,W] tensor, any strides) receives dL/d(input): the cycle path back-propagates through
     one generator into the other (models/model.py:677-706); the paired step never asks for it.
     accumulate: add into grads_into instead of overwriting (a generator applied several times in
-    one cycle iteration)."""
+    one cycle iteration).  g_mask (optional [N, H, W], any strides): dL/d(last_attention_mask), for a
+    loss that reads the mask (models/model_architectures.py:396 keeps it in the autograd graph)."""
     ready = ready or (lambda name: None)
     x = S["x"]
     G = _Grads(P, grads_into, accumulate, device=x.device)
@@ -369,9 +370,10 @@ def gen_backward(P, S, g_out, grads_into=None, ready=None, input_grad=None, accu
     if attention:
         al = S["al"]
         gal = Buf.empty(N, H, W, ATT_ALLOC, 0, dev)
-        ops.tail_bwd(cl, al, x, g_out, gcl, gal, gx=input_grad)     # input_grad[:, :3] = g_out * attention10
+        ops.tail_bwd(cl, al, x, g_out, gcl, gal, gx=input_grad, g_mask=g_mask)   # input_grad[:, :3] = g_out * att10
         ha = S["heads"]["attention"]
     else:
+        assert g_mask is None, "the CycleGAN generator has no attention mask"
         ops.tanh_head_bwd(cl, 3, g_out, gcl)
     # ---- deconv3_content: 7x7 over reflect-padded (3) ad2
     _wgrad_conv(P, G, "deconv3_content", gcl, hc["ad2"], 3, 7, 1)

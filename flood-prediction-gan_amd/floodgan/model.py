@@ -177,7 +177,8 @@ class Model:
                  num_epochs=1, topography="all", resize=256, crop=None, save_model_interval=0,
                  save_images_interval=0, verbose=False, load_pretrained_model=False, pretrained_model_path=None,
                  add_identity_loss=False, training_model=True, seed=47, device="cuda", train_loader=None,
-                 val_loader=None, test_loader=None):
+                 val_loader=None, test_loader=None, batch_size=1, num_workers=0,
+                 csv_path="metadata/dataset_split.csv"):
         saved = None
         if load_pretrained_model:
             # models/model.py:52-57: the checkpoint, not the `model` argument, names the architecture
@@ -236,8 +237,18 @@ class Model:
             self.starting_epoch = 1
             self.all_losses = self.initialise_loss_storage(overall=True)
         self.current_epoch = self.starting_epoch
-        # The tile pipeline (tifffile decode, resize, crop; models/data.py) is outside this
-        # build's scope: assign any iterable of (input [N,C,H,W], target [N,3,H,W], names).
+        # the data (models/model.py:150-156): with a data_path the three loaders are built as the reference
+        # builds them -- floodgan.data's staged TileLoaders over the same split table (csv_path: the
+        # reference reads metadata/dataset_split.csv relative to the working directory), batch_size images
+        # per step (the reference's is 1) and, under torch.distributed, this rank's shard of every global
+        # batch.  Loaders passed in explicitly (any iterable of (input, target, names)) take precedence.
+        self.batch_size = batch_size
+        if data_path is not None and train_loader is None:
+            from .data import create_flood_dataset
+            ws, rank = world()
+            train_loader, val_loader, test_loader = create_flood_dataset(
+                dataset_subset, dataset_dem, data_path, self.topography, resize=resize, crop=crop,
+                batch_size=batch_size, num_workers=num_workers, csv_path=csv_path, device=device, rank=rank, world=ws)
         self.train_loader, self.val_loader, self.test_loader = train_loader, val_loader, test_loader
         self._step = None
 
@@ -295,7 +306,8 @@ class Model:
     def train_paired(self):
         """models/model.py:598-658 on the fused device step."""
         if self.train_loader is None:
-            raise RuntimeError("assign Model.train_loader (iterable of (input, target, names)) first")
+            raise RuntimeError("no training data: pass data_path (floodgan.data loaders, as models/model.py:150-156) "
+                               "or train_loader (an iterable of (input, target, names))")
         keys = ["losses_discriminator_real", "losses_discriminator_synthetic", "losses_generator_synthetic",
                 "l1_losses_generator_synthetic"]
         for epoch in range(self.starting_epoch, self.num_epochs + 1):
@@ -327,7 +339,8 @@ class Model:
         if not self.model_is_cycle:
             raise RuntimeError("train_cycle needs model='AttentionGAN' or 'CycleGAN'")
         if self.train_loader is None:
-            raise RuntimeError("assign Model.train_loader (iterable of (input, target, names)) first")
+            raise RuntimeError("no training data: pass data_path (floodgan.data loaders, as models/model.py:150-156) "
+                               "or train_loader (an iterable of (input, target, names))")
         for epoch in range(self.starting_epoch, self.num_epochs + 1):
             t0 = time.time()
             losses = self.initialise_loss_storage(overall=False)
@@ -358,14 +371,38 @@ class Model:
         seg = seg_model if seg_model is not None else segmentation_model(seg_model_path, self.device)
         gen = self.pre_to_post_generator if self.model_is_cycle else self.generator
         res = calculate_metrics(gen, loader, seg, self.topography, self.device)
-        df = pd.DataFrame([res])
+        # the reference's table (models/model.py:419-422): one row, a "0" index column, written to
+        # create_path("metric")
+        df = pd.DataFrame([(k, v) for k, v in res.items()]).set_index(0).transpose()
         if self.verbose:
             print(df)
         if self.data_path:
             import os
-            os.makedirs(f"{self.data_path}/metrics", exist_ok=True)
-            df.to_csv(f"{self.data_path}/metrics/{self.model}_metrics_epoch{self.current_epoch - 1}.csv", index=False)
+            path = self.create_path("metric")
+            os.makedirs(os.path.dirname(path), exist_ok=True)
+            df.to_csv(path)
         return df
+
+    def prettify_model_name(self, model_name=None):
+        """models/model.py:231-239"""
+        pretty = {"pix2pix": "Pix2Pix", "cyclegan": "CycleGAN", "attentiongan": "AttentionGAN",
+                  "pairedattention": "PairedAttention"}
+        return pretty[model_name.lower()] if model_name else pretty[self.model]
+
+    def create_path(self, save_type, info=""):
+        """models/model.py:241-258: the reference's file naming for models, metrics and images"""
+        from datetime import datetime
+        ext = {"image": ".png", "figure": ".png", "model": ".pth.tar", "metric": ".csv"}[save_type]
+        now = str(datetime.now())[:-7].replace(" ", "-").replace(":", "-")
+        identity = f"identity{self.add_identity_loss}" if self.model_is_cycle else ""
+        path = (f"{self.data_path}/{save_type}s/"
+                f"{self.prettify_model_name()}_{info}_epoch"
+                f"{self.current_epoch if self.training_model else self.current_epoch - 1}_"
+                f"{self.topography}Topography_{identity}_"
+                f"{self.dataset_subset}Data_{self.dataset_dem}DEM_"
+                f"resize{self.resize}_crop{self.crop}_"
+                f"date{now}{ext}")
+        return path.replace("__", "_")
 
     def save_results(self, epoch, losses, epoch_start_time):
         """models/model.py:322-358 (loss bookkeeping + checkpoint; plots are out of scope)."""
@@ -376,9 +413,10 @@ class Model:
             print(f"Epoch {epoch} ({time.time() - epoch_start_time:.2f} seconds) | "
                   + " | ".join(f"{k} = {v[-1]:.2f}" for k, v in self.all_losses.items()))
         if self.save_model_interval != 0 and epoch % self.save_model_interval == 0:
-            name = {"attentiongan": "AttentionGAN", "cyclegan": "CycleGAN", "pix2pix": "Pix2Pix"}.get(self.model,
-                                                                                               "PairedAttention")
-            torch.save(self.checkpoint(epoch), f"{self.data_path}/models/{name}_epoch{epoch}.pth.tar")
+            path = self.create_path("model")                      # models/model.py:355-357
+            if self.verbose:
+                print(f"Saving {self.prettify_model_name()} model to {path}")
+            torch.save(self.checkpoint(epoch), path)
 
     def checkpoint(self, epoch):
         if self.model_is_cycle:                                   # models/model.py:335-355 (cycle keys)

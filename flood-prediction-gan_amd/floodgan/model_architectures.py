@@ -48,16 +48,24 @@ class _GeneratorFn(torch.autograd.Function):
         # the caller-visible tensors the backward reads (input, parameters) go through
         # save_for_backward so an in-place change between forward and backward raises
         ctx.save_for_backward(x, *params)
-        ctx.mark_non_differentiable(mask)
+        if mask.numel() == 0:
+            ctx.mark_non_differentiable(mask)
+        # the mask stays in the graph as in the reference (attention10, models/model_architectures.py:396):
+        # a loss on last_attention_mask back-propagates through the softmax; unused outputs arrive as None
+        ctx.set_materialize_grads(False)
         return out, mask
 
     @staticmethod
-    def backward(ctx, g_out, _g_mask):
+    def backward(ctx, g_out, g_mask):
         _ = ctx.saved_tensors          # version check of the input and the parameters
+        x = ctx.S["x"]
+        if g_out is None:
+            g_out = torch.zeros(x.shape[0], 3, x.shape[2], x.shape[3], dtype=torch.float32, device=x.device)
         gx = None
         if ctx.needs_input_grad[1]:   # the cycle path: G(cat(G'(x), conditions)) (models/model.py:677-706)
-            gx = torch.empty(ctx.S["x"].shape, dtype=torch.float32, device=g_out.device)
-        grads = X.gen_backward(ctx.P, ctx.S, g_out, input_grad=gx)
+            gx = torch.empty(x.shape, dtype=torch.float32, device=g_out.device)
+        grads = X.gen_backward(ctx.P, ctx.S, g_out, input_grad=gx,
+                               g_mask=None if g_mask is None or g_mask.numel() == 0 else g_mask)
         ctx.S = None
         return (None, gx) + tuple(grads[k] if need else None
                                   for k, need in zip(ctx.keys, ctx.needs_input_grad[2:]))
@@ -70,12 +78,13 @@ class _DiscriminatorFn(torch.autograd.Function):
         buf = X.disc_pack([(x, None)], x.shape[1])
         pred, S = X.disc_forward(P, buf, save=any(ctx.needs_input_grad))
         ctx.P, ctx.S, ctx.xshape = P, S, tuple(x.shape)
-        ctx.save_for_backward(*params)
+        # the input too: an in-place change of D's input between forward and backward raises, as in autograd
+        ctx.save_for_backward(x, *params)
         return pred
 
     @staticmethod
     def backward(ctx, g_pred):
-        _ = ctx.saved_tensors          # version check of the parameters
+        _ = ctx.saved_tensors          # version check of the input and the parameters
         need_params = any(ctx.needs_input_grad[1:])
         gx = None
         if ctx.needs_input_grad[0]:

@@ -690,10 +690,12 @@ def tail_fwd(cl, al, x, out, mask):
     L.check(_lib().fg_tail_fwd(view(cl), view(al), sview(x), L.ptr(out), L.ptr(mask), L.stream_handle()), "tail_fwd")
 
 
-def tail_bwd(cl, al, x, g_out, gc, ga, gx=None):
-    """gx (optional [N, C, H, W] tensor): channels 0..2 receive the background term's input gradient"""
+def tail_bwd(cl, al, x, g_out, gc, ga, gx=None, g_mask=None):
+    """gx (optional [N, C, H, W] tensor): channels 0..2 receive the background term's input gradient;
+    g_mask (optional [N, H, W]): dL/d(last_attention_mask), added to attention channel 9's gradient"""
     _wrote(gx)
-    L.check(_lib().fg_tail_bwd(view(cl), view(al), sview(x), sview(g_out), view(gc), view(ga), sview(gx),
+    gm = None if g_mask is None else g_mask.unsqueeze(1)
+    L.check(_lib().fg_tail_bwd(view(cl), view(al), sview(x), sview(g_out), sview(gm), view(gc), view(ga), sview(gx),
                                L.ptr(_amax_out(gc)), L.ptr(_amax_out(ga)), L.stream_handle()), "tail_bwd")
 
 

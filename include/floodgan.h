@@ -182,6 +182,10 @@ int fg_set_f3_persistent(int on);
 /* A/B hook: 1 (default) = a pipelined-kernel launch that would leave at least half the CUs without a tile
  * runs on narrower / shorter tiles (conv_f3.hip auto_cfg); 0 = the tile chosen by output channels only. */
 int fg_set_f3_fill(int on);
+/* A/B hook: 1 (default) = a pipelined-kernel launch of problems with equal tile counts (the four phases of a
+ * transposed conv or of a stride-2 input gradient) interleaves their tiles (tile t -> problem t % count), so
+ * the phases read each input row at the same time; 0 = problem after problem. */
+int fg_set_f3_interleave(int on);
 /* A/B hook of the pipelined f16x3 weight-gradient kernel (conv_wgrad_f3.hip, n_a >= 128): 0 off,
  * 1 = staging as one burst per stage, 3 = staging slots interleaved with the MFMA groups,
  * 2 (default) = the measured choice per tile (interleaved for 128-row tiles). */
@@ -358,10 +362,12 @@ int fg_tail_fwd(fg_view content_logits, fg_view att_logits, fg_sview x, float* o
  * `input[:, :3] * attention10` (models/model_architectures.py:393, :251) -- the input
  * gradient that the cycle path (models/model.py:677-706) back-propagates into G.  absmax_content /
  * absmax_att (optional absmax slots, initialised by the caller) are raised to bound |g_content| / |g_att|:
- * the f16x3 scale sources of the convs reading them, with no separate pass. */
+ * the f16x3 scale sources of the convs reading them, with no separate pass.  g_mask (optional, NULL ptr =
+ * none): a strided [N,1,H,W] view of dL/d(last_attention_mask), the mask being attention10
+ * (models/model_architectures.py:396); it joins attention channel 9's gradient before the softmax backward. */
 int fg_tail_bwd(fg_view content_logits, fg_view att_logits, fg_sview x, fg_sview g_out,
-                fg_view g_content, fg_view g_att, fg_wview g_x, float* absmax_content, float* absmax_att,
-                hipStream_t stream);
+                fg_sview g_mask, fg_view g_content, fg_view g_att, fg_wview g_x, float* absmax_content,
+                float* absmax_att, hipStream_t stream);
 
 /* CycleGAN generator head (models/model_architectures.py:115-117, conv 7x7 64->3 + nn.Tanh):
  * out (strided [N,c,H,W]) = tanh(logits[..., :c]). */

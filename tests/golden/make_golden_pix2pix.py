@@ -17,7 +17,11 @@ Recorded (R=256 -- the U-Net-256's smallest input --, batch N=2, input_channels=
     8192 strided samples) -- the model's own state and the training RNG
     stream are untouched by the recording
 
-Usage:  python tests/golden/make_golden_pix2pix.py   (~1 minute on 8 vCPU)
+A second fixture, pix2pix_step_256_rgb_bs1.npz, records the same quantities for BASELINE.json configs[0]:
+topography=None (3-ch RGB input, D over 3 + 3 channels), batch N=1, x ~ U[-1, 1)^(1,3,R,R) then
+y ~ U[-1, 1)^(1,3,R,R) from the same generator.
+
+Usage:  python tests/golden/make_golden_pix2pix.py [all|rgb]   (~1 minute each on 8 vCPU)
 """
 import copy
 import os
@@ -42,15 +46,26 @@ def probe(G, D, x0, y0):
     return np.concatenate([[g.sum().item(), g.abs().sum().item()], g[idx].numpy()]), d
 
 
-def run(R=256, N=2):
+def synth_c(R, N, C, gen):
+    x = torch.rand((N, C, R, R), generator=gen) * 2 - 1
+    y = torch.rand((N, 3, R, R), generator=gen) * 2 - 1
+    return x, y
+
+
+def run(R=256, N=2, topography="all"):
     from models import model as M  # noqa: E402  (reference, imported read-only)
 
     torch.set_num_threads(8)
     m = M.Model(model="pix2pix", dataset_subset="usa", dataset_dem="same", data_path="/nonexistent",
-                num_epochs=2, topography="all", resize=R, verbose=False)
+                num_epochs=2, topography=topography, resize=R, verbose=False)
     gen = torch.Generator().manual_seed(1234)
-    x0, y0 = synth(R, N, gen)
-    x1, y1 = synth(R, N, gen)
+    if topography == "all":
+        x0, y0 = synth(R, N, gen)
+        x1, y1 = synth(R, N, gen)
+    else:
+        C = m.generator.model.model[0].weight.shape[1]
+        x0, y0 = synth_c(R, N, C, gen)
+        x1, y1 = synth_c(R, N, C, gen)
     rec = {}   # the inputs are not stored: torch.Generator().manual_seed(1234) regenerates them
     G, D = m.generator, m.discriminator
     rec["init_g_out"], rec["init_d_out"] = probe(G, D, x0, y0)
@@ -105,9 +120,10 @@ def main():
     sys.path.insert(0, REF)
     cwd = os.getcwd()
     os.chdir(REF)
+    which = sys.argv[1] if len(sys.argv) > 1 else "all"
     try:
-        rec = run()
-        out = os.path.join(HERE, "pix2pix_step_256.npz")
+        rec = run() if which == "all" else run(N=1, topography=None)
+        out = os.path.join(HERE, "pix2pix_step_256.npz" if which == "all" else "pix2pix_step_256_rgb_bs1.npz")
         np.savez_compressed(out, **{k.replace(".", "__"): v for k, v in rec.items()})
         print("wrote", out, "losses it0", rec["it0_losses"], "it1", rec["it1_losses"])
     finally:

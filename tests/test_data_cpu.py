@@ -124,3 +124,68 @@ def test_crop_window_and_resize_size():
     assert [crop_window(512, 512, 4, i) for i in range(4)] == [(0, 0, 256, 256), (0, 256, 256, 256),
                                                               (256, 0, 256, 256), (256, 256, 256, 256)]
     assert crop_window(512, 512, None, 0) == (0, 0, 512, 512)
+
+
+class _Items:
+    """a dataset stand-in: only its length matters to the loader's index order"""
+
+    def __init__(self, n):
+        self.n = n
+
+    def __len__(self):
+        return self.n
+
+
+@pytest.mark.parametrize("n,bs,world", [(20, 1, 1), (20, 3, 1), (23, 2, 2), (7, 4, 1)])
+def test_tile_loader_order_is_the_reference_dataloaders(n, bs, world):
+    """TileLoader's item order under torch.manual_seed(epoch) (models/model.py:609) is the order of the
+    reference's DataLoader(batch_size=1, shuffle=True) (models/data.py:28-32): its iterator draws a base
+    seed from the global generator before RandomSampler draws its own; DP ranks take consecutive slices
+    of each global batch.  The global generator is left in the same state too."""
+    import torch
+    from torch.utils.data import DataLoader
+
+    from floodgan.data import TileLoader
+    ld = [TileLoader(_Items(n), batch_size=bs, device="cpu", rank=r, world=world) for r in range(world)]
+    torch.manual_seed(5)
+    flat = [int(i) for b in DataLoader(range(n), batch_size=1, shuffle=True) for i in b]
+    after = torch.rand(1)
+    g = bs * world
+    for r in range(world):
+        torch.manual_seed(5)
+        got = list(ld[r]._batches())
+        assert torch.equal(torch.rand(1), after)
+        glob = [flat[i:i + g] for i in range(0, n, g)]
+        if world > 1:
+            glob = [b for b in glob if len(b) == g]
+        assert got == [b[r * bs:(r + 1) * bs] for b in glob]
+
+
+def test_model_builds_loaders_from_data_path(tmp_path, monkeypatch):
+    """Model(**train.py's args) builds its three loaders from data_path (models/model.py:150-156): the split
+    table read relative to the working directory, the batch size, the topography channels, the crop
+    suffixes, and under DP the shard of this rank (here world 1).  Construction only (no compute)."""
+    import numpy as np
+
+    from floodgan.model import Model
+    from tiff_util import write_tiff
+    root = tmp_path
+    for d in ("dataset_input", "dataset_output", "metadata"):
+        (root / d).mkdir()
+    rows = ["image,best_DEM,same_DEM,version,split,disaster,country"]
+    for i, split in enumerate(["train"] * 5 + ["validation"] * 2 + ["test"]):
+        name = f"hurricane-harvey_{i:08d}"
+        write_tiff(str(root / "dataset_input" / f"{name}_10m.tif"), np.zeros((16, 16, 9), np.float32))
+        write_tiff(str(root / "dataset_output" / f"{name}.tif"), np.zeros((16, 16, 3), np.float32))
+        rows.append(f"{name},10m,10m,original,{split},hurricane-harvey,usa")
+    (root / "metadata" / "dataset_split.csv").write_text("\n".join(rows) + "\n")
+    monkeypatch.chdir(root)
+    m = Model(model="pairedattention", dataset_subset="hurricane-harvey", dataset_dem="same", data_path=str(root),
+              num_epochs=1, topography="map", resize=None, crop=4, device="cpu", batch_size=3)
+    assert (len(m.train_loader.ds), len(m.val_loader.ds), len(m.test_loader.ds)) == (20, 8, 4)   # x4 crops
+    assert m.train_loader.bs == 3 and len(m.train_loader) == 7
+    assert m.train_loader.ds.item(0)[4].endswith(("_0", "_1", "_2", "_3"))
+    assert m.train_loader.ds.chan == [0, 1, 2, 6, 7, 8]
+    # explicit loaders still take precedence (the bench / tests feed resident batches)
+    m2 = Model(model="pairedattention", data_path=str(root), device="cpu", train_loader=[1])
+    assert m2.train_loader == [1] and m2.val_loader is None

@@ -92,7 +92,7 @@ def test_tile_loader_vs_reference_items(tmp_path, crop, resize, topo):
     batch equal to the reference's per-item pipeline, names with the crop suffix (models/utils.py:56),
     and data-parallel sharding of each global batch (rank order)."""
     from floodgan.data import create_flood_dataset
-    from torch.utils.data import BatchSampler, RandomSampler
+    from torch.utils.data import DataLoader
     root = str(tmp_path)
     arrays = _dataset_dir(root)
     csv = os.path.join(root, "metadata", "dataset_split.csv")
@@ -100,7 +100,8 @@ def test_tile_loader_vs_reference_items(tmp_path, crop, resize, topo):
                                        csv_path=csv, prefetch=2)
     ds = train.ds
     torch.manual_seed(5)
-    order = [i for b in BatchSampler(RandomSampler(ds), 3, False) for i in b]
+    # the reference's own loader form (models/data.py:28-32: batch_size 1, shuffle=True) over the item indices
+    order = [int(i) for b in DataLoader(range(len(ds)), batch_size=1, shuffle=True) for i in b]
     torch.manual_seed(5)
     seen = []
     for xb, yb, names in train:
@@ -122,7 +123,8 @@ def test_tile_loader_vs_reference_items(tmp_path, crop, resize, topo):
         torch.manual_seed(9)
         shards.append([n for _, _, names in tr for n in names])
     torch.manual_seed(9)
-    glob = [b for b in BatchSampler(RandomSampler(ds), 4, True)]
+    flat = [int(i) for b in DataLoader(range(len(ds)), batch_size=1, shuffle=True) for i in b]
+    glob = [flat[i:i + 4] for i in range(0, len(flat) - 3, 4)]
     assert shards[0] == [ds.item(i)[4] for b in glob for i in b[:2]]
     assert shards[1] == [ds.item(i)[4] for b in glob for i in b[2:]]
 
@@ -140,3 +142,45 @@ def test_cycle_training_through_the_loader(tmp_path):
     m.train_cycle()
     vals = [v[-1] for v in m.all_losses.values()]
     assert len(vals) == 8 and all(np.isfinite(vals))
+
+
+def test_model_builds_its_loaders_like_train_py(tmp_path, monkeypatch):
+    """train.py's own call (models/model.py:150-156 via train.py:33-38): Model(**vars(args)) with the
+    reference's argument set over a dataset on disk -- the Model builds its train / validation / test loaders
+    from data_path (metadata/dataset_split.csv read relative to the working directory, as the reference
+    does) and train_paired runs on them.  Its per-epoch losses equal the same batches (the same
+    torch.manual_seed(epoch) order) fed to a fresh Model's fused step, and so do the trained weights."""
+    import argparse
+
+    from floodgan.model import Model
+    root = str(tmp_path)
+    _dataset_dir(root, n_img=5, h=64)
+    monkeypatch.chdir(root)
+    args = argparse.Namespace(model="pairedattention", dataset_subset="hurricane-harvey", dataset_dem="same",
+                              data_path=root, num_epochs=2, topography="all", resize=32, crop=None,
+                              save_model_interval=0, save_images_interval=0, verbose=False,
+                              load_pretrained_model=False, pretrained_model_path=None, add_identity_loss=False,
+                              seed=47)
+    args.training_model = True
+    m = Model(**vars(args), batch_size=2)
+    assert len(m.train_loader) == 4 and m.val_loader is not None and m.test_loader is not None   # 7 items, bs 2
+    m.train_paired()
+    ref = Model(**vars(args), batch_size=2)
+    keys = ["losses_discriminator_real", "losses_discriminator_synthetic", "losses_generator_synthetic",
+            "l1_losses_generator_synthetic"]
+    means = {k: [] for k in keys}
+    for epoch in (1, 2):
+        torch.manual_seed(epoch)                        # models/model.py:609
+        per = {k: [] for k in keys}
+        for xb, yb, names in ref.train_loader:
+            assert xb.shape[1:] == (9, 32, 32) and yb.shape[1:] == (3, 32, 32)
+            for k, v in zip(keys, ref.step_fn(xb, yb).cpu().tolist()):
+                per[k].append(v)
+        for k in keys:
+            means[k].append(float(np.mean(per[k])))
+        ref.scheduler_discriminator.step()
+        ref.scheduler_generator.step()
+    for k in keys:
+        assert np.allclose(m.all_losses["all_" + k], means[k], rtol=1e-6, atol=0), (k, m.all_losses["all_" + k], means[k])
+    for (k, a), (_, b) in zip(m.generator.named_parameters(), ref.generator.named_parameters()):
+        assert torch.equal(a, b), k

@@ -517,7 +517,7 @@ def test_tail():
     a = torch.softmax(al, 1)
     out = sum(t[:, 3 * i:3 * i + 3] * a[:, i:i + 1] for i in range(9)) + x[:, :3] * a[:, 9:10]
     g = torch.randn_like(out)
-    gcl_ref, gal_ref = torch.autograd.grad(out, (cl, al), g)
+    gcl_ref, gal_ref = torch.autograd.grad(out, (cl, al), g, retain_graph=True)
     CL = buf_from(cl.detach(), 0, "constant", 32)
     AL = buf_from(al.detach(), 0, "constant", 16)
     xd = x.float().to(DEV)
@@ -537,6 +537,13 @@ def test_tail():
         assert float(GC.t._fg_amax.max()) == float(GC.t.abs().max())
         assert float(GA.t._fg_amax.max()) == float(GA.t.abs().max())
         assert ops.absmax(GC) is GC.t._fg_amax          # cached: no separate pass
+    # a loss on last_attention_mask (attention10) as well: its gradient joins attention channel 9's
+    gm = torch.randn(N, H, H, dtype=torch.float64)
+    gcl_ref2, gal_ref2 = torch.autograd.grad((out, a[:, 9]), (cl, al), (g, gm))
+    gm_d = gm.float().to(DEV).permute(1, 2, 0).contiguous().permute(2, 0, 1)     # a strided [N, H, W] view
+    ops.tail_bwd(CL, AL, xd, g.float().to(DEV), GC, GA, g_mask=gm_d)
+    torch.cuda.synchronize()
+    assert nrel(nchw(GC, 27), gcl_ref2) < KTOL and nrel(nchw(GA, 10), gal_ref2) < KTOL
 
 
 def test_losses_and_adam():

@@ -23,7 +23,7 @@ from oracle import paired_attention as O
 from oracle import pix2pix as OP
 from test_gpu_northstar import KINK, _update_agreement
 from test_gpu_parity import DEV, NTOL, nrel
-from test_oracle_pix2pix_golden import GOLD, probe_sample, synth_inputs
+from test_oracle_pix2pix_golden import CASES, load_gold, probe_sample, synth_inputs
 
 pytestmark = pytest.mark.gpu
 
@@ -37,9 +37,11 @@ def _lib():
     torch.set_num_threads(min(16, max(1, len(__import__("os").sched_getaffinity(0)))))
 
 
-def _model(**kw):
+def _model(case="all_bs2", **kw):
+    """case: a tests/test_oracle_pix2pix_golden.CASES key -- topography="all" (9-ch input) or, for BASELINE.json
+    configs[0], topography=None (3-ch RGB input)"""
     from floodgan.model import Model
-    return Model(model="Pix2Pix", num_epochs=2, **kw)
+    return Model(model="Pix2Pix", num_epochs=2, topography="all" if CASES[case][2] == 9 else None, **kw)
 
 
 def _state(mod):
@@ -47,18 +49,20 @@ def _state(mod):
             {k: v.detach().cpu().clone() for k, v in mod.named_buffers()})
 
 
-def test_p1_forward_and_running_stats(report):
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_p1_forward_and_running_stats(case, report):
     from floodgan import executor as X
     from floodgan import pix2pix as P2P
-    m = _model()
-    (x, y), _ = synth_inputs()
+    _, n, c = CASES[case]
+    m = _model(case)
+    (x, y), _ = synth_inputs(N=n, C=c)
     (gp, gb), (dp, db) = _state(m.generator), _state(m.discriminator)
     torch.manual_seed(5)
-    masks = P2P.draw_dropout_masks(2, R, R)
+    masks = P2P.draw_dropout_masks(n, R, R)
     xd, yd = x.to(DEV), y.to(DEV)
     G, D = m.generator, m.discriminator
     fake, _ = P2P.gen_forward(G.param_dict(), G.buffer_dict(), xd, masks=masks, save=False)
-    pred, _ = P2P.disc_forward(D.param_dict(), D.buffer_dict(), X.disc_pack([(xd, fake), (xd, yd)], 12), groups=2,
+    pred, _ = P2P.disc_forward(D.param_dict(), D.buffer_dict(), X.disc_pack([(xd, fake), (xd, yd)], c + 3), groups=2,
                                save=False)
     torch.cuda.synchronize()
     with torch.no_grad():
@@ -66,10 +70,10 @@ def test_p1_forward_and_running_stats(report):
         fake_r = OP.generator_forward(gp, gb_r, x, masks=dict(masks))
         pf = OP.discriminator_forward(dp, db_r, torch.cat((x, fake_r), 1))
         pr = OP.discriminator_forward(dp, db_r, torch.cat((x, y), 1))
-    e = dict(g_out=nrel(fake, fake_r), d_fake=nrel(pred[:2], pf), d_real=nrel(pred[2:], pr))
+    e = dict(g_out=nrel(fake, fake_r), d_fake=nrel(pred[:n], pf), d_real=nrel(pred[n:], pr))
     run = [(k, nrel(v, gb_r[k])) for k, v in G.named_buffers() if v.is_floating_point()]
     run += [(k, nrel(v, db_r[k])) for k, v in D.named_buffers() if v.is_floating_point()]
-    report("pix2pix_p1_256", **e, worst_running_stat=max(run, key=lambda t: t[1]))
+    report("pix2pix_p1_256", case=case, **e, worst_running_stat=max(run, key=lambda t: t[1]))
     assert max(e.values()) < 1e-4, e
     assert max(r for _, r in run) < 1e-5, max(run, key=lambda t: t[1])
     # one BatchNorm call per generator layer, two (fake, real) per discriminator layer
@@ -77,21 +81,24 @@ def test_p1_forward_and_running_stats(report):
     assert all(int(v) == 2 for k, v in D.named_buffers() if k.endswith("num_batches_tracked"))
 
 
-def test_update_teacher_forced(report):
-    """Two fused iterations at 256x256, batch 2 (the golden inputs), each checked against the fp64
-    oracle continuing from the HIP state with the HIP masks and decisions."""
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_update_teacher_forced(case, report):
+    """Two fused iterations at 256x256 on the golden inputs (batch 2 with topography="all"; batch 1 with
+    the 3-ch RGB input of BASELINE.json configs[0]), each checked against the fp64 oracle continuing from
+    the HIP state with the HIP masks and decisions."""
     from floodgan import pix2pix as P2P
-    m = _model()
+    _, n, c = CASES[case]
+    m = _model(case)
     G, D = m.generator, m.discriminator
     step = m.step_fn
     step.record_decisions = True
-    for it, (x, y) in enumerate(synth_inputs()):
+    for it, (x, y) in enumerate(synth_inputs(N=n, C=c)):
         lr = 2e-4 if it == 0 else 1e-4
         for opt in (m.optimizer_generator, m.optimizer_discriminator):
             for grp in opt.param_groups:
                 grp["lr"] = lr
         (g0, gb0), (d0, db0) = _state(G), _state(D)
-        st = OP.Pix2PixStepOracle(dtype=torch.float64, lr=lr)
+        st = OP.Pix2PixStepOracle(dtype=torch.float64, lr=lr, c_in=c)
         st.load_state(g0, gb0, d0, db0, m.optimizer_generator.state_dict() if it else None,
                       m.optimizer_discriminator.state_dict() if it else None)
         torch.manual_seed(it + 1)
@@ -99,7 +106,7 @@ def test_update_teacher_forced(report):
         torch.cuda.synchronize()
         rec = {}
         dec = O.ActDecisions(step.decisions)
-        masks = {k: v.cpu() for k, v in P2P.dropout_masks(step.last_masks, 2, R, R).items()}
+        masks = {k: v.cpu() for k, v in P2P.dropout_masks(step.last_masks, n, R, R).items()}
         st.step(x, y, record=rec, masks=masks, decisions=dec,
                 d_after={k: v.detach().cpu() for k, v in D.named_parameters()})
         rows, bad = [], []
@@ -115,7 +122,7 @@ def test_update_teacher_forced(report):
                 if ge > 1e-4 or agree < 1.0 or uerr > NTOL:
                     bad.append(rows[-1])
         run = [(k, nrel(v, st.GB[k])) for k, v in G.named_buffers() if v.is_floating_point()]
-        report("pix2pix_update_teacher_forced", R=R, it=it, worst_grad=max(rows, key=lambda r: r[2])[1:3],
+        report("pix2pix_update_teacher_forced", case=case, R=R, it=it, worst_grad=max(rows, key=lambda r: r[2])[1:3],
                min_agree=min(r[3] for r in rows), worst_update=max(rows, key=lambda r: r[4])[1:5:3],
                min_decided=min(r[5] for r in rows), decisions_differing=sum(r[2] for r in dec.log),
                worst_kink=dec.worst(), worst_running_stat_G=max(run, key=lambda t: t[1]), bad=bad)
@@ -124,15 +131,16 @@ def test_update_teacher_forced(report):
         assert max(r for _, r in run) < 1e-5
 
 
-def _reference_envelope(gold, sigma=1e-6, trials=2):
+def _reference_envelope(gold, case, sigma=1e-6, trials=2):
     """how far the reference algorithm (fp32 oracle) itself lands from the golden run when its inputs
     carry `sigma` relative noise: per iteration (G probe, D probe, losses)"""
     from test_oracle_pix2pix_golden import probe
-    batches = synth_inputs()
+    _, n, c = CASES[case]
+    batches = synth_inputs(N=n, C=c)
     x0, y0 = batches[0]
     env = [[0.0, 0.0, 0.0], [0.0, 0.0, 0.0]]
     for trial in range(1, trials + 1):
-        st = OP.Pix2PixStepOracle()
+        st = OP.Pix2PixStepOracle(c_in=c)
         for it, (x, y) in enumerate(batches):
             st.set_lr(float(gold[f"it{it}_lr"][0]))
             noise = torch.randn(x.shape, generator=torch.Generator().manual_seed(trial * 10 + it))
@@ -146,13 +154,15 @@ def _reference_envelope(gold, sigma=1e-6, trials=2):
     return env
 
 
-def test_train_paired_vs_reference_golden(report):
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_train_paired_vs_reference_golden(case, report):
     """Model("Pix2Pix").train_paired over the golden's two epochs (one batch each; torch.manual_seed(epoch)
     fixes the Dropout masks exactly as in the reference) vs the reference's recorded losses and its
     training-mode G / D probes after each epoch."""
-    gold = {k.replace("__", "."): v for k, v in np.load(GOLD).items()}
-    env = _reference_envelope(gold)
-    batches = synth_inputs()
+    gold = load_gold(case)
+    env = _reference_envelope(gold, case)
+    _, n, c = CASES[case]
+    batches = synth_inputs(N=n, C=c)
     x0, y0 = (t.to(DEV) for t in batches[0])
     recorded = []
 
@@ -163,9 +173,9 @@ def test_train_paired_vs_reference_golden(report):
         def __iter__(self):
             x, y = batches[self.epoch]
             self.epoch += 1
-            return iter([(x, y, ["synthetic"] * 2)])
+            return iter([(x, y, ["synthetic"] * n)])
 
-    m = _model(train_loader=_Loader())
+    m = _model(case, train_loader=_Loader())
     m.generator.dropout_rng = "host"          # the reference's CPU draws, mask for mask
     orig = m.save_results
 
@@ -187,7 +197,7 @@ def test_train_paired_vs_reference_golden(report):
         lrel = np.abs(np.array(losses) - ref) / np.abs(ref)
         e_g = nrel(torch.from_numpy(g[2:]), torch.from_numpy(gold[f"it{it}_g_out"][2:]))
         e_d = nrel(torch.from_numpy(d), torch.from_numpy(gold[f"it{it}_d_out"]))
-        report("pix2pix_train_vs_reference_golden", it=it, loss_rel=lrel.tolist(), g_probe=e_g, d_probe=e_d,
+        report("pix2pix_train_vs_reference_golden", case=case, it=it, loss_rel=lrel.tolist(), g_probe=e_g, d_probe=e_d,
                reference_envelope=env[it])
         if it == 0:       # P1: the D losses and the L1 term are evaluated before any update
             assert lrel[[0, 1, 3]].max() < 1e-4, lrel

@@ -12,21 +12,33 @@ import torch
 
 from oracle import pix2pix as OP
 
-GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "pix2pix_step_256.npz")
+GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+# (file, batch, generator input channels): topography="all" at batch 2, and BASELINE.json configs[0] --
+# topography=None (3-ch RGB), batch 1
+CASES = {"all_bs2": ("pix2pix_step_256.npz", 2, 9), "rgb_bs1": ("pix2pix_step_256_rgb_bs1.npz", 1, 3)}
 
 
-@pytest.fixture(scope="module")
-def gold():
-    z = np.load(GOLD)
+def load_gold(case):
+    z = np.load(os.path.join(GOLDEN_DIR, CASES[case][0]))
     return {k.replace("__", "."): z[k] for k in z.files}
 
 
-def synth_inputs(R=256, N=2):
-    """tests/golden/make_golden.py synth(): x ~ U[-1,1)^(N,9,R,R), then y ~ U[-1,1)^(N,3,R,R), twice"""
+@pytest.fixture(scope="module", params=sorted(CASES))
+def case(request):
+    return request.param
+
+
+@pytest.fixture(scope="module")
+def gold(case):
+    return load_gold(case)
+
+
+def synth_inputs(R=256, N=2, C=9):
+    """tests/golden/make_golden.py synth(): x ~ U[-1,1)^(N,C,R,R), then y ~ U[-1,1)^(N,3,R,R), twice"""
     gen = torch.Generator().manual_seed(1234)
     out = []
     for _ in range(2):
-        x = torch.rand((N, 9, R, R), generator=gen) * 2 - 1
+        x = torch.rand((N, C, R, R), generator=gen) * 2 - 1
         y = torch.rand((N, 3, R, R), generator=gen) * 2 - 1
         out.append((x, y))
     return out
@@ -71,15 +83,15 @@ def _check(gold, prefix, P, rtol, elementwise=True):
             assert np.abs(mine[2:] - ref[2:]).max() < 0.1 * 3e-4, (prefix, name)
 
 
-def test_layout_names_match_golden(gold):
-    (gp, gb), (dp, db) = OP.init_params()
+def test_layout_names_match_golden(gold, case):
+    (gp, gb), (dp, db) = OP.init_params(c_in=CASES[case][2])
     mine = {f"init_G/{k}" for k in list(gp) + list(gb)} | {f"init_D/{k}" for k in list(dp) + list(db)}
     theirs = {k for k in gold if k.startswith("init_G/") or k.startswith("init_D/")}
     assert mine == theirs
 
 
-def test_init_rng_parity(gold):
-    (gp, gb), (dp, db) = OP.init_params(seed=47, c_in=9)
+def test_init_rng_parity(gold, case):
+    (gp, gb), (dp, db) = OP.init_params(seed=47, c_in=CASES[case][2])
     for prefix, P in (("init_G", {**gp, **gb}), ("init_D", {**dp, **db})):
         for name, t in P.items():
             ref = gold[f"{prefix}/{name}"]
@@ -89,18 +101,20 @@ def test_init_rng_parity(gold):
             assert abs(t.sum().item() - ref[0]) <= 1e-9 * max(1.0, abs(ref[1])), name
 
 
-def test_init_forward_training_mode(gold):
-    (x0, y0), _ = synth_inputs()
-    g, d = probe(OP.init_params(), x0, y0)
+def test_init_forward_training_mode(gold, case):
+    _, n, c = CASES[case]
+    (x0, y0), _ = synth_inputs(N=n, C=c)
+    g, d = probe(OP.init_params(c_in=c), x0, y0)
     assert nrel(g[2:], gold["init_g_out"][2:]) < 1e-6
     assert abs(g[0] - gold["init_g_out"][0]) <= 1e-5 * gold["init_g_out"][1]
     assert nrel(d, gold["init_d_out"]) < 1e-6
 
 
-def test_two_training_iterations(gold):
-    batches = synth_inputs()
+def test_two_training_iterations(gold, case):
+    _, n, c = CASES[case]
+    batches = synth_inputs(N=n, C=c)
     x0, y0 = batches[0]
-    st = OP.Pix2PixStepOracle()
+    st = OP.Pix2PixStepOracle(c_in=c)
     for it, (x, y) in enumerate(batches):
         st.set_lr(float(gold[f"it{it}_lr"][0]))
         torch.manual_seed(it + 1)                        # train_paired: torch.manual_seed(epoch)
