@@ -191,7 +191,8 @@ __device__ __forceinline__ f32x4 load_grad(const fg_view& g, int fp, const fg_vi
 }
 
 __global__ void in_bwd_stats_kernel(fg_view g, int fp, fg_view gadd, fg_view src, const float* __restrict__ mean,
-                                    const float* __restrict__ rstd, int act, int chunks, double* __restrict__ work) {
+                                    const float* __restrict__ rstd, int act, int chunks, double* __restrict__ work,
+                                    fg_view gsum) {
     const int C = src.c_alloc, L = C / 4, PG = NT / L;
     const int n = blockIdx.y, chunk = blockIdx.x;
     const int h = src.h, w = src.w, HW = h * w;
@@ -207,6 +208,7 @@ __global__ void in_bwd_stats_kernel(fg_view g, int fp, fg_view gadd, fg_view src
         for (int p = p0 + gi; p < p1; p += PG) {
             const f32x4 xh = (ld4(src.ptr + fg::vidx(src, n, y, x) + 4 * c4) - m) * r;
             f32x4 gv = load_grad(g, fp, gadd, n, y, x, h, w, c4);
+            if (gsum.ptr) *reinterpret_cast<f32x4*>(gsum.ptr + fg::vidx(gsum, n, y, x) + 4 * c4) = gv;
 #pragma unroll
             for (int e = 0; e < 4; ++e) gv[e] *= fg::act_grad(xh[e], act);
             sg += gv;
@@ -591,8 +593,8 @@ FG_API int fg_in_apply(fg_view src, const float* mean, const float* rstd, int ac
 }
 
 FG_API int fg_in_bwd(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, const float* mean, const float* rstd,
-                     int act, fg_view dst, float* bias_grad, int bias_accumulate, double* work, float* absmax,
-                     hipStream_t stream) {
+                     int act, fg_view dst, float* bias_grad, int bias_accumulate, fg_view gsum, double* work,
+                     float* absmax, hipStream_t stream) {
     if (!ok_view(gsrc) || !ok_view(src) || !ok_view(dst) || !mean || !rstd || !work || src.c_alloc % 4 ||
         (NT % (src.c_alloc / 4)) != 0 || gsrc.c_alloc != src.c_alloc || dst.c_alloc != src.c_alloc ||
         dst.h != src.h || dst.w != src.w || dst.n != src.n)
@@ -603,11 +605,13 @@ FG_API int fg_in_bwd(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, cons
                         fold_pad);
     if (gadd.ptr && (gadd.c_alloc != src.c_alloc || gadd.h != src.h || gadd.w != src.w))
         return fg::fail(FG_ERR_INVALID, "fg_in_bwd: gadd shape");
+    if (gsum.ptr && (gsum.c_alloc != src.c_alloc || gsum.h != src.h || gsum.w != src.w || gsum.n != src.n))
+        return fg::fail(FG_ERR_INVALID, "fg_in_bwd: gsum shape");
     const int chunks = choose_chunks(src.n, (long long)src.h * src.w);
     const int C = src.c_alloc;
     float* coef = reinterpret_cast<float*>(work + (size_t)src.n * C * MAX_CHUNKS * 3);
     hipLaunchKernelGGL(in_bwd_stats_kernel, dim3(chunks, src.n), dim3(NT), 0, stream, gsrc, fold_pad, gadd, src,
-                       mean, rstd, act, chunks, work);
+                       mean, rstd, act, chunks, work, gsum);
     int e = fg::launched("in_bwd_stats");
     if (e) return e;
     double* bpart = work + (size_t)src.n * C * MAX_CHUNKS * 3 + (size_t)src.n * C;
@@ -622,8 +626,11 @@ FG_API int fg_in_bwd(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, cons
         if (e) return e;
     }
     const long long total = (long long)dst.n * (dst.h + 2 * dst.pad) * (dst.w + 2 * dst.pad) * (C / 4);
-    hipLaunchKernelGGL(in_bwd_apply_kernel, dim3(fg::blocks_for(total, 256, 4096)), dim3(256), 0, stream, gsrc,
-                       fold_pad, gadd, src, mean, rstd, coef, act, dst, reinterpret_cast<unsigned*>(absmax));
+    // with gsum the apply pass reads the gathered gradient the statistics pass wrote (one read, no fold)
+    const fg_view none = {nullptr, 0, 0, 0, 0, 0};
+    hipLaunchKernelGGL(in_bwd_apply_kernel, dim3(fg::blocks_for(total, 256, 4096)), dim3(256), 0, stream,
+                       gsum.ptr ? gsum : gsrc, gsum.ptr ? 0 : fold_pad, gsum.ptr ? none : gadd, src, mean, rstd, coef,
+                       act, dst, reinterpret_cast<unsigned*>(absmax));
     return fg::launched("in_bwd_apply");
 }
 

@@ -235,22 +235,28 @@ def _block_fwd(P, pre, h, out_mode):
     return hn, dict(h=h, cb1=cb1, mb1=mb1, rb1=rb1, rb=rb, cb2=cb2, mb2=mb2, rb2=rb2)
 
 
-def _block_bwd(P, pre, b, g_h, G):
-    """Backward of _block_fwd: g_h = dL/d(block output) (compact) -> dL/d(block input).  The caller
-    joins G's side stream."""
-    N, Hh, Ww, Cc = g_h.n, g_h.h, g_h.w, g_h.c
-    dev = g_h.t.device
+def _block_bwd(P, pre, b, grad, G):
+    """Backward of _block_fwd: grad = dL/d(block output) -> dL/d(block input), both as a lazy sum
+    (gsrc, fold_pad, gadd): the gradient is fold(gsrc) + gadd -- the next block's input gradient is the
+    reflect-pad adjoint of its conv1 input gradient plus the residual path's gradient, and its norm
+    backward's statistics pass gathers that sum directly (and writes it out once, for this block's own
+    residual path: gsum), so no separate fold + add pass runs.  The caller joins G's side stream."""
+    gsrc, fold, gadd = grad
+    cb2 = b["cb2"]
+    N, Hh, Ww, Cc = cb2.n, cb2.h, cb2.w, cb2.c
+    dev = cb2.t.device
+    lazy = fold > 0 or gadd is not None
+    g_h = Buf.empty(N, Hh, Ww, Cc, 0, dev) if lazy else gsrc
     g_cb2 = Buf.empty(N, Hh, Ww, Cc, 2, dev)          # zero border 2: full correlation of a 3x3
-    ops.in_bwd(g_h, 0, None, b["cb2"], b["mb2"], b["rb2"], FG_ACT_NONE, g_cb2, G.get(pre + "conv2.bias"), G.acc)
+    ops.in_bwd(gsrc, fold, gadd, cb2, b["mb2"], b["rb2"], FG_ACT_NONE, g_cb2, G.get(pre + "conv2.bias"), G.acc,
+               gsum=g_h if lazy else None)
     _wgrad_conv(P, G, pre + "conv2", g_cb2, b["rb"], 1, 3, 1)
     g_rbp = _dgrad_s1_padded(P, pre + "conv2", g_cb2)  # gradient w.r.t. the reflect-padded relu output
     g_cb1 = Buf.empty(N, Hh, Ww, Cc, 2, dev)
     ops.in_bwd(g_rbp, 1, None, b["cb1"], b["mb1"], b["rb1"], FG_ACT_RELU, g_cb1, G.get(pre + "conv1.bias"), G.acc)
     _wgrad_conv(P, G, pre + "conv1", g_cb1, b["h"], 1, 3, 1)
     g_hp = _dgrad_s1_padded(P, pre + "conv1", g_cb1)
-    g_new = Buf.empty(N, Hh, Ww, Cc, 0, dev)
-    ops.fold_add(g_hp, 1, g_h, g_new)                 # reflect-pad adjoint + residual path
-    return g_new
+    return g_hp, 1, g_h                               # reflect-pad adjoint + residual path, summed lazily
 
 
 def _dgrad_s1_padded(P, name, gy):
@@ -301,7 +307,9 @@ def block_backward_nchw(S, g, need_input=True):
     gb = Buf.empty(N, Hh, Ww, Cc, 0, g.device)
     ops.pack_input(g, Cc, None, 0, gb, 0, N, FG_PAD_ZERO)
     G = _Grads(S["P"], device=g.device)
-    g_new = _block_bwd(S["P"], "", S["b"], gb, G)
+    g_hp, fold, g_res = _block_bwd(S["P"], "", S["b"], (gb, 0, None), G)
+    g_new = Buf.empty(N, Hh, Ww, Cc, 0, g.device)
+    ops.fold_add(g_hp, fold, g_res, g_new)
     G.join()
     grads = {"w1": G.out["conv1.weight"], "b1": G.out["conv1.bias"],
              "w2": G.out["conv2.weight"], "b2": G.out["conv2.bias"]}
@@ -418,12 +426,13 @@ def gen_backward(P, S, g_out, grads_into=None, ready=None, input_grad=None, accu
         ops.conv([PL.conv_problem(g_d1, 1, 3, 2, ops.pack_weight(w, m), m, g_h, accumulate=idx)])
     G.ready(ready, "deconv1_content")
     # ---- resnet blocks in reverse: out = h + IN(conv2(pad(relu(IN(conv1(pad(h)))))))
+    grad = (g_h, 0, None)
     for i in reversed(range(N_BLOCKS)):
-        g_h = _block_bwd(P, f"resnet_blocks.{i}.", S["blocks"][i], g_h, G)
+        grad = _block_bwd(P, f"resnet_blocks.{i}.", S["blocks"][i], grad, G)
         G.ready(ready, _blk(i, 1))
-    # ---- encoder
+    # ---- encoder (the first block's input gradient, fold + residual, gathered by conv3's norm backward)
     g_c3 = Buf.empty(N, H // 4, W // 4, 256, 1, dev)
-    ops.in_bwd(g_h, 0, None, S["c3"], S["m3"], S["r3"], FG_ACT_RELU, g_c3, G.get("conv3.bias"), G.acc)
+    ops.in_bwd(grad[0], grad[1], grad[2], S["c3"], S["m3"], S["r3"], FG_ACT_RELU, g_c3, G.get("conv3.bias"), G.acc)
     _wgrad_conv(P, G, "conv3", g_c3, S["a2"], 1, 3, 2)
     g_a2 = Buf.empty(N, H // 2, W // 2, 128, 0, dev)
     _dgrad_s2(P, "conv3", g_c3, 3, Y=g_a2)

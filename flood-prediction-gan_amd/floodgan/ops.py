@@ -563,9 +563,13 @@ def in_apply(src, mean, rstd, act, residual, dst, pad_mode):
                                L.ptr(_amax_out(dst)), L.stream_handle()), "in_apply")
 
 
-def in_bwd(gsrc, fold_pad, gadd, src, mean, rstd, act, dst, bias_grad=None, bias_accumulate=False):
+def in_bwd(gsrc, fold_pad, gadd, src, mean, rstd, act, dst, bias_grad=None, bias_accumulate=False, gsum=None):
+    """InstanceNorm (+ activation, reflect-pad fold, residual gradient gadd) backward into dst.  gsum (Buf): also
+    receives the gathered gradient fold(gsrc) + gadd (written by the statistics pass that reads it anyway)."""
+    work = _work(src.n, src.c, src.t.device)
+    _wrote(gsum)
     L.check(_lib().fg_in_bwd(view(gsrc), fold_pad, view(gadd), view(src), L.ptr(mean), L.ptr(rstd), act, view(dst),
-                             L.ptr(bias_grad), int(bias_accumulate), L.ptr(_work(src.n, src.c, src.t.device)),
+                             L.ptr(bias_grad), int(bias_accumulate), view(gsum), L.ptr(work),
                              L.ptr(_amax_out(dst)), L.stream_handle()), "in_bwd")
 
 

@@ -334,10 +334,14 @@ int fg_in_apply(fg_view src, const float* mean, const float* rstd, int act, fg_v
  * padding of width fold_pad when fold_pad > 0 (gsrc then holds the gradient of the padded
  * tensor); optional gadd (compact) is added.  dst receives dL/dsrc (border zeroed);
  * bias_grad (optional, [c]) receives (or, with bias_accumulate, is raised by) sum over n,y,x
- * of dst = grad of the conv bias that feeds this norm. */
+ * of dst = grad of the conv bias that feeds this norm.  gsum (optional, NULL ptr = none): receives
+ * g = fold(gsrc) + gadd itself in its interior (the gradient of a PairedAttentionBlock's input, which the
+ * residual path needs again: models/model_architectures.py:418), written by the statistics pass that reads
+ * it anyway -- the separate reflect-fold + residual-add pass (fg_fold_add) is not needed. */
 int fg_in_bwd(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, const float* mean,
-              const float* rstd, int act, fg_view dst, float* bias_grad, int bias_accumulate, double* work,
-              float* absmax, hipStream_t stream);
+              const float* rstd, int act, fg_view dst, float* bias_grad, int bias_accumulate, fg_view gsum,
+              double* work, float* absmax, hipStream_t stream);
+
 
 /* g *= act'(y) in place over the interior (y = saved activation output).  absmax (optional absmax slot,
  * initialised by the caller) is raised to max |g| over the interior -- a bound for the whole buffer when its

@@ -178,62 +178,89 @@ def test_bs8_per_sample_equals_bs1_512(report):
     assert np.isfinite(losses).all()
 
 
-def _separable_grads(m, xs, ys, c1, c2):
-    """HIP executor gradients of L = sum_i [c1 * sum (D(cat(x_i, G(x_i))) - 1)^2 + c2 * sum (G(x_i) - y_i)^2]
-    with FIXED scales c1, c2 (not the batch means): the loss is a sum over samples, so its gradients at
-    batch B are the sum of the batch-1 gradients of each sample (InstanceNorm and the PatchGAN are per
-    sample).  Returns (G grads, D grads, activation decisions), cloned."""
+def _separable_grads(m, xs, ys, c1, c2, weights=None, g_only=False):
+    """HIP executor gradients of L = sum_i w_i [c1 * sum (D(cat(x_i, G(x_i))) - 1)^2 + c2 * sum (G(x_i) - y_i)^2]
+    with FIXED scales c1, c2 (not the batch means) and per-sample weights w (default 1): the loss is a sum over
+    samples, so its gradients at batch B are the sum of the batch-1 gradients of each sample (InstanceNorm and
+    the PatchGAN are per sample).  g_only: the generator term alone (no discriminator).  Returns (G grads,
+    D grads, activation decisions {"G": [...], "D": [...]}), cloned."""
     from floodgan import executor as X
     gp, dp = m.generator.param_dict(), m.discriminator.param_dict()
-    C = xs.shape[1]
+    N, C = xs.shape[0], xs.shape[1]
+    w = torch.ones(N, device=xs.device) if weights is None else weights.to(xs.device)
     fake, _, S = X.gen_forward(gp, xs, save=True)
-    pred, dS = X.disc_forward(dp, X.disc_pack([(xs, fake)], C + 3), save=True)
-    g_fake = (c2 * (fake - ys)).contiguous()
-    gD = X.disc_backward(dp, dS, (c1 * (pred - 1)).contiguous(), param_grads=True, input_grad=g_fake,
-                         input_grad_channels=(C, 3), input_grad_accumulate=True)
+    g_fake = (c2 * w.view(-1, 1, 1, 1) * (fake - ys)).contiguous()
+    gD, dec = {}, {"G": [X.gen_act_decisions(S)]}
+    if not g_only:
+        pred, dS = X.disc_forward(dp, X.disc_pack([(xs, fake)], C + 3), save=True)
+        gD = X.disc_backward(dp, dS, (c1 * w.view(-1, 1, 1, 1) * (pred - 1)).contiguous(), param_grads=True,
+                             input_grad=g_fake, input_grad_channels=(C, 3), input_grad_accumulate=True)
+        dec["D"] = [X.disc_act_decisions(dS)]
+        del dS
     gG = X.gen_backward(gp, S, g_fake)
-    dec = {"G": X.gen_act_decisions(S), "D": X.disc_act_decisions(dS)}
     torch.cuda.synchronize()
     return {k: v.clone() for k, v in gG.items()}, {k: v.clone() for k, v in gD.items()}, dec
 
 
-def test_bs8_backward_equals_sum_of_bs1_512(report):
-    """The bench's own backward (batch 8 at 512x512: the resblock weight gradients' split reductions over
-    M = 131072 rows, conv_wgrad_f3_kernel<256,0>; the batch-8 input-gradient tile streams; the 2N
-    discriminator) under a per-sample-separable smooth loss: every G and D weight gradient equals the sum
-    of the eight batch-1 HIP runs (norm-relative 1e-5; IN-cancelled biases excluded).  Two
-    samples' batch-1 gradients are also checked against the fp64 oracle with the HIP decisions
-    teacher-forced (1e-4, as P2), which pins the sum to the reference's arithmetic."""
+C1_512, C2_512 = 2.0 / (62 * 62), 200.0 / (3 * R * R)     # the batch-1 mean scales of compare_smooth_grads
+
+
+def test_bs8_generator_backward_equals_sum_of_bs1_512(report):
+    """The generator backward at the bench's batch 8 (512x512: the resblock weight gradients' split reductions
+    over M = 131072 rows, conv_wgrad_f3_kernel<256,0>; the batch-8 input-gradient tile streams) under a
+    per-sample-separable smooth loss on G's output: every weight gradient equals the sum of the eight batch-1
+    HIP runs to 1e-5 (IN-cancelled biases excluded) when both evaluations take the same
+    activation decisions.  They usually do -- the forward reads the same per-sample values -- but where the
+    f16x3 operand scale (a power of two from the BATCH absmax) differs between the batch-8 and the batch-1
+    evaluation of a tensor, rounding-level differences can flip a ReLU sitting at its kink, and one flip moves
+    a whole network's gradients by ~1e-4 (P2); the tolerance is then the flip envelope, 3e-3, and the flips
+    are reported.  The exact pin of the batch-8 backward is test_bs8_backward_vs_fp64_512 (teacher-forced)."""
     x, y = _inputs(8, seed=17)
     m = _model()
     xd, yd = x.to(DEV), y.to(DEV)
-    c1, c2 = 2.0 / (62 * 62), 200.0 / (3 * R * R)      # the batch-1 mean scales of compare_smooth_grads
-    g8, d8, dec8 = _separable_grads(m, xd, yd, c1, c2)
-    gs, ds, flips = None, None, 0
+    g8, _, dec8 = _separable_grads(m, xd, yd, C1_512, C2_512, g_only=True)
+    gs, flips = None, 0
     for i in range(8):
-        g1, d1, dec1 = _separable_grads(m, xd[i:i + 1], yd[i:i + 1], c1, c2)
+        g1, _, dec1 = _separable_grads(m, xd[i:i + 1], yd[i:i + 1], C1_512, C2_512, g_only=True)
         gs = g1 if gs is None else {k: gs[k] + v for k, v in g1.items()}
-        ds = d1 if ds is None else {k: ds[k] + v for k, v in d1.items()}
-        for net in ("G", "D"):
-            for k, v in dec1[net].items():
-                flips += int((v[0] != dec8[net][k][i]).sum())
-        del g1, d1, dec1
-    skip_g, skip_d = O.cancelled_biases()
+        for k, v in dec1["G"][0].items():
+            flips += int((v[0] != dec8["G"][0][k][i]).sum())
+        del g1, dec1
+    skip_g, _ = O.cancelled_biases()
     eg = _worst([(k, nrel(v, gs[k])) for k, v in g8.items() if k not in skip_g])
-    ed = _worst([(k, nrel(v, ds[k])) for k, v in d8.items() if k not in skip_d])
-    report("bs8_512_backward_vs_sum_bs1", worst_G=eg, worst_D=ed, decisions_differing_bs8_vs_bs1=flips)
-    # a decision that differs between the batch-8 and batch-1 evaluations (rounding at a kink) moves a whole
-    # network's gradients by ~1e-4 (see P2); none is expected, as both read the same per-sample values
-    tol = 1e-5 if flips == 0 else 1e-4
-    assert eg[1] < tol and ed[1] < tol, (eg, ed, flips)
-    assert flips <= 16, flips
-    del g8, d8, gs, ds
-    torch.cuda.empty_cache()
-    for i in (0, 5):
-        eg1, ed1, fl1, kink = compare_smooth_grads(m, x[i:i + 1], y[i:i + 1])
-        report("bs8_512_sample_vs_fp64", sample=i, worst_G=eg1, worst_D=ed1, decisions_differing=fl1, worst_kink=kink)
-        assert eg1[1] < 1e-4 and ed1[1] < 1e-4, (i, eg1, ed1)
-        assert kink < KINK, kink
+    report("bs8_512_G_backward_vs_sum_bs1", worst_G=eg, decisions_differing_bs8_vs_bs1=flips)
+    assert flips <= 200, flips
+    assert eg[1] < (1e-5 if flips == 0 else 3e-3), (eg, flips)
+
+
+def test_bs8_backward_vs_fp64_512(report):
+    """The whole smooth G + D loss at batch 8, 512x512 (the D pass on 8 images, D's input gradient into G, the
+    G backward) with per-sample weights that keep samples 0 and 5: the batch-8 HIP gradients of every G and
+    D parameter equal the fp64 oracle's (the sum of its two batch-1 runs, each with the HIP batch-8 decisions
+    of that sample teacher-forced) to 1e-4, every differing decision within rounding of its kink (P2's
+    criterion at the bench's shape: the batch-8 kernels, their split reductions and tile streams)."""
+    keep = (0, 5)
+    x, y = _inputs(8, seed=23)
+    m = _model()
+    w = torch.zeros(8)
+    w[list(keep)] = 1.0
+    g8, d8, dec8 = _separable_grads(m, x.to(DEV), y.to(DEV), C1_512, C2_512, weights=w)
+    Gp, Dp = O.init_params()
+    rG, rD, flips, kink = None, None, 0, 0.0
+    for i in keep:
+        dec = O.ActDecisions({net: [{k: v[i:i + 1] for k, v in dec8[net][0].items()}] for net in ("G", "D")})
+        gG, gD = oracle_smooth_grads(Gp, Dp, x[i:i + 1], y[i:i + 1], dec)
+        rG = gG if rG is None else {k: rG[k] + v for k, v in gG.items()}
+        rD = gD if rD is None else {k: rD[k] + v for k, v in gD.items()}
+        flips += sum(n for _, _, n, _ in dec.log)
+        kink = max(kink, dec.worst())
+    skip_g, skip_d = O.cancelled_biases()
+    eg = _worst([(k, nrel(v, rG[k])) for k, v in g8.items() if k not in skip_g])
+    ed = _worst([(k, nrel(v, rD[k])) for k, v in d8.items() if k not in skip_d])
+    report("bs8_512_backward_vs_fp64", samples=list(keep), worst_G=eg, worst_D=ed, decisions_differing=flips,
+           worst_kink=kink)
+    assert eg[1] < 1e-4 and ed[1] < 1e-4, (eg, ed)
+    assert kink < KINK, kink
 
 
 # ---------------------------------------------------------------------------------------------- U
