@@ -97,7 +97,7 @@ def p2p_step_gflop_per_img(res):
     return tot / 1e9
 
 
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "round2", "r2_pmc_resblock_fwd.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "round3", "r3_pmc_resblock_fwd.json")
 
 
 def pmc_traffic(kernel_tag):
@@ -116,10 +116,31 @@ def pmc_traffic(kernel_tag):
             "mfma_busy": s.get("mfma_busy"), "clock_ghz": s.get("clock_ghz")}
 
 
+def cgroup_cpu_limit():
+    """The CPU bandwidth the job's cgroup grants (cgroup v2 cpu.max "quota period" -> quota / period CPUs, or
+    None when unlimited / unreadable), with the raw file content as evidence."""
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            raw = open(path).read().strip()
+        except OSError:
+            continue
+        quota, _, period = raw.partition(" ")
+        cpus = None if quota == "max" else round(int(quota) / int(period or 100000), 2)
+        return {"path": path, "raw": raw, "cpus": cpus}
+    try:                                   # cgroup v1
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return {"path": "/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "raw": f"{q} {p}", "cpus": None if q < 0 else round(q / p, 2)}
+    except (OSError, ValueError):
+        return None
+
+
 def host_cpus():
-    """What the host offers: lscpu's sockets x cores per socket (physical cores), logical CPUs, and the
-    CPU share this process may use (affinity; OMP_NUM_THREADS on the GPU box = the box's share)."""
-    info = {"logical": os.cpu_count(), "affinity": len(os.sched_getaffinity(0))}
+    """What the host offers: lscpu's sockets x cores per socket (physical cores), logical CPUs, the CPU share
+    this process may use (affinity; OMP_NUM_THREADS on the GPU box = the box's share) and the cgroup's CPU
+    bandwidth limit (the evidence that the share, not the host, bounds the baseline's threads)."""
+    info = {"logical": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "cgroup_cpu_max": cgroup_cpu_limit(),
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
     try:
         import subprocess
         out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
@@ -160,8 +181,10 @@ def cpu_baseline(res, threads, steps=3, workload="paired", batches=(1, 8)):
             "by_batch": {str(b): round(v, 4) for b, v in rates.items()}, "host": host,
             "sample": f"{steps} timed iterations at batch " + " and ".join(map(str, batches)) +
                       f" (+1 warm-up) of the CPU oracle {workload} step, {res}x{res}, torch-CPU fp32 with {threads} "
-                      f"threads (the box's CPU share; host: {host.get('physical_cores')} physical cores, "
-                      f"{host.get('logical')} logical); value = the batch-{batches[-1]} rate"}
+                      f"threads (the job's CPU share: cgroup cpu.max "
+                      f"{(host.get('cgroup_cpu_max') or {}).get('raw')}, OMP_NUM_THREADS {host.get('omp_num_threads')}; "
+                      f"host: {host.get('physical_cores')} physical cores, {host.get('logical')} logical); value = the "
+                      f"batch-{batches[-1]} rate"}
 
 
 def main():

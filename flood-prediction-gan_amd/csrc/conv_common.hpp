@@ -57,6 +57,22 @@ __device__ __forceinline__ void split_f16(const float (&v)[8], float s, f16x8& h
     }
 }
 
+// f16x3 split of a pair with the scale folded into mixed-precision FMAs: v_fma_mixlo/mixhi_f16 compute an fp32
+// fma and round it to fp16 into one half of the destination, so h = fp16(x*s) and l = fp16(x*s - h) take four
+// instructions per pair instead of two v_mul, two v_fma_mix_f32 and two v_cvt_pk (bit-identical: x*s with a
+// power-of-two s and x*s - h are exact in fp32 and both are rounded once, to nearest even).
+__device__ __forceinline__ void split_pair_mix(float x0, float x1, float s, unsigned& h, unsigned& l) {
+    unsigned hv, lv;
+    asm("v_fma_mixlo_f16 %0, %1, %2, 0\n\t"
+        "v_fma_mixhi_f16 %0, %3, %2, 0"
+        : "=&v"(hv) : "v"(x0), "v"(s), "v"(x1));
+    asm("v_fma_mixlo_f16 %0, %1, %2, -%4 op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixhi_f16 %0, %3, %2, -%4 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+        : "=&v"(lv) : "v"(x0), "v"(s), "v"(x1), "v"(hv));
+    h = hv;
+    l = lv;
+}
+
 // 16-B chunk swizzle of a pre-split pixel (fg_split_pixels): chunk k of [h | l] of the pixel in
 // padded column x is stored at k ^ swz_pixel(x) -- conflict-free shifted fragment reads
 // (exhaustive search over the ds_read_b128 lane groups and every row offset)

@@ -41,12 +41,17 @@ __device__ __forceinline__ f16x8 tr_frag(const char* base, int a0, int a1) {
 }
 
 __device__ __forceinline__ void split4(const f32x4& v, float s, f16x4& h, f16x4& l) {
+    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+    u32x2 hu, lu;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        const float x = v[e] * s;
-        h[e] = (_Float16)x;
-        l[e] = (_Float16)(x - (float)h[e]);
+    for (int e = 0; e < 2; ++e) {
+        unsigned a, b;
+        fgc::split_pair_mix(v[2 * e], v[2 * e + 1], s, a, b);     // the mixed-FMA split (conv_common.hpp)
+        hu[e] = a;
+        lu[e] = b;
     }
+    h = __builtin_bit_cast(f16x4, hu);
+    l = __builtin_bit_cast(f16x4, lu);
 }
 
 // SCH 0: each stage = store (split + LDS writes of the staged registers) and the next global

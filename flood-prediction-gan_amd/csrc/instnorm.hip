@@ -279,18 +279,21 @@ __global__ void __launch_bounds__(64 * FG) in_bwd_finalize_kernel(int N, int C, 
     bpart[idx] = -(double)rstd[idx] * sx * sgx / HW;
 }
 
-__global__ void in_bwd_bias_kernel(int N, int C, const double* __restrict__ bpart, float* __restrict__ bias_grad,
-                                   int accumulate) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
-    double s = 0;
-    for (int n = 0; n < N; ++n) s += bpart[(size_t)n * C + c];
-    bias_grad[c] = accumulate ? bias_grad[c] + (float)s : (float)s;
-}
 
 __global__ void in_bwd_apply_kernel(fg_view g, int fp, fg_view gadd, fg_view src, const float* __restrict__ mean,
                                     const float* __restrict__ rstd, const float* __restrict__ coef, int act,
-                                    fg_view dst, unsigned* __restrict__ amax) {
+                                    fg_view dst, unsigned* __restrict__ amax, const double* __restrict__ bpart,
+                                    float* __restrict__ bias_grad, int bias_accumulate) {
+    // block 0 also sums the per-plane bias-gradient parts of the finalize over the images (the finalize
+    // has completed: kernel boundary) -- no launch of its own for a few hundred values
+    if (bias_grad && blockIdx.x == 0) {
+        const int C = dst.c_alloc;
+        for (int c = threadIdx.x; c < C; c += blockDim.x) {
+            double s = 0;
+            for (int n = 0; n < dst.n; ++n) s += bpart[(size_t)n * C + c];
+            bias_grad[c] = bias_accumulate ? bias_grad[c] + (float)s : (float)s;
+        }
+    }
     unsigned am = 0;
     const int C = dst.c_alloc, C4 = C / 4;
     const int h = dst.h, w = dst.w;
@@ -619,18 +622,12 @@ FG_API int fg_in_bwd(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, cons
                        src.h * src.w, chunks, work, rstd, coef, bpart);
     e = fg::launched("in_bwd_finalize");
     if (e) return e;
-    if (bias_grad) {
-        hipLaunchKernelGGL(in_bwd_bias_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, src.n, C, bpart,
-                           bias_grad, bias_accumulate);
-        e = fg::launched("in_bwd_bias");
-        if (e) return e;
-    }
     const long long total = (long long)dst.n * (dst.h + 2 * dst.pad) * (dst.w + 2 * dst.pad) * (C / 4);
     // with gsum the apply pass reads the gathered gradient the statistics pass wrote (one read, no fold)
     const fg_view none = {nullptr, 0, 0, 0, 0, 0};
     hipLaunchKernelGGL(in_bwd_apply_kernel, dim3(fg::blocks_for(total, 256, 4096)), dim3(256), 0, stream,
                        gsum.ptr ? gsum : gsrc, gsum.ptr ? 0 : fold_pad, gsum.ptr ? none : gadd, src, mean, rstd, coef,
-                       act, dst, reinterpret_cast<unsigned*>(absmax));
+                       act, dst, reinterpret_cast<unsigned*>(absmax), bpart, bias_grad, bias_accumulate);
     return fg::launched("in_bwd_apply");
 }
 

@@ -56,12 +56,12 @@ __global__ void l1_kernel(fg_sview a, fg_sview b, int C, int H, int W, long long
     if (threadIdx.x == 0) work[blockIdx.x] = s;
 }
 
-__global__ void mean_finalize(const double* __restrict__ work, int parts, long long n, float* loss) {
+__global__ void mean_finalize(const double* __restrict__ work, int parts, long long n, float* loss, float scale) {
     __shared__ double red[NT];
     double acc = 0;
     for (int i = threadIdx.x; i < parts; i += NT) acc += work[i];
     const double s = block_sum(acc, red);
-    if (threadIdx.x == 0) loss[0] = (float)(s / (double)n);
+    if (threadIdx.x == 0) loss[0] = (float)(s / (double)n) * scale;
 }
 
 // ---- Adam ----
@@ -125,12 +125,12 @@ FG_API int fg_mse_const(const float* p, long long n, float target, float gscale,
     hipLaunchKernelGGL(mse_kernel, dim3(parts), dim3(NT), 0, stream, p, n, target, gscale, g, work);
     int e = fg::launched("mse");
     if (e) return e;
-    hipLaunchKernelGGL(mean_finalize, dim3(1), dim3(NT), 0, stream, work, parts, n, loss);
+    hipLaunchKernelGGL(mean_finalize, dim3(1), dim3(NT), 0, stream, work, parts, n, loss, 1.f);
     return fg::launched("mse_finalize");
 }
 
-FG_API int fg_l1(fg_sview a, fg_sview b, int N, int C, int H, int W, float gscale, float* loss, float* g,
-                 int accumulate, double* work, hipStream_t stream) {
+FG_API int fg_l1(fg_sview a, fg_sview b, int N, int C, int H, int W, float gscale, float loss_scale, float* loss,
+                 float* g, int accumulate, double* work, hipStream_t stream) {
     if (!a.ptr || !b.ptr || !loss || !work || N < 1 || C < 1 || H < 1 || W < 1)
         return fg::fail(FG_ERR_INVALID, "fg_l1: bad args");
     const long long n = (long long)N * C * H * W;
@@ -138,7 +138,7 @@ FG_API int fg_l1(fg_sview a, fg_sview b, int N, int C, int H, int W, float gscal
     hipLaunchKernelGGL(l1_kernel, dim3(parts), dim3(NT), 0, stream, a, b, C, H, W, n, gscale, g, accumulate, work);
     int e = fg::launched("l1");
     if (e) return e;
-    hipLaunchKernelGGL(mean_finalize, dim3(1), dim3(NT), 0, stream, work, parts, n, loss);
+    hipLaunchKernelGGL(mean_finalize, dim3(1), dim3(NT), 0, stream, work, parts, n, loss, loss_scale);
     return fg::launched("l1_finalize");
 }
 

@@ -145,8 +145,8 @@ SIGNATURES = {
     "fg_tanh_head_bwd": [fg_view, C.c_int, fg_sview, fg_view, C.c_void_p],
     "fg_mse_const": [C.c_void_p, C.c_longlong, C.c_float, C.c_float, C.c_void_p, C.c_void_p, C.c_void_p,
                      C.c_void_p],
-    "fg_l1": [fg_sview, fg_sview, C.c_int, C.c_int, C.c_int, C.c_int, C.c_float, C.c_void_p, C.c_void_p,
-              C.c_int, C.c_void_p, C.c_void_p],
+    "fg_l1": [fg_sview, fg_sview, C.c_int, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float, C.c_void_p,
+              C.c_void_p, C.c_int, C.c_void_p, C.c_void_p],
     "fg_adam_step": [C.POINTER(fg_adam_tensor), C.c_int, C.c_double, C.c_double, C.c_double, C.c_double,
                      C.c_longlong, C.c_void_p],
     "fg_bn_workspace_doubles": [C.c_int, C.c_int],

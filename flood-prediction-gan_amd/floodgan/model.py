@@ -80,7 +80,7 @@ class PairedStep:
         g_pred = torch.empty_like(pred)
         ops.mse_const(pred, 1.0, inv, losses[2:3], g_pred)
         g_fake = torch.empty(N, 3, x.shape[2], x.shape[3], dtype=torch.float32, device=dev)
-        ops.l1(fake, y, 100.0 * inv, losses[3:4], g_fake)
+        ops.l1(fake, y, 100.0 * inv, losses[3:4], g_fake, loss_scale=100.0)     # logged as 100 * L1 (:643-651)
         X.disc_backward(self.dp, dS, g_pred, param_grads=False, input_grad=g_fake, input_grad_channels=(C, 3),
                         input_grad_accumulate=True)
         if rec is not None:
@@ -93,7 +93,7 @@ class PairedStep:
         self.gflat.finish()
         self.opt_g.step()
         self.last_mask, self.last_output = mask, fake
-        return losses * torch.tensor([1.0, 1.0, 1.0, 100.0], device=dev)
+        return losses
 
     @staticmethod
     def _grads(params):
@@ -152,7 +152,7 @@ class Pix2PixStep(PairedStep):
         g_pred = torch.empty_like(pred)
         ops.mse_const(pred, 1.0, inv, losses[2:3], g_pred)
         g_fake = torch.empty(N, 3, H, W, dtype=torch.float32, device=dev)
-        ops.l1(fake, y, 100.0 * inv, losses[3:4], g_fake)
+        ops.l1(fake, y, 100.0 * inv, losses[3:4], g_fake, loss_scale=100.0)     # logged as 100 * L1 (:643-651)
         P2P.disc_backward(self.dp, dS, g_pred, param_grads=False, input_grad=g_fake, input_grad_channels=(C, 3),
                           input_grad_accumulate=True)
         if rec is not None:
@@ -165,7 +165,7 @@ class Pix2PixStep(PairedStep):
         self.gflat.finish()
         self.opt_g.step()
         self.last_output = fake
-        return losses * torch.tensor([1.0, 1.0, 1.0, 100.0], device=dev)
+        return losses
 
 
 class Model:

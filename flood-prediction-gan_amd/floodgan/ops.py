@@ -381,7 +381,8 @@ def conv_win(prob, tag=None):
     _wrote(prob["y"][0])
 
 
-WIN_WGRAD_SPLITS = 146   # x 7 kernel rows = ~1024 workgroups of 4 waves (several resident per CU)
+WIN_WGRAD_SPLITS = 144   # x 7 kernel rows = 1008 workgroups of 4 waves (several resident per CU); a multiple of 8:
+#                          the 7 workgroups of a split then share an XCD (conv_wgrad_win.hip)
 
 
 def wgrad_win_eligible(prob):
@@ -722,12 +723,13 @@ def mse_const(p, target, gscale, loss_out, g=None):
                                 L.ptr(g), L.ptr(work), L.stream_handle()), "mse")
 
 
-def l1(a, b, gscale, loss_out, g=None, accumulate=False):
-    """loss_out[0] = mean|a - b| over [N,C,H,W]; g (contiguous NCHW) = gscale * dL/da"""
+def l1(a, b, gscale, loss_out, g=None, accumulate=False, loss_scale=1.0):
+    """loss_out[0] = loss_scale * mean|a - b| over [N,C,H,W]; g (contiguous NCHW) = gscale * dL/da"""
     N, Cc, H, W = a.shape
     work = torch.empty(1024, dtype=torch.float64, device=a.device)
     _wrote(g)
-    L.check(_lib().fg_l1(sview(a), sview(b), N, Cc, H, W, C.c_float(gscale), L.ptr(loss_out), L.ptr(g),
+    L.check(_lib().fg_l1(sview(a), sview(b), N, Cc, H, W, C.c_float(gscale), C.c_float(loss_scale), L.ptr(loss_out),
+                         L.ptr(g),
                          int(accumulate), L.ptr(work), L.stream_handle()), "l1")
 
 

@@ -386,9 +386,10 @@ int fg_tanh_head_bwd(fg_view logits, int c, fg_sview g_out, fg_view g_logits, hi
 /* loss[0] = mean((p - target)^2);  g (optional) = gscale * 2 (p - target) / n */
 int fg_mse_const(const float* p, long long n, float target, float gscale, float* loss,
                  float* g, double* work, hipStream_t stream);
-/* loss[0] = mean(|a - b|) over [N,C,H,W] strided views; g (optional, NCHW contiguous)
+/* loss[0] = loss_scale * mean(|a - b|) over [N,C,H,W] strided views (the mean rounded to fp32 first, then
+ * scaled in fp32: the reference logs 100 * L1, models/model.py:643-651); g (optional, NCHW contiguous)
  * = gscale * sign(a - b) / n  (or += when accumulate). */
-int fg_l1(fg_sview a, fg_sview b, int N, int C, int H, int W, float gscale, float* loss,
+int fg_l1(fg_sview a, fg_sview b, int N, int C, int H, int W, float gscale, float loss_scale, float* loss,
           float* g, int accumulate, double* work, hipStream_t stream);
 
 /* ---------------------------------------------------------------------------------------- */

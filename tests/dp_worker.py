@@ -65,12 +65,19 @@ def main():
         import random
         for pool in (m.cycle_step_fn.pre_pool, m.cycle_step_fn.post_pool):
             pool.rng = random.Random(5)
+    record = kind == "paired" and os.environ.get("FG_RECORD_DECISIONS") == "1"
+    if record:                     # the activation decisions of this rank's passes (teacher forcing, test only)
+        m.step_fn.record_decisions = True
     losses = run(m, kind, xs, ys, 1)
     grads0 = grads(m, kind)
+    dec = m.step_fn.decisions if record else None
     losses += run(m, kind, xs, ys, iters - 1)
     torch.cuda.synchronize()
     state = {f"{net}/{k}": v.detach().cpu() for net, mod in nets(m, kind).items() for k, v in mod.state_dict().items()}
-    torch.save({"losses": torch.stack(losses), "state": state, "grads0": grads0}, f"{out}.rank{rank}")
+    out_d = {"losses": torch.stack(losses), "state": state, "grads0": grads0}
+    if dec is not None:
+        out_d["decisions"] = dec
+    torch.save(out_d, f"{out}.rank{rank}")
     dist.barrier()
     dist.destroy_process_group()
 

@@ -184,3 +184,66 @@ def test_model_builds_its_loaders_like_train_py(tmp_path, monkeypatch):
         assert np.allclose(m.all_losses["all_" + k], means[k], rtol=1e-6, atol=0), (k, m.all_losses["all_" + k], means[k])
     for (k, a), (_, b) in zip(m.generator.named_parameters(), ref.generator.named_parameters()):
         assert torch.equal(a, b), k
+
+
+def test_configs4_attentiongan_crop4_256_tiles_vs_reference(tmp_path, report):
+    """BASELINE.json configs[4] at its tile shape: the reference's README recipe --resize=512 --crop=4
+    (models/utils.py:41-56) gives 256x256 quadrant tiles; AttentionGAN's train_cycle (models/model.py:660-758)
+    fed by the staged TileLoader at batch 8.  Every loader batch equals the reference's per-item pipeline
+    (fliplr version, Resize(512, bicubic, antialias), quadrant, Normalize; 1e-5), and the eight iteration-0
+    losses of the fused cycle step on the first batch (all evaluated before any update) equal the fp32
+    oracle's on that same batch (1e-5, as test_cycle_p1_losses_512)."""
+    import torch.nn.functional as F
+
+    from floodgan.data import create_flood_dataset
+    from floodgan.model import Model
+    from oracle import attention_cycle as OC
+    from oracle import paired_attention as O
+    root = str(tmp_path)
+    arrays = _dataset_dir(root, n_img=3, h=640)           # raw tiles larger than the resize (downscaling taps)
+    train, _, _ = create_flood_dataset("hurricane-harvey", "same", root, "all", resize=512, crop=4, batch_size=8,
+                                       csv_path=os.path.join(root, "metadata", "dataset_split.csv"))
+    ds = train.ds
+    assert len(ds) == 16 and len(train) == 2                # (3 + 1 flipped) x 4 quadrants
+    from torch.utils.data import DataLoader
+    torch.manual_seed(1)                                    # models/model.py:676
+    order = [int(i) for b in DataLoader(range(len(ds)), batch_size=1, shuffle=True) for i in b]
+    torch.manual_seed(1)
+    batches = []
+    for xb, yb, names in train:
+        assert xb.shape == (8, 9, 256, 256) and yb.shape == (8, 3, 256, 256)
+        batches.append((xb, yb, names))
+    worst = 0.0
+    for bi, (xb, yb, names) in enumerate(batches):
+        for k, name in enumerate(names):
+            _, _, flip, ci, want = ds.item(order[bi * 8 + k])     # the original and flipped versions share a name
+            assert name == want
+            x, y = arrays[name[:len("hurricane-harvey_00000000")]]
+            rx, ry = reference_item(x, y, flip, "all", 512, 4, ci)
+            worst = max(worst, float((xb[k].cpu() - rx).abs().max()), float((yb[k].cpu() - ry).abs().max()))
+    assert worst < TOL, worst
+    # iteration-0 losses of the cycle step on the first batch vs the fp32 oracle's forwards
+    x, y = batches[0][0], batches[0][1]
+    m = Model(model="AttentionGAN", num_epochs=2, topography="all")
+    losses = m.cycle_step_fn(x, y).cpu().numpy().astype(np.float64)
+    xc, yc = x.cpu().contiguous(), y.cpu().contiguous()
+    P = OC.init_cycle_params(model="attentiongan")
+    D = O.discriminator_forward
+    cond = xc[:, 3:]
+    with torch.no_grad():
+        def gen(p, t):
+            return O.generator_forward(p, t)[0]
+        post_real = torch.cat((yc, cond), 1)
+        sp = torch.cat((gen(P["pre_to_post"], xc), cond), 1)
+        spre = torch.cat((gen(P["post_to_pre"], post_real), cond), 1)
+        rp = gen(P["pre_to_post"], spre)
+        rq = gen(P["post_to_pre"], sp)
+
+        def mse(p, t):
+            return float(F.mse_loss(p, torch.full_like(p, t)))
+        ref = np.array([mse(D(P["post_d"], sp), 1), mse(D(P["pre_d"], spre), 1), 10 * float(F.l1_loss(rq, xc[:, :3])),
+                        10 * float(F.l1_loss(rp, yc)), mse(D(P["pre_d"], xc), 1), mse(D(P["post_d"], post_real), 1),
+                        mse(D(P["pre_d"], spre), 0), mse(D(P["post_d"], sp), 0)])
+    lrel = np.abs(losses - ref) / np.abs(ref)
+    report("configs4_attentiongan_crop4_256", loader_vs_reference_items=worst, loss_rel=lrel.tolist())
+    assert lrel.max() < 1e-5, lrel

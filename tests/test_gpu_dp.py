@@ -117,3 +117,48 @@ def test_two_rank_step_equals_single_rank(kind, n, res, tmp_path, report):
     # after updates: the iteration-0 gradients agree to summation order (above), so only elements whose
     # gradient is at rounding level can take a different Adam direction -- the P3 bound
     assert lrel.max() < 1e-3 and worst[1] < 1e-3, (lrel, worst)
+
+
+def test_two_rank_paired_f16x3_vs_fp64(tmp_path, report):
+    """The production DP path: the default f16x3 conv math, two ranks each on half of a global batch of 4
+    (64x64), bucketed asynchronous SUM all-reduces.  Iteration 0's all-reduced G and D gradients equal the fp64
+    oracle's whole-batch gradients (models/model.py:611-646) with the two ranks' activation decisions
+    teacher-forced (the per-rank operand scales differ from a whole batch's by powers of two, so kink
+    decisions may differ from any other evaluation): 1e-4 as P2, every differing decision at its kink, and the
+    replicas identical after the update."""
+    out = str(tmp_path / "dp")
+    port = _free_port()
+    env = dict(os.environ, WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), OMP_NUM_THREADS="2",
+               FG_RECORD_DECISIONS="1")
+    env.pop("FLOODGAN_CONV_MATH", None)
+    n, res = 4, 64
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dp_worker.py"), out, "paired", str(n), str(res),
+                               "1"], env=dict(env, RANK=str(r), LOCAL_RANK=str(r))) for r in range(2)]
+    try:
+        rcs = [p.wait(timeout=240) for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert rcs == [0, 0], rcs
+    ranks = [torch.load(f"{out}.rank{r}", weights_only=True) for r in range(2)]
+    for k, v in ranks[0]["state"].items():
+        assert torch.equal(v, ranks[1]["state"][k]), k              # replicas stay identical
+    merged = {net: [{k: torch.cat((a[k], b[k]), 0) for k in a} for a, b in zip(ranks[0]["decisions"][net],
+                                                                             ranks[1]["decisions"][net])]
+              for net in ("G", "D")}
+    dec = O.ActDecisions(merged)
+    x, y = W.global_batch("paired", n, res)
+    st = O.PairedStepOracle(dtype=torch.float64)
+    rec = {}
+    d_after = {k.split("/", 1)[1]: v for k, v in ranks[0]["state"].items() if k.startswith("discriminator/")}
+    st.step(x, y, record=rec, d_after=d_after, decisions=dec)
+    skip_g, skip_d = O.cancelled_biases()
+    eg = max(((k, nrel(ranks[0]["grads0"]["generator/" + k], v)) for k, v in rec["g_grads"].items()
+              if k not in skip_g), key=lambda t: t[1])
+    ed = max(((k, nrel(ranks[0]["grads0"]["discriminator/" + k], v)) for k, v in rec["d_grads"].items()
+              if k not in skip_d), key=lambda t: t[1])
+    report("dp_two_rank_f16x3_vs_fp64", n=n, res=res, worst_G=eg, worst_D=ed,
+           decisions_differing=sum(c for _, _, c, _ in dec.log), worst_kink=dec.worst())
+    assert eg[1] < 1e-4 and ed[1] < 1e-4, (eg, ed)
+    assert dec.worst() < 1e-4, dec.worst()

@@ -565,6 +565,9 @@ def test_losses_and_adam():
     ref = F.l1_loss(ar, b.double())
     (gr,) = torch.autograd.grad(ref * 100, ar)
     assert abs(float(loss) - float(ref)) < 1e-6 and nrel(gl, gr) < 1e-6
+    l1v = float(loss)
+    ops.l1(a.to(DEV), b.to(DEV), 100.0, loss, gl, loss_scale=100.0)      # the logged 100 * L1, scaled in fp32
+    assert float(loss) == float(torch.tensor(l1v, dtype=torch.float32) * 100.0)
     # Adam against torch.optim.Adam on the CPU (the oracle's optimiser), 3 steps
     from floodgan.optim import FusedAdam
     w0 = torch.randn(1000) * 0.02
