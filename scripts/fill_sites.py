@@ -31,12 +31,11 @@ def main():
     for ev in prof.events():
         if not ev.name.startswith("aten::") or ev.device_type != torch.autograd.DeviceType.CPU:
             continue
-        if not any(k.device_type == torch.autograd.DeviceType.CUDA for k in ev.kernels):
-            continue
         frames = [f for f in (ev.stack or []) if "floodgan" in f or "bench" in f]
-        sites[(ev.name, frames[0] if frames else "?")] += 1
-    for (name, frame), c in sites.most_common(60):
-        print(f"{c:5d}  {name:28s} {frame}")
+        sites[(ev.name, bool(ev.kernels), frames[0] if frames else "?")] += 1
+    print("count  op  launched-a-kernel  innermost floodgan frame")
+    for (name, k, frame), c in sites.most_common(80):
+        print(f"{c:5d}  {name:28s} {'K' if k else '-'} {frame}")
 
 
 if __name__ == "__main__":
