@@ -97,8 +97,7 @@ __device__ __forceinline__ void wait_vmcnt() {
 // first MFMAs need only the cheap h half of the split and the l half overlaps them; 2 = as 1, with
 // the B fragments double-buffered in 2-block groups, pinned (group g+1 is read while group g's
 // products run; group 0 is read together with A, ahead of the DMA issue); 3 = as 1, with the
-// next stage's LDS-DMA pieces spread between the column groups instead of one burst; 7 = a rolling
-// ring of B fragments (compute7).
+// next stage's LDS-DMA pieces spread between the column groups instead of one burst.
 template <int BM, int BN, int WM, int WN, int NS, int SCH, bool STATS = false>
 __global__ void __launch_bounds__((BM / WM) * (BN / WN) * 64, 1)
 conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
@@ -225,11 +224,8 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
     // ~60 issue cycles among MFMAs but 100-185 in a burst beside the fragment reads)
     int p_koff = 0, p_soffb = 0, p_buf = 0;   // p_buf: byte offset of the target stage in smem
     bool p_on = false;
-    const __amdgpu_buffer_rsrc_t xr_off = __builtin_amdgcn_make_buffer_rsrc((void*)batch.p[0].x, 0, 0, 0x00020000);
-    const __amdgpu_buffer_rsrc_t wr_off = xr_off;
     auto issue_prep = [&](int buf) {
         p_on = it < total_tiles;
-        p_buf = buf * STAGE;
         if (!p_on) return;
         const int r = irev ? i_kh - 1 - ir : ir;
         const int jb = is * i_c + ic * 32;
@@ -247,26 +243,6 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
             dma_piece(smem + __builtin_amdgcn_readfirstlane(p_buf + (wave * A_GL + i) * 1024), xr, a_off[i], p_koff);
         else
             dma_piece(smem + __builtin_amdgcn_readfirstlane(p_buf + A_BYTES + (wave * B_GL + (i - A_GL)) * 1024), wr,
-                      b_off[i - A_GL], p_soffb);
-    };
-    // SCH 7: issue_prep without a branch (past the end of the stream the offsets are unused)
-    auto issue_prep7 = [&](int buf) {
-        p_on = it < total_tiles;
-        p_buf = buf * STAGE;
-        const int r = irev ? i_kh - 1 - ir : ir;
-        const int jb = is * i_c + ic * 32;
-        p_koff = __builtin_amdgcn_readfirstlane((r * i_sxr + jb) * 4);
-        p_soffb = __builtin_amdgcn_readfirstlane((r * (i_jp / 32) + jb / 32) * 128);
-    };
-    // SCH 7: the same piece without a branch (a branch ends the scheduling region, so the column steps
-    // around it could not be interleaved): past the end of the stream the piece reads through an empty
-    // buffer resource (num_records 0: no memory access, zeros) into the ring buffer nobody reads again
-    auto issue_piece_nb = [&](int i) {
-        const __amdgpu_buffer_rsrc_t ra = p_on ? xr : xr_off, rb = p_on ? wr : wr_off;
-        if (i < A_GL)
-            dma_piece(smem + __builtin_amdgcn_readfirstlane(p_buf + (wave * A_GL + i) * 1024), ra, a_off[i], p_koff);
-        else
-            dma_piece(smem + __builtin_amdgcn_readfirstlane(p_buf + A_BYTES + (wave * B_GL + (i - A_GL)) * 1024), rb,
                       b_off[i - A_GL], p_soffb);
     };
     auto issue_advance = [&]() {
@@ -383,61 +359,6 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
                     for (int t = 0; t < TG; ++t)
                         acc[tm][t0 + t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[tm], bh[t], acc[tm][t0 + t], 0, 0, 0);
             }
-        }
-    };
-
-    // SCH 7: B fragments as a rolling ring of RB column blocks.  The stage walks its column blocks in
-    // steps of two; a block's slot is refilled (the block RB further on) as soon as its three products
-    // are issued, so every read has RB/2 - 1 steps of MFMAs (12 per step per wave) to land instead of
-    // being read just before its group as in SCH 3.  Per accumulator the products still run hh, hl, lh
-    // (bit-identical to SCH 1-5); sched_barriers pin the step boundaries, and the stage's DMA pieces
-    // go one or two per step (branch-free, issue_piece_nb).
-    constexpr int RB = SCH == 8 ? (TN < 6 ? TN : 6) : (TN < 4 ? TN : 4);   // 8: a 6-block ring
-    constexpr int SU = TN < 2 ? TN : 2;                  // column blocks per step
-    constexpr int NSTEP = TN / SU;
-    constexpr int NP7 = A_GL + B_GL, PPS = (NP7 + NSTEP - 1) / NSTEP;
-    static_assert(TN % SU == 0 && RB % SU == 0, "rolling ring shape");
-    auto read_b = [&](const char* sbuf, int t, f16x8& bh, f16x8& bl) {
-        const char* rowp = sbuf + A_BYTES + (wn * WN + t * 16 + fr) * 64 + b_c;
-        bh = *reinterpret_cast<const f16x8*>(rowp);
-        bl = *reinterpret_cast<const f16x8*>(rowp + BN * 64);
-    };
-    auto compute7 = [&](int buf, const f32x4 (&va)[TM][2], f16x8 (&bh)[RB], f16x8 (&bl)[RB]) {
-        const char* sbuf = smem + buf * STAGE;
-        f16x8 ah[TM], al[TM];
-#pragma unroll
-        for (int tm = 0; tm < TM; ++tm) {
-            const float v[8] = {va[tm][0][0], va[tm][0][1], va[tm][0][2], va[tm][0][3],
-                                va[tm][1][0], va[tm][1][1], va[tm][1][2], va[tm][1][3]};
-            split_scalar(v, sa, ah[tm], al[tm]);
-        }
-#pragma unroll
-        for (int st = 0; st < NSTEP; ++st) {
-            const int t0 = st * SU;
-#pragma unroll
-            for (int u = 0; u < SU; ++u)
-#pragma unroll
-                for (int tm = 0; tm < TM; ++tm)
-                    acc[tm][t0 + u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[tm], bh[(t0 + u) % RB], acc[tm][t0 + u],
-                                                                             0, 0, 0);
-#pragma unroll
-            for (int u = 0; u < SU; ++u)
-#pragma unroll
-                for (int tm = 0; tm < TM; ++tm)
-                    acc[tm][t0 + u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[tm], bl[(t0 + u) % RB], acc[tm][t0 + u],
-                                                                             0, 0, 0);
-#pragma unroll
-            for (int u = 0; u < SU; ++u)
-#pragma unroll
-                for (int tm = 0; tm < TM; ++tm)
-                    acc[tm][t0 + u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[tm], bh[(t0 + u) % RB], acc[tm][t0 + u],
-                                                                             0, 0, 0);
-#pragma unroll
-            for (int u = 0; u < SU; ++u)
-                if (t0 + u + RB < TN) read_b(sbuf, t0 + u + RB, bh[(t0 + u) % RB], bl[(t0 + u) % RB]);
-#pragma unroll
-            for (int i = st * PPS; i < (st + 1) * PPS && i < NP7; ++i) issue_piece_nb(i);
-            __builtin_amdgcn_sched_barrier(0);
         }
     };
 
@@ -609,6 +530,9 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
     while (true) {
         if (NS == 3 && issued - done >= 2) wait_vmcnt<NS == 3 ? A_GL + B_GL : 0>();
         else wait_vmcnt<0>();
+#ifdef FG_F3_DIAG
+        if (!((alt_order >> 7) & 1))                     // diag bit 3: no barrier (timing only)
+#endif
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
         f32x4 va[TM][2];
@@ -625,16 +549,6 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
             load_a(cur, va);
             if (issue_next(nxt)) ++issued;
             compute(cur, va);
-        } else if constexpr (SCH == 7 || SCH == 8) {
-            // the A fragments and the first RB column blocks of B are read together, ahead of everything
-            f16x8 bh[RB], bl[RB];
-            load_a(cur, va);
-#pragma unroll
-            for (int s = 0; s < RB; ++s) read_b(smem + cur * STAGE, s, bh[s], bl[s]);
-            __builtin_amdgcn_sched_barrier(0);     // (the scheduler would sink the B reads below the A split)
-            issue_prep7(nxt);
-            compute7(cur, va, bh, bl);
-            if (issue_advance()) ++issued;
         } else if constexpr (SCH >= 3) {
             load_a(cur, va);
             issue_prep(nxt);
@@ -713,26 +627,13 @@ int launch_cfg(const ConvBatch& in, int nprob, hipStream_t stream) {
     // the launches without statistics keep the plain epilogue's code
     if constexpr (WM == 32) {
         if (stats) {
-            if (sched == 7)
-                hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 7, true>), dim3(grid), dim3(NT), 0, stream,
-                                   b, total, g_f3_alt);
-            else if (sched == 8)
-                hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 8, true>), dim3(grid), dim3(NT), 0, stream,
-                                   b, total, g_f3_alt);
-            else
-                hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 3, true>), dim3(grid), dim3(NT), 0, stream,
-                                   b, total, g_f3_alt);
+            hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 3, true>), dim3(grid), dim3(NT), 0, stream, b,
+                               total, g_f3_alt);
             return fg::launched("conv_fwd_f3");
         }
     }
     if (stats) return fg::fail(FG_ERR_INVALID, "conv_fwd_f3: epilogue statistics need a WM = 32 tile");
-    if (sched == 7)
-        hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 7>), dim3(grid), dim3(NT), 0, stream, b, total,
-                           g_f3_alt);
-    else if (sched == 8)
-        hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 8>), dim3(grid), dim3(NT), 0, stream, b, total,
-                           g_f3_alt);
-    else if (sched == 5)
+    if (sched == 5)
         hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 5>), dim3(grid), dim3(NT), 0, stream, b, total,
                            g_f3_alt);
     else if (sched == 4)
@@ -853,7 +754,7 @@ FG_API int fg_set_f3_persistent(int on) {
 }
 
 FG_API int fg_set_f3_sched(int sched) {
-    if (sched < -1 || sched > 8 || sched == 6) return fg::fail(FG_ERR_INVALID, "fg_set_f3_sched: %d", sched);
+    if (sched < -1 || sched > 5) return fg::fail(FG_ERR_INVALID, "fg_set_f3_sched: %d", sched);
     g_f3_sched = sched;
     return 0;
 }

@@ -1,8 +1,9 @@
 """Timing diagnosis of the pipelined forward kernel (needs a library built with -DFG_F3_DIAG, see
 scripts/gpu_diag.sh; the outputs of modes 1/2 are garbage): per geometry, the time of the full
 kernel (mode 0), of its compute alone (mode 1: no data movement after the first stages) and of
-its data movement alone (mode 2: DMA + barriers, no MFMA work).
-  python scripts/diag_f3.py"""
+its data movement alone (mode 2: DMA + barriers, no MFMA work); 4/5 without the A split, 9/13 as 1/5
+without the per-stage barrier.
+  python scripts/diag_f3.py [modes, default 0,1,2,4,5]"""
 import os
 import sys
 
@@ -13,6 +14,11 @@ sys.path.insert(0, os.path.join(ROOT, "scripts"))
 
 from floodgan import _lib as L, ops  # noqa: E402
 from bench_conv import make, time_it  # noqa: E402
+
+
+TAGS = {0: "full", 1: "compute only", 2: "data movement only", 4: "no A split", 5: "compute only, no A split",
+        9: "compute only, no barrier", 13: "compute, no split, no barrier"}
+MODES = [int(v) for v in sys.argv[1].split(",")] if len(sys.argv) > 1 else [0, 1, 2, 4, 5]
 
 
 def main():
@@ -27,12 +33,13 @@ def main():
         prob = mk(True)
         res = {}
         for _ in range(3):
-            for mode in (0, 1, 2, 4, 5):
+            for mode in MODES:
                 os.environ["FG_F3_DIAG"] = str(mode)
                 res.setdefault(mode, []).append(time_it(lambda: ops.conv([prob])))
         os.environ["FG_F3_DIAG"] = "0"
-        for mode, tag in ((0, "full"), (1, "compute only"), (2, "data movement only"), (4, "no A split"),
-                          (5, "compute only, no A split")):
+        for mode, tag in TAGS.items():
+            if mode not in MODES:
+                continue
             ms = min(res[mode])
             print(f"{name:36s} {tag:20s} {ms:8.3f} ms {flops / ms / 1e9:7.1f} TFLOP/s", flush=True)
 

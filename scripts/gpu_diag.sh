@@ -18,5 +18,5 @@ EOF
   exit $?
 fi
 mkdir -p gpurun_out
-FLOODGAN_LIB=$PWD/$DIAG/libfloodgan.so timeout -k 10 300 python -u scripts/diag_f3.py > gpurun_out/diag_f3.log 2>&1
+FLOODGAN_LIB=$PWD/$DIAG/libfloodgan.so timeout -k 10 300 python -u scripts/diag_f3.py "$@" > gpurun_out/diag_f3.log 2>&1
 rc=$?; cat gpurun_out/diag_f3.log; exit $rc
