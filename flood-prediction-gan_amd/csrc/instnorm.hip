@@ -165,6 +165,65 @@ __global__ void in_apply_kernel(fg_view src, const float* __restrict__ mean, con
     if (amax) absmax_flush(am, amax);
 }
 
+// Row form of the apply pass (channel quads dividing the block: C/4 | 256): block = one padded output
+// row (n, yp), thread = (pixel lane gi, channel quad c4); mean / rstd read once per thread, U pixels'
+// loads issued before any of them is used (the grid-stride form above re-derived (n, y, x, c) with
+// 64-bit divisions per element and held one load in flight: 5.0 TB/s).
+constexpr int kRowU = 4;
+
+__global__ void __launch_bounds__(NT) in_apply_rows_kernel(fg_view src, const float* __restrict__ mean,
+                                                           const float* __restrict__ rstd, int act, fg_view res,
+                                                           fg_view dst, int pad_mode, int lshift,
+                                                           unsigned* __restrict__ amax) {
+    const int L = 1 << lshift, PG = NT >> lshift;
+    const int C = dst.c_alloc, h = dst.h, w = dst.w, pad = dst.pad;
+    const int hp = h + 2 * pad, wp = w + 2 * pad;
+    const int n = blockIdx.x / hp, yp = blockIdx.x - n * hp;
+    const int gi = threadIdx.x >> lshift, c4 = threadIdx.x & (L - 1);
+    float* drow = dst.ptr + (size_t)(n * hp + yp) * wp * C + 4 * c4;
+    unsigned am = 0;
+    int y = yp - pad;
+    const bool reflect = pad_mode == FG_PAD_REFLECT;
+    if ((y < 0 || y >= h) && !reflect) {
+        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+        for (int xp = gi; xp < wp; xp += PG) *reinterpret_cast<f32x4*>(drow + (size_t)xp * C) = z;
+    } else {
+        y = fg::reflect_idx(y, h);
+        const f32x4 m = ld4(mean + (size_t)n * C + 4 * c4), r = ld4(rstd + (size_t)n * C + 4 * c4);
+        const float* srow = src.ptr + fg::vidx(src, n, y, 0) + 4 * c4;
+        const float* rrow = res.ptr ? res.ptr + fg::vidx(res, n, y, 0) + 4 * c4 : nullptr;
+        for (int xp0 = gi; xp0 < wp; xp0 += kRowU * PG) {
+            f32x4 v[kRowU], rv[kRowU];
+            bool ok[kRowU];
+#pragma unroll
+            for (int k = 0; k < kRowU; ++k) {
+                const int xp = xp0 + k * PG;
+                int x = xp - pad;
+                const bool inside = x >= 0 && x < w;
+                ok[k] = xp < wp && (inside || reflect);
+                x = ok[k] ? fg::reflect_idx(x, w) : 0;
+                v[k] = ok[k] ? ld4(srow + (size_t)x * C) : f32x4{0.f, 0.f, 0.f, 0.f};
+                rv[k] = (ok[k] && rrow) ? ld4(rrow + (size_t)x * C) : f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+#pragma unroll
+            for (int k = 0; k < kRowU; ++k) {
+                const int xp = xp0 + k * PG;
+                if (xp >= wp) break;
+                f32x4 o = {0.f, 0.f, 0.f, 0.f};
+                if (ok[k]) {
+                    o = (v[k] - m) * r;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) o[e] = fg::act_fwd(o[e], act);
+                    o += rv[k];
+                }
+                am = max(am, absbits4(o));
+                *reinterpret_cast<f32x4*>(drow + (size_t)xp * C) = o;
+            }
+        }
+    }
+    if (amax) absmax_flush(am, amax);
+}
+
 // ---- backward ----
 
 __device__ __forceinline__ int fold_src(int y, int h, int p, int* out) {
@@ -188,6 +247,96 @@ __device__ __forceinline__ f32x4 load_grad(const fg_view& g, int fp, const fg_vi
     }
     if (gadd.ptr) v += ld4(gadd.ptr + fg::vidx(gadd, n, y, x) + 4 * c4);
     return v;
+}
+
+// every fold term of interior pixel (y, x) except the main one (y + fp, x + fp): the reflect-pad adjoint's
+// extra terms, nonzero only within fp + 1 of the border
+__device__ __forceinline__ bool fold_border(int y, int x, int h, int w, int fp) {
+    return fp > 0 && (y <= fp || y >= h - 1 - fp || x <= fp || x >= w - 1 - fp);
+}
+// (added to v = the main term in load_grad's order: bit-identical sums)
+__device__ __forceinline__ f32x4 fold_extra(f32x4 v, const fg_view& g, int fp, int n, int y, int x, int h, int w,
+                                            int c4) {
+    int ys[3], xs[3];
+    const int ny = fold_src(y, h, fp, ys), nx = fold_src(x, w, fp, xs);
+    for (int iy = 0; iy < ny; ++iy)
+        for (int ix = 0; ix < nx; ++ix)
+            if (iy | ix) v += ld4(g.ptr + fg::vidx(g, n, ys[iy], xs[ix]) + 4 * c4);
+    return v;
+}
+
+// statistics pass with kRowU pixels' loads in flight per thread (same chunking / work layout and the same
+// fp32 accumulation order per thread as in_bwd_stats_kernel: results are bit-identical)
+__global__ void __launch_bounds__(NT) in_bwd_stats_u_kernel(fg_view g, int fp, fg_view gadd, fg_view src,
+                                                            const float* __restrict__ mean,
+                                                            const float* __restrict__ rstd, int act, int chunks,
+                                                            double* __restrict__ work, fg_view gsum) {
+    const int C = src.c_alloc, L = C / 4, PG = NT / L;
+    const int n = blockIdx.y, chunk = blockIdx.x;
+    const int h = src.h, w = src.w, HW = h * w;
+    const int per = (HW + chunks - 1) / chunks;
+    const int p0 = chunk * per, p1 = min(HW, p0 + per);
+    const int gi = threadIdx.x / L, c4 = threadIdx.x - (threadIdx.x / L) * L;
+    __shared__ double red[NT][12];
+    f32x4 sg = {0.f, 0.f, 0.f, 0.f}, sgx = sg, sx = sg;
+    if (gi < PG) {
+        const f32x4 m = ld4(mean + (size_t)n * C + 4 * c4);
+        const f32x4 r = ld4(rstd + (size_t)n * C + 4 * c4);
+        int y = (p0 + gi) / w, x = (p0 + gi) - ((p0 + gi) / w) * w;
+        for (int p = p0 + gi; p < p1; p += kRowU * PG) {
+            int ys[kRowU], xs[kRowU];
+            f32x4 sv[kRowU], gv[kRowU], av[kRowU];
+#pragma unroll
+            for (int k = 0; k < kRowU; ++k) {
+                ys[k] = y;
+                xs[k] = x;
+                const bool ok = p + k * PG < p1;
+                sv[k] = ok ? ld4(src.ptr + fg::vidx(src, n, y, x) + 4 * c4) : f32x4{0.f, 0.f, 0.f, 0.f};
+                gv[k] = ok ? ld4(g.ptr + fg::vidx(g, n, y + fp, x + fp) + 4 * c4) : f32x4{0.f, 0.f, 0.f, 0.f};
+                av[k] = (ok && gadd.ptr) ? ld4(gadd.ptr + fg::vidx(gadd, n, y, x) + 4 * c4)
+                                         : f32x4{0.f, 0.f, 0.f, 0.f};
+                x += PG;
+                while (x >= w) {
+                    x -= w;
+                    ++y;
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < kRowU; ++k) {
+                if (p + k * PG >= p1) break;
+                f32x4 gk = gv[k];
+                if (fold_border(ys[k], xs[k], h, w, fp)) gk = fold_extra(gk, g, fp, n, ys[k], xs[k], h, w, c4);
+                gk += av[k];
+                if (gsum.ptr) *reinterpret_cast<f32x4*>(gsum.ptr + fg::vidx(gsum, n, ys[k], xs[k]) + 4 * c4) = gk;
+                const f32x4 xh = (sv[k] - m) * r;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) gk[e] *= fg::act_grad(xh[e], act);
+                sg += gk;
+                sgx += gk * xh;
+                sx += xh;
+            }
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        red[threadIdx.x][e] = sg[e];
+        red[threadIdx.x][4 + e] = sgx[e];
+        red[threadIdx.x][8 + e] = sx[e];
+    }
+    __syncthreads();
+    if (threadIdx.x < L) {
+        double a[12] = {0};
+        for (int gg = 0; gg < PG; ++gg)
+#pragma unroll
+            for (int e = 0; e < 12; ++e) a[e] += red[gg * L + threadIdx.x][e];
+        double* wk = work + ((size_t)(n * chunks + chunk) * C + 4 * threadIdx.x) * 3;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            wk[3 * e] = a[e];
+            wk[3 * e + 1] = a[4 + e];
+            wk[3 * e + 2] = a[8 + e];
+        }
+    }
 }
 
 __global__ void in_bwd_stats_kernel(fg_view g, int fp, fg_view gadd, fg_view src, const float* __restrict__ mean,
@@ -322,6 +471,75 @@ __global__ void in_bwd_apply_kernel(fg_view g, int fp, fg_view gadd, fg_view src
         }
         am = max(am, absbits4(out));
         *reinterpret_cast<f32x4*>(dst.ptr + ((size_t)(n * hp + yp) * wp + xp) * C + 4 * c4) = out;
+    }
+    if (amax) absmax_flush(am, amax);
+}
+
+// row form of the backward apply (C/4 | 256): block = one padded output row, kRowU pixels' loads in flight
+__global__ void __launch_bounds__(NT) in_bwd_apply_rows_kernel(fg_view g, int fp, fg_view gadd, fg_view src,
+                                                               const float* __restrict__ mean,
+                                                               const float* __restrict__ rstd,
+                                                               const float* __restrict__ coef, int act, fg_view dst,
+                                                               unsigned* __restrict__ amax,
+                                                               const double* __restrict__ bpart,
+                                                               float* __restrict__ bias_grad, int bias_accumulate,
+                                                               int lshift) {
+    if (bias_grad && blockIdx.x == 0) {
+        const int C = dst.c_alloc;
+        for (int c = threadIdx.x; c < C; c += blockDim.x) {
+            double s = 0;
+            for (int n = 0; n < dst.n; ++n) s += bpart[(size_t)n * C + c];
+            bias_grad[c] = bias_accumulate ? bias_grad[c] + (float)s : (float)s;
+        }
+    }
+    const int L = 1 << lshift, PG = NT >> lshift;
+    const int C = dst.c_alloc, h = dst.h, w = dst.w, pad = dst.pad;
+    const int hp = h + 2 * pad, wp = w + 2 * pad;
+    const int n = blockIdx.x / hp, yp = blockIdx.x - n * hp;
+    const int gi = threadIdx.x >> lshift, c4 = threadIdx.x & (L - 1);
+    float* drow = dst.ptr + (size_t)(n * hp + yp) * wp * C + 4 * c4;
+    unsigned am = 0;
+    const int y = yp - pad;
+    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+    if (y < 0 || y >= h) {
+        for (int xp = gi; xp < wp; xp += PG) *reinterpret_cast<f32x4*>(drow + (size_t)xp * C) = z;
+    } else {
+        const size_t nc = (size_t)n * C + 4 * c4;
+        const f32x4 m = ld4(mean + nc), r = ld4(rstd + nc);
+        const f32x4 k01 = ld4(coef + nc * 2), k23 = ld4(coef + nc * 2 + 4);
+        const f32x4 c1 = {k01[0], k01[2], k23[0], k23[2]}, c2 = {k01[1], k01[3], k23[1], k23[3]};
+        const float* srow = src.ptr + fg::vidx(src, n, y, 0) + 4 * c4;
+        const float* grow = g.ptr + fg::vidx(g, n, y + fp, fp) + 4 * c4;
+        const float* arow = gadd.ptr ? gadd.ptr + fg::vidx(gadd, n, y, 0) + 4 * c4 : nullptr;
+        for (int xp0 = gi; xp0 < wp; xp0 += kRowU * PG) {
+            f32x4 sv[kRowU], gv[kRowU], av[kRowU];
+            bool ok[kRowU];
+#pragma unroll
+            for (int k = 0; k < kRowU; ++k) {
+                const int x = xp0 + k * PG - pad;
+                ok[k] = x >= 0 && x < w;
+                sv[k] = ok[k] ? ld4(srow + (size_t)x * C) : z;
+                gv[k] = ok[k] ? ld4(grow + (size_t)x * C) : z;
+                av[k] = (ok[k] && arow) ? ld4(arow + (size_t)x * C) : z;
+            }
+#pragma unroll
+            for (int k = 0; k < kRowU; ++k) {
+                const int xp = xp0 + k * PG;
+                if (xp >= wp) break;
+                f32x4 out = z;
+                if (ok[k]) {
+                    const int x = xp - pad;
+                    f32x4 gk = gv[k];
+                    if (fold_border(y, x, h, w, fp)) gk = fold_extra(gk, g, fp, n, y, x, h, w, c4);
+                    gk += av[k];
+                    const f32x4 xh = (sv[k] - m) * r;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) out[e] = r[e] * (gk[e] * fg::act_grad(xh[e], act) - c1[e] - xh[e] * c2[e]);
+                }
+                am = max(am, absbits4(out));
+                *reinterpret_cast<f32x4*>(drow + (size_t)xp * C) = out;
+            }
+        }
     }
     if (amax) absmax_flush(am, amax);
 }
@@ -565,6 +783,21 @@ FG_API int fg_in_stats_partials(const float* partials, int nprob, int n_img, int
     return fg::launched("in_stats_partials");
 }
 
+namespace {
+int g_in_rows = 1;   // fg_set_in_rows (A/B hook): 1 = row / load-batched forms of the norm passes
+int ilog2(int v) {
+    int l = 0;
+    while ((1 << l) < v) ++l;
+    return l;
+}
+}  // namespace
+
+FG_API int fg_set_in_rows(int on) {
+    if (on < 0 || on > 1) return fg::fail(FG_ERR_INVALID, "fg_set_in_rows: %d", on);
+    g_in_rows = on;
+    return 0;
+}
+
 FG_API long long fg_in_workspace_doubles(int n, int c) { return (long long)n * c * (MAX_CHUNKS * 3 + 2) + 64; }
 // layout: [stats n*c*MAX_CHUNKS*3][coef n*c*2 floats = n*c doubles][bias partials n*c]
 
@@ -589,6 +822,12 @@ FG_API int fg_in_apply(fg_view src, const float* mean, const float* rstd, int ac
         return fg::fail(FG_ERR_INVALID, "fg_in_apply: residual shape");
     if (pad_mode == FG_PAD_REFLECT && (dst.pad >= dst.h || dst.pad >= dst.w))
         return fg::fail(FG_ERR_INVALID, "fg_in_apply: reflect pad too large");
+    const int C4 = dst.c_alloc / 4;
+    if (g_in_rows && NT % C4 == 0) {
+        hipLaunchKernelGGL(in_apply_rows_kernel, dim3(dst.n * (dst.h + 2 * dst.pad)), dim3(NT), 0, stream, src, mean,
+                           rstd, act, residual, dst, pad_mode, ilog2(C4), reinterpret_cast<unsigned*>(absmax));
+        return fg::launched("in_apply_rows");
+    }
     const long long total = (long long)dst.n * (dst.h + 2 * dst.pad) * (dst.w + 2 * dst.pad) * (dst.c_alloc / 4);
     hipLaunchKernelGGL(in_apply_kernel, dim3(fg::blocks_for(total, 256, 4096)), dim3(256), 0, stream, src, mean,
                        rstd, act, residual, dst, pad_mode, reinterpret_cast<unsigned*>(absmax));
@@ -613,8 +852,8 @@ FG_API int fg_in_bwd(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, cons
     const int chunks = choose_chunks(src.n, (long long)src.h * src.w);
     const int C = src.c_alloc;
     float* coef = reinterpret_cast<float*>(work + (size_t)src.n * C * MAX_CHUNKS * 3);
-    hipLaunchKernelGGL(in_bwd_stats_kernel, dim3(chunks, src.n), dim3(NT), 0, stream, gsrc, fold_pad, gadd, src,
-                       mean, rstd, act, chunks, work, gsum);
+    hipLaunchKernelGGL(g_in_rows ? in_bwd_stats_u_kernel : in_bwd_stats_kernel, dim3(chunks, src.n), dim3(NT), 0,
+                       stream, gsrc, fold_pad, gadd, src, mean, rstd, act, chunks, work, gsum);
     int e = fg::launched("in_bwd_stats");
     if (e) return e;
     double* bpart = work + (size_t)src.n * C * MAX_CHUNKS * 3 + (size_t)src.n * C;
@@ -625,6 +864,13 @@ FG_API int fg_in_bwd(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, cons
     const long long total = (long long)dst.n * (dst.h + 2 * dst.pad) * (dst.w + 2 * dst.pad) * (C / 4);
     // with gsum the apply pass reads the gathered gradient the statistics pass wrote (one read, no fold)
     const fg_view none = {nullptr, 0, 0, 0, 0, 0};
+    if (g_in_rows) {
+        hipLaunchKernelGGL(in_bwd_apply_rows_kernel, dim3(dst.n * (dst.h + 2 * dst.pad)), dim3(NT), 0, stream,
+                           gsum.ptr ? gsum : gsrc, gsum.ptr ? 0 : fold_pad, gsum.ptr ? none : gadd, src, mean, rstd,
+                           coef, act, dst, reinterpret_cast<unsigned*>(absmax), bpart, bias_grad, bias_accumulate,
+                           ilog2(C / 4));
+        return fg::launched("in_bwd_apply_rows");
+    }
     hipLaunchKernelGGL(in_bwd_apply_kernel, dim3(fg::blocks_for(total, 256, 4096)), dim3(256), 0, stream,
                        gsum.ptr ? gsum : gsrc, gsum.ptr ? 0 : fold_pad, gsum.ptr ? none : gadd, src, mean, rstd, coef,
                        act, dst, reinterpret_cast<unsigned*>(absmax), bpart, bias_grad, bias_accumulate);

@@ -186,6 +186,10 @@ int fg_set_f3_fill(int on);
  * transposed conv or of a stride-2 input gradient) interleaves their tiles (tile t -> problem t % count), so
  * the phases read each input row at the same time; 0 = problem after problem. */
 int fg_set_f3_interleave(int on);
+/* A/B hook of the InstanceNorm passes (instnorm.hip): 1 (default) = the apply / backward-apply passes one
+ * padded row per workgroup and the backward statistics with four pixels' loads in flight per thread
+ * (bit-identical results); 0 = the grid-stride forms. */
+int fg_set_in_rows(int on);
 /* A/B hook of the pipelined f16x3 weight-gradient kernel (conv_wgrad_f3.hip, n_a >= 128): 0 off,
  * 1 = staging as one burst per stage, 3 = staging slots interleaved with the MFMA groups,
  * 2 (default) = the measured choice per tile (interleaved for 128-row tiles). */

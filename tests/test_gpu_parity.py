@@ -438,6 +438,49 @@ def test_instnorm_fwd_bwd(act, fold, residual, C, gadd):
     assert abs(float(bias_g.sum())) < 1e-3
 
 
+@pytest.mark.parametrize("act,fold,residual,C,gadd,gsum,H,W", [
+    (1, 1, False, 256, True, True, 24, 20), (1, 1, False, 256, False, False, 17, 23),
+    (0, 0, True, 256, True, False, 16, 16), (2, 0, False, 64, False, False, 33, 9),
+    (1, 3, False, 32, True, True, 12, 15), (2, 1, False, 16, True, False, 11, 11),
+    (1, 1, True, 512, False, False, 8, 8), (0, 0, True, 128, True, False, 10, 14)])
+def test_instnorm_row_forms_bit_identical(act, fold, residual, C, gadd, gsum, H, W):
+    """The row / load-batched forms of the norm passes (fg_set_in_rows 1, the default) give bit-identical
+    outputs, gathered gradients, bias gradients and absmax slots to the grid-stride forms (0): ragged widths,
+    fold 0 / 1 / 3, residual, gadd, gsum, C = 16 ... 512"""
+    from floodgan import _lib as L, ops
+    from floodgan.plans import Buf
+    lib = L.load()
+    torch.manual_seed(11)
+    c = torch.randn(2, C, H, W, dtype=torch.float64) * 2 + 0.7
+    cb = buf_from(c, 0, "constant")
+    rb = buf_from(torch.randn(2, C, H, W, dtype=torch.float64), 0, "constant") if residual else None
+    gsrc = Buf(buf_from(torch.randn(2, C, H + 2 * fold, W + 2 * fold, dtype=torch.float64), 0, "constant").t,
+               2, H + 2 * fold, W + 2 * fold, C, 0)
+    gab = buf_from(torch.randn(2, C, H, W, dtype=torch.float64), 0, "constant") if gadd else None
+    mean, rstd = ops.in_stats(cb)
+    outs = []
+    try:
+        for rows in (0, 1):
+            assert lib.fg_set_in_rows(rows) == 0
+            pad = max(fold, 1)
+            out = Buf.empty(2, H, W, C, pad, DEV)
+            out.t.fill_(7.0)
+            ops.in_apply(cb, mean, rstd, act, rb, out, 1 if fold else 0)
+            gdst = Buf.empty(2, H, W, C, 1, DEV)
+            gdst.t.fill_(7.0)
+            gs = Buf.empty(2, H, W, C, 0, DEV) if gsum else None
+            bias_g = torch.full((C,), 3.0, device=DEV)
+            ops.in_bwd(gsrc, fold, gab, cb, mean, rstd, act, gdst, bias_g, bias_accumulate=True, gsum=gs)
+            torch.cuda.synchronize()
+            # absmax slots: sharded by workgroup, so only their max is compared
+            outs.append([out.t.clone(), out.t._fg_amax.max().clone(), gdst.t.clone(), gdst.t._fg_amax.max().clone(),
+                         bias_g.clone()] + ([gs.t.clone()] if gsum else []))
+    finally:
+        lib.fg_set_in_rows(1)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 FUSED_CASES = [("resblock 3x3 s1 256->256", 256, 256, 3, 1, 1, 32, False, 0.0),
                ("resblock, large mean", 256, 256, 3, 1, 1, 32, False, 40.0),
                ("conv2 3x3 s2 64->128", 64, 128, 3, 2, 1, 64, False, 0.0),
