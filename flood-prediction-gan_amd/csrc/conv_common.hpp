@@ -23,11 +23,35 @@ struct ConvBatch {
     int interleave;
 };
 
+// n / d for 0 <= n < 2^22, 1 <= d < 2^22 by a float reciprocal: |n*rcp(d) - n/d| < 2^22 * 2^-22.4 < 1, so
+// one correction step is exact (an integer division is a ~30-instruction VALU sequence; this is ~8)
+__device__ __forceinline__ int div_small(int n, int d) {
+    int q = (int)((float)n * __builtin_amdgcn_rcpf((float)d));
+    const int r = n - q * d;
+    q += r >= d ? 1 : (r < 0 ? -1 : 0);
+    return q;
+}
+
 __device__ __forceinline__ void decomp(int m, int mb, int mab, int& img, int& a, int& b) {
-    img = m / mab;
-    const int rem = m - img * mab;
-    a = rem / mb;
-    b = rem - a * mb;
+    if (m < (1 << 22) && mab < (1 << 22)) {
+        img = div_small(m, mab);
+        const int rem = m - img * mab;
+        a = div_small(rem, mb);
+        b = rem - a * mb;
+    } else {
+        img = m / mab;
+        const int rem = m - img * mab;
+        a = rem / mb;
+        b = rem - a * mb;
+    }
+}
+
+// the power-of-two scale s = 2^(14-e) of a bound m < 2^e (1 for 0 / non-finite): |v * s| < 2^14
+__device__ __forceinline__ float pow2_of(float m) {
+    if (!(m > 0.f) || !(m < 3.0e38f)) return 1.f;
+    int e;
+    frexpf(m, &e);                                        // m < 2^e
+    return ldexpf(1.f, 14 - e);
 }
 
 // power-of-two operand scale from an absmax slot (max over its FG_AMAX_SHARDS shards, one per
@@ -36,11 +60,7 @@ __device__ __forceinline__ float pow2_scale(const float* amax) {
     unsigned b = amax ? __float_as_uint(amax[threadIdx.x & (FG_AMAX_SHARDS - 1)]) & 0x7fffffffu : 0u;
 #pragma unroll
     for (int off = 1; off < FG_AMAX_SHARDS; off <<= 1) b = max(b, (unsigned)__shfl_xor((int)b, off));
-    const float m = __uint_as_float(b);
-    if (!(m > 0.f) || !(m < 3.0e38f)) return 1.f;
-    int e;
-    frexpf(m, &e);                                        // m < 2^e
-    return ldexpf(1.f, 14 - e);
+    return pow2_of(__uint_as_float(b));
 }
 
 // f16x3 split of 8 fp32 values: v*s = h + l, h = fp16(v*s), l = fp16(v*s - h)

@@ -98,7 +98,9 @@ __device__ __forceinline__ void wait_vmcnt() {
 // the B fragments double-buffered in 2-block groups, pinned (group g+1 is read while group g's
 // products run; group 0 is read together with A, ahead of the DMA issue); 3 = as 1, with the
 // next stage's LDS-DMA pieces spread between the column groups instead of one burst.
-template <int BM, int BN, int WM, int WN, int NS, int SCH, bool STATS = false>
+// PS: the A operand is in the FG_PRESPLIT format (include/floodgan.h: per 8 channels h[8] | l[8], written
+// by the norm pass that produced it) -- the two 16-B chunks a lane reads ARE its h and l fragments.
+template <int BM, int BN, int WM, int WN, int NS, int SCH, bool STATS = false, bool PS = false>
 __global__ void __launch_bounds__((BM / WM) * (BN / WN) * 64, 1)
 conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
     constexpr int NWN = BN / WN;
@@ -130,18 +132,20 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
     auto geo = [&](int t) {
         Geo q;
         int local;
+        // (tile counts stay far below 2^22: fgc::div_small is exact)
         if (batch.interleave) {
             // the count consecutive tiles of one local index are the count problems, rotated by the round
             // t / G so that every workgroup takes each problem in turn (the phases differ in K)
-            q.pi = (t % batch.count + t / G) % batch.count;
-            local = t / batch.count;
+            local = fgc::div_small(t, batch.count);
+            const int r = t - local * batch.count + fgc::div_small(t, G);
+            q.pi = r - fgc::div_small(r, batch.count) * batch.count;
         } else {
             q.pi = 0;
             while (q.pi + 1 < batch.count && t >= batch.blk_start[q.pi + 1]) ++q.pi;
             local = t - batch.blk_start[q.pi];
         }
         const int ntn = batch.ntiles_n[q.pi];
-        q.mt = local / ntn;
+        q.mt = fgc::div_small(local, ntn);
         q.m0 = q.mt * BM;
         q.n0 = (local - q.mt * ntn) * BN;
         q.nkt = batch.p[q.pi].kh * (batch.p[q.pi].jp / 32);
@@ -297,6 +301,13 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
     auto compute = [&](int buf, const f32x4 (&va)[TM][2]) {
         const char* sbuf = smem + buf * STAGE;
         f16x8 ah[TM], al[TM];
+        if constexpr (PS) {
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm) {
+                ah[tm] = __builtin_bit_cast(f16x8, va[tm][0]);
+                al[tm] = __builtin_bit_cast(f16x8, va[tm][1]);
+            }
+        } else
 #ifdef FG_F3_DIAG
         if ((alt_order >> 6) & 1) {                      // diag bit 2: no split (A bits reinterpreted)
 #pragma unroll
@@ -496,12 +507,20 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
         }
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm) {
+            // the lane's 4 consecutive rows: one decomposition, then (b, a, img) advanced with wrap-around
+            const int m0 = cg.m0 + wm * WM + tm * 16 + 4 * g;
+            int img, a, b;
+            fgc::decomp(min(m0, M - 1), P.m_b, mab, img, a, b);
 #pragma unroll
             for (int reg = 0; reg < 4; ++reg) {
-                const int m = cg.m0 + wm * WM + tm * 16 + 4 * g + reg;
+                if (reg) {
+                    if (++b == P.m_b) {
+                        b = 0;
+                        if (++a == P.m_a) { a = 0; ++img; }
+                    }
+                }
+                const int m = m0 + reg;
                 if (m >= M) continue;
-                int img, a, b;
-                fgc::decomp(m, P.m_b, mab, img, a, b);
                 float* yrow = P.y + img * P.syn + a * P.sya + b * P.syb;
 #pragma unroll
                 for (int tn = 0; tn < TN; ++tn) {
@@ -602,6 +621,7 @@ int launch_cfg(const ConvBatch& in, int nprob, hipStream_t stream) {
     b.blk_start[nprob] = total;
     b.blk_start[4] = total;
     if (total == 0) return 0;
+    if (total >= (1 << 22)) return fg::fail(FG_ERR_INVALID, "conv_fwd_f3: %d tiles (the tile walk assumes < 2^22)", total);
     // phase-interleaved tile order when every problem has the same tile count (the 4 phases of an even-sized
     // transposed conv / stride-2 input gradient): the phases gather the same input rows at the same time
     // persistent: as many workgroups as fit at once (LDS-limited), each looping over tiles
@@ -623,6 +643,20 @@ int launch_cfg(const ConvBatch& in, int nprob, hipStream_t stream) {
 #endif
     bool stats = false;
     for (int i = 0; i < nprob; ++i) stats |= b.p[i].in_stats != nullptr;
+    // pre-split A operands (every problem of the batch, checked by the caller): their own instantiations
+    // (WM = 32 configs, default order)
+    if (b.p[0].x_presplit) {
+        if constexpr (WM == 32) {
+            if (stats)
+                hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 3, true, true>), dim3(grid), dim3(NT), 0,
+                                   stream, b, total, g_f3_alt);
+            else
+                hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 3, false, true>), dim3(grid), dim3(NT), 0,
+                                   stream, b, total, g_f3_alt);
+            return fg::launched("conv_fwd_f3_presplit");
+        }
+        return fg::fail(FG_ERR_INVALID, "conv_fwd_f3: pre-split operands need a WM = 32 tile");
+    }
     // the epilogue-statistics variant is its own instantiation (WM = 32 configs, default order), so that
     // the launches without statistics keep the plain epilogue's code
     if constexpr (WM == 32) {
@@ -692,10 +726,21 @@ int auto_cfg(const fg_conv_problem* p, int nprob, int max_n) {
     return cfg;
 }
 
+// a pre-split A operand: every k group of 8 is one pixel's 8-channel group (32-B aligned, whole groups)
+bool presplit_ok(const fg_conv_problem& p) {
+    return p.jp % 32 == 0 && p.jc % 8 == 0 && p.jc > 0 && ((uintptr_t)p.x & 31) == 0 &&
+           (p.sxn | p.sxa | p.sxb | p.sxr) % 8 == 0;
+}
+
 bool f3_takes(const fg_conv_problem* probs, int nprob, int max_n) {
     if (g_f3_tile == -2 || f3_config(max_n) < 0) return false;
+    if (probs[0].x_presplit) {
+        const int cfg = auto_cfg(probs, nprob, max_n);
+        if (!(cfg == 0 || cfg == 3 || cfg == 4 || cfg == 6 || cfg == 7 || cfg == 9)) return false;   // WM = 32
+    }
     for (int i = 0; i < nprob; ++i) {
         const fg_conv_problem& p = probs[i];
+        if ((p.x_presplit != 0) != (probs[0].x_presplit != 0) || (p.x_presplit && !presplit_ok(p))) return false;
         // no K padding (every staged k is a real tap: padded j would gather past the row run); ldw may exceed
         // kh * jp (a kernel-row range of a larger pack: the resblock input gradient's row strips)
         if (p.w_split != 2 || p.jp % 32 || p.j_valid != p.jp || p.ldw < p.kh * p.jp || !p.x_absmax || !p.w_absmax ||

@@ -1337,6 +1337,11 @@ FG_API int fg_conv_fwd(const fg_conv_problem* probs, int nprob, hipStream_t stre
     if ((ws == 1 && (!x6 || f16)) || (ws == 2 && !f16))
         return fg::fail(FG_ERR_INVALID, "fg_conv_fwd: pre-split weights (w_split=%d) do not match the conv math %d",
                         ws, g_conv_math);
+    int nps = 0;
+    for (int i = 0; i < nprob; ++i) nps += probs[i].x_presplit != 0;
+    if (nps && (nps != nprob || !f16 || !vec || ws != 2 || g_fwd_tile >= 0))
+        return fg::fail(FG_ERR_INVALID, "fg_conv_fwd: pre-split x (FG_PRESPLIT) needs every problem pre-split, the f16x3 "
+                                        "math and the pipelined kernel");
     if (x6) {
         // the split-math kernels address operands with 31-bit buffer offsets: split oversized
         // problems over images (each chunk launched on its own)
@@ -1375,6 +1380,7 @@ FG_API int fg_conv_fwd(const fg_conv_problem* probs, int nprob, hipStream_t stre
         int rc = 0;
         if (fgc::launch_fwd_f3(b, nprob, max_n, stream, &rc)) return rc;
     }
+    if (nps) return fg::fail(FG_ERR_INVALID, "fg_conv_fwd: the pipelined kernel declined pre-split problems (geometry)");
     int cfg = -1, BM, BN;
     if (x6) {
         cfg = g_fwd_tile >= 0 ? g_fwd_tile : (max_n > 128 ? 0 : max_n > 64 ? 1 : max_n > 32 ? 2 : 3);
@@ -1451,10 +1457,15 @@ FG_API int fg_conv_wgrad(const fg_wgrad_problem* prob, hipStream_t stream) {
                 return fg::fail(FG_ERR_INVALID, "fg_conv_wgrad: the f16x3 math needs p_absmax and x_absmax");
             int rc = 0;
             if (g_wgrad_tile < 0 && fgc::launch_wgrad_f3(p, stream, &rc)) return rc;   // conv_wgrad_f3.hip
+            if (p.p_presplit || p.x_presplit)
+                return fg::fail(FG_ERR_INVALID, "fg_conv_wgrad: pre-split operands need the pipelined kernel");
             return launch_wgrad_split_cfg<MathF16x3>(cfg, p, vx, vp, stream);
         }
+        if (p.p_presplit || p.x_presplit)
+            return fg::fail(FG_ERR_INVALID, "fg_conv_wgrad: pre-split operands need the f16x3 math");
         return launch_wgrad_split_cfg<MathBF16x6>(cfg, p, vx, vp, stream);
     }
+    if (p.p_presplit || p.x_presplit) return fg::fail(FG_ERR_INVALID, "fg_conv_wgrad: pre-split operands need f16x3");
     if (p.n_a > 64) return launch_wgrad<128, 128, 64, 64>(p, vx, vp, stream);
     if (p.n_a > 32) return launch_wgrad<64, 256, 64, 64>(p, vx, vp, stream);
     return launch_wgrad<32, 256, 32, 64>(p, vx, vp, stream);

@@ -58,7 +58,9 @@ __device__ __forceinline__ void split4(const f32x4& v, float s, f16x4& h, f16x4&
 // loads as one burst, then the MFMAs; SCH 1: the stage's MFMAs in four column groups with one
 // staging slot's store + reload in front of each (the VALU split and the LDS writes run beside
 // the partner wave's MFMAs instead of stalling the SIMD at the top of every stage).
-template <int TA, int SCH>
+// PS bit 0 / bit 1: P / X arrive in the FG_PRESPLIT format (include/floodgan.h): a float4 slot then holds
+// the h (col % 8 == 0) or the l (col % 8 == 4) piece of its 8-channel group, written to its image as it stands
+template <int TA, int SCH, int PS = 0>
 __global__ void __launch_bounds__(512, 1)
 conv_wgrad_f3_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
     // 8 waves as NWA (a) x NWK (k); wave tile 64 (a) x WK (k): TA 256 -> 4 x 2, 64 x 128; TA 128 -> 2 x 4, 64 x 64
@@ -140,15 +142,25 @@ conv_wgrad_f3_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
         {
             f16x4 h, l;
             if (p_slot) {
-                const int op = img_off<TA>(prow0 + 8 * i, col);
-                split4(rp[i], sp, h, l);
-                *reinterpret_cast<f16x4*>(b + op) = h;
-                *reinterpret_cast<f16x4*>(b + IMGP + op) = l;
+                if constexpr (PS & 1) {
+                    const int op = img_off<TA>(prow0 + 8 * i, col & ~7) + ((col & 4) ? IMGP : 0);
+                    *reinterpret_cast<f16x8*>(b + op) = __builtin_bit_cast(f16x8, rp[i]);
+                } else {
+                    const int op = img_off<TA>(prow0 + 8 * i, col);
+                    split4(rp[i], sp, h, l);
+                    *reinterpret_cast<f16x4*>(b + op) = h;
+                    *reinterpret_cast<f16x4*>(b + IMGP + op) = l;
+                }
             }
-            const int ox = img_off<TK>(prow0 + 8 * i, col);
-            split4(rx[i], sx, h, l);
-            *reinterpret_cast<f16x4*>(b + 2 * IMGP + ox) = h;
-            *reinterpret_cast<f16x4*>(b + 2 * IMGP + IMGX + ox) = l;
+            if constexpr (PS & 2) {
+                const int ox = img_off<TK>(prow0 + 8 * i, col & ~7) + ((col & 4) ? IMGX : 0);
+                *reinterpret_cast<f16x8*>(b + 2 * IMGP + ox) = __builtin_bit_cast(f16x8, rx[i]);
+            } else {
+                const int ox = img_off<TK>(prow0 + 8 * i, col);
+                split4(rx[i], sx, h, l);
+                *reinterpret_cast<f16x4*>(b + 2 * IMGP + ox) = h;
+                *reinterpret_cast<f16x4*>(b + 2 * IMGP + IMGX + ox) = l;
+            }
         }
     };
     auto store = [&](int buf) {
@@ -262,6 +274,21 @@ int launch_wgrad_f3(const fg_wgrad_problem& p, hipStream_t stream, int* rc) {
     const int TA = p.n_a >= 256 ? 256 : 128;
     const int ta = (p.n_a + TA - 1) / TA, tk = (p.kh * p.j_valid + TK - 1) / TK;
     const dim3 grid(ta * tk * p.splits);
+    const int ps = (p.p_presplit ? 1 : 0) | (p.x_presplit ? 2 : 0);
+    if (ps) {
+        // whole 8-channel groups at 32-B aligned bases (FG_PRESPLIT); the 256-row tile, staging schedule 0
+        if (TA != 256 || p.n_a % 8 || p.j_valid % 8 || (p.p_presplit && (((uintptr_t)p.p & 31) || (p.spn | p.spa | p.spb) % 8)) ||
+            (p.x_presplit && (((uintptr_t)p.x & 31) || (p.sxn | p.sxa | p.sxb | p.sxr) % 8)))
+            return 0;
+        if (ps == 1)
+            hipLaunchKernelGGL((conv_wgrad_f3_kernel<256, 0, 1>), grid, dim3(512), 0, stream, p, ta, tk);
+        else if (ps == 2)
+            hipLaunchKernelGGL((conv_wgrad_f3_kernel<256, 0, 2>), grid, dim3(512), 0, stream, p, ta, tk);
+        else
+            hipLaunchKernelGGL((conv_wgrad_f3_kernel<256, 0, 3>), grid, dim3(512), 0, stream, p, ta, tk);
+        *rc = fg::launched("conv_wgrad_f3_presplit");
+        return 1;
+    }
     // measured: the interleaved staging pays off on the 128-row tiles only
     const int sch = g_wgrad_f3 == 3 || (g_wgrad_f3 == 2 && TA == 128) ? 1 : 0;
     if (TA == 256 && sch == 1)

@@ -7,7 +7,7 @@
 // Backward: dL/dx = rstd * (g' - mean(g') - xhat * mean(g' xhat)), g' = g * act'(xhat).
 #include <algorithm>
 
-#include "fg_common.hpp"
+#include "conv_common.hpp"
 
 namespace {
 
@@ -165,6 +165,28 @@ __global__ void in_apply_kernel(fg_view src, const float* __restrict__ mean, con
     if (amax) absmax_flush(am, amax);
 }
 
+// FG_PRESPLIT store (include/floodgan.h) of this lane's 4 channels o (scaled by s) at p = its fp32 position:
+// lanes 2q, 2q+1 hold channels 8q..8q+3, 8q+4..8q+7 of one pixel; the even lane stores h[8] there, the odd
+// lane l[8] (one swap of 8 bytes between the pair: quad_perm [1,0,3,2])
+__device__ __forceinline__ void store_presplit(float* p, const f32x4& o, float s, int odd) {
+    f16x4 h, l;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const float x = o[e] * s;
+        h[e] = (_Float16)x;
+        l[e] = (_Float16)(x - (float)h[e]);
+    }
+    typedef int i32x2 __attribute__((ext_vector_type(2)));
+    const i32x2 hv = __builtin_bit_cast(i32x2, h), lv = __builtin_bit_cast(i32x2, l);
+    const i32x2 send = odd ? hv : lv;
+    i32x2 recv;
+    recv[0] = __builtin_amdgcn_update_dpp(0, send[0], 0xB1, 0xF, 0xF, false);
+    recv[1] = __builtin_amdgcn_update_dpp(0, send[1], 0xB1, 0xF, 0xF, false);
+    typedef int i32x4 __attribute__((ext_vector_type(4)));
+    const i32x4 out = odd ? i32x4{recv[0], recv[1], lv[0], lv[1]} : i32x4{hv[0], hv[1], recv[0], recv[1]};
+    *reinterpret_cast<i32x4*>(p) = out;
+}
+
 // Row form of the apply pass (channel quads dividing the block: C/4 | 256): block = one padded output
 // row (n, yp), thread = (pixel lane gi, channel quad c4); mean / rstd read once per thread, U pixels'
 // loads issued before any of them is used (the grid-stride form above re-derived (n, y, x, c) with
@@ -174,7 +196,7 @@ constexpr int kRowU = 4;
 __global__ void __launch_bounds__(NT) in_apply_rows_kernel(fg_view src, const float* __restrict__ mean,
                                                            const float* __restrict__ rstd, int act, fg_view res,
                                                            fg_view dst, int pad_mode, int lshift,
-                                                           unsigned* __restrict__ amax) {
+                                                           unsigned* __restrict__ amax, float* __restrict__ split_slot) {
     const int L = 1 << lshift, PG = NT >> lshift;
     const int C = dst.c_alloc, h = dst.h, w = dst.w, pad = dst.pad;
     const int hp = h + 2 * pad, wp = w + 2 * pad;
@@ -184,6 +206,14 @@ __global__ void __launch_bounds__(NT) in_apply_rows_kernel(fg_view src, const fl
     unsigned am = 0;
     int y = yp - pad;
     const bool reflect = pad_mode == FG_PAD_REFLECT;
+    // pre-split output: |act(xhat)| <= |xhat| <= sqrt(HW - 1) (Samuelson), the static bound of the scale,
+    // published in the output's scale slot by block 0 (the slot comes zeroed)
+    float ss = 0.f;
+    if (split_slot) {
+        const float bound = sqrtf((float)(h * w - 1)) * 1.001f;
+        ss = fgc::pow2_of(bound);
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicMax(reinterpret_cast<unsigned*>(split_slot), __float_as_uint(bound));
+    }
     if ((y < 0 || y >= h) && !reflect) {
         const f32x4 z = {0.f, 0.f, 0.f, 0.f};
         for (int xp = gi; xp < wp; xp += PG) *reinterpret_cast<f32x4*>(drow + (size_t)xp * C) = z;
@@ -216,8 +246,12 @@ __global__ void __launch_bounds__(NT) in_apply_rows_kernel(fg_view src, const fl
                     for (int e = 0; e < 4; ++e) o[e] = fg::act_fwd(o[e], act);
                     o += rv[k];
                 }
-                am = max(am, absbits4(o));
-                *reinterpret_cast<f32x4*>(drow + (size_t)xp * C) = o;
+                if (split_slot) {
+                    store_presplit(drow + (size_t)xp * C, o, ss, c4 & 1);
+                } else {
+                    am = max(am, absbits4(o));
+                    *reinterpret_cast<f32x4*>(drow + (size_t)xp * C) = o;
+                }
             }
         }
     }
@@ -270,8 +304,10 @@ __device__ __forceinline__ f32x4 fold_extra(f32x4 v, const fg_view& g, int fp, i
 __global__ void __launch_bounds__(NT) in_bwd_stats_u_kernel(fg_view g, int fp, fg_view gadd, fg_view src,
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ rstd, int act, int chunks,
-                                                            double* __restrict__ work, fg_view gsum) {
+                                                            double* __restrict__ work, fg_view gsum,
+                                                            float* __restrict__ gmax_part) {
     const int C = src.c_alloc, L = C / 4, PG = NT / L;
+    unsigned gm = 0;
     const int n = blockIdx.y, chunk = blockIdx.x;
     const int h = src.h, w = src.w, HW = h * w;
     const int per = (HW + chunks - 1) / chunks;
@@ -311,10 +347,22 @@ __global__ void __launch_bounds__(NT) in_bwd_stats_u_kernel(fg_view g, int fp, f
                 const f32x4 xh = (sv[k] - m) * r;
 #pragma unroll
                 for (int e = 0; e < 4; ++e) gk[e] *= fg::act_grad(xh[e], act);
+                gm = max(gm, absbits4(gk));
                 sg += gk;
                 sgx += gk * xh;
                 sx += xh;
             }
+        }
+    }
+    if (gmax_part) {     // this block's max |g'| (the pre-split output's scale bound, fg_in_bwd_presplit)
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) gm = max(gm, (unsigned)__shfl_xor((int)gm, off));
+        __shared__ unsigned gred[NT / 64];
+        if ((threadIdx.x & 63) == 0) gred[threadIdx.x >> 6] = gm;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int i = 1; i < NT / 64; ++i) gm = max(gm, gred[i]);
+            gmax_part[n * chunks + chunk] = __uint_as_float(gm);
         }
     }
 #pragma unroll
@@ -398,9 +446,19 @@ __global__ void __launch_bounds__(64 * FG) in_bwd_finalize_kernel(int N, int C, 
                                                                    const double* __restrict__ work,
                                                                    const float* __restrict__ rstd,
                                                                    float* __restrict__ coef,
-                                                                   double* __restrict__ bpart) {
+                                                                   double* __restrict__ bpart,
+                                                                   const float* __restrict__ gmax_part,
+                                                                   float* __restrict__ split_slot) {
     const int n = blockIdx.x, c = blockIdx.y * 64 + (threadIdx.x & 63), g = threadIdx.x >> 6;
     __shared__ double red[FG][64][3];
+    __shared__ unsigned gmx, bmx;
+    if (split_slot) {
+        if (threadIdx.x == 0) gmx = bmx = 0;
+        __syncthreads();
+        unsigned m = 0;
+        for (int k = threadIdx.x; k < chunks; k += blockDim.x) m = max(m, __float_as_uint(gmax_part[n * chunks + k]));
+        atomicMax(&gmx, m);
+    }
     double sg = 0, sgx = 0, sx = 0;
     if (c < C)
         for (int k = g; k < chunks; k += FG) {
@@ -413,19 +471,31 @@ __global__ void __launch_bounds__(64 * FG) in_bwd_finalize_kernel(int N, int C, 
     red[g][threadIdx.x & 63][1] = sgx;
     red[g][threadIdx.x & 63][2] = sx;
     __syncthreads();
-    if (g != 0 || c >= C) return;
-    sg = sgx = sx = 0;
-    for (int gg = 0; gg < FG; ++gg) {
-        sg += red[gg][threadIdx.x][0];
-        sgx += red[gg][threadIdx.x][1];
-        sx += red[gg][threadIdx.x][2];
+    if (g == 0 && c < C) {
+        sg = sgx = sx = 0;
+        for (int gg = 0; gg < FG; ++gg) {
+            sg += red[gg][threadIdx.x][0];
+            sgx += red[gg][threadIdx.x][1];
+            sx += red[gg][threadIdx.x][2];
+        }
+        const double HW = (double)HWi;
+        const int idx = n * C + c;
+        const float c1 = (float)(sg / HW), c2 = (float)(sgx / HW);
+        coef[(size_t)idx * 2] = c1;
+        coef[(size_t)idx * 2 + 1] = c2;
+        // sum_hw rstd*(g' - mean g' - xhat*mean(g'xhat)) = -rstd * sx * sgx / HW
+        bpart[idx] = -(double)rstd[idx] * sx * sgx / HW;
+        if (split_slot) {
+            // |rstd (g' - c1 - xhat c2)| <= rstd (max|g'| + |c1| + sqrt(HW - 1) |c2|), with rounding slack
+            const float b = rstd[idx] * (__uint_as_float(gmx) + fabsf(c1) + sqrtf((float)(HWi - 1)) * fabsf(c2)) * 1.001f;
+            atomicMax(&bmx, __float_as_uint(b));
+        }
     }
-    const double HW = (double)HWi;
-    const int idx = n * C + c;
-    coef[(size_t)idx * 2] = (float)(sg / HW);
-    coef[(size_t)idx * 2 + 1] = (float)(sgx / HW);
-    // sum_hw rstd*(g' - mean g' - xhat*mean(g'xhat)) = -rstd * sx * sgx / HW
-    bpart[idx] = -(double)rstd[idx] * sx * sgx / HW;
+    if (split_slot) {
+        __syncthreads();
+        if (threadIdx.x == 0)
+            atomicMax(reinterpret_cast<unsigned*>(split_slot) + ((n * gridDim.y + blockIdx.y) & (FG_AMAX_SHARDS - 1)), bmx);
+    }
 }
 
 
@@ -483,7 +553,9 @@ __global__ void __launch_bounds__(NT) in_bwd_apply_rows_kernel(fg_view g, int fp
                                                                unsigned* __restrict__ amax,
                                                                const double* __restrict__ bpart,
                                                                float* __restrict__ bias_grad, int bias_accumulate,
-                                                               int lshift) {
+                                                               int lshift, const float* __restrict__ split_slot) {
+    // pre-split output: the scale of the bound the finalize published (the consumer derives the same one)
+    const float ss = split_slot ? fgc::pow2_scale(split_slot) : 0.f;
     if (bias_grad && blockIdx.x == 0) {
         const int C = dst.c_alloc;
         for (int c = threadIdx.x; c < C; c += blockDim.x) {
@@ -536,8 +608,12 @@ __global__ void __launch_bounds__(NT) in_bwd_apply_rows_kernel(fg_view g, int fp
 #pragma unroll
                     for (int e = 0; e < 4; ++e) out[e] = r[e] * (gk[e] * fg::act_grad(xh[e], act) - c1[e] - xh[e] * c2[e]);
                 }
-                am = max(am, absbits4(out));
-                *reinterpret_cast<f32x4*>(drow + (size_t)xp * C) = out;
+                if (split_slot) {
+                    store_presplit(drow + (size_t)xp * C, out, ss, c4 & 1);
+                } else {
+                    am = max(am, absbits4(out));
+                    *reinterpret_cast<f32x4*>(drow + (size_t)xp * C) = out;
+                }
             }
         }
     }
@@ -798,8 +874,11 @@ FG_API int fg_set_in_rows(int on) {
     return 0;
 }
 
-FG_API long long fg_in_workspace_doubles(int n, int c) { return (long long)n * c * (MAX_CHUNKS * 3 + 2) + 64; }
-// layout: [stats n*c*MAX_CHUNKS*3][coef n*c*2 floats = n*c doubles][bias partials n*c]
+FG_API long long fg_in_workspace_doubles(int n, int c) {
+    return (long long)n * c * (MAX_CHUNKS * 3 + 2) + (long long)n * MAX_CHUNKS / 2 + 64;
+}
+// layout: [stats n*c*MAX_CHUNKS*3][coef n*c*2 floats = n*c doubles][bias partials n*c][max |g'| per (n, chunk):
+// n*MAX_CHUNKS floats]
 
 FG_API int fg_in_stats(fg_view src, float eps, float* mean, float* rstd, double* work, hipStream_t stream) {
     if (!ok_view(src) || !mean || !rstd || !work || src.c_alloc % 4 || (NT % (src.c_alloc / 4)) != 0)
@@ -813,8 +892,31 @@ FG_API int fg_in_stats(fg_view src, float eps, float* mean, float* rstd, double*
     return fg::launched("in_finalize");
 }
 
+namespace {
+int in_apply_impl(fg_view src, const float* mean, const float* rstd, int act, fg_view residual, fg_view dst,
+                  int pad_mode, float* absmax, float* split_slot, hipStream_t stream);
+int in_bwd_impl(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, const float* mean, const float* rstd, int act,
+                fg_view dst, float* bias_grad, int bias_accumulate, fg_view gsum, double* work, float* absmax,
+                float* split_slot, hipStream_t stream);
+}  // namespace
+
 FG_API int fg_in_apply(fg_view src, const float* mean, const float* rstd, int act, fg_view residual, fg_view dst,
                        int pad_mode, float* absmax, hipStream_t stream) {
+    return in_apply_impl(src, mean, rstd, act, residual, dst, pad_mode, absmax, nullptr, stream);
+}
+
+FG_API int fg_in_apply_presplit(fg_view src, const float* mean, const float* rstd, int act, fg_view dst, int pad_mode,
+                                float* scale_slot, hipStream_t stream) {
+    if (!scale_slot || dst.c_alloc % 8 || NT % (dst.c_alloc / 4) || ((uintptr_t)dst.ptr & 31))
+        return fg::fail(FG_ERR_INVALID, "fg_in_apply_presplit: needs a zeroed scale slot, C %% 8 == 0, C <= 1024, "
+                                        "a 32-B aligned dst (C=%d)", dst.c_alloc);
+    return in_apply_impl(src, mean, rstd, act, fg_view{nullptr, 0, 0, 0, 0, 0}, dst, pad_mode, nullptr, scale_slot,
+                         stream);
+}
+
+namespace {
+int in_apply_impl(fg_view src, const float* mean, const float* rstd, int act, fg_view residual, fg_view dst,
+                  int pad_mode, float* absmax, float* split_slot, hipStream_t stream) {
     if (!ok_view(src) || !ok_view(dst) || !mean || !rstd || src.c_alloc % 4 || dst.c_alloc != src.c_alloc ||
         dst.h != src.h || dst.w != src.w || dst.n != src.n)
         return fg::fail(FG_ERR_INVALID, "fg_in_apply: bad args");
@@ -823,9 +925,10 @@ FG_API int fg_in_apply(fg_view src, const float* mean, const float* rstd, int ac
     if (pad_mode == FG_PAD_REFLECT && (dst.pad >= dst.h || dst.pad >= dst.w))
         return fg::fail(FG_ERR_INVALID, "fg_in_apply: reflect pad too large");
     const int C4 = dst.c_alloc / 4;
-    if (g_in_rows && NT % C4 == 0) {
+    if ((g_in_rows || split_slot) && NT % C4 == 0) {
         hipLaunchKernelGGL(in_apply_rows_kernel, dim3(dst.n * (dst.h + 2 * dst.pad)), dim3(NT), 0, stream, src, mean,
-                           rstd, act, residual, dst, pad_mode, ilog2(C4), reinterpret_cast<unsigned*>(absmax));
+                           rstd, act, residual, dst, pad_mode, ilog2(C4), reinterpret_cast<unsigned*>(absmax),
+                           split_slot);
         return fg::launched("in_apply_rows");
     }
     const long long total = (long long)dst.n * (dst.h + 2 * dst.pad) * (dst.w + 2 * dst.pad) * (dst.c_alloc / 4);
@@ -833,10 +936,29 @@ FG_API int fg_in_apply(fg_view src, const float* mean, const float* rstd, int ac
                        rstd, act, residual, dst, pad_mode, reinterpret_cast<unsigned*>(absmax));
     return fg::launched("in_apply");
 }
+}  // namespace
 
 FG_API int fg_in_bwd(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, const float* mean, const float* rstd,
                      int act, fg_view dst, float* bias_grad, int bias_accumulate, fg_view gsum, double* work,
                      float* absmax, hipStream_t stream) {
+    return in_bwd_impl(gsrc, fold_pad, gadd, src, mean, rstd, act, dst, bias_grad, bias_accumulate, gsum, work, absmax,
+                       nullptr, stream);
+}
+
+FG_API int fg_in_bwd_presplit(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, const float* mean,
+                              const float* rstd, int act, fg_view dst, float* bias_grad, int bias_accumulate,
+                              fg_view gsum, double* work, float* scale_slot, hipStream_t stream) {
+    if (!scale_slot || dst.c_alloc % 8 || ((uintptr_t)dst.ptr & 31))
+        return fg::fail(FG_ERR_INVALID, "fg_in_bwd_presplit: needs a zeroed scale slot, C %% 8 == 0, a 32-B aligned "
+                                        "dst (C=%d)", dst.c_alloc);
+    return in_bwd_impl(gsrc, fold_pad, gadd, src, mean, rstd, act, dst, bias_grad, bias_accumulate, gsum, work, nullptr,
+                       scale_slot, stream);
+}
+
+namespace {
+int in_bwd_impl(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, const float* mean, const float* rstd, int act,
+                fg_view dst, float* bias_grad, int bias_accumulate, fg_view gsum, double* work, float* absmax,
+                float* split_slot, hipStream_t stream) {
     if (!ok_view(gsrc) || !ok_view(src) || !ok_view(dst) || !mean || !rstd || !work || src.c_alloc % 4 ||
         (NT % (src.c_alloc / 4)) != 0 || gsrc.c_alloc != src.c_alloc || dst.c_alloc != src.c_alloc ||
         dst.h != src.h || dst.w != src.w || dst.n != src.n)
@@ -852,23 +974,28 @@ FG_API int fg_in_bwd(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, cons
     const int chunks = choose_chunks(src.n, (long long)src.h * src.w);
     const int C = src.c_alloc;
     float* coef = reinterpret_cast<float*>(work + (size_t)src.n * C * MAX_CHUNKS * 3);
-    hipLaunchKernelGGL(g_in_rows ? in_bwd_stats_u_kernel : in_bwd_stats_kernel, dim3(chunks, src.n), dim3(NT), 0,
-                       stream, gsrc, fold_pad, gadd, src, mean, rstd, act, chunks, work, gsum);
+    double* bpart = work + (size_t)src.n * C * MAX_CHUNKS * 3 + (size_t)src.n * C;
+    float* gmax_part = split_slot ? reinterpret_cast<float*>(bpart + (size_t)src.n * C) : nullptr;
+    if (g_in_rows || split_slot)
+        hipLaunchKernelGGL(in_bwd_stats_u_kernel, dim3(chunks, src.n), dim3(NT), 0, stream, gsrc, fold_pad, gadd, src,
+                           mean, rstd, act, chunks, work, gsum, gmax_part);
+    else
+        hipLaunchKernelGGL(in_bwd_stats_kernel, dim3(chunks, src.n), dim3(NT), 0, stream, gsrc, fold_pad, gadd, src,
+                           mean, rstd, act, chunks, work, gsum);
     int e = fg::launched("in_bwd_stats");
     if (e) return e;
-    double* bpart = work + (size_t)src.n * C * MAX_CHUNKS * 3 + (size_t)src.n * C;
     hipLaunchKernelGGL(in_bwd_finalize_kernel, dim3(src.n, (C + 63) / 64), dim3(64 * FG), 0, stream, src.n, C,
-                       src.h * src.w, chunks, work, rstd, coef, bpart);
+                       src.h * src.w, chunks, work, rstd, coef, bpart, gmax_part, split_slot);
     e = fg::launched("in_bwd_finalize");
     if (e) return e;
     const long long total = (long long)dst.n * (dst.h + 2 * dst.pad) * (dst.w + 2 * dst.pad) * (C / 4);
     // with gsum the apply pass reads the gathered gradient the statistics pass wrote (one read, no fold)
     const fg_view none = {nullptr, 0, 0, 0, 0, 0};
-    if (g_in_rows) {
+    if (g_in_rows || split_slot) {
         hipLaunchKernelGGL(in_bwd_apply_rows_kernel, dim3(dst.n * (dst.h + 2 * dst.pad)), dim3(NT), 0, stream,
                            gsum.ptr ? gsum : gsrc, gsum.ptr ? 0 : fold_pad, gsum.ptr ? none : gadd, src, mean, rstd,
                            coef, act, dst, reinterpret_cast<unsigned*>(absmax), bpart, bias_grad, bias_accumulate,
-                           ilog2(C / 4));
+                           ilog2(C / 4), split_slot);
         return fg::launched("in_bwd_apply_rows");
     }
     hipLaunchKernelGGL(in_bwd_apply_kernel, dim3(fg::blocks_for(total, 256, 4096)), dim3(256), 0, stream,
@@ -876,6 +1003,7 @@ FG_API int fg_in_bwd(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, cons
                        act, dst, reinterpret_cast<unsigned*>(absmax), bpart, bias_grad, bias_accumulate);
     return fg::launched("in_bwd_apply");
 }
+}  // namespace
 
 FG_API int fg_act_bwd(fg_view g, fg_view y, int act, float* absmax, hipStream_t stream) {
     unsigned* am = reinterpret_cast<unsigned*>(absmax);

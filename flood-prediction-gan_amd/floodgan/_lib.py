@@ -41,7 +41,7 @@ class fg_conv_problem(C.Structure):
                 ("kh", C.c_int), ("j_valid", C.c_int), ("jp", C.c_int),
                 ("n_out", C.c_int), ("ldw", C.c_int), ("act", C.c_int), ("accumulate", C.c_int),
                 ("w_split", C.c_int), ("x_absmax", C.c_void_p), ("w_absmax", C.c_void_p), ("jc", C.c_int),
-                ("in_stats", C.c_void_p)]
+                ("in_stats", C.c_void_p), ("x_presplit", C.c_int)]
 
 
 class fg_wgrad_problem(C.Structure):
@@ -50,7 +50,8 @@ class fg_wgrad_problem(C.Structure):
                 ("sxn", C.c_longlong), ("sxa", C.c_longlong), ("sxb", C.c_longlong), ("sxr", C.c_longlong),
                 ("m_img", C.c_int), ("m_a", C.c_int), ("m_b", C.c_int),
                 ("n_a", C.c_int), ("kh", C.c_int), ("j_valid", C.c_int),
-                ("splits", C.c_int), ("m_chunk", C.c_int), ("p_absmax", C.c_void_p), ("x_absmax", C.c_void_p)]
+                ("splits", C.c_int), ("m_chunk", C.c_int), ("p_absmax", C.c_void_p), ("x_absmax", C.c_void_p),
+                ("p_presplit", C.c_int), ("x_presplit", C.c_int)]
 
 
 class fg_weight_map(C.Structure):
@@ -136,6 +137,9 @@ SIGNATURES = {
     "fg_in_apply": [fg_view, C.c_void_p, C.c_void_p, C.c_int, fg_view, fg_view, C.c_int, C.c_void_p, C.c_void_p],
     "fg_in_bwd": [fg_view, C.c_int, fg_view, fg_view, C.c_void_p, C.c_void_p, C.c_int, fg_view, C.c_void_p,
                   C.c_int, fg_view, C.c_void_p, C.c_void_p, C.c_void_p],
+    "fg_in_apply_presplit": [fg_view, C.c_void_p, C.c_void_p, C.c_int, fg_view, C.c_int, C.c_void_p, C.c_void_p],
+    "fg_in_bwd_presplit": [fg_view, C.c_int, fg_view, fg_view, C.c_void_p, C.c_void_p, C.c_int, fg_view, C.c_void_p,
+                           C.c_int, fg_view, C.c_void_p, C.c_void_p, C.c_void_p],
     "fg_act_bwd": [fg_view, fg_view, C.c_int, C.c_void_p, C.c_void_p],
     "fg_channel_sum": [fg_view, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p],
     "fg_channel_sum_workspace_doubles": [C.c_int],

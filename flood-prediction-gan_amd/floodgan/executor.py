@@ -140,12 +140,12 @@ def _convT_fwd(P, name, X, Y):
     return ops.conv(PL.phase_problems(X, w.shape, 3, 1, Y, wps, maps, bias=P[name + ".bias"]), in_stats=True)
 
 
-def _norm(c, act, pad, mode, residual=None, stats=None):
+def _norm(c, act, pad, mode, residual=None, stats=None, presplit=False):
     """InstanceNorm + activation of conv output c; stats = (mean, rstd) from the conv's epilogue, or
-    computed here"""
+    computed here.  presplit: the output is written in the FG_PRESPLIT format (read only by convs)"""
     mean, rstd = stats if stats is not None else ops.in_stats(c)
     out = Buf.empty(c.n, c.h, c.w, c.c, pad, c.t.device)
-    ops.in_apply(c, mean, rstd, act, residual, out, mode)
+    ops.in_apply(c, mean, rstd, act, residual, out, mode, presplit=presplit)
     return mean, rstd, out
 
 
@@ -228,7 +228,8 @@ def _block_fwd(P, pre, h, out_mode):
     dev = h.t.device
     cb1 = Buf.empty(N, Hh, Ww, Cc, 0, dev)
     st = _conv_fwd(P, pre + "conv1", h, 1, 3, 1, cb1, tag="resblock_conv_fwd", in_stats=True)
-    mb1, rb1, rb = _norm(cb1, FG_ACT_RELU, 1, FG_PAD_REFLECT, stats=st)
+    # rb is read only by conv2 and conv2's weight gradient: pre-split for both (ops.PRESPLIT)
+    mb1, rb1, rb = _norm(cb1, FG_ACT_RELU, 1, FG_PAD_REFLECT, stats=st, presplit=ops.presplit_on())
     cb2 = Buf.empty(N, Hh, Ww, Cc, 0, dev)
     st = _conv_fwd(P, pre + "conv2", rb, 1, 3, 1, cb2, tag="resblock_conv_fwd", in_stats=True)
     mb2, rb2, hn = _norm(cb2, FG_ACT_NONE, 1, out_mode, residual=h, stats=st)
@@ -248,12 +249,15 @@ def _block_bwd(P, pre, b, grad, G):
     lazy = fold > 0 or gadd is not None
     g_h = Buf.empty(N, Hh, Ww, Cc, 0, dev) if lazy else gsrc
     g_cb2 = Buf.empty(N, Hh, Ww, Cc, 2, dev)          # zero border 2: full correlation of a 3x3
+    # the conv-output gradients are read only by the input-gradient convs and the weight gradients: pre-split
+    ps = ops.presplit_on()
     ops.in_bwd(gsrc, fold, gadd, cb2, b["mb2"], b["rb2"], FG_ACT_NONE, g_cb2, G.get(pre + "conv2.bias"), G.acc,
-               gsum=g_h if lazy else None)
+               gsum=g_h if lazy else None, presplit=ps)
     _wgrad_conv(P, G, pre + "conv2", g_cb2, b["rb"], 1, 3, 1)
     g_rbp = _dgrad_s1_padded(P, pre + "conv2", g_cb2)  # gradient w.r.t. the reflect-padded relu output
     g_cb1 = Buf.empty(N, Hh, Ww, Cc, 2, dev)
-    ops.in_bwd(g_rbp, 1, None, b["cb1"], b["mb1"], b["rb1"], FG_ACT_RELU, g_cb1, G.get(pre + "conv1.bias"), G.acc)
+    ops.in_bwd(g_rbp, 1, None, b["cb1"], b["mb1"], b["rb1"], FG_ACT_RELU, g_cb1, G.get(pre + "conv1.bias"), G.acc,
+               presplit=ps)
     _wgrad_conv(P, G, pre + "conv1", g_cb1, b["h"], 1, 3, 1)
     g_hp = _dgrad_s1_padded(P, pre + "conv1", g_cb1)
     return g_hp, 1, g_h                               # reflect-pad adjoint + residual path, summed lazily
@@ -467,7 +471,12 @@ def gen_act_decisions(S):
     instrumentation: oracle ActDecisions teacher-forces them to compare gradients at full size)."""
     out = {"conv1": _decided(S["a1"]), "conv2": _decided(S["a2"]), "conv3": _decided(S["blocks"][0]["h"])}
     for i, b in enumerate(S["blocks"]):
-        out[f"block{i}"] = _decided(b["rb"])
+        if ops.is_presplit(b["rb"]):
+            # relu((c - mean) * rstd) > 0 <=> c > mean (rstd > 0; fp32 subtraction keeps the sign)
+            cb, mean = b["cb1"], b["mb1"]
+            out[f"block{i}"] = (cb.interior() > mean.view(cb.n, 1, 1, cb.c)).permute(0, 3, 1, 2).contiguous().cpu()
+        else:
+            out[f"block{i}"] = _decided(b["rb"])
     for tag, hd in S["heads"].items():
         out[f"deconv1_{tag}"], out[f"deconv2_{tag}"] = _decided(hd["ad1"]), _decided(hd["ad2"])
     return out

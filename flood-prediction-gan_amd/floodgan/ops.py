@@ -91,7 +91,7 @@ def _tensor(obj):
 
 
 def _wrote(*objs):
-    """an op wrote these buffers: forget their cached absmax slots and split copies"""
+    """an op wrote these buffers: forget their cached absmax slots, split copies and pre-split format"""
     for o in objs:
         if o is not None:
             t = _tensor(o)
@@ -99,6 +99,32 @@ def _wrote(*objs):
                 t._fg_amax = None
             if getattr(t, "_fg_split", None) is not None:
                 t._fg_split = None
+            if getattr(t, "_fg_presplit", False):
+                t._fg_presplit = False
+
+
+# Pre-split operands (FG_PRESPLIT, include/floodgan.h): the norm passes that feed a resblock conv write its
+# operand as the fp16 (h, l) pieces the f16x3 kernels would otherwise split on the fly (FLOODGAN_PRESPLIT=0:
+# off).  The format is recorded on the tensor with its version counter: only the pipelined kernels read it.
+PRESPLIT = os.environ.get("FLOODGAN_PRESPLIT", "1") != "0"
+
+
+def presplit_on():
+    return PRESPLIT and L.fwd_f16x3() and L.wgrad_f16x3() and L.wgrad_f3_on()
+
+
+def is_presplit(obj):
+    t = _tensor(obj)
+    if not getattr(t, "_fg_presplit", False):
+        return False
+    if getattr(t, "_fg_presplit_ver", None) != t._version:
+        raise RuntimeError("a pre-split (FG_PRESPLIT) buffer was written by torch since its producer ran")
+    return True
+
+
+def _mark_presplit(dst):
+    t = _tensor(dst)
+    t._fg_presplit, t._fg_presplit_ver = True, t._version
 
 
 def absmax(t):
@@ -106,6 +132,11 @@ def absmax(t):
     tensor or of a Buf (border and padding channels included: everything a gather can read);
     cached on the tensor until an op writes it."""
     t = _tensor(t)
+    if getattr(t, "_fg_presplit", False) and getattr(t, "_fg_presplit_ver", None) == t._version:
+        # the producer's scale slot is the only valid scale source of a pre-split buffer
+        if getattr(t, "_fg_amax", None) is None or getattr(t, "_fg_amax_ver", None) != t._version:
+            raise RuntimeError("pre-split buffer without its producer's scale slot")
+        return t._fg_amax
     cached = getattr(t, "_fg_amax", None)
     # a slot is valid only together with the version counter it was recorded at: an in-place torch
     # write since then (or a slot recorded without a version) means it may no longer bound t
@@ -273,6 +304,7 @@ def _conv(probs, in_stats=False):
         for k in _CONV_FIELDS:
             setattr(s, k, int(p[k]))
         s.jc = getattr(p["x"][0], "c", 0)
+        s.x_presplit = int(is_presplit(p["x"][0]))
         if f16:
             xb = p["x"][0]
             if id(xb) not in keep:
@@ -327,6 +359,8 @@ def split_pixels(X):
     """fg_split_pixels copy of a Buf (32 or 64 channels): fp16 h/l pieces of the scaled values,
     the window-conv operand.  Cached on the buffer's tensor until an op writes it."""
     t = X.t
+    if is_presplit(X):
+        raise RuntimeError("split_pixels of a pre-split buffer")
     cached = getattr(t, "_fg_split", None)
     if cached is not None and getattr(t, "_fg_split_ver", None) == t._version:
         return cached
@@ -451,6 +485,7 @@ def wgrad(prob, wmap, dw, accumulate=False):
     if L.wgrad_f16x3():
         pa, xa = absmax(prob["p"][0]), absmax(prob["x"][0])
         s.p_absmax, s.x_absmax = pa.data_ptr(), xa.data_ptr()
+    s.p_presplit, s.x_presplit = int(is_presplit(prob["p"][0])), int(is_presplit(prob["x"][0]))
     st = L.stream_handle()
     L.check(_lib().fg_conv_wgrad(C.byref(s), st), "conv_wgrad")
     m = wmap_struct(wmap)
@@ -559,16 +594,34 @@ def in_stats(src):
     return mean, rstd
 
 
-def in_apply(src, mean, rstd, act, residual, dst, pad_mode):
+def in_apply(src, mean, rstd, act, residual, dst, pad_mode, presplit=False):
+    """presplit: dst is written in the FG_PRESPLIT format (no residual; the f16x3 math)"""
+    if presplit:
+        assert residual is None and L.fwd_f16x3()
+        slot = _amax_out(dst)
+        L.check(_lib().fg_in_apply_presplit(view(src), L.ptr(mean), L.ptr(rstd), act, view(dst), pad_mode,
+                                            L.ptr(slot), L.stream_handle()), "in_apply_presplit")
+        _mark_presplit(dst)
+        return
     L.check(_lib().fg_in_apply(view(src), L.ptr(mean), L.ptr(rstd), act, view(residual), view(dst), pad_mode,
                                L.ptr(_amax_out(dst)), L.stream_handle()), "in_apply")
 
 
-def in_bwd(gsrc, fold_pad, gadd, src, mean, rstd, act, dst, bias_grad=None, bias_accumulate=False, gsum=None):
+def in_bwd(gsrc, fold_pad, gadd, src, mean, rstd, act, dst, bias_grad=None, bias_accumulate=False, gsum=None,
+           presplit=False):
     """InstanceNorm (+ activation, reflect-pad fold, residual gradient gadd) backward into dst.  gsum (Buf): also
-    receives the gathered gradient fold(gsrc) + gadd (written by the statistics pass that reads it anyway)."""
+    receives the gathered gradient fold(gsrc) + gadd (written by the statistics pass that reads it anyway).
+    presplit: dst is written in the FG_PRESPLIT format (the f16x3 math)."""
     work = _work(src.n, src.c, src.t.device)
     _wrote(gsum)
+    if presplit:
+        assert L.fwd_f16x3()
+        slot = _amax_out(dst)
+        L.check(_lib().fg_in_bwd_presplit(view(gsrc), fold_pad, view(gadd), view(src), L.ptr(mean), L.ptr(rstd), act,
+                                          view(dst), L.ptr(bias_grad), int(bias_accumulate), view(gsum), L.ptr(work),
+                                          L.ptr(slot), L.stream_handle()), "in_bwd_presplit")
+        _mark_presplit(dst)
+        return
     L.check(_lib().fg_in_bwd(view(gsrc), fold_pad, view(gadd), view(src), L.ptr(mean), L.ptr(rstd), act, view(dst),
                              L.ptr(bias_grad), int(bias_accumulate), view(gsum), L.ptr(work),
                              L.ptr(_amax_out(dst)), L.stream_handle()), "in_bwd")

@@ -101,7 +101,19 @@ typedef struct fg_conv_problem {
                              consecutive rows rb = m / 32 and column n < n_out, (mean, M2) of the 32
                              stored values at in_stats[(rb * n_out + n) * 2] -- combined per image by
                              fg_in_stats_partials                                                   */
+    int x_presplit;       /* 1: x holds the PRE-SPLIT f16x3 format (FG_PRESPLIT below) written by
+                             fg_in_apply_presplit / fg_in_bwd_presplit, whose scale is the pow2 scale
+                             of x_absmax; the pipelined kernel reads its fragments as they stand (no
+                             split).  Only the pipelined f16x3 kernel takes such problems.          */
 } fg_conv_problem;
+
+/*
+ * FG_PRESPLIT: an NHWC fp32-sized buffer whose every 8-channel group of a pixel holds, in its 32 bytes,
+ * the fp16 pieces h[0..7] then l[0..7] of v*s = h + l (h = fp16(v*s), l = fp16(v*s - h)) for the group's
+ * 8 channels, s = 2^(14-e) the power-of-two scale of the tensor's scale slot (max < 2^e): the operand the
+ * f16x3 kernels would otherwise split on the fly, produced once by the norm pass that writes it.
+ * Channel counts are multiples of 8.
+ */
 
 /*
  * Weight-gradient problem: out[split][a][k] = sum_{m in split} p[row_p(m) + a] * x[row_x(m) + koff(k)]
@@ -119,6 +131,8 @@ typedef struct fg_wgrad_problem {
     int splits, m_chunk;
     const float* p_absmax;   /* f16x3: absmax slots bounding |p|, |x| over the elements read */
     const float* x_absmax;
+    int p_presplit, x_presplit;   /* 1: p / x in the FG_PRESPLIT format (scale = pow2 of its absmax slot;
+                                     pipelined f16x3 weight-gradient kernel only)                     */
 } fg_wgrad_problem;
 
 /* Maps packed-K coordinates to PyTorch weight coordinates (see fg_pack_weight). */
@@ -345,6 +359,21 @@ int fg_in_apply(fg_view src, const float* mean, const float* rstd, int act, fg_v
 int fg_in_bwd(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, const float* mean,
               const float* rstd, int act, fg_view dst, float* bias_grad, int bias_accumulate, fg_view gsum,
               double* work, float* absmax, hipStream_t stream);
+
+/* fg_in_apply without residual whose dst is written in the FG_PRESPLIT format (C % 8 == 0, 32-B aligned):
+ * the f16x3 pieces of act(xhat) at the static scale of |xhat| <= sqrt(HW - 1) (Samuelson), which the call
+ * publishes in scale_slot (a zeroed absmax slot) -- the slot the consuming conv / weight gradient reads as
+ * x_absmax.  Saves the consumer's on-the-fly split (a resblock's conv1 -> conv2 hop). */
+int fg_in_apply_presplit(fg_view src, const float* mean, const float* rstd, int act, fg_view dst, int pad_mode,
+                         float* scale_slot, hipStream_t stream);
+
+/* fg_in_bwd whose dst is written in the FG_PRESPLIT format: the statistics pass also takes max |g'| per
+ * image, the coefficient pass bounds |dst| per plane by rstd (max|g'| + |mean g'| + sqrt(HW-1) |mean g'xhat|)
+ * and publishes the bound in scale_slot (a zeroed absmax slot), the apply pass writes the pieces at its
+ * scale (the input of the next input-gradient conv and the weight gradient's gradient operand). */
+int fg_in_bwd_presplit(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, const float* mean,
+                       const float* rstd, int act, fg_view dst, float* bias_grad, int bias_accumulate, fg_view gsum,
+                       double* work, float* scale_slot, hipStream_t stream);
 
 
 /* g *= act'(y) in place over the interior (y = saved activation output).  absmax (optional absmax slot,

@@ -533,6 +533,111 @@ def test_fused_in_stats(case, conv_math):
     assert nrel(st[1].view(N, co), (var + 1e-5).rsqrt()) < KTOL
 
 
+def _decode_presplit(B, slot):
+    """values of a FG_PRESPLIT buffer (include/floodgan.h): per 8 channels h[8] | l[8] of v * s, s the pow2
+    scale of the slot's max (pow2_of in conv_common.hpp)"""
+    import math
+    e = math.frexp(float(slot.max()))[1]
+    s = 2.0 ** (14 - e)
+    hl = B.t.view(torch.float16).view(-1, 2, 8).double()
+    return ((hl[:, 0] + hl[:, 1]) / s).reshape(-1), s
+
+
+@pytest.mark.parametrize("act,fold,C,H,W,gadd", [(1, 1, 256, 16, 20, True), (0, 1, 256, 12, 12, False),
+                                                 (1, 0, 64, 9, 13, False), (0, 0, 128, 8, 8, True)])
+def test_presplit_norm_outputs(act, fold, C, H, W, gadd):
+    """fg_in_apply_presplit / fg_in_bwd_presplit: the FG_PRESPLIT pieces decode to the fp32 passes' outputs within
+    the pieces' 22-bit precision (plus the fp16 subnormal floor at the scale), and the published scale slot bounds
+    the output (the f16x3 convs derive their scale from it)"""
+    from floodgan import ops
+    from floodgan.plans import Buf
+    torch.manual_seed(5)
+    c = torch.randn(2, C, H, W, dtype=torch.float64) * 1.5 + 0.3
+    cb = buf_from(c, 0, "constant")
+    mean, rstd = ops.in_stats(cb)
+    pad = max(fold, 1)
+    ref = Buf.empty(2, H, W, C, pad, DEV)
+    ops.in_apply(cb, mean, rstd, act, None, ref, 1 if fold else 0)
+    ps = Buf.empty(2, H, W, C, pad, DEV)
+    ops.in_apply(cb, mean, rstd, act, None, ps, 1 if fold else 0, presplit=True)
+    assert ops.is_presplit(ps) and not ops.is_presplit(ref)
+    torch.cuda.synchronize()
+    dec, s = _decode_presplit(ps, ps.t._fg_amax)
+    r = ref.t.double()
+    assert float(ps.t._fg_amax.max()) >= float(r.abs().max())
+    assert bool(((dec - r).abs() <= 2.0 ** -21 * r.abs() + 4 * 2.0 ** -24 / s).all())
+    # backward (fold / gadd / gsum as the resblock uses them)
+    gsrc = Buf(buf_from(torch.randn(2, C, H + 2 * fold, W + 2 * fold, dtype=torch.float64), 0, "constant").t,
+               2, H + 2 * fold, W + 2 * fold, C, 0)
+    gab = buf_from(torch.randn(2, C, H, W, dtype=torch.float64), 0, "constant") if gadd else None
+    outs = []
+    for presplit in (False, True):
+        g = Buf.empty(2, H, W, C, 2, DEV)
+        gs = Buf.empty(2, H, W, C, 0, DEV) if gadd else None
+        bias_g = torch.zeros(C, device=DEV)
+        ops.in_bwd(gsrc, fold, gab, cb, mean, rstd, act, g, bias_g, gsum=gs, presplit=presplit)
+        outs.append((g, gs, bias_g))
+    torch.cuda.synchronize()
+    (gr, gsr, br), (gp, gsp, bp) = outs
+    dec, s = _decode_presplit(gp, gp.t._fg_amax)
+    r = gr.t.double()
+    assert float(gp.t._fg_amax.max()) >= float(r.abs().max())
+    assert bool(((dec - r).abs() <= 2.0 ** -21 * r.abs() + 4 * 2.0 ** -24 / s).all())
+    assert torch.equal(br, bp)
+    if gadd:
+        assert torch.equal(gsr.t, gsp.t)
+
+
+@pytest.mark.parametrize("N,H", [(2, 16), (1, 24)])
+def test_presplit_resblock_convs(N, H):
+    """The resblock convs on FG_PRESPLIT operands (the pipelined forward, its input-gradient interior + edge strips,
+    the pipelined weight gradient with pre-split gradient and / or activation) vs fp64, and vs the same convs on the
+    fp32 buffers"""
+    from floodgan import executor as X, ops, plans as PL
+    from floodgan.plans import Buf
+    C = 256
+    torch.manual_seed(7)
+    c = torch.randn(N, C, H, H, dtype=torch.float64)
+    w = torch.randn(C, C, 3, 3, dtype=torch.float64) * 0.03
+    P = {"conv.weight": w.float().to(DEV), "conv.bias": torch.zeros(C, device=DEV)}
+    cb = buf_from(c, 0, "constant")
+    mean, rstd = ops.in_stats(cb)
+    xs = {}
+    for presplit in (False, True):
+        xb = Buf.empty(N, H, H, C, 1, DEV)
+        ops.in_apply(cb, mean, rstd, 1, None, xb, 1, presplit=presplit)
+        xs[presplit] = xb
+    x64 = F.relu(F.instance_norm(c, eps=1e-5))
+    y64 = F.conv2d(F.pad(x64, (1,) * 4, mode="reflect"), w)
+    gy64 = torch.randn_like(y64)
+    # gradient operand: the fp32 / pre-split outputs of one norm backward (act none, no fold)
+    gsrc = buf_from(gy64, 0, "constant")
+    gys = {}
+    for presplit in (False, True):
+        g = Buf.empty(N, H, H, C, 2, DEV)
+        ops.in_bwd(gsrc, 0, None, cb, mean, rstd, 0, g, None, presplit=presplit)
+        gys[presplit] = g
+    gref = nchw(gys[False]).double()
+    gx64, gw64 = torch.autograd.grad(F.conv2d(F.pad(x64.requires_grad_(True), (1,) * 4, mode="reflect"),
+                                              w.requires_grad_(True)), (x64, w), gref)
+    res = {}
+    for presplit in (False, True):
+        Y = Buf.empty(N, H, H, C, 0, DEV)
+        X._conv_fwd(P, "conv", xs[presplit], 1, 3, 1, Y)
+        dw = torch.empty(C, C, 3, 3, device=DEV)
+        ops.wgrad(PL.wgrad_conv(gys[presplit], xs[presplit], 1, 3, 1, C), PL.wmap_wgrad(w.shape, True, C, 3), dw)
+        dw_p = torch.empty(C, C, 3, 3, device=DEV)      # gradient pre-split, activation fp32
+        ops.wgrad(PL.wgrad_conv(gys[presplit], xs[False], 1, 3, 1, C), PL.wmap_wgrad(w.shape, True, C, 3), dw_p)
+        gxp = X._dgrad_s1_padded(P, "conv", gys[presplit])
+        torch.cuda.synchronize()
+        res[presplit] = (nchw(Y), dw.cpu(), dw_p.cpu(), _fold_cpu(nchw(gxp).double(), 1))
+    for presplit in (False, True):
+        y, dw, dw_p, gx = res[presplit]
+        assert nrel(y, y64) < KTOL and nrel(dw, gw64) < KTOL and nrel(dw_p, gw64) < KTOL and nrel(gx, gx64) < KTOL
+    for a, b in zip(res[False], res[True]):
+        assert nrel(b, a) < 2e-6
+
+
 def test_fused_in_stats_declined():
     """a conv the epilogue statistics cannot cover (output rows per image not a multiple of 32, e.g. the
     discriminator's 4x4 stride-1 conv) returns None and the caller computes the statistics itself"""
