@@ -65,6 +65,10 @@ __device__ __forceinline__ void dma_stage(char* sb, int wave, __amdgpu_buffer_rs
                                                  soff_b, 0, 0);
 }
 
+// output buffer resource: byte offsets below kYRecords are stored, kYOOB is dropped (the host keeps every output
+// extent below kYRecords, f3_takes)
+constexpr int kYRecords = 0x7fffff00, kYOOB = 0x7ffffff0;
+
 // one 1-KiB LDS-DMA piece (per-lane byte offset, per-stage scalar offset)
 __device__ __forceinline__ void dma_piece(char* dst, __amdgpu_buffer_rsrc_t r, int voff, int soff) {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)dst, 16, voff, soff, 0, 0);
@@ -72,23 +76,8 @@ __device__ __forceinline__ void dma_piece(char* dst, __amdgpu_buffer_rsrc_t r, i
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
-    static_assert(N >= 0 && N <= 15, "vmcnt immediate");
-    if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-    else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-    else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-    else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else if constexpr (N == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
-    else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if constexpr (N == 9) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
-    else if constexpr (N == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-    else if constexpr (N == 11) asm volatile("s_waitcnt vmcnt(11)" ::: "memory");
-    else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-    else if constexpr (N == 13) asm volatile("s_waitcnt vmcnt(13)" ::: "memory");
-    else if constexpr (N == 14) asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
-    else if constexpr (N == 15) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+    static_assert(N >= 0 && N <= 63, "vmcnt immediate (6 bits)");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
 // SCH selects the per-stage instruction order: 0 = read+split all of A, then the three products
@@ -437,6 +426,7 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
     };
 
     // ---- epilogue of the compute tile: scale, bias, activation, strided store (or accumulate)
+    int issued = 0, done = 0, epi_issued = 0;
     auto epilogue = [&]() {
         const fg_conv_problem& P = batch.p[cg.pi];
         const int mab = P.m_a * P.m_b, M = P.m_img * mab;
@@ -505,6 +495,13 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
                 }
             }
         }
+        // the stores: TM x 4 x TN buffer stores per lane, ALWAYS issued (rows past M / columns past n_out get an
+        // out-of-range offset, which the hardware drops), so the stage waits after this epilogue can leave
+        // exactly that many younger VMEM operations in flight (see wait_stage) instead of draining them
+        const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc((void*)P.y, 0, kYRecords, 0x00020000);
+        int coff[TN];
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) coff[tn] = ncol[tn] * (int)P.syc;
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm) {
             // the lane's 4 consecutive rows: one decomposition, then (b, a, img) advanced with wrap-around
@@ -519,19 +516,18 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
                         if (++a == P.m_a) { a = 0; ++img; }
                     }
                 }
-                const int m = m0 + reg;
-                if (m >= M) continue;
-                float* yrow = P.y + img * P.syn + a * P.sya + b * P.syb;
+                const bool row_ok = m0 + reg < M;
+                const int roff = img * (int)P.syn + a * (int)P.sya + b * (int)P.syb;
 #pragma unroll
                 for (int tn = 0; tn < TN; ++tn) {
-                    if (!full_n && ncol[tn] >= P.n_out) continue;
+                    const bool ok = row_ok && (full_n || ncol[tn] < P.n_out);
                     float v = fg::act_fwd(acc[tm][tn][reg] * out_scale + bias_v[tn], act);
-                    float* dst = yrow + ncol[tn] * P.syc;
-                    if (accum) v += *dst;
-                    *dst = v;
+                    if (accum && ok) v += P.y[roff + coff[tn]];
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), yr, ok ? (roff + coff[tn]) * 4 : kYOOB, 0, 0);
                 }
             }
         }
+        epi_issued = issued;
     };
 
     // ---- NS-deep ring over the stage stream: stage s+NS-1 is issued right after the barrier that
@@ -541,14 +537,24 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
     if (first >= total_tiles) return;
     setup_issue();
     setup_compute();
-    int issued = 0, done = 0;
 #pragma unroll
     for (int s0 = 0; s0 < NS - 1; ++s0)
         if (issue_next(s0)) ++issued;
     int cur = 0, nxt = NS - 1;
-    while (true) {
-        if (NS == 3 && issued - done >= 2) wait_vmcnt<NS == 3 ? A_GL + B_GL : 0>();
+    // wait for stage `done`'s own DMAs: the VMEM operations younger than them are the stages issued after it
+    // and, when stage `done` was issued before the last epilogue, that epilogue's NST stores (vmcnt counts
+    // loads, LDS-DMA and stores together, in issue order).  Any smaller count is safe (it waits for more).
+    constexpr int D = A_GL + B_GL, NST = TM * 4 * TN;
+    constexpr int W1 = D < 63 ? D : 63, WS = NST < 63 ? NST : 63, WSD = NST + D < 63 ? NST + D : 63;
+    auto wait_stage = [&]() {
+        const int younger = (issued - done - 1) * D + (done < epi_issued ? NST : 0);
+        if (younger >= NST + D) wait_vmcnt<WSD>();
+        else if (younger >= NST) wait_vmcnt<WS>();
+        else if (younger >= D) wait_vmcnt<W1>();
         else wait_vmcnt<0>();
+    };
+    while (true) {
+        wait_stage();
 #ifdef FG_F3_DIAG
         if (!((alt_order >> 7) & 1))                     // diag bit 3: no barrier (timing only)
 #endif
@@ -584,6 +590,9 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
         cur = cur == NS - 1 ? 0 : cur + 1;
         nxt = nxt == NS - 1 ? 0 : nxt + 1;
         if (++ckt == cg.nkt) {
+#ifdef FG_F3_DIAG
+            if (!((alt_order >> 8) & 1))                 // diag bit 4: no epilogue (timing only)
+#endif
             epilogue();
 #pragma unroll
             for (int tm = 0; tm < TM; ++tm)
@@ -741,6 +750,10 @@ bool f3_takes(const fg_conv_problem* probs, int nprob, int max_n) {
     for (int i = 0; i < nprob; ++i) {
         const fg_conv_problem& p = probs[i];
         if ((p.x_presplit != 0) != (probs[0].x_presplit != 0) || (p.x_presplit && !presplit_ok(p))) return false;
+        // the epilogue's buffer stores address the output with 31-bit byte offsets
+        const long long yext = 4 * ((long long)(p.m_img - 1) * p.syn + (long long)(p.m_a - 1) * p.sya +
+                                    (long long)(p.m_b - 1) * p.syb + (long long)(p.n_out - 1) * p.syc + 1);
+        if (p.syn < 0 || p.sya < 0 || p.syb < 0 || p.syc < 0 || yext >= kYRecords) return false;
         // no K padding (every staged k is a real tap: padded j would gather past the row run); ldw may exceed
         // kh * jp (a kernel-row range of a larger pack: the resblock input gradient's row strips)
         if (p.w_split != 2 || p.jp % 32 || p.j_valid != p.jp || p.ldw < p.kh * p.jp || !p.x_absmax || !p.w_absmax ||

@@ -276,16 +276,25 @@ int launch_wgrad_f3(const fg_wgrad_problem& p, hipStream_t stream, int* rc) {
     const dim3 grid(ta * tk * p.splits);
     const int ps = (p.p_presplit ? 1 : 0) | (p.x_presplit ? 2 : 0);
     if (ps) {
-        // whole 8-channel groups at 32-B aligned bases (FG_PRESPLIT); the 256-row tile, staging schedule 0
-        if (TA != 256 || p.n_a % 8 || p.j_valid % 8 || (p.p_presplit && (((uintptr_t)p.p & 31) || (p.spn | p.spa | p.spb) % 8)) ||
+        // whole 8-channel groups at 32-B aligned bases (FG_PRESPLIT); the measured staging schedule per tile
+        if (p.n_a % 8 || p.j_valid % 8 || (p.p_presplit && (((uintptr_t)p.p & 31) || (p.spn | p.spa | p.spb) % 8)) ||
             (p.x_presplit && (((uintptr_t)p.x & 31) || (p.sxn | p.sxa | p.sxb | p.sxr) % 8)))
             return 0;
-        if (ps == 1)
-            hipLaunchKernelGGL((conv_wgrad_f3_kernel<256, 0, 1>), grid, dim3(512), 0, stream, p, ta, tk);
-        else if (ps == 2)
-            hipLaunchKernelGGL((conv_wgrad_f3_kernel<256, 0, 2>), grid, dim3(512), 0, stream, p, ta, tk);
-        else
-            hipLaunchKernelGGL((conv_wgrad_f3_kernel<256, 0, 3>), grid, dim3(512), 0, stream, p, ta, tk);
+        if (TA == 256) {
+            if (ps == 1)
+                hipLaunchKernelGGL((conv_wgrad_f3_kernel<256, 0, 1>), grid, dim3(512), 0, stream, p, ta, tk);
+            else if (ps == 2)
+                hipLaunchKernelGGL((conv_wgrad_f3_kernel<256, 0, 2>), grid, dim3(512), 0, stream, p, ta, tk);
+            else
+                hipLaunchKernelGGL((conv_wgrad_f3_kernel<256, 0, 3>), grid, dim3(512), 0, stream, p, ta, tk);
+        } else {
+            if (ps == 1)
+                hipLaunchKernelGGL((conv_wgrad_f3_kernel<128, 1, 1>), grid, dim3(512), 0, stream, p, ta, tk);
+            else if (ps == 2)
+                hipLaunchKernelGGL((conv_wgrad_f3_kernel<128, 1, 2>), grid, dim3(512), 0, stream, p, ta, tk);
+            else
+                hipLaunchKernelGGL((conv_wgrad_f3_kernel<128, 1, 3>), grid, dim3(512), 0, stream, p, ta, tk);
+        }
         *rc = fg::launched("conv_wgrad_f3_presplit");
         return 1;
     }

@@ -176,10 +176,11 @@ def gen_forward(P, x, save=True, x_extra=None):
     ops.pack_input(x, Cin, x_extra, Ce, X0, 0, N, FG_PAD_REFLECT)             # F.pad(input, 3, reflect)
     c1 = Buf.empty(N, H, W, 64, 0, dev)
     st = _conv_fwd(P, "conv1", X0, 3, 7, 1, c1, in_stats=True)
-    m1, r1, a1 = _norm(c1, FG_ACT_RELU, 1, FG_PAD_ZERO, stats=st)
+    ps = ops.presplit_on()     # norm outputs read only by pipelined convs / weight gradients: FG_PRESPLIT
+    m1, r1, a1 = _norm(c1, FG_ACT_RELU, 1, FG_PAD_ZERO, stats=st, presplit=ps)
     c2 = Buf.empty(N, H // 2, W // 2, 128, 0, dev)
     st = _conv_fwd(P, "conv2", a1, 1, 3, 2, c2, in_stats=True)
-    m2, r2, a2 = _norm(c2, FG_ACT_RELU, 1, FG_PAD_ZERO, stats=st)
+    m2, r2, a2 = _norm(c2, FG_ACT_RELU, 1, FG_PAD_ZERO, stats=st, presplit=ps)
     c3 = Buf.empty(N, H // 4, W // 4, 256, 0, dev)
     st = _conv_fwd(P, "conv3", a2, 1, 3, 2, c3, in_stats=True)
     m3, r3, h = _norm(c3, FG_ACT_RELU, 1, FG_PAD_REFLECT, stats=st)
@@ -196,7 +197,7 @@ def gen_forward(P, x, save=True, x_extra=None):
     for tag, pad2, mode2 in (("content", 3, FG_PAD_REFLECT), ("attention", 0, FG_PAD_ZERO))[:1 + attention]:
         d1 = Buf.empty(N, H // 2, W // 2, 128, 0, dev)
         st = _convT_fwd(P, f"deconv1_{tag}", h, d1)
-        md1, rd1, ad1 = _norm(d1, FG_ACT_RELU, 1, FG_PAD_ZERO, stats=st)
+        md1, rd1, ad1 = _norm(d1, FG_ACT_RELU, 1, FG_PAD_ZERO, stats=st, presplit=ps)
         d2 = Buf.empty(N, H, W, 64, 0, dev)
         st = _convT_fwd(P, f"deconv2_{tag}", ad1, d2)
         md2, rd2, ad2 = _norm(d2, FG_ACT_RELU, pad2, mode2, stats=st)
@@ -408,10 +409,11 @@ def gen_backward(P, S, g_out, grads_into=None, ready=None, input_grad=None, accu
         heads.append(("attention", ha, g_ad2a, 0))
     # ---- deconv2 / deconv1 of both heads
     g_h = Buf.empty(N, H // 4, W // 4, 256, 0, dev)
+    ps = ops.presplit_on()     # conv-output gradients read only by pipelined convs / weight gradients
     for idx, (tag, hd, g_ad2, fold) in enumerate(heads):
         g_d2 = Buf.empty(N, H, W, 64, 1, dev)
         ops.in_bwd(g_ad2, fold, None, hd["d2"], hd["md2"], hd["rd2"], FG_ACT_RELU, g_d2,
-                   G.get(f"deconv2_{tag}.bias"), G.acc)
+                   G.get(f"deconv2_{tag}.bias"), G.acc, presplit=ps)
         name = f"deconv2_{tag}"
         w = P[name + ".weight"]
         G.wgrad(PL.wgrad_convT(hd["ad1"], g_d2, 3, 1, w.shape[0]), PL.wmap_wgrad(w.shape, True, g_d2.c, 3),
@@ -421,7 +423,7 @@ def gen_backward(P, S, g_out, grads_into=None, ready=None, input_grad=None, accu
         ops.conv([PL.conv_problem(g_d2, 1, 3, 2, ops.pack_weight(w, m), m, g_ad1)])
         g_d1 = Buf.empty(N, H // 2, W // 2, 128, 1, dev)
         ops.in_bwd(g_ad1, 0, None, hd["d1"], hd["md1"], hd["rd1"], FG_ACT_RELU, g_d1, G.get(f"deconv1_{tag}.bias"),
-                   G.acc)
+                   G.acc, presplit=ps)
         name = f"deconv1_{tag}"
         w = P[name + ".weight"]
         G.wgrad(PL.wgrad_convT(S["h"], g_d1, 3, 1, w.shape[0]), PL.wmap_wgrad(w.shape, True, g_d1.c, 3),
@@ -436,12 +438,13 @@ def gen_backward(P, S, g_out, grads_into=None, ready=None, input_grad=None, accu
         G.ready(ready, _blk(i, 1))
     # ---- encoder (the first block's input gradient, fold + residual, gathered by conv3's norm backward)
     g_c3 = Buf.empty(N, H // 4, W // 4, 256, 1, dev)
-    ops.in_bwd(grad[0], grad[1], grad[2], S["c3"], S["m3"], S["r3"], FG_ACT_RELU, g_c3, G.get("conv3.bias"), G.acc)
+    ops.in_bwd(grad[0], grad[1], grad[2], S["c3"], S["m3"], S["r3"], FG_ACT_RELU, g_c3, G.get("conv3.bias"), G.acc,
+               presplit=ps)
     _wgrad_conv(P, G, "conv3", g_c3, S["a2"], 1, 3, 2)
     g_a2 = Buf.empty(N, H // 2, W // 2, 128, 0, dev)
     _dgrad_s2(P, "conv3", g_c3, 3, Y=g_a2)
     g_c2 = Buf.empty(N, H // 2, W // 2, 128, 1, dev)
-    ops.in_bwd(g_a2, 0, None, S["c2"], S["m2"], S["r2"], FG_ACT_RELU, g_c2, G.get("conv2.bias"), G.acc)
+    ops.in_bwd(g_a2, 0, None, S["c2"], S["m2"], S["r2"], FG_ACT_RELU, g_c2, G.get("conv2.bias"), G.acc, presplit=ps)
     _wgrad_conv(P, G, "conv2", g_c2, S["a1"], 1, 3, 2)
     g_a1 = Buf.empty(N, H, W, 64, 0, dev)
     _dgrad_s2(P, "conv2", g_c2, 3, Y=g_a1)
@@ -460,32 +463,34 @@ def gen_backward(P, S, g_out, grads_into=None, ready=None, input_grad=None, accu
     return G.out
 
 
-def _decided(B, lo=0, hi=None):
+def _decided(B, lo=0, hi=None, pre=None, mean=None):
     """activation decisions of an activation-output Buf (output > 0 <=> input > 0 for ReLU and
-    LeakyReLU): NCHW bool on the host"""
+    LeakyReLU): NCHW bool on the host.  A pre-split output (FG_PRESPLIT) is decided from the norm's input
+    `pre` and `mean` instead: act((c - mean) * rstd) > 0 <=> c > mean (rstd > 0; fp32 subtraction keeps the
+    sign)."""
+    if ops.is_presplit(B):
+        d = pre.interior() > mean.view(pre.n, 1, 1, pre.c)
+        return d[lo:hi].permute(0, 3, 1, 2).contiguous().cpu()
     return (B.interior()[lo:hi] > 0).permute(0, 3, 1, 2).contiguous().cpu()
 
 
 def gen_act_decisions(S):
     """The generator's ReLU decisions in a saved forward, keyed by the oracle's layer names (test
     instrumentation: oracle ActDecisions teacher-forces them to compare gradients at full size)."""
-    out = {"conv1": _decided(S["a1"]), "conv2": _decided(S["a2"]), "conv3": _decided(S["blocks"][0]["h"])}
+    out = {"conv1": _decided(S["a1"], pre=S["c1"], mean=S["m1"]), "conv2": _decided(S["a2"], pre=S["c2"], mean=S["m2"]),
+           "conv3": _decided(S["blocks"][0]["h"])}
     for i, b in enumerate(S["blocks"]):
-        if ops.is_presplit(b["rb"]):
-            # relu((c - mean) * rstd) > 0 <=> c > mean (rstd > 0; fp32 subtraction keeps the sign)
-            cb, mean = b["cb1"], b["mb1"]
-            out[f"block{i}"] = (cb.interior() > mean.view(cb.n, 1, 1, cb.c)).permute(0, 3, 1, 2).contiguous().cpu()
-        else:
-            out[f"block{i}"] = _decided(b["rb"])
+        out[f"block{i}"] = _decided(b["rb"], pre=b["cb1"], mean=b["mb1"])
     for tag, hd in S["heads"].items():
-        out[f"deconv1_{tag}"], out[f"deconv2_{tag}"] = _decided(hd["ad1"]), _decided(hd["ad2"])
+        out[f"deconv1_{tag}"] = _decided(hd["ad1"], pre=hd["d1"], mean=hd["md1"])
+        out[f"deconv2_{tag}"] = _decided(hd["ad2"])
     return out
 
 
 def disc_act_decisions(S, lo=0, hi=None):
     """The discriminator's LeakyReLU decisions for images lo..hi of a saved forward (test instrumentation)"""
-    return {"model.0": _decided(S["e0"], lo, hi), "model.2": _decided(S["a1"], lo, hi),
-            "model.5": _decided(S["a2"], lo, hi), "model.8": _decided(S["a3"], lo, hi)}
+    return {"model.0": _decided(S["e0"], lo, hi), "model.2": _decided(S["a1"], lo, hi, S["e1"], S["m1"]),
+            "model.5": _decided(S["a2"], lo, hi, S["e2"], S["m2"]), "model.8": _decided(S["a3"], lo, hi)}
 
 
 # ======================================================================================
@@ -522,11 +527,12 @@ def disc_forward(P, inp, save=True):
     h2, w2 = PL.out_size(h1, 4, 2, 1), PL.out_size(w1, 4, 2, 1)
     e1 = Buf.empty(N, h2, w2, 128, 0, dev)
     st = _conv_fwd(P, "model.2", e0, 1, 4, 2, e1, in_stats=True)
-    m1, r1, a1 = _norm(e1, FG_ACT_LRELU, 1, FG_PAD_ZERO, stats=st)
+    ps = ops.presplit_on()     # a1, a2 are read only by pipelined convs / weight gradients: FG_PRESPLIT
+    m1, r1, a1 = _norm(e1, FG_ACT_LRELU, 1, FG_PAD_ZERO, stats=st, presplit=ps)
     h3, w3 = PL.out_size(h2, 4, 2, 1), PL.out_size(w2, 4, 2, 1)
     e2 = Buf.empty(N, h3, w3, 256, 0, dev)
     st = _conv_fwd(P, "model.5", a1, 1, 4, 2, e2, in_stats=True)
-    m2, r2, a2 = _norm(e2, FG_ACT_LRELU, 1, FG_PAD_ZERO, stats=st)
+    m2, r2, a2 = _norm(e2, FG_ACT_LRELU, 1, FG_PAD_ZERO, stats=st, presplit=ps)
     h4, w4 = PL.out_size(h3, 4, 1, 1), PL.out_size(w3, 4, 1, 1)
     e3 = Buf.empty(N, h4, w4, 512, 0, dev)
     st = _conv_fwd(P, "model.8", a2, 1, 4, 1, e3, in_stats=True)
@@ -564,8 +570,9 @@ def disc_backward(P, S, g_pred, param_grads=True, grads_into=None, input_grad=No
     _dgrad_s1(P, "model.11", g11, 2, 4, g_a3)
     # model.8 (k4 s1 p1) + IN + LReLU
     g_e3 = Buf.empty(N, a3.h, a3.w, 512, 2, dev)
+    ps = ops.presplit_on()     # the conv-output gradients feed only pipelined convs / weight gradients
     ops.in_bwd(g_a3, 0, None, S["e3"], S["m3"], S["r3"], FG_ACT_LRELU, g_e3,
-               G.get("model.8.bias") if param_grads else None)
+               G.get("model.8.bias") if param_grads else None, presplit=ps)
     a2 = S["a2"]
     if param_grads:
         _wgrad_conv(P, G, "model.8", g_e3, a2, 1, 4, 1)
@@ -575,7 +582,7 @@ def disc_backward(P, S, g_pred, param_grads=True, grads_into=None, input_grad=No
     # model.5 (k4 s2 p1)
     g_e2 = Buf.empty(N, a2.h, a2.w, 256, 1, dev)
     ops.in_bwd(g_a2, 0, None, S["e2"], S["m2"], S["r2"], FG_ACT_LRELU, g_e2,
-               G.get("model.5.bias") if param_grads else None)
+               G.get("model.5.bias") if param_grads else None, presplit=ps)
     a1 = S["a1"]
     if param_grads:
         _wgrad_conv(P, G, "model.5", g_e2, a1, 1, 4, 2)
@@ -585,7 +592,7 @@ def disc_backward(P, S, g_pred, param_grads=True, grads_into=None, input_grad=No
     # model.2
     g_e1 = Buf.empty(N, a1.h, a1.w, 128, 1, dev)
     ops.in_bwd(g_a1, 0, None, S["e1"], S["m1"], S["r1"], FG_ACT_LRELU, g_e1,
-               G.get("model.2.bias") if param_grads else None)
+               G.get("model.2.bias") if param_grads else None, presplit=ps)
     e0 = S["e0"]
     if param_grads:
         _wgrad_conv(P, G, "model.2", g_e1, e0, 1, 4, 2)
