@@ -441,24 +441,28 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
         }
         const bool full_n = cg.n0 + BN <= P.n_out;
         if (STATS && P.in_stats) {
-            // InstanceNorm partials of this wave's 32-row block (WM = 32: tm x g x reg), per column: two
-            // passes (mean, then M2) over the raw accumulators, each reduced over the 4 lanes of the column
-            // (g); out_scale (a power of 2) and the bias are applied to the results.  Columns go in groups of
-            // SG so that a group's cross-lane exchanges are in flight together
-            const int rb0 = cg.m0 + wm * WM;
+            // InstanceNorm partials of each 32-row block of this wave's rows (WM / 32 of them: tm blocks
+            // hb*TB .. hb*TB+TB-1, x g x reg), per column: two passes (mean, then M2) over the raw accumulators, each
+            // reduced over the 4 lanes of the column (g); out_scale (a power of 2) and the bias are applied to the
+            // results.  Columns go in groups of SG so that a group's cross-lane exchanges are in flight together
+            constexpr int NB = WM / 32, TB = TM / NB;
+            static_assert(WM % 32 == 0 && TB * 16 == 32, "32-row statistics blocks");
+#pragma unroll
+            for (int hb = 0; hb < NB; ++hb) {
+            const int rb0 = cg.m0 + wm * WM + hb * 32;
             if (rb0 < M) {
                 constexpr int SG = TN < 4 ? TN : 4;
                 const float sc = out_scale;
-                float* const dst0 = P.in_stats + (size_t)(rb0 / WM) * P.n_out * 2;
+                float* const dst0 = P.in_stats + (size_t)(rb0 / 32) * P.n_out * 2;
 #pragma unroll
                 for (int t0 = 0; t0 < TN; t0 += SG) {
                     float sm[SG], sq[SG];
 #pragma unroll
                     for (int u = 0; u < SG; ++u) {
-                        f32x2 s2 = f32x2{acc[0][t0 + u][0], acc[0][t0 + u][1]} +
-                                   f32x2{acc[0][t0 + u][2], acc[0][t0 + u][3]};
+                        f32x2 s2 = f32x2{acc[hb * TB][t0 + u][0], acc[hb * TB][t0 + u][1]} +
+                                   f32x2{acc[hb * TB][t0 + u][2], acc[hb * TB][t0 + u][3]};
 #pragma unroll
-                        for (int tm = 1; tm < TM; ++tm)
+                        for (int tm = hb * TB + 1; tm < hb * TB + TB; ++tm)
                             s2 += f32x2{acc[tm][t0 + u][0], acc[tm][t0 + u][1]} +
                                   f32x2{acc[tm][t0 + u][2], acc[tm][t0 + u][3]};
                         sm[u] = s2[0] + s2[1];
@@ -469,15 +473,15 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
                     for (int u = 0; u < SG; ++u) sm[u] += __shfl_xor(sm[u], 32);
 #pragma unroll
                     for (int u = 0; u < SG; ++u) {
-                        const float mu = sm[u] * (1.f / (TM * 16));
+                        const float mu = sm[u] * (1.f / 32);
                         sm[u] = mu;
                         const f32x2 m2 = {mu, mu};
                         f32x2 q2;
 #pragma unroll
-                        for (int tm = 0; tm < TM; ++tm) {
+                        for (int tm = hb * TB; tm < hb * TB + TB; ++tm) {
                             const f32x2 d0 = f32x2{acc[tm][t0 + u][0], acc[tm][t0 + u][1]} - m2;
                             const f32x2 d1 = f32x2{acc[tm][t0 + u][2], acc[tm][t0 + u][3]} - m2;
-                            q2 = tm ? q2 + d0 * d0 + d1 * d1 : d0 * d0 + d1 * d1;
+                            q2 = tm > hb * TB ? q2 + d0 * d0 + d1 * d1 : d0 * d0 + d1 * d1;
                         }
                         sq[u] = q2[0] + q2[1];
                     }
@@ -493,6 +497,7 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
                                     f32x2{sm[u] * sc + bias_v[t0 + u], sq[u] * (sc * sc)};
                     }
                 }
+            }
             }
         }
         // the stores: TM x 4 x TN buffer stores per lane, ALWAYS issued (rows past M / columns past n_out get an
@@ -655,16 +660,14 @@ int launch_cfg(const ConvBatch& in, int nprob, hipStream_t stream) {
     // pre-split A operands (every problem of the batch, checked by the caller): their own instantiations
     // (WM = 32 configs, default order)
     if (b.p[0].x_presplit) {
-        if constexpr (WM == 32) {
-            if (stats)
-                hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 3, true, true>), dim3(grid), dim3(NT), 0,
-                                   stream, b, total, g_f3_alt);
-            else
-                hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 3, false, true>), dim3(grid), dim3(NT), 0,
-                                   stream, b, total, g_f3_alt);
+        if (stats) {
+            hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 3, true, true>), dim3(grid), dim3(NT), 0,
+                               stream, b, total, g_f3_alt);
             return fg::launched("conv_fwd_f3_presplit");
         }
-        return fg::fail(FG_ERR_INVALID, "conv_fwd_f3: pre-split operands need a WM = 32 tile");
+        hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 3, false, true>), dim3(grid), dim3(NT), 0, stream, b,
+                           total, g_f3_alt);
+        return fg::launched("conv_fwd_f3_presplit");
     }
     // the epilogue-statistics variant is its own instantiation (WM = 32 configs, default order), so that
     // the launches without statistics keep the plain epilogue's code
@@ -723,9 +726,16 @@ long long batch_tiles(const fg_conv_problem* p, int nprob, int bm, int bn) {
 // wave stays (D model.8's forward, 250 tiles: 322 us on cfg 4, 367 on cfg 6).  All have 32-row wave blocks.
 int g_f3_fill = 1;    // fg_set_f3_fill: 0 = keep the tile f3_config picks by N (A/B hook)
 
+int g_f3_ps_wide = 5;  // fg_set_f3_ps_wide: the N > 128 tile of pre-split operands (4: 8 waves of 32 x 256; 5: of
+                       // 64 x 128 -- a third fewer fragment bytes per MFMA, the operand needing no split: resblock
+                       // 0.371 -> 0.348 ms, profiles/round3/r3v_f3_presplit_cfg.log.  4 waves of 128 x 128 with the
+                       // accumulators in AGPRs ran 3.26 ms: not kept)
+
 int auto_cfg(const fg_conv_problem* p, int nprob, int max_n) {
     int cfg = f3_config(max_n);
-    if (g_f3_tile >= 0 || cfg < 0 || !g_f3_fill) return cfg;
+    if (g_f3_tile >= 0 || cfg < 0) return cfg;
+    if (cfg == 4 && p[0].x_presplit && 2 * batch_tiles(p, nprob, 256, 256) > fg::num_cus()) return g_f3_ps_wide;
+    if (!g_f3_fill) return cfg;
     const int cus = fg::num_cus();
     while (cfg == 4 || cfg == 6 || cfg == 7) {
         const int bn = cfg == 4 ? 256 : cfg == 6 ? 128 : 64;
@@ -743,10 +753,6 @@ bool presplit_ok(const fg_conv_problem& p) {
 
 bool f3_takes(const fg_conv_problem* probs, int nprob, int max_n) {
     if (g_f3_tile == -2 || f3_config(max_n) < 0) return false;
-    if (probs[0].x_presplit) {
-        const int cfg = auto_cfg(probs, nprob, max_n);
-        if (!(cfg == 0 || cfg == 3 || cfg == 4 || cfg == 6 || cfg == 7 || cfg == 9)) return false;   // WM = 32
-    }
     for (int i = 0; i < nprob; ++i) {
         const fg_conv_problem& p = probs[i];
         if ((p.x_presplit != 0) != (probs[0].x_presplit != 0) || (p.x_presplit && !presplit_ok(p))) return false;
@@ -763,11 +769,13 @@ bool f3_takes(const fg_conv_problem* probs, int nprob, int max_n) {
     return true;
 }
 
-// the epilogue statistics need whole 32-row wave blocks inside one image (WM = 32 in every config)
+// the epilogue statistics need whole 32-row wave blocks inside one image (WM = 32 configs; every config on pre-split
+// operands, whose instantiations take 32-row blocks of taller wave tiles)
 bool f3_stats_ok(const fg_conv_problem* probs, int nprob, int max_n) {
     if (!f3_takes(probs, nprob, max_n)) return false;
     const int cfg = auto_cfg(probs, nprob, max_n);
-    if (!(cfg == 0 || cfg == 3 || cfg == 4 || cfg == 6 || cfg == 7 || cfg == 9)) return false;   // WM = 32 configs
+    if (!probs[0].x_presplit && !(cfg == 0 || cfg == 3 || cfg == 4 || cfg == 6 || cfg == 7 || cfg == 9))
+        return false;   // WM = 32 configs
     for (int i = 0; i < nprob; ++i) {
         const fg_conv_problem& p = probs[i];
         if ((p.m_a * p.m_b) % 32 || p.act != 0 || p.accumulate) return false;
@@ -826,6 +834,12 @@ FG_API int fg_set_f3_order(int alt) {
 FG_API int fg_set_f3_interleave(int on) {
     if (on < 0 || on > 1) return fg::fail(FG_ERR_INVALID, "fg_set_f3_interleave: %d", on);
     g_f3_interleave = on;
+    return 0;
+}
+
+FG_API int fg_set_f3_ps_wide(int cfg) {
+    if (cfg != 4 && cfg != 5) return fg::fail(FG_ERR_INVALID, "fg_set_f3_ps_wide: %d", cfg);
+    fgc::g_f3_ps_wide = cfg;
     return 0;
 }
 

@@ -105,6 +105,7 @@ SIGNATURES = {
     "fg_set_f3_interleave": [C.c_int],
     "fg_set_wgrad_f3": [C.c_int],
     "fg_set_in_rows": [C.c_int],
+    "fg_set_f3_ps_wide": [C.c_int],
     "fg_conv_wgrad": [C.POINTER(fg_wgrad_problem), C.c_void_p],
     "fg_wgrad_reduce": [C.c_void_p, C.c_int, C.POINTER(fg_weight_map), C.c_void_p, C.c_int, C.c_void_p],
     "fg_pack_weight": [C.c_void_p, C.POINTER(fg_weight_map), C.c_void_p, C.c_void_p],

@@ -196,6 +196,9 @@ int fg_set_f3_persistent(int on);
 /* A/B hook: 1 (default) = a pipelined-kernel launch that would leave at least half the CUs without a tile
  * runs on narrower / shorter tiles (conv_f3.hip auto_cfg); 0 = the tile chosen by output channels only. */
 int fg_set_f3_fill(int on);
+/* A/B hook: the tile of the pipelined kernel for pre-split (FG_PRESPLIT) operands with N > 128 that fill the
+ * chip: 4 = 256x256 as 8 waves of 32x256, 5 (default) = 8 waves of 64x128. */
+int fg_set_f3_ps_wide(int cfg);
 /* A/B hook: 1 (default) = a pipelined-kernel launch of problems with equal tile counts (the four phases of a
  * transposed conv or of a stride-2 input gradient) interleaves their tiles (tile t -> problem t % count), so
  * the phases read each input row at the same time; 0 = problem after problem. */

@@ -638,6 +638,54 @@ def test_presplit_resblock_convs(N, H):
         assert nrel(b, a) < 2e-6
 
 
+@pytest.mark.parametrize("persistent", [1, 3])
+@pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("case", [(256, 256, 3, 1, 1, 20), (128, 64, 3, 2, 1, 24), (64, 128, 3, 1, 1, 17)])
+def test_presplit_f3_tiles_and_stats(case, cfg, persistent):
+    """every pipelined tile config (and the automatic choice, -1) on a FG_PRESPLIT operand, with and without the
+    InstanceNorm statistics epilogue (32-row blocks of 32- and 64-row wave tiles), ragged tiles and the
+    tile-crossing stream (persistent 3): output vs fp64, statistics vs fg_in_stats of the same output, output
+    bit-identical with and without the epilogue statistics"""
+    from floodgan import _lib as L, ops, plans as PL
+    from floodgan.plans import Buf
+    cin, cout, k, s, p, H = case
+    lib = L.load()
+    try:
+        L.set_f3_tile(cfg)
+        lib.fg_set_f3_persistent(persistent)
+        torch.manual_seed(13)
+        N = 2
+        c = torch.randn(N, cin, H, H, dtype=torch.float64) * 1.3 + 0.2
+        cb = buf_from(c, 0, "constant")
+        mean, rstd = ops.in_stats(cb)
+        X = Buf.empty(N, H, H, cin, p, DEV)
+        ops.in_apply(cb, mean, rstd, 1, None, X, 1, presplit=True)
+        x64 = F.relu(F.instance_norm(c, eps=1e-5))
+        w = torch.randn(cout, cin, k, k, dtype=torch.float64) * 0.05
+        b = torch.randn(cout, dtype=torch.float64) * 0.1
+        y64 = F.conv2d(F.pad(x64, (p,) * 4, mode="reflect"), w, b, stride=s)
+        wd = w.float().to(DEV)
+        m = PL.wmap_conv_fwd(wd.shape, cin)
+        wp = ops.pack_weight(wd, m)
+        Ho = PL.out_size(H, k, s, p)
+        Ys = []
+        for stats in (False, True):
+            Y = Buf.empty(N, Ho, Ho, cout, 0, DEV)
+            st = ops.conv([PL.conv_problem(X, p, k, s, wp, m, Y, bias=b.float().to(DEV))], in_stats=stats)
+            Ys.append((Y, st))
+        torch.cuda.synchronize()
+        (Y0, _), (Y1, st) = Ys
+        assert nrel(nchw(Y0), y64) < KTOL
+        assert torch.equal(Y0.interior(), Y1.interior())
+        if (Ho * Ho) % 32 == 0:
+            assert st is not None
+            mean_ref, rstd_ref = ops.in_stats(Y1)
+            assert nrel(st[0], mean_ref) < KTOL and nrel(st[1], rstd_ref) < KTOL
+    finally:
+        L.set_f3_tile(-1)
+        lib.fg_set_f3_persistent(1)
+
+
 def test_fused_in_stats_declined():
     """a conv the epilogue statistics cannot cover (output rows per image not a multiple of 32, e.g. the
     discriminator's 4x4 stride-1 conv) returns None and the caller computes the statistics itself"""
