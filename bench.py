@@ -97,23 +97,36 @@ def p2p_step_gflop_per_img(res):
     return tot / 1e9
 
 
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "round3", "r3_pmc_resblock_fwd.json")
+# the timed resblock forward launches are the step's conv1s (fp32 operand, 8 waves of 32x256) and conv2s (FG_PRESPLIT
+# operand, 8 waves of 64x128), 9 of each per step: one counter summary per kind, averaged
+PMC_SUMMARIES = [os.path.join(ROOT, "profiles", "round3", "r3x_pmc_resblock_fwd_stats.json"),
+                 os.path.join(ROOT, "profiles", "round3", "r3x_pmc_resblock_fwd_stats_ps.json")]
 
 
 def pmc_traffic(kernel_tag):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 counter passes
     (scripts/gpu_pmc.sh + scripts/pmc_summary.py: FETCH_SIZE x2 per the gfx950 correction of
-    MI355X_MICROARCH.md, plus WRITE_SIZE), or None when that summary does not match the kernel."""
-    try:
-        with open(PMC_SUMMARY) as f:
-            s = json.load(f)
-    except (OSError, ValueError):
+    MI355X_MICROARCH.md, plus WRITE_SIZE) averaged over its launch kinds, or None when a summary is missing or does
+    not match the kernel."""
+    ss = []
+    for path in PMC_SUMMARIES:
+        try:
+            with open(path) as f:
+                ss.append(json.load(f))
+        except (OSError, ValueError):
+            return None
+    if any(s.get("kernel_tag") != kernel_tag or "hbm_bytes" not in s for s in ss):
         return None
-    if s.get("kernel_tag") != kernel_tag or "hbm_bytes" not in s:
-        return None
-    return {"bytes_per_launch": s["hbm_bytes"], "read": s["hbm_read_bytes"], "write": s["hbm_write_bytes"],
-            "source": os.path.relpath(PMC_SUMMARY, ROOT), "l2_hit": s.get("l2_hit"),
-            "mfma_busy": s.get("mfma_busy"), "clock_ghz": s.get("clock_ghz")}
+
+    def avg(k):
+        v = [s.get(k) for s in ss]
+        return None if any(x is None for x in v) else sum(v) / len(v)
+    return {"bytes_per_launch": avg("hbm_bytes"), "read": avg("hbm_read_bytes"), "write": avg("hbm_write_bytes"),
+            "source": [os.path.relpath(p, ROOT) for p in PMC_SUMMARIES], "l2_hit": avg("l2_hit"),
+            "mfma_busy": avg("mfma_busy"), "clock_ghz": avg("clock_ghz"),
+            "per_kind": {s.get("kind", str(i)): {k: s.get(k) for k in ("hbm_bytes", "l2_hit", "mfma_busy", "clock_ghz",
+                                                                        "launch_s")}
+                         for i, s in enumerate(ss)}}
 
 
 def cgroup_cpu_limit():
@@ -320,8 +333,9 @@ def main():
                        "parallelism": f"dp{world}"},
             "conv_math": math,
             "roofline": {"bound": "mfma",
-                         "kernel": ("conv_fwd_f3_kernel<256,256,32,256,2> (LDS-DMA ring, 8 waves, 16x16x32 f16 MFMA, "
-                                    "InstanceNorm statistics epilogue)"
+                         "kernel": ("conv_fwd_f3_kernel<256,256,...,STATS> (LDS-DMA ring, 8 waves, 16x16x32 f16 MFMA, "
+                                    "InstanceNorm statistics epilogue; conv1: fp32 operand, waves of 32x256; conv2: "
+                                    "FG_PRESPLIT operand, waves of 64x128)"
                                     if nprod == 3 else
                                     f"conv_fwd_x6_kernel<MathBF16x6,128,256,64,64>" if fwd_x6 else
                                     "conv_fwd_kernel<128,128,64,64>") + (
@@ -332,7 +346,7 @@ def main():
                                         if fwd_x6 else "fp32 MFMA dense peak"),
                          "frac": round(achieved / peak, 4),
                          "traffic": (None if p2p else
-                                     pmc_traffic("conv_fwd_f3_kernel<256,256,32,256,2>" if nprod == 3 else None)),
+                                     pmc_traffic("conv_fwd_f3_kernel<256,256,...,STATS>" if nprod == 3 else None)),
                          "avg_launch_ms": round(avg_ms, 4), "launches": len(durs),
                          "flop_per_launch": flops},
             "step_tflops": (None if cycle else

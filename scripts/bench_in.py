@@ -36,8 +36,23 @@ def main():
         t_apply = time_it(lambda: ops.in_apply(src, mean, rstd, 1, None, dst, 1))
         t_bwd = time_it(lambda: ops.in_bwd(g, fold, ga, src, mean, rstd, 1, gd, None))
         nb_bwd = plane * (2 + 2 + (2 if gadd else 0) + 1)     # stats: src, g (+gadd); apply: src, g (+gadd), dst
+        lib = L.load()
+        lib.fg_set_in_rows(0)
+        t_apply0 = time_it(lambda: ops.in_apply(src, mean, rstd, 1, None, dst, 1))
+        t_bwd0 = time_it(lambda: ops.in_bwd(g, fold, ga, src, mean, rstd, 1, gd, None))
+        lib.fg_set_in_rows(1)
+        t_apply_ps = time_it(lambda: ops.in_apply(src, mean, rstd, 1, None, dst, 1, presplit=True))
+        t_bwd_ps = time_it(lambda: ops.in_bwd(g, fold, ga, src, mean, rstd, 1, gd, None, presplit=True))
+        # what torch's own streaming kernels reach on the same bytes
+        a, b = src.t, g.t[:src.t.numel()]
+        c = torch.empty_like(a)
+        t_copy = time_it(lambda: c.copy_(a))
+        t_add = time_it(lambda: torch.add(a, b, out=c))
         for tag, t, nb in (("in_stats", t_stats, plane), ("in_apply", t_apply, 2 * plane),
-                           ("in_bwd (stats+apply)", t_bwd, nb_bwd)):
+                           ("in_apply grid-stride", t_apply0, 2 * plane), ("in_apply presplit", t_apply_ps, 2 * plane),
+                           ("in_bwd (stats+apply)", t_bwd, nb_bwd), ("in_bwd grid-stride", t_bwd0, nb_bwd),
+                           ("in_bwd presplit", t_bwd_ps, nb_bwd),
+                           ("torch copy_", t_copy, 2 * plane), ("torch add", t_add, 3 * plane)):
             print(f"{name:44s} {tag:22s} {t * 1e3:8.1f} us  {nb / t / 1e6:7.0f} GB/s", flush=True)
 
 

@@ -1,6 +1,7 @@
 """Run one conv-engine launch shape repeatedly (for rocprofv3 counter passes).
-  python scripts/conv_one.py [fwd|fwd_stats|wgrad] [reps]  -- resblock 3x3 256->256 @128, bs 8
-  (fwd_stats: with the InstanceNorm statistics epilogue, as the step's resblock forward runs)"""
+  python scripts/conv_one.py [fwd|fwd_stats|fwd_stats_ps|wgrad] [reps]  -- resblock 3x3 256->256 @128, bs 8
+  (fwd_stats: with the InstanceNorm statistics epilogue, as the step's conv1 runs; fwd_stats_ps: on a FG_PRESPLIT
+  operand written by the norm pass, as the step's conv2 runs)"""
 import os
 import sys
 
@@ -25,9 +26,14 @@ def main():
     m = PL.wmap_conv_fwd(w.shape, C)
     Y = Buf.empty(N, H, H, C, 0, dev)
     Y.t.uniform_(-1, 1)
-    if kind in ("fwd", "fwd_stats"):
+    if kind == "fwd_stats_ps":
+        c = Buf.empty(N, H, H, C, 0, dev)
+        c.t.normal_()
+        mean, rstd = ops.in_stats(c)
+        ops.in_apply(c, mean, rstd, 1, None, X, 1, presplit=True)      # relu(IN(c)) with the reflect border
+    if kind in ("fwd", "fwd_stats", "fwd_stats_ps"):
         prob = PL.conv_problem(X, 1, k, 1, ops.pack_weight(w, m), m, Y, bias=torch.zeros(C, device=dev))
-        fn = lambda: ops.conv([prob], in_stats=kind == "fwd_stats")  # noqa: E731
+        fn = lambda: ops.conv([prob], in_stats=kind != "fwd")  # noqa: E731
     else:
         wprob = PL.wgrad_conv(Y, X, 1, k, 1, C)
         dw = torch.empty_like(w)

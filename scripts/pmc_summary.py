@@ -1,5 +1,5 @@
 """Summarise scripts/gpu_pmc.sh counter passes for the conv kernel into JSON.
-  python scripts/pmc_summary.py gpurun_out/pmc_<tag> [kernel-substring] [kernel_tag] > profiles/....json
+  python scripts/pmc_summary.py gpurun_out/pmc_<tag> [kernel-substring] [kernel_tag] [kind] > profiles/....json
 Per launch (median over the timed launches): duration, effective clock (GRBM_GUI_ACTIVE / 8
 XCDs / wall), MFMA-busy fraction, HBM bytes (FETCH_SIZE x2 -- the gfx950 correction of
 MI355X_MICROARCH.md -- and WRITE_SIZE, both reported in KiB by rocprofv3), L2 hit rate, LDS
@@ -30,6 +30,8 @@ dur = statistics.median(durs[2:] if len(durs) > 4 else durs)
 out = {"source": d, "kernel_match": key, "launch_s": dur}
 if len(sys.argv) > 3:                      # the kernel the bench's roofline names (bench.pmc_traffic checks it)
     out["kernel_tag"] = sys.argv[3]
+if len(sys.argv) > 4:                      # which of its launch kinds (scripts/conv_one.py KIND)
+    out["kind"] = sys.argv[4]
 if "GRBM_GUI_ACTIVE" in med:
     clk = med["GRBM_GUI_ACTIVE"] / 8 / dur
     out["clock_ghz"] = round(clk / 1e9, 3)
