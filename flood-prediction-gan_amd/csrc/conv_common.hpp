@@ -54,6 +54,14 @@ __device__ __forceinline__ float pow2_of(float m) {
     return ldexpf(1.f, 14 - e);
 }
 
+// max over an absmax slot's FG_AMAX_SHARDS shards (every lane of the wave gets it)
+__device__ __forceinline__ float pow2_scale_max(const float* amax) {
+    unsigned b = __float_as_uint(amax[threadIdx.x & (FG_AMAX_SHARDS - 1)]) & 0x7fffffffu;
+#pragma unroll
+    for (int off = 1; off < FG_AMAX_SHARDS; off <<= 1) b = max(b, (unsigned)__shfl_xor((int)b, off));
+    return __uint_as_float(b);
+}
+
 // power-of-two operand scale from an absmax slot (max over its FG_AMAX_SHARDS shards, one per
 // lane, reduced across the wave): |v * s| < 2^14
 __device__ __forceinline__ float pow2_scale(const float* amax) {

@@ -196,7 +196,9 @@ constexpr int kRowU = 4;
 __global__ void __launch_bounds__(NT) in_apply_rows_kernel(fg_view src, const float* __restrict__ mean,
                                                            const float* __restrict__ rstd, int act, fg_view res,
                                                            fg_view dst, int pad_mode, int lshift,
-                                                           unsigned* __restrict__ amax, float* __restrict__ split_slot) {
+                                                           unsigned* __restrict__ amax, float* __restrict__ split_slot,
+                                                           float* __restrict__ ps_ptr, float* __restrict__ ps_slot,
+                                                           const float* __restrict__ res_amax) {
     const int L = 1 << lshift, PG = NT >> lshift;
     const int C = dst.c_alloc, h = dst.h, w = dst.w, pad = dst.pad;
     const int hp = h + 2 * pad, wp = w + 2 * pad;
@@ -214,9 +216,22 @@ __global__ void __launch_bounds__(NT) in_apply_rows_kernel(fg_view src, const fl
         ss = fgc::pow2_of(bound);
         if (blockIdx.x == 0 && threadIdx.x == 0) atomicMax(reinterpret_cast<unsigned*>(split_slot), __float_as_uint(bound));
     }
+    // dual output (ps_ptr): dst in fp32 AND a pre-split copy at the scale of |act(xhat) + res| <= sqrt(HW - 1) +
+    // max|res| (the residual's absmax slot, reduced over its shards by every block alike)
+    float* psrow = nullptr;
+    if (ps_ptr) {
+        const float rmax = res_amax ? fgc::pow2_scale_max(res_amax) : 0.f;
+        const float bound = (sqrtf((float)(h * w - 1)) + rmax) * 1.001f;
+        ss = fgc::pow2_of(bound);
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicMax(reinterpret_cast<unsigned*>(ps_slot), __float_as_uint(bound));
+        psrow = ps_ptr + (size_t)(n * hp + yp) * wp * C + 4 * c4;
+    }
     if ((y < 0 || y >= h) && !reflect) {
         const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-        for (int xp = gi; xp < wp; xp += PG) *reinterpret_cast<f32x4*>(drow + (size_t)xp * C) = z;
+        for (int xp = gi; xp < wp; xp += PG) {
+            *reinterpret_cast<f32x4*>(drow + (size_t)xp * C) = z;
+            if (psrow) *reinterpret_cast<f32x4*>(psrow + (size_t)xp * C) = z;
+        }
     } else {
         y = fg::reflect_idx(y, h);
         const f32x4 m = ld4(mean + (size_t)n * C + 4 * c4), r = ld4(rstd + (size_t)n * C + 4 * c4);
@@ -251,6 +266,7 @@ __global__ void __launch_bounds__(NT) in_apply_rows_kernel(fg_view src, const fl
                 } else {
                     am = max(am, absbits4(o));
                     *reinterpret_cast<f32x4*>(drow + (size_t)xp * C) = o;
+                    if (psrow) store_presplit(psrow + (size_t)xp * C, o, ss, c4 & 1);
                 }
             }
         }
@@ -914,7 +930,8 @@ FG_API int fg_in_stats(fg_view src, float eps, float* mean, float* rstd, double*
 
 namespace {
 int in_apply_impl(fg_view src, const float* mean, const float* rstd, int act, fg_view residual, fg_view dst,
-                  int pad_mode, float* absmax, float* split_slot, hipStream_t stream);
+                  int pad_mode, float* absmax, float* split_slot, hipStream_t stream, float* ps_ptr = nullptr,
+                  float* ps_slot = nullptr, const float* res_amax = nullptr);
 int in_bwd_impl(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, const float* mean, const float* rstd, int act,
                 fg_view dst, float* bias_grad, int bias_accumulate, fg_view gsum, double* work, float* absmax,
                 float* split_slot, hipStream_t stream);
@@ -923,6 +940,17 @@ int in_bwd_impl(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, const flo
 FG_API int fg_in_apply(fg_view src, const float* mean, const float* rstd, int act, fg_view residual, fg_view dst,
                        int pad_mode, float* absmax, hipStream_t stream) {
     return in_apply_impl(src, mean, rstd, act, residual, dst, pad_mode, absmax, nullptr, stream);
+}
+
+FG_API int fg_in_apply_dual(fg_view src, const float* mean, const float* rstd, int act, fg_view residual,
+                            const float* residual_absmax, fg_view dst, int pad_mode, float* absmax, float* ps_dst,
+                            float* ps_slot, hipStream_t stream) {
+    if (!ps_dst || !ps_slot || dst.c_alloc % 8 || NT % (dst.c_alloc / 4) || ((uintptr_t)ps_dst & 31) ||
+        (residual.ptr && !residual_absmax))
+        return fg::fail(FG_ERR_INVALID, "fg_in_apply_dual: needs ps_dst (32-B aligned), a zeroed ps_slot, C %% 8 == 0, "
+                                        "C <= 1024 and the residual's absmax slot (C=%d)", dst.c_alloc);
+    return in_apply_impl(src, mean, rstd, act, residual, dst, pad_mode, absmax, nullptr, stream, ps_dst, ps_slot,
+                         residual.ptr ? residual_absmax : nullptr);
 }
 
 FG_API int fg_in_apply_presplit(fg_view src, const float* mean, const float* rstd, int act, fg_view dst, int pad_mode,
@@ -936,7 +964,8 @@ FG_API int fg_in_apply_presplit(fg_view src, const float* mean, const float* rst
 
 namespace {
 int in_apply_impl(fg_view src, const float* mean, const float* rstd, int act, fg_view residual, fg_view dst,
-                  int pad_mode, float* absmax, float* split_slot, hipStream_t stream) {
+                  int pad_mode, float* absmax, float* split_slot, hipStream_t stream, float* ps_ptr, float* ps_slot,
+                  const float* res_amax) {
     if (!ok_view(src) || !ok_view(dst) || !mean || !rstd || src.c_alloc % 4 || dst.c_alloc != src.c_alloc ||
         dst.h != src.h || dst.w != src.w || dst.n != src.n)
         return fg::fail(FG_ERR_INVALID, "fg_in_apply: bad args");
@@ -945,10 +974,10 @@ int in_apply_impl(fg_view src, const float* mean, const float* rstd, int act, fg
     if (pad_mode == FG_PAD_REFLECT && (dst.pad >= dst.h || dst.pad >= dst.w))
         return fg::fail(FG_ERR_INVALID, "fg_in_apply: reflect pad too large");
     const int C4 = dst.c_alloc / 4;
-    if ((g_in_rows || split_slot) && NT % C4 == 0) {
+    if ((g_in_rows || split_slot || ps_ptr) && NT % C4 == 0) {
         hipLaunchKernelGGL(in_apply_rows_kernel, dim3(dst.n * (dst.h + 2 * dst.pad)), dim3(NT), 0, stream, src, mean,
                            rstd, act, residual, dst, pad_mode, ilog2(C4), reinterpret_cast<unsigned*>(absmax),
-                           split_slot);
+                           split_slot, ps_ptr, ps_slot, res_amax);
         return fg::launched("in_apply_rows");
     }
     const long long total = (long long)dst.n * (dst.h + 2 * dst.pad) * (dst.w + 2 * dst.pad) * (dst.c_alloc / 4);

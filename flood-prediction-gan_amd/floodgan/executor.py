@@ -140,13 +140,16 @@ def _convT_fwd(P, name, X, Y):
     return ops.conv(PL.phase_problems(X, w.shape, 3, 1, Y, wps, maps, bias=P[name + ".bias"]), in_stats=True)
 
 
-def _norm(c, act, pad, mode, residual=None, stats=None, presplit=False):
+def _norm(c, act, pad, mode, residual=None, stats=None, presplit=False, ps_copy=False):
     """InstanceNorm + activation of conv output c; stats = (mean, rstd) from the conv's epilogue, or
-    computed here.  presplit: the output is written in the FG_PRESPLIT format (read only by convs)"""
+    computed here.  presplit: the output is written in the FG_PRESPLIT format (read only by convs).  ps_copy: also a
+    FG_PRESPLIT copy of the fp32 output (returned as a 4th value, None when the f16x3 pre-split path is off)"""
     mean, rstd = stats if stats is not None else ops.in_stats(c)
     out = Buf.empty(c.n, c.h, c.w, c.c, pad, c.t.device)
-    ops.in_apply(c, mean, rstd, act, residual, out, mode, presplit=presplit)
-    return mean, rstd, out
+    ps = (Buf.empty(c.n, c.h, c.w, c.c, pad, c.t.device)
+          if ps_copy and ops.presplit_on() and ops.PRESPLIT_RESID else None)
+    ops.in_apply(c, mean, rstd, act, residual, out, mode, presplit=presplit, ps_copy=ps)
+    return (mean, rstd, out, ps) if ps_copy else (mean, rstd, out)
 
 
 def has_attention(P):
@@ -183,20 +186,21 @@ def gen_forward(P, x, save=True, x_extra=None):
     m2, r2, a2 = _norm(c2, FG_ACT_RELU, 1, FG_PAD_ZERO, stats=st, presplit=ps)
     c3 = Buf.empty(N, H // 4, W // 4, 256, 0, dev)
     st = _conv_fwd(P, "conv3", a2, 1, 3, 2, c3, in_stats=True)
-    m3, r3, h = _norm(c3, FG_ACT_RELU, 1, FG_PAD_REFLECT, stats=st)
+    # block inputs / outputs: fp32 (the residual stream) and a pre-split copy for the convs that read them
+    m3, r3, h, h_ps = _norm(c3, FG_ACT_RELU, 1, FG_PAD_REFLECT, stats=st, ps_copy=True)
     S.update(x=x, X0=X0, c1=c1, m1=m1, r1=r1, a1=a1, c2=c2, m2=m2, r2=r2, a2=a2, c3=c3, m3=m3, r3=r3)
     blocks = []
     for i in range(N_BLOCKS):
         # block output feeds the next block (reflect pad) or the deconv heads (zero pad)
         mode = FG_PAD_REFLECT if i < N_BLOCKS - 1 else FG_PAD_ZERO
-        h, b = _block_fwd(P, f"resnet_blocks.{i}.", h, mode)
+        h, h_ps, b = _block_fwd(P, f"resnet_blocks.{i}.", h, mode, h_ps)
         blocks.append(b)
-    S.update(blocks=blocks, h=h)
+    S.update(blocks=blocks, h=h, h_ps=h_ps)
     heads = {}
     attention = has_attention(P)
     for tag, pad2, mode2 in (("content", 3, FG_PAD_REFLECT), ("attention", 0, FG_PAD_ZERO))[:1 + attention]:
         d1 = Buf.empty(N, H // 2, W // 2, 128, 0, dev)
-        st = _convT_fwd(P, f"deconv1_{tag}", h, d1)
+        st = _convT_fwd(P, f"deconv1_{tag}", h if h_ps is None else h_ps, d1)
         md1, rd1, ad1 = _norm(d1, FG_ACT_RELU, 1, FG_PAD_ZERO, stats=st, presplit=ps)
         d2 = Buf.empty(N, H, W, 64, 0, dev)
         st = _convT_fwd(P, f"deconv2_{tag}", ad1, d2)
@@ -222,19 +226,24 @@ def gen_forward(P, x, save=True, x_extra=None):
     return out, mask, (S if save else None)
 
 
-def _block_fwd(P, pre, h, out_mode):
-    """PairedAttentionBlock (models/model_architectures.py:412-418) over h (reflect border 1):
-    returns (block output with `out_mode` border 1, saved tensors)."""
+def _block_fwd(P, pre, h, out_mode, h_ps=None):
+    """PairedAttentionBlock (models/model_architectures.py:412-418) over h (reflect border 1; h_ps: its pre-split copy,
+    which conv1 reads when given): returns (block output with `out_mode` border 1, its pre-split copy or None, saved
+    tensors)."""
     N, Hh, Ww, Cc = h.n, h.h, h.w, h.c
     dev = h.t.device
     cb1 = Buf.empty(N, Hh, Ww, Cc, 0, dev)
-    st = _conv_fwd(P, pre + "conv1", h, 1, 3, 1, cb1, tag="resblock_conv_fwd", in_stats=True)
+    st = _conv_fwd(P, pre + "conv1", h if h_ps is None else h_ps, 1, 3, 1, cb1, tag="resblock_conv_fwd", in_stats=True)
     # rb is read only by conv2 and conv2's weight gradient: pre-split for both (ops.PRESPLIT)
     mb1, rb1, rb = _norm(cb1, FG_ACT_RELU, 1, FG_PAD_REFLECT, stats=st, presplit=ops.presplit_on())
     cb2 = Buf.empty(N, Hh, Ww, Cc, 0, dev)
     st = _conv_fwd(P, pre + "conv2", rb, 1, 3, 1, cb2, tag="resblock_conv_fwd", in_stats=True)
-    mb2, rb2, hn = _norm(cb2, FG_ACT_NONE, 1, out_mode, residual=h, stats=st)
-    return hn, dict(h=h, cb1=cb1, mb1=mb1, rb1=rb1, rb=rb, cb2=cb2, mb2=mb2, rb2=rb2)
+    if h_ps is None:          # a lone block (block_forward_nchw): no copies
+        mb2, rb2, hn = _norm(cb2, FG_ACT_NONE, 1, out_mode, residual=h, stats=st)
+        hn_ps = None
+    else:
+        mb2, rb2, hn, hn_ps = _norm(cb2, FG_ACT_NONE, 1, out_mode, residual=h, stats=st, ps_copy=True)
+    return hn, hn_ps, dict(h=h, h_ps=h_ps, cb1=cb1, mb1=mb1, rb1=rb1, rb=rb, cb2=cb2, mb2=mb2, rb2=rb2)
 
 
 def _block_bwd(P, pre, b, grad, G):
@@ -259,7 +268,7 @@ def _block_bwd(P, pre, b, grad, G):
     g_cb1 = Buf.empty(N, Hh, Ww, Cc, 2, dev)
     ops.in_bwd(g_rbp, 1, None, b["cb1"], b["mb1"], b["rb1"], FG_ACT_RELU, g_cb1, G.get(pre + "conv1.bias"), G.acc,
                presplit=ps)
-    _wgrad_conv(P, G, pre + "conv1", g_cb1, b["h"], 1, 3, 1)
+    _wgrad_conv(P, G, pre + "conv1", g_cb1, b["h"] if b.get("h_ps") is None else b["h_ps"], 1, 3, 1)
     g_hp = _dgrad_s1_padded(P, pre + "conv1", g_cb1)
     return g_hp, 1, g_h                               # reflect-pad adjoint + residual path, summed lazily
 
@@ -303,7 +312,7 @@ def block_forward_nchw(x, params, save=True):
          "conv2.weight": params["w2"], "conv2.bias": params["b2"]}
     h = Buf.empty(N, Hh, Ww, Cc, 1, x.device)
     ops.pack_input(x, Cc, None, 0, h, 0, N, FG_PAD_REFLECT)
-    hn, b = _block_fwd(P, "", h, FG_PAD_ZERO)
+    hn, _, b = _block_fwd(P, "", h, FG_PAD_ZERO)
     return _to_nchw(hn), (dict(P=P, b=b) if save else None)
 
 
@@ -426,8 +435,9 @@ def gen_backward(P, S, g_out, grads_into=None, ready=None, input_grad=None, accu
                    G.acc, presplit=ps)
         name = f"deconv1_{tag}"
         w = P[name + ".weight"]
-        G.wgrad(PL.wgrad_convT(S["h"], g_d1, 3, 1, w.shape[0]), PL.wmap_wgrad(w.shape, True, g_d1.c, 3),
-                name + ".weight", (S["h"], g_d1))
+        hx = S["h"] if S.get("h_ps") is None else S["h_ps"]
+        G.wgrad(PL.wgrad_convT(hx, g_d1, 3, 1, w.shape[0]), PL.wmap_wgrad(w.shape, True, g_d1.c, 3),
+                name + ".weight", (hx, g_d1))
         m = PL.wmap_convT_dgrad(w.shape, g_d1.c)
         ops.conv([PL.conv_problem(g_d1, 1, 3, 2, ops.pack_weight(w, m), m, g_h, accumulate=idx)])
     G.ready(ready, "deconv1_content")

@@ -109,6 +109,11 @@ def _wrote(*objs):
 PRESPLIT = os.environ.get("FLOODGAN_PRESPLIT", "1") != "0"
 
 
+# the resblock chain's block inputs / outputs also get a pre-split copy beside the fp32 residual stream
+# (fg_in_apply_dual; FLOODGAN_PRESPLIT_RESID=0: off)
+PRESPLIT_RESID = os.environ.get("FLOODGAN_PRESPLIT_RESID", "1") != "0"
+
+
 def presplit_on():
     return PRESPLIT and L.fwd_f16x3() and L.wgrad_f16x3() and L.wgrad_f3_on()
 
@@ -594,8 +599,18 @@ def in_stats(src):
     return mean, rstd
 
 
-def in_apply(src, mean, rstd, act, residual, dst, pad_mode, presplit=False):
-    """presplit: dst is written in the FG_PRESPLIT format (no residual; the f16x3 math)"""
+def in_apply(src, mean, rstd, act, residual, dst, pad_mode, presplit=False, ps_copy=None):
+    """presplit: dst is written in the FG_PRESPLIT format (no residual; the f16x3 math).  ps_copy (Buf of dst's
+    geometry): dst in fp32 AND a FG_PRESPLIT copy there (fg_in_apply_dual)"""
+    if ps_copy is not None:
+        assert not presplit and L.fwd_f16x3()
+        ra = absmax(residual) if residual is not None else None
+        slot, ps_slot = _amax_out(dst), _amax_out(ps_copy)
+        L.check(_lib().fg_in_apply_dual(view(src), L.ptr(mean), L.ptr(rstd), act, view(residual), L.ptr(ra), view(dst),
+                                        pad_mode, L.ptr(slot), L.ptr(ps_copy.t), L.ptr(ps_slot), L.stream_handle()),
+                "in_apply_dual")
+        _mark_presplit(ps_copy)
+        return
     if presplit:
         assert residual is None and L.fwd_f16x3()
         slot = _amax_out(dst)

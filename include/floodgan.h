@@ -370,6 +370,14 @@ int fg_in_bwd(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, const float
 int fg_in_apply_presplit(fg_view src, const float* mean, const float* rstd, int act, fg_view dst, int pad_mode,
                          float* scale_slot, hipStream_t stream);
 
+/* fg_in_apply writing dst in fp32 (absmax raised as there) AND a FG_PRESPLIT copy into ps_dst (same geometry, 32-B
+ * aligned) at the scale of the bound sqrt(HW - 1) + max|residual| (residual_absmax: the residual's absmax slot,
+ * required with a residual), published in ps_slot (a zeroed absmax slot): the block outputs of the resblock chain,
+ * whose fp32 values the next residual add needs and whose copy the next conv and its weight gradient read. */
+int fg_in_apply_dual(fg_view src, const float* mean, const float* rstd, int act, fg_view residual,
+                     const float* residual_absmax, fg_view dst, int pad_mode, float* absmax, float* ps_dst,
+                     float* ps_slot, hipStream_t stream);
+
 /* fg_in_bwd whose dst is written in the FG_PRESPLIT format: the statistics pass also takes max |g'| per
  * image, the coefficient pass bounds |dst| per plane by rstd (max|g'| + |mean g'| + sqrt(HW-1) |mean g'xhat|)
  * and publishes the bound in scale_slot (a zeroed absmax slot), the apply pass writes the pieces at its

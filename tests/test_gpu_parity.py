@@ -588,6 +588,31 @@ def test_presplit_norm_outputs(act, fold, C, H, W, gadd):
         assert torch.equal(gsr.t, gsp.t)
 
 
+@pytest.mark.parametrize("act,residual,pad_mode", [(0, True, 1), (0, True, 0), (1, False, 1)])
+def test_in_apply_dual(act, residual, pad_mode):
+    """fg_in_apply_dual: the fp32 output equals fg_in_apply's bit for bit (absmax slot included), and the pre-split copy
+    decodes to it within the pieces' precision, its published bound (sqrt(HW-1) + max|residual|) covering it"""
+    from floodgan import ops
+    from floodgan.plans import Buf
+    torch.manual_seed(23)
+    N, H, W, C = 2, 12, 10, 256
+    c = torch.randn(N, C, H, W, dtype=torch.float64) * 2 + 0.5
+    cb = buf_from(c, 0, "constant")
+    rb = buf_from(torch.randn(N, C, H, W, dtype=torch.float64) * 3, 0, "constant") if residual else None
+    mean, rstd = ops.in_stats(cb)
+    ref = Buf.empty(N, H, W, C, 1, DEV)
+    ops.in_apply(cb, mean, rstd, act, rb, ref, pad_mode)
+    out, ps = Buf.empty(N, H, W, C, 1, DEV), Buf.empty(N, H, W, C, 1, DEV)
+    ops.in_apply(cb, mean, rstd, act, rb, out, pad_mode, ps_copy=ps)
+    torch.cuda.synchronize()
+    assert torch.equal(out.t, ref.t) and float(out.t._fg_amax.max()) == float(ref.t._fg_amax.max())
+    assert ops.is_presplit(ps) and not ops.is_presplit(out)
+    dec, s = _decode_presplit(ps, ps.t._fg_amax)
+    r = ref.t.double()
+    assert float(ps.t._fg_amax.max()) >= float(r.abs().max())
+    assert bool(((dec - r).abs() <= 2.0 ** -21 * r.abs() + 4 * 2.0 ** -24 / s).all())
+
+
 @pytest.mark.parametrize("N,H", [(2, 16), (1, 24)])
 def test_presplit_resblock_convs(N, H):
     """The resblock convs on FG_PRESPLIT operands (the pipelined forward, its input-gradient interior + edge strips,
