@@ -97,10 +97,10 @@ def p2p_step_gflop_per_img(res):
     return tot / 1e9
 
 
-# the timed resblock forward launches are the step's conv1s (fp32 operand, 8 waves of 32x256) and conv2s (FG_PRESPLIT
-# operand, 8 waves of 64x128), 9 of each per step: one counter summary per kind, averaged
-PMC_SUMMARIES = [os.path.join(ROOT, "profiles", "round3", "r3x_pmc_resblock_fwd_stats.json"),
-                 os.path.join(ROOT, "profiles", "round3", "r3x_pmc_resblock_fwd_stats_ps.json")]
+# the timed resblock forward launches (conv1 and conv2 of the 9 blocks) all read FG_PRESPLIT operands (conv2: the norm
+# pass's output; conv1: the block input's pre-split copy) on 8 waves of 64x128 with the statistics epilogue: the
+# counter summary of that kind (averaged if several are listed)
+PMC_SUMMARIES = [os.path.join(ROOT, "profiles", "round3", "r3x_pmc_resblock_fwd_stats_ps.json")]
 
 
 def pmc_traffic(kernel_tag):
@@ -333,9 +333,8 @@ def main():
                        "parallelism": f"dp{world}"},
             "conv_math": math,
             "roofline": {"bound": "mfma",
-                         "kernel": ("conv_fwd_f3_kernel<256,256,...,STATS> (LDS-DMA ring, 8 waves, 16x16x32 f16 MFMA, "
-                                    "InstanceNorm statistics epilogue; conv1: fp32 operand, waves of 32x256; conv2: "
-                                    "FG_PRESPLIT operand, waves of 64x128)"
+                         "kernel": ("conv_fwd_f3_kernel<256,256,...,STATS> (LDS-DMA ring, 8 waves of 64x128, 16x16x32 "
+                                    "f16 MFMA on FG_PRESPLIT operands, InstanceNorm statistics epilogue)"
                                     if nprod == 3 else
                                     f"conv_fwd_x6_kernel<MathBF16x6,128,256,64,64>" if fwd_x6 else
                                     "conv_fwd_kernel<128,128,64,64>") + (
