@@ -29,7 +29,8 @@ __device__ __forceinline__ int swz_tr(int row) { return ((row & 3) | (((row >> 3
 
 template <int COLS>
 __device__ __forceinline__ int img_off(int row, int col) {   // byte offset of fp16 column col of row
-    return row * (COLS * 2) + (((col >> 3) ^ swz_tr(row)) << 4) + ((col & 7) << 1);
+    // (the swizzle stays inside the row's COLS / 8 chunks: a 64-column image has 8)
+    return row * (COLS * 2) + (((col >> 3) ^ (swz_tr(row) & (COLS / 8 - 1))) << 4) + ((col & 7) << 1);
 }
 
 __device__ __forceinline__ f16x8 tr_frag(const char* base, int a0, int a1) {
@@ -63,7 +64,8 @@ __device__ __forceinline__ void split4(const f32x4& v, float s, f16x4& h, f16x4&
 template <int TA, int SCH, int PS = 0>
 __global__ void __launch_bounds__(512, 1)
 conv_wgrad_f3_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
-    // 8 waves as NWA (a) x NWK (k); wave tile 64 (a) x WK (k): TA 256 -> 4 x 2, 64 x 128; TA 128 -> 2 x 4, 64 x 64
+    // 8 waves as NWA (a) x NWK (k); wave tile 64 (a) x WK (k): TA 256 -> 4 x 2, 64 x 128; TA 128 -> 2 x 4, 64 x 64;
+    // TA 64 -> 1 x 8, 64 x 32 (the 64-output-channel stem / D model.0 weight gradients)
     constexpr int NT = 512, NWA = TA / 64, NWK = 8 / NWA, WK = TK / NWK, TM = 4, TN = WK / 16;
     constexpr int SPT = BR * TK / 4 / NT;           // float4 slots per thread per operand per stage (4)
     constexpr int IMGP = BR * TA * 2, IMGX = BR * TK * 2;   // bytes per piece image
@@ -177,7 +179,7 @@ conv_wgrad_f3_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
     // transposed-read lane roles: group g reads pixel rows 8g + q (and 8g + 4 + q), lane 4q+p of
     // the group addresses columns 4p..4p+3 of the 16-column block
     const int g = lane >> 4, q = (lane >> 2) & 3, p4 = (lane & 3) * 4;
-    constexpr int TG = SCH == 0 ? 4 : TN / SPT;          // column blocks per group (SCH 1: one slot per group)
+    constexpr int TG = SCH == 0 ? (TN < 4 ? TN : 4) : TN / SPT;   // column blocks per group (SCH 1: a slot per group)
     static_assert(TN % TG == 0 && (SCH == 0 || TN / TG == SPT), "groups");
     auto compute = [&](int buf, bool stage_next) {
         const char* b = smem + buf * BUF;
@@ -267,11 +269,12 @@ namespace fgc {
 
 // Returns 1 when the pipelined kernel took the problem (status in *rc), 0 when it does not apply.
 int launch_wgrad_f3(const fg_wgrad_problem& p, hipStream_t stream, int* rc) {
-    if (!g_wgrad_f3 || p.n_a < 128 || p.kh * p.j_valid < 256 || p.n_a % 4 || p.j_valid % 4 || !p.p_absmax ||
+    // (K >= 256: D model.0's K = 192 ran 199 us here against 185 on the register-staged kernel, r3ae)
+    if (!g_wgrad_f3 || p.n_a < 64 || p.kh * p.j_valid < 256 || p.n_a % 4 || p.j_valid % 4 || !p.p_absmax ||
         !p.x_absmax || ((uintptr_t)p.p & 15) || ((uintptr_t)p.x & 15) || (p.spn | p.spa | p.spb) % 4 ||
         (p.sxn | p.sxa | p.sxb | p.sxr) % 4)
         return 0;
-    const int TA = p.n_a >= 256 ? 256 : 128;
+    const int TA = p.n_a >= 256 ? 256 : p.n_a > 64 ? 128 : 64;
     const int ta = (p.n_a + TA - 1) / TA, tk = (p.kh * p.j_valid + TK - 1) / TK;
     const dim3 grid(ta * tk * p.splits);
     const int ps = (p.p_presplit ? 1 : 0) | (p.x_presplit ? 2 : 0);
@@ -280,7 +283,14 @@ int launch_wgrad_f3(const fg_wgrad_problem& p, hipStream_t stream, int* rc) {
         if (p.n_a % 8 || p.j_valid % 8 || (p.p_presplit && (((uintptr_t)p.p & 31) || (p.spn | p.spa | p.spb) % 8)) ||
             (p.x_presplit && (((uintptr_t)p.x & 31) || (p.sxn | p.sxa | p.sxb | p.sxr) % 8)))
             return 0;
-        if (TA == 256) {
+        if (TA == 64) {
+            if (ps == 1)
+                hipLaunchKernelGGL((conv_wgrad_f3_kernel<64, 0, 1>), grid, dim3(512), 0, stream, p, ta, tk);
+            else if (ps == 2)
+                hipLaunchKernelGGL((conv_wgrad_f3_kernel<64, 0, 2>), grid, dim3(512), 0, stream, p, ta, tk);
+            else
+                hipLaunchKernelGGL((conv_wgrad_f3_kernel<64, 0, 3>), grid, dim3(512), 0, stream, p, ta, tk);
+        } else if (TA == 256) {
             if (ps == 1)
                 hipLaunchKernelGGL((conv_wgrad_f3_kernel<256, 0, 1>), grid, dim3(512), 0, stream, p, ta, tk);
             else if (ps == 2)
@@ -300,7 +310,9 @@ int launch_wgrad_f3(const fg_wgrad_problem& p, hipStream_t stream, int* rc) {
     }
     // measured: the interleaved staging pays off on the 128-row tiles only
     const int sch = g_wgrad_f3 == 3 || (g_wgrad_f3 == 2 && TA == 128) ? 1 : 0;
-    if (TA == 256 && sch == 1)
+    if (TA == 64)
+        hipLaunchKernelGGL((conv_wgrad_f3_kernel<64, 0>), grid, dim3(512), 0, stream, p, ta, tk);
+    else if (TA == 256 && sch == 1)
         hipLaunchKernelGGL((conv_wgrad_f3_kernel<256, 1>), grid, dim3(512), 0, stream, p, ta, tk);
     else if (TA == 256)
         hipLaunchKernelGGL((conv_wgrad_f3_kernel<256, 0>), grid, dim3(512), 0, stream, p, ta, tk);

@@ -152,6 +152,12 @@ def _norm(c, act, pad, mode, residual=None, stats=None, presplit=False, ps_copy=
     return (mean, rstd, out, ps) if ps_copy else (mean, rstd, out)
 
 
+# FLOODGAN_STEM_PAD4=1: the generator input buffer's channels padded to a multiple of 4.  The stem's weight gradient
+# then takes the pipelined kernel (its 64-row tile), but the stem forward pays for the zero channels: step A/B 47.97
+# (off) vs 48.24 ms (on), profiles/round3/r3af_ab_stem_pad4.log -- off by default
+STEM_PAD4 = os.environ.get("FLOODGAN_STEM_PAD4", "0") == "1"
+
+
 def has_attention(P):
     """PairedAttention / AttentionGAN generators carry the attention head; CycleGAN's does not"""
     return "deconv3_attention.weight" in P
@@ -175,7 +181,8 @@ def gen_forward(P, x, save=True, x_extra=None):
         raise RuntimeError(f"PairedAttentionGenerator needs H, W divisible by 4 and >= 8 (got {H}x{W})")
     dev = x.device
     S = {}
-    X0 = Buf.empty(N, H, W, Cin + Ce, 3, dev)
+    # STEM_PAD4: 9-channel inputs padded to 12 zero-filled channels (16-B rows; see STEM_PAD4)
+    X0 = Buf.empty(N, H, W, PL.rup(Cin + Ce, 4) if STEM_PAD4 and Cin + Ce > 8 else Cin + Ce, 3, dev)
     ops.pack_input(x, Cin, x_extra, Ce, X0, 0, N, FG_PAD_REFLECT)             # F.pad(input, 3, reflect)
     c1 = Buf.empty(N, H, W, 64, 0, dev)
     st = _conv_fwd(P, "conv1", X0, 3, 7, 1, c1, in_stats=True)
@@ -188,7 +195,7 @@ def gen_forward(P, x, save=True, x_extra=None):
     st = _conv_fwd(P, "conv3", a2, 1, 3, 2, c3, in_stats=True)
     # block inputs / outputs: fp32 (the residual stream) and a pre-split copy for the convs that read them
     m3, r3, h, h_ps = _norm(c3, FG_ACT_RELU, 1, FG_PAD_REFLECT, stats=st, ps_copy=True)
-    S.update(x=x, X0=X0, c1=c1, m1=m1, r1=r1, a1=a1, c2=c2, m2=m2, r2=r2, a2=a2, c3=c3, m3=m3, r3=r3)
+    S.update(x=x, X0=X0, cin=Cin + Ce, c1=c1, m1=m1, r1=r1, a1=a1, c2=c2, m2=m2, r2=r2, a2=a2, c3=c3, m3=m3, r3=r3)
     blocks = []
     for i in range(N_BLOCKS):
         # block output feeds the next block (reflect pad) or the deconv heads (zero pad)
@@ -380,7 +387,7 @@ def gen_backward(P, S, g_out, grads_into=None, ready=None, input_grad=None, accu
     G = _Grads(P, grads_into, accumulate, device=x.device)
     assert not accumulate or grads_into is not None
     N, _, H, W = x.shape
-    Cin = S["X0"].c            # input channels, including a fused x_extra
+    Cin = S["cin"]             # input channels, including a fused x_extra
     dev = x.device
     attention = has_attention(P)
     n_content = 27 if attention else 3

@@ -291,7 +291,7 @@ def wgrad_splits(n_a, K, M, f3=False):
     """(splits, pixels per split) of a weight-gradient problem: about one resident wave of
     workgroups.  f3: the pipelined f16x3 kernel's 256 x 256 tiles and 32-pixel stages."""
     if f3:
-        ba, bk, blocks, q = (256 if n_a >= 256 else 128), 256, F3_WG_BLOCKS, 32
+        ba, bk, blocks, q = (256 if n_a >= 256 else 128 if n_a > 64 else 64), 256, F3_WG_BLOCKS, 32
     else:
         (ba, bk), blocks, q = wgrad_tile(n_a), WG_BLOCKS, 16
     tiles = -(-n_a // ba) * -(-K // bk)
@@ -303,7 +303,7 @@ def wgrad_splits(n_a, K, M, f3=False):
 
 def f3_wgrad_eligible(prob):
     """the shapes the pipelined f16x3 weight-gradient kernel takes (conv_wgrad_f3.hip)"""
-    return prob["n_a"] >= 128 and prob["kh"] * prob["j_valid"] >= 256 and prob["n_a"] % 4 == 0 \
+    return prob["n_a"] >= 64 and prob["kh"] * prob["j_valid"] >= 256 and prob["n_a"] % 4 == 0 \
         and prob["j_valid"] % 4 == 0
 
 

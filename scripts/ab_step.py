@@ -1,7 +1,7 @@
 """A/B of engine switches on the full bs-8 512^2 training step, interleaved in ONE process (device
 clocks and boxes differ by several percent, so separate bench runs cannot resolve small gains).
   python scripts/ab_step.py f3_persistent [rounds] [steps] [values, default 0,1]
-Switches: f3_persistent, f3_sched, f3_order, f3_fill, f3_interleave, head_1x1, win_waves (values 4,8), wgrad_f3, use_win, in_rows, presplit, ps_wide (values 4,5), ps_resid."""
+Switches: f3_persistent, f3_sched, f3_order, f3_fill, f3_interleave, head_1x1, win_waves (values 4,8), wgrad_f3, use_win, in_rows, presplit, ps_wide (values 4,5), ps_resid, stem_pad4."""
 import os
 import sys
 import time
@@ -29,6 +29,9 @@ def switch(name, on):
         lib.fg_set_f3_fill(int(on))
     elif name == "presplit":
         ops.PRESPLIT = bool(on)
+    elif name == "stem_pad4":
+        from floodgan import executor
+        executor.STEM_PAD4 = bool(on)
     elif name == "ps_resid":
         ops.PRESPLIT_RESID = bool(on)
     elif name == "ps_wide":

@@ -210,7 +210,11 @@ def test_conv_f3_tiles(case, cfg, persistent, sched, order):
 @pytest.mark.parametrize("on", [0, 1, 2, 3])
 @pytest.mark.parametrize("case", [(256, 256, 3, 1, 1, "reflect", 40), (128, 256, 4, 2, 1, "constant", 34),
                                   (256, 512, 4, 1, 1, "constant", 17), (64, 128, 3, 2, 1, "constant", 36),
-                                  (128, 128, 4, 2, 1, "constant", 30)])
+                                  (128, 128, 4, 2, 1, "constant", 30),
+                                  # 64 output channels (the 64-row tile): the stem 7x7 over 12 channels, a 3x3 64->64
+                                  (12, 64, 7, 1, 3, "reflect", 38), (64, 64, 3, 1, 1, "reflect", 33),
+                                  # D model.0: 4x4 s2 over 12 channels, K = 192 (the register-staged kernel)
+                                  (12, 64, 4, 2, 1, "constant", 40)])
 def test_wgrad_f3(case, on):
     """the pipelined f16x3 weight-gradient kernel (conv_wgrad_f3.hip; on=0: the register-staged
     kernel) on multi-split problems with ragged pixel chunks, against fp64"""
