@@ -31,8 +31,8 @@ constexpr int NT = 256;
 constexpr int MAX_CHUNKS = 256;
 constexpr int CS_CHUNKS = 1024;     // channel-sum blocks (workspace: fg_channel_sum_workspace_doubles)
 
-int choose_chunks(int n, long long hw) {
-    long long c = (2048 + n - 1) / n;      // ~2048 workgroups: enough loads in flight per CU
+int choose_chunks(int n, long long hw, int target = 2048) {
+    long long c = (target + n - 1) / n;    // ~target workgroups: enough loads in flight per CU
     if (c > hw / 64) c = hw / 64;
     if (c > MAX_CHUNKS) c = MAX_CHUNKS;
     if (c < 1) c = 1;
@@ -1020,6 +1020,8 @@ int in_bwd_impl(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, const flo
         return fg::fail(FG_ERR_INVALID, "fg_in_bwd: gadd shape");
     if (gsum.ptr && (gsum.c_alloc != src.c_alloc || gsum.h != src.h || gsum.w != src.w || gsum.n != src.n))
         return fg::fail(FG_ERR_INVALID, "fg_in_bwd: gsum shape");
+    // ~2048 workgroups (measured against 1024 / 512 / 256 / 128 at bs 8: 512 within noise, fewer slower,
+    // profiles/round3/r3ai_bwd_wg.log)
     const int chunks = choose_chunks(src.n, (long long)src.h * src.w);
     const int C = src.c_alloc;
     float* coef = reinterpret_cast<float*>(work + (size_t)src.n * C * MAX_CHUNKS * 3);
