@@ -456,17 +456,21 @@ __global__ void in_bwd_stats_kernel(fg_view g, int fp, fg_view gadd, fg_view src
     }
 }
 
-// block (n, 64-channel group) as in in_finalize_kernel: coefficients of the apply pass and the
-// per-plane part of the (mathematically cancelled) conv-bias gradient
-__global__ void __launch_bounds__(64 * FG) in_bwd_finalize_kernel(int N, int C, int HWi, int chunks,
-                                                                   const double* __restrict__ work,
-                                                                   const float* __restrict__ rstd,
-                                                                   float* __restrict__ coef,
-                                                                   double* __restrict__ bpart,
-                                                                   const float* __restrict__ gmax_part,
-                                                                   float* __restrict__ split_slot) {
-    const int n = blockIdx.x, c = blockIdx.y * 64 + (threadIdx.x & 63), g = threadIdx.x >> 6;
-    __shared__ double red[FG][64][3];
+// block (n, 16-channel group), 1024 threads = 16 channels x 64 chunk slices (the partials of one image are ~1.5 MB:
+// 64-channel blocks, 32 of them at bs 8, were bandwidth-bound on their CU -- 12.6 us per call): coefficients of the
+// apply pass and the per-plane part of the (mathematically cancelled) conv-bias gradient; a fixed-order tree over the
+// slices (deterministic)
+constexpr int kFinC = 16, kFinS = 64;
+
+__global__ void __launch_bounds__(kFinC * kFinS) in_bwd_finalize_kernel(int N, int C, int HWi, int chunks,
+                                                                        const double* __restrict__ work,
+                                                                        const float* __restrict__ rstd,
+                                                                        float* __restrict__ coef,
+                                                                        double* __restrict__ bpart,
+                                                                        const float* __restrict__ gmax_part,
+                                                                        float* __restrict__ split_slot) {
+    const int n = blockIdx.x, cl = threadIdx.x % kFinC, sl = threadIdx.x / kFinC, c = blockIdx.y * kFinC + cl;
+    __shared__ double red[kFinS][kFinC][3];
     __shared__ unsigned gmx, bmx;
     if (split_slot) {
         if (threadIdx.x == 0) gmx = bmx = 0;
@@ -477,14 +481,12 @@ __global__ void __launch_bounds__(64 * FG) in_bwd_finalize_kernel(int N, int C, 
     }
     double sg = 0, sgx = 0, sx = 0;
     if (c < C) {
-        // four chunks' loads in flight per step (a 16-deep dependent walk was latency-bound: 13.8 us per call);
-        // the same summation order
-        int k = g;
-        for (; k + 3 * FG < chunks; k += 4 * FG) {
+        int k = sl;
+        for (; k + 3 * kFinS < chunks; k += 4 * kFinS) {       // four chunks' loads in flight
             double v[4][3];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const double* wk = work + ((size_t)(n * chunks + k + u * FG) * C + c) * 3;
+                const double* wk = work + ((size_t)(n * chunks + k + u * kFinS) * C + c) * 3;
                 v[u][0] = wk[0];
                 v[u][1] = wk[1];
                 v[u][2] = wk[2];
@@ -496,24 +498,30 @@ __global__ void __launch_bounds__(64 * FG) in_bwd_finalize_kernel(int N, int C, 
                 sx += v[u][2];
             }
         }
-        for (; k < chunks; k += FG) {
+        for (; k < chunks; k += kFinS) {
             const double* wk = work + ((size_t)(n * chunks + k) * C + c) * 3;
             sg += wk[0];
             sgx += wk[1];
             sx += wk[2];
         }
     }
-    red[g][threadIdx.x & 63][0] = sg;
-    red[g][threadIdx.x & 63][1] = sgx;
-    red[g][threadIdx.x & 63][2] = sx;
-    __syncthreads();
-    if (g == 0 && c < C) {
-        sg = sgx = sx = 0;
-        for (int gg = 0; gg < FG; ++gg) {
-            sg += red[gg][threadIdx.x][0];
-            sgx += red[gg][threadIdx.x][1];
-            sx += red[gg][threadIdx.x][2];
+    red[sl][cl][0] = sg;
+    red[sl][cl][1] = sgx;
+    red[sl][cl][2] = sx;
+#pragma unroll
+    for (int st = kFinS / 2; st > 0; st >>= 1) {
+        __syncthreads();
+        if (sl < st) {
+            red[sl][cl][0] += red[sl + st][cl][0];
+            red[sl][cl][1] += red[sl + st][cl][1];
+            red[sl][cl][2] += red[sl + st][cl][2];
         }
+    }
+    __syncthreads();
+    if (sl == 0 && c < C) {
+        sg = red[0][cl][0];
+        sgx = red[0][cl][1];
+        sx = red[0][cl][2];
         const double HW = (double)HWi;
         const int idx = n * C + c;
         const float c1 = (float)(sg / HW), c2 = (float)(sgx / HW);
@@ -533,7 +541,6 @@ __global__ void __launch_bounds__(64 * FG) in_bwd_finalize_kernel(int N, int C, 
             atomicMax(reinterpret_cast<unsigned*>(split_slot) + ((n * gridDim.y + blockIdx.y) & (FG_AMAX_SHARDS - 1)), bmx);
     }
 }
-
 
 __global__ void in_bwd_apply_kernel(fg_view g, int fp, fg_view gadd, fg_view src, const float* __restrict__ mean,
                                     const float* __restrict__ rstd, const float* __restrict__ coef, int act,
@@ -1035,7 +1042,7 @@ int in_bwd_impl(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, const flo
                            mean, rstd, act, chunks, work, gsum);
     int e = fg::launched("in_bwd_stats");
     if (e) return e;
-    hipLaunchKernelGGL(in_bwd_finalize_kernel, dim3(src.n, (C + 63) / 64), dim3(64 * FG), 0, stream, src.n, C,
+    hipLaunchKernelGGL(in_bwd_finalize_kernel, dim3(src.n, (C + kFinC - 1) / kFinC), dim3(kFinC * kFinS), 0, stream, src.n, C,
                        src.h * src.w, chunks, work, rstd, coef, bpart, gmax_part, split_slot);
     e = fg::launched("in_bwd_finalize");
     if (e) return e;
