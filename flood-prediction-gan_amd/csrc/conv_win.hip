@@ -67,6 +67,7 @@ __global__ void split_pixels_kernel(const float* __restrict__ src, long long npi
 }
 
 int g_win_waves = 8;   // FLOODGAN_WIN_WAVES overrides (A/B)
+int g_win_apf = 0;     // strip fragments of tap t+1 read before tap t+1's barrier; FLOODGAN_WIN_APF overrides (A/B)
 
 struct WinArgs {
     fg_conv_problem P;
@@ -75,7 +76,10 @@ struct WinArgs {
     int tiles_per_img;
 };
 
-template <int C, int KW, int TN, int NW = 4>
+// APF: the strip fragments of the next tap of the same kernel row are read from LDS right after this
+// tap's MFMAs, so their latency runs under the next barrier instead of after it (only the weight
+// fragments, whose DMA the barrier publishes, are read behind it)
+template <int C, int KW, int TN, int NW = 4, bool APF = false>
 __global__ void __launch_bounds__(NW * 64, 1) conv_win_kernel(const WinArgs args) {
     constexpr int BM = 256, WM = BM / NW, TM = WM / 16;
     constexpr int PB = 4 * C;                                   // strip bytes per pixel (h | l)
@@ -174,20 +178,26 @@ __global__ void __launch_bounds__(NW * 64, 1) conv_win_kernel(const WinArgs args
 #pragma unroll
         for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    auto compute = [&](int t) {
+    constexpr int CC = C / 32;
+    f16x8 ah[CC][TM], al[CC][TM];
+    auto load_a = [&](int t) {
         const int r = t / KW, s = t - (t / KW) * KW;
         const char* sb_ = smem + S_OFF + (r & 1) * STRIP_PIECES * 1024;
-        const char* wb = smem + W_OFF + (t & 1) * W_BYTES;
 #pragma unroll
-        for (int cc = 0; cc < C / 32; ++cc) {
-            f16x8 ah[TM], al[TM], bh[TN], bl[TN];
+        for (int cc = 0; cc < CC; ++cc)
 #pragma unroll
             for (int tm = 0; tm < TM; ++tm) {
                 const char* px = sb_ + (q0[tm] + s) * PB;
                 const int sw = swz_strip<C>(x0[tm] + s);
-                ah[tm] = *reinterpret_cast<const f16x8*>(px + ((cc * 4 + g) ^ sw) * 16);
-                al[tm] = *reinterpret_cast<const f16x8*>(px + ((C / 8 + cc * 4 + g) ^ sw) * 16);
+                ah[cc][tm] = *reinterpret_cast<const f16x8*>(px + ((cc * 4 + g) ^ sw) * 16);
+                al[cc][tm] = *reinterpret_cast<const f16x8*>(px + ((C / 8 + cc * 4 + g) ^ sw) * 16);
             }
+    };
+    auto compute = [&](int t) {
+        const char* wb = smem + W_OFF + (t & 1) * W_BYTES;
+#pragma unroll
+        for (int cc = 0; cc < CC; ++cc) {
+            f16x8 bh[TN], bl[TN];
 #pragma unroll
             for (int tn = 0; tn < TN; ++tn) {
                 const int n = tn * 16 + fr;
@@ -199,23 +209,25 @@ __global__ void __launch_bounds__(NW * 64, 1) conv_win_kernel(const WinArgs args
             for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
                 for (int tn = 0; tn < TN; ++tn)
-                    acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[tm], bh[tn], acc[tm][tn], 0, 0, 0);
+                    acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[cc][tm], bh[tn], acc[tm][tn], 0, 0, 0);
 #pragma unroll
             for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
                 for (int tn = 0; tn < TN; ++tn)
-                    acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[tm], bl[tn], acc[tm][tn], 0, 0, 0);
+                    acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[cc][tm], bl[tn], acc[tm][tn], 0, 0, 0);
 #pragma unroll
             for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
                 for (int tn = 0; tn < TN; ++tn)
-                    acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[tm], bh[tn], acc[tm][tn], 0, 0, 0);
+                    acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[cc][tm], bh[tn], acc[tm][tn], 0, 0, 0);
         }
     };
 
     // ---- tap loop.  Issue order per tap: weights of the next tap, then (taps s < NSP) one group
     // of the next kernel row's strip.  At tap t this wave waits for its weight DMAs of t, which
-    // only the strip group issued with them at t-1 may follow.
+    // only the strip group issued with them at t-1 may follow.  The strip of row r is complete
+    // from the barrier of tap (r, 0) until the barrier of tap (r + 1, 0) (only then is its buffer
+    // refilled), so with APF the fragments of tap (r, s + 1) are read before that tap's barrier.
     const int KH = P.kh;
     const int ntap = KH * KW;
     issue_s(0, 0);
@@ -230,7 +242,9 @@ __global__ void __launch_bounds__(NW * 64, 1) conv_win_kernel(const WinArgs args
         __builtin_amdgcn_sched_barrier(0);
         if (t + 1 < ntap) issue_w(t + 1);
         if (s < NSP && r + 1 < KH) issue_s(r + 1, s);
+        if (!APF || s == 0) load_a(t);
         compute(t);
+        if (APF && s + 1 < KW) load_a(t + 1);
     }
 
     // ---- epilogue
@@ -266,10 +280,16 @@ template <int C, int KW, int TN>
 int launch_win(const WinArgs& a, int tiles, hipStream_t stream) {
     const char* e = getenv("FLOODGAN_WIN_WAVES");
     const int nw = e ? atoi(e) : g_win_waves;
-    if (nw == 8)
-        hipLaunchKernelGGL((conv_win_kernel<C, KW, TN, 8>), dim3(tiles), dim3(512), 0, stream, a);
+    const char* ea = getenv("FLOODGAN_WIN_APF");
+    const bool apf = ea ? atoi(ea) != 0 : g_win_apf != 0;
+    if (nw == 8 && apf)
+        hipLaunchKernelGGL((conv_win_kernel<C, KW, TN, 8, true>), dim3(tiles), dim3(512), 0, stream, a);
+    else if (nw == 8)
+        hipLaunchKernelGGL((conv_win_kernel<C, KW, TN, 8, false>), dim3(tiles), dim3(512), 0, stream, a);
+    else if (apf)
+        hipLaunchKernelGGL((conv_win_kernel<C, KW, TN, 4, true>), dim3(tiles), dim3(256), 0, stream, a);
     else
-        hipLaunchKernelGGL((conv_win_kernel<C, KW, TN, 4>), dim3(tiles), dim3(256), 0, stream, a);
+        hipLaunchKernelGGL((conv_win_kernel<C, KW, TN, 4, false>), dim3(tiles), dim3(256), 0, stream, a);
     return fg::launched("conv_win");
 }
 

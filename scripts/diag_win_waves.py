@@ -1,4 +1,5 @@
-"""A/B (GPU) of the row-strip window kernel's workgroup shape (FLOODGAN_WIN_WAVES 4 or 8 waves) on the content
+"""A/B (GPU) of the row-strip window kernel's workgroup shape (FLOODGAN_WIN_WAVES 4 or 8 waves) and strip-fragment
+prefetch (FLOODGAN_WIN_APF 0/1) on the content
 head's forward (7x7 64 -> 27 at 512^2) and input gradient (7x7 27(32) -> 64 over 518^2), bs 8; outputs compared.
   python scripts/diag_win_waves.py"""
 import os
@@ -35,16 +36,19 @@ def main():
     for name, prob, out, flops in (("content fwd 7x7 64->27 @512", fwd, cl, 2.0 * N * 512 * 512 * 27 * 64 * 49),
                                    ("content dgrad 7x7 27->64 @518", dgr, Y, 2.0 * N * 518 * 518 * 64 * 27 * 49)):
         res = {}
-        for nw in ("4", "8", "4", "8"):
+        for nw, apf in (("8", "0"), ("8", "1"), ("4", "1"), ("8", "0"), ("8", "1"), ("4", "1")):
             os.environ["FLOODGAN_WIN_WAVES"] = nw
+            os.environ["FLOODGAN_WIN_APF"] = apf
+            out.t.zero_()
             ops.conv_win(prob)
             torch.cuda.synchronize()
-            res[nw] = out.t.clone()
+            res[nw + apf] = out.t.clone()
             ms = min(time_it(lambda: ops.conv_win(prob)) for _ in range(3))
-            d = float((res[nw] - res["4"]).norm() / res["4"].norm())
-            print(f"{name:32s} waves {nw} {ms * 1e3:8.1f} us {flops / ms / 1e9:7.1f} TFLOP/s  rel diff vs 4 {d:.1e}",
-                  flush=True)
+            d = float((res[nw + apf] - res["80"]).norm() / res["80"].norm())
+            print(f"{name:32s} waves {nw} apf {apf} {ms * 1e3:8.1f} us {flops / ms / 1e9:7.1f} TFLOP/s  "
+                  f"rel diff vs 8/0 {d:.1e}", flush=True)
     os.environ.pop("FLOODGAN_WIN_WAVES")
+    os.environ.pop("FLOODGAN_WIN_APF")
 
 
 if __name__ == "__main__":
