@@ -67,7 +67,10 @@ __global__ void split_pixels_kernel(const float* __restrict__ src, long long npi
 }
 
 int g_win_waves = 8;   // FLOODGAN_WIN_WAVES overrides (A/B)
-int g_win_apf = 0;     // strip fragments of tap t+1 read before tap t+1's barrier; FLOODGAN_WIN_APF overrides (A/B)
+// strip fragments of tap t+1 read before tap t+1's barrier: -1 = for C 32 only (input gradient 1372 -> 1326 us;
+// the C 64 forward, which holds twice the fragments across the barrier, 1318 -> 1360 us:
+// profiles/round3/r3ap_win_apf.log); FLOODGAN_WIN_APF 0/1 overrides (A/B)
+int g_win_apf = -1;
 
 struct WinArgs {
     fg_conv_problem P;
@@ -281,7 +284,7 @@ int launch_win(const WinArgs& a, int tiles, hipStream_t stream) {
     const char* e = getenv("FLOODGAN_WIN_WAVES");
     const int nw = e ? atoi(e) : g_win_waves;
     const char* ea = getenv("FLOODGAN_WIN_APF");
-    const bool apf = ea ? atoi(ea) != 0 : g_win_apf != 0;
+    const bool apf = ea ? atoi(ea) != 0 : g_win_apf < 0 ? C == 32 : g_win_apf != 0;
     if (nw == 8 && apf)
         hipLaunchKernelGGL((conv_win_kernel<C, KW, TN, 8, true>), dim3(tiles), dim3(512), 0, stream, a);
     else if (nw == 8)
