@@ -420,8 +420,9 @@ def conv_win(prob, tag=None):
     _wrote(prob["y"][0])
 
 
-WIN_WGRAD_SPLITS = 144   # x 7 kernel rows = 1008 workgroups of 4 waves (several resident per CU); a multiple of 8:
-#                          the 7 workgroups of a split then share an XCD (conv_wgrad_win.hip)
+WIN_WGRAD_SPLITS = 216   # x 7 kernel rows = 1512 workgroups of 4 waves (several resident per CU); a multiple of 8:
+#                          the 7 workgroups of a split then share an XCD (conv_wgrad_win.hip).  bs 8, 512^2:
+#                          72 / 144 / 216 / 288 splits 1218 / 1290 / 1065 / 1085 us (profiles/round3/r3ar_*)
 
 
 def wgrad_win_eligible(prob):
