@@ -6,8 +6,13 @@ One "step" = one full iteration of models/model.py:615-651 (G forward, D step + 
 G step against the updated D + Adam(G), the four logged losses read back) over a synthetic
 batch already resident in HBM.  Prints ONE JSON line (rank 0).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 8] [--res 512]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 8] [--res 512] [--dist-backend nccl|gloo]
   N>1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+       or plain `python bench.py --gpus N`: with WORLD_SIZE unset the parent starts the N ranks
+       itself (launch_ranks) before anything touches the GPU, relays rank 0's JSON line and
+       exits non-zero if any rank fails.  `--dist-backend gloo` lets N ranks share fewer GPUs
+       (rank r on device r mod device_count): a functional check of the N-rank path on one GPU,
+       not an RCCL / xGMI measurement.
 
 --workload attentiongan | cyclegan times the cycle path instead (SURVEY.md §8(f) row 1,
 BASELINE.json configs[3]/[4]): one iteration of models/model.py:677-752 (two generators, the
@@ -200,9 +205,79 @@ def cpu_baseline(res, threads, steps=3, workload="paired", batches=(1, 8)):
                       f"batch-{batches[-1]} rate"}
 
 
+def rank_envs(n, port, base=None, backend="nccl"):
+    """The environments of the N ranks `launch_ranks` starts: what torch.distributed.run would set
+    (RANK, LOCAL_RANK, WORLD_SIZE, LOCAL_WORLD_SIZE, MASTER_ADDR / MASTER_PORT on 127.0.0.1) plus the
+    backend, over a copy of `base` (os.environ by default; HSA_ENABLE_IPC_MODE_LEGACY=0 is kept)."""
+    base = dict(os.environ if base is None else base)
+    envs = []
+    for r in range(n):
+        e = dict(base)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FLOODGAN_DIST_BACKEND=backend)
+        e.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        envs.append(e)
+    return envs
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv, backend="nccl", script=None, timeout=None):
+    """Start N rank processes of this script (one per GPU) and wait for them.  Called before any
+    GPU call in the parent, so the children are fresh processes (never an exec of a GPU process).
+    Rank 0's stdout (the JSON line) is relayed to our stdout; the other ranks' stdout goes to our
+    stderr.  When a rank fails the others are terminated (they would block in a collective) and
+    the first non-zero exit code is returned."""
+    import subprocess
+    import threading
+    script = script or os.path.abspath(__file__)
+    procs = []
+    for env in rank_envs(n, _free_port(), backend=backend):
+        out = subprocess.PIPE if env["RANK"] == "0" else sys.stderr
+        procs.append(subprocess.Popen([sys.executable, "-u", script] + list(argv), env=env, stdout=out,
+                                      text=True if out is subprocess.PIPE else None))
+
+    def relay(stream):
+        for line in stream:
+            sys.stdout.write(line)
+            sys.stdout.flush()
+    th = threading.Thread(target=relay, args=(procs[0].stdout,), daemon=True)
+    th.start()
+    t0, rc = time.time(), 0
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad or (timeout is not None and time.time() - t0 > timeout):
+            rc = bad[0] if bad else 124
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+            break
+        if all(c == 0 for c in codes):
+            break
+        time.sleep(0.2)
+    th.join(timeout=10)
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default=None,
+                    help="process-group backend for N > 1 (default nccl = RCCL; gloo lets N ranks share one GPU)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=8, help="images per GPU")
@@ -218,13 +293,28 @@ def main():
     ap.add_argument("--tiles", type=int, default=8, help="distinct synthetic tiles for --data tiles")
     args = ap.parse_args()
 
+    backend = args.dist_backend or os.environ.get("FLOODGAN_DIST_BACKEND", "nccl")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # nothing has touched the GPU yet: start the N ranks as children and relay rank 0's line
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:], backend=backend))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: refusing to report a "
+                 f"{world}-rank run as {args.gpus} GPUs")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = torch.cuda.device_count()               # counting devices does not initialise the GPU
+    if world > 1 and backend == "nccl" and ndev < int(os.environ.get("LOCAL_WORLD_SIZE", world)):
+        sys.exit(f"bench.py: {world} RCCL ranks need one GPU each, {ndev} visible (use --dist-backend gloo "
+                 f"to share)")
+    local_dev = local % max(ndev, 1)
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(local_dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_dev))
+        else:
+            dist.init_process_group("gloo")
+    dev = torch.device("cuda", local_dev)
 
     from floodgan import _lib, ops
     from floodgan.model import Model

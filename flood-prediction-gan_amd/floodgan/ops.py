@@ -132,6 +132,46 @@ def _mark_presplit(dst):
     t._fg_presplit, t._fg_presplit_ver = True, t._version
 
 
+# Self-checking scale caches (FLOODGAN_CHECK_SCALES=1, a debug mode: one device reduction and a host sync per
+# operand).  Before every f16x3 launch the operands are re-measured and the launch is refused unless the absmax
+# slot it will derive its power-of-two scale from still bounds them: fp32 operands max |v| <= slot; pre-split
+# operands |h| <= 2^14 (the producer split v * s with s = 2^(14-e) from the same slot, so a slot that no longer
+# bounds v shows as an h piece beyond 2^14, inf or NaN); cached weight packs and window-kernel split copies are
+# rebuilt and compared bit for bit with the cached ones.  SCALE_CHECKS counts the checks per kind.
+CHECK_SCALES = os.environ.get("FLOODGAN_CHECK_SCALES", "0") != "0"
+SCALE_CHECKS = {}
+
+
+def _count_check(kind):
+    SCALE_CHECKS[kind] = SCALE_CHECKS.get(kind, 0) + 1
+
+
+def _region(obj):
+    """what a gather can read: the padded extent of a Buf (a Slice's whole buffer), else the tensor"""
+    if isinstance(obj, Slice):
+        obj = obj.buf
+    return obj.nhwc() if isinstance(obj, Buf) else obj
+
+
+def check_scale(obj, slot, what):
+    """FLOODGAN_CHECK_SCALES: raise unless `slot` (the absmax slot a launch scales obj by) bounds obj"""
+    reg = _region(obj)
+    if is_presplit(obj):
+        pieces = reg.reshape(-1, 8).view(torch.float16).view(-1, 2, 8)[:, 0]
+        worst = float(pieces.abs().float().max()) if pieces.numel() else 0.0
+        ok = worst <= 2.0 ** 14
+        kind = "presplit"
+    else:
+        worst = float(reg.abs().max()) if reg.numel() else 0.0
+        bound = float(slot.max())
+        ok = worst <= bound
+        kind = "fp32"
+    if not ok:
+        raise RuntimeError(f"FLOODGAN_CHECK_SCALES: the {kind} operand '{what}' is not bounded by its cached scale "
+                           f"slot (max {worst!r}" + (f" > slot {bound!r})" if kind == "fp32" else " > 2^14 in h)"))
+    _count_check(kind)
+
+
 def absmax(t):
     """Device scalar >= max |t| (the f16x3 operand-scale source), over the whole storage of a
     tensor or of a Buf (border and padding channels included: everything a gather can read);
@@ -223,7 +263,11 @@ def pack_weight(w, m, split=None):
         packs = w.__dict__.setdefault("_fg_packs", {}) if PACK_CACHE else None
         key = bytes(s)
         if packs is not None and key in packs and packs[key].absmax is amax:
+            if CHECK_SCALES:
+                _check_pack(w, s, amax, packs[key])
             return packs[key]          # packed from the current values (re-packed by the last adam_step)
+        if CHECK_SCALES:
+            check_scale(w, amax, "weight")
         wp = torch.empty(2 * packed_numel(m), dtype=torch.float16, device=w.device)
         L.check(_lib().fg_pack_weight_f16(L.ptr(w), C.byref(s), L.ptr(amax), L.ptr(wp), L.stream_handle()),
                 "pack_weight_f16")
@@ -239,6 +283,18 @@ def pack_weight(w, m, split=None):
     wp = torch.empty(packed_numel(m), dtype=torch.float32, device=w.device)
     L.check(_lib().fg_pack_weight(L.ptr(w), C.byref(s), L.ptr(wp), L.stream_handle()), "pack_weight")
     return wp
+
+
+def _check_pack(w, s, amax, cached):
+    """FLOODGAN_CHECK_SCALES: a cached f16x3 pack must equal a fresh pack of the current weights by a slot
+    that bounds them"""
+    check_scale(w, amax, "weight")
+    fresh = torch.empty_like(cached)
+    L.check(_lib().fg_pack_weight_f16(L.ptr(w), C.byref(s), L.ptr(amax), L.ptr(fresh), L.stream_handle()),
+            "pack_weight_f16")
+    if not torch.equal(fresh.view(torch.int16), cached.view(torch.int16)):
+        raise RuntimeError("FLOODGAN_CHECK_SCALES: a cached weight pack differs from a fresh pack of the weights")
+    _count_check("pack")
 
 
 _CONV_FIELDS = ("sxn", "sxa", "sxb", "sxr", "syn", "sya", "syb", "syc", "m_img", "m_a", "m_b", "kh", "j_valid",
@@ -315,6 +371,8 @@ def _conv(probs, in_stats=False):
             if id(xb) not in keep:
                 keep[id(xb)] = absmax(xb)
             s.x_absmax = keep[id(xb)].data_ptr()
+            if CHECK_SCALES:
+                check_scale(xb, keep[id(xb)], "conv input")
             wa = getattr(wt, "absmax", None)
             if wa is None:              # fp32 weights split on the fly: scale from their own max
                 if ("w", id(wt)) not in keep:
@@ -323,6 +381,8 @@ def _conv(probs, in_stats=False):
                                              L.stream_handle()), "absmax")
                 wa = keep[("w", id(wt))]
             s.w_absmax = wa.data_ptr()
+            if CHECK_SCALES and wt.dtype == torch.float32:
+                check_scale(wt, wa, "fp32 weight")
     stats = _stats_partials(probs, arr) if (in_stats and FUSED_IN_STATS) else None
     L.check(_lib().fg_conv_fwd(arr, len(probs), L.stream_handle()), "conv_fwd")
     _wrote(*[p["y"][0] for p in probs])
@@ -368,9 +428,21 @@ def split_pixels(X):
         raise RuntimeError("split_pixels of a pre-split buffer")
     cached = getattr(t, "_fg_split", None)
     if cached is not None and getattr(t, "_fg_split_ver", None) == t._version:
+        if CHECK_SCALES:
+            check_scale(X, cached.absmax, "split-copy source")
+            if cached.absmax is not absmax(t):
+                raise RuntimeError("FLOODGAN_CHECK_SCALES: a cached split copy was scaled by another slot")
+            fresh = torch.empty_like(cached)
+            L.check(_lib().fg_split_pixels(L.ptr(t), X.n * X.hp * X.wp, X.c, X.wp, L.ptr(cached.absmax), L.ptr(fresh),
+                                           L.stream_handle()), "split_pixels")
+            if not torch.equal(fresh.view(torch.int16), cached.view(torch.int16)):
+                raise RuntimeError("FLOODGAN_CHECK_SCALES: a cached split copy differs from its source")
+            _count_check("split_copy")
         return cached
     npix = X.n * X.hp * X.wp
     out = torch.empty(npix * 2 * X.c, dtype=torch.float16, device=t.device)
+    if CHECK_SCALES:
+        check_scale(X, absmax(t), "split-copy source")
     L.check(_lib().fg_split_pixels(L.ptr(t), npix, X.c, X.wp, L.ptr(absmax(t)), L.ptr(out), L.stream_handle()),
             "split_pixels")
     out.absmax = absmax(t)
@@ -491,6 +563,9 @@ def wgrad(prob, wmap, dw, accumulate=False):
     if L.wgrad_f16x3():
         pa, xa = absmax(prob["p"][0]), absmax(prob["x"][0])
         s.p_absmax, s.x_absmax = pa.data_ptr(), xa.data_ptr()
+        if CHECK_SCALES:
+            check_scale(prob["p"][0], pa, "wgrad gradient")
+            check_scale(prob["x"][0], xa, "wgrad input")
     s.p_presplit, s.x_presplit = int(is_presplit(prob["p"][0])), int(is_presplit(prob["x"][0]))
     st = L.stream_handle()
     L.check(_lib().fg_conv_wgrad(C.byref(s), st), "conv_wgrad")
@@ -534,10 +609,15 @@ def pack_input(a, ca, b, cb, dst, img0, nimg, pad_mode, amax=None):
         if slot is None:
             _wrote(dst)
     else:
+        # a part of a multi-launch fill: the slot must be the one amax_slot(dst) recorded on dst, at dst's
+        # current version (the kernels write through raw pointers, so the counter has not moved since)
         slot = amax
         t = _tensor(dst)
-        if getattr(t, "_fg_split", None) is not None:
-            t._fg_split = None
+        if getattr(t, "_fg_amax", None) is not amax or getattr(t, "_fg_amax_ver", None) != t._version:
+            raise RuntimeError("pack_input: the shared absmax slot is not the one amax_slot(dst) recorded on dst "
+                               "(or dst was written by torch since)")
+        t._fg_split = None
+        t._fg_presplit = False
     L.check(_lib().fg_pack_input(sview(a), ca, sview(b), cb, view(dst), img0, nimg, pad_mode, L.ptr(slot),
                                  L.stream_handle()), "pack_input")
 

@@ -1,6 +1,7 @@
 #!/bin/bash
-# One GPU session: tile micro-bench, parity tests + smoke + bench, kernel profile, counter
-# passes on the resblock conv.  Every GPU step has its own limit; stop at the first failure.
+# One GPU session: tile micro-bench, parity tests + smoke + bench, a 2-rank gloo bench on the one GPU
+# (DP2=1), kernel profile, counter passes on the resblock conv.  Every GPU step has its own limit;
+# stop at the first failure.
 cd "$(dirname "$0")/.." || exit 1
 TAG=${TAG:-run}
 mkdir -p gpurun_out
@@ -11,6 +12,11 @@ fi
 BENCH_ARGS=--no-cpu-baseline scripts/gpu_check.sh > gpurun_out/check.log 2>&1
 rc=$?; grep -a "passed\|failed\|smoke:\|rc=" gpurun_out/check.log; [ $rc -eq 0 ] || exit $rc
 grep -o '"value": [0-9.]*' gpurun_out/bench.log
+if [ -n "$DP2" ]; then
+  timeout -k 10 400 python bench.py --gpus 2 --dist-backend gloo --steps 3 --warmup 1 > gpurun_out/bench_dp2_gloo.log 2>&1 \
+    || { echo "dp2 bench failed"; tail -20 gpurun_out/bench_dp2_gloo.log; exit 1; }
+  grep -o '"value": [0-9.]*\|"n_gpus": [0-9]*\|"parallelism": "[a-z0-9]*"' gpurun_out/bench_dp2_gloo.log
+fi
 scripts/gpu_profile.sh $TAG > /dev/null 2>&1 || { echo "profile failed"; exit 1; }
 if [ -n "$PMC" ]; then
   scripts/gpu_pmc.sh ${TAG}_fwd > /dev/null && KIND=wgrad scripts/gpu_pmc.sh ${TAG}_wgrad > /dev/null || { echo "pmc failed"; exit 1; }

@@ -244,16 +244,21 @@ def test_wgrad_f3(case, on):
         L.set_conv_math(prev)
 
 
-def test_wgrad_window():
+@pytest.mark.parametrize("splits,H,W", [(None, 5, 288), (8, 12, 512), (7, 12, 512), (216, 30, 512)])
+def test_wgrad_window(splits, H, W):
     """the row-strip content-head weight gradient (fg_conv_wgrad_win): gradient 27(32) channels
     with its 6-wide zero border, input 64 channels reflect-padded by 3, against fp64 and against
-    the generic f16x3 weight-gradient kernel"""
+    the generic f16x3 weight-gradient kernel.  The split counts walk several 32-px chunks per split across
+    column-block, row and image edges: 8 splits (XCD-grouped, 48 chunks each), 7 (the ungrouped mapping, a
+    short last split) and the production 216 over 960 chunks (4-5 each); None = the default over 90 chunks"""
     from floodgan import _lib as L, ops, plans as PL
     prev = L.get_conv_math()
+    prev_splits = ops.WIN_WGRAD_SPLITS
     L.set_conv_math("f16x3")
     try:
+        if splits is not None:
+            ops.WIN_WGRAD_SPLITS = splits
         torch.manual_seed(6)
-        H, W = 5, 288
         x = torch.randn(2, 64, H, W, dtype=torch.float64)
         gy = torch.randn(2, 27, H, W, dtype=torch.float64) * 1e-4
         w = torch.zeros(27, 64, 7, 7, dtype=torch.float64)
@@ -274,6 +279,7 @@ def test_wgrad_window():
         assert nrel(dw2, gw_ref) < KTOL
     finally:
         ops.USE_WIN = True
+        ops.WIN_WGRAD_SPLITS = prev_splits
         L.set_conv_math(prev)
 
 
