@@ -54,6 +54,38 @@ def resblock_conv_bytes(batch, res):
     return 4.0 * batch * ((hw + 2) ** 2 * 256 + hw * hw * 256 + hw * hw // 32 * 256 * 2) + 2 * 2 * 256 * 2304
 
 
+def resblock_dgrad_bytes(batch, res):
+    """algorithmic HBM bytes of one resblock input-gradient interior launch (executor._dgrad_s1_padded): the
+    pre-split conv-output gradient (fp16 h + l = 4 B per element) over its 2-px zero border read once, the
+    pre-split flipped weights, the (H x W) interior of the padded-domain gradient written once"""
+    hw = res // 4
+    return 4.0 * batch * ((hw + 4) ** 2 * 256 + hw * hw * 256) + 2 * 2 * 256 * 2304
+
+
+def resblock_wgrad_bytes(batch, res):
+    """algorithmic HBM bytes of one resblock weight-gradient launch (conv_wgrad_f3_kernel<256,0,3>): the pre-split
+    gradient's interior rows and the pre-split input over its reflect border 1 read once, one fp32 256 x 2304
+    partial slab per pixel split written (plans.wgrad_splits; fg_wgrad_reduce sums them in its own launch)"""
+    from floodgan.plans import wgrad_splits
+    hw = res // 4
+    splits, _ = wgrad_splits(256, 2304, batch * hw * hw, f3=True)
+    return 4.0 * batch * (hw * hw * 256 + (hw + 2) ** 2 * 256) + 4.0 * splits * 256 * 2304
+
+
+# the three resblock conv kinds the bench times live (KernelTimer tags), with their committed counter passes
+# (scripts/gpu_pmc.sh KIND=<conv_one kind> + scripts/pmc_summary.py): fwd = the conv1 / conv2 forward launches
+# with the InstanceNorm statistics epilogue; dgrad = the input-gradient interior; wgrad = the weight gradient
+RESBLOCK_KINDS = {
+    "resblock_conv_fwd": dict(kernel="conv_fwd_f3_kernel<256,256,...,STATS>", bytes=resblock_conv_bytes,
+                              pmc=[os.path.join(ROOT, "profiles", "round4", "r4_pmc_resblock_fwd_stats_ps.json")]),
+    "resblock_conv_dgrad": dict(kernel="conv_fwd_f3_kernel<256,256,...> (input-gradient interior)",
+                                bytes=resblock_dgrad_bytes,
+                                pmc=[os.path.join(ROOT, "profiles", "round4", "r4_pmc_resblock_dgrad_ps.json")]),
+    "resblock_conv_wgrad": dict(kernel="conv_wgrad_f3_kernel<256,0,3>", bytes=resblock_wgrad_bytes,
+                                pmc=[os.path.join(ROOT, "profiles", "round4", "r4_pmc_resblock_wgrad_ps.json")]),
+}
+
+
 def step_roofline(img_s_per_gpu, res, peak_conv):
     """The whole step against its ceilings: the conv math's MFMA roof
     (1593.5 GFLOP per 512^2 image), the exact-fp32 MFMA roof, and HBM (3.96 GB per image)."""
@@ -102,19 +134,13 @@ def p2p_step_gflop_per_img(res):
     return tot / 1e9
 
 
-# the timed resblock forward launches (conv1 and conv2 of the 9 blocks) all read FG_PRESPLIT operands (conv2: the norm
-# pass's output; conv1: the block input's pre-split copy) on 8 waves of 64x128 with the statistics epilogue: the
-# counter summary of that kind (averaged if several are listed)
-PMC_SUMMARIES = [os.path.join(ROOT, "profiles", "round3", "r3x_pmc_resblock_fwd_stats_ps.json")]
-
-
-def pmc_traffic(kernel_tag):
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 counter passes
+def pmc_traffic(kernel_tag, paths):
+    """HBM bytes per launch of a kernel from the committed rocprofv3 counter passes
     (scripts/gpu_pmc.sh + scripts/pmc_summary.py: FETCH_SIZE x2 per the gfx950 correction of
     MI355X_MICROARCH.md, plus WRITE_SIZE) averaged over its launch kinds, or None when a summary is missing or does
     not match the kernel."""
     ss = []
-    for path in PMC_SUMMARIES:
+    for path in paths:
         try:
             with open(path) as f:
                 ss.append(json.load(f))
@@ -127,7 +153,7 @@ def pmc_traffic(kernel_tag):
         v = [s.get(k) for s in ss]
         return None if any(x is None for x in v) else sum(v) / len(v)
     return {"bytes_per_launch": avg("hbm_bytes"), "read": avg("hbm_read_bytes"), "write": avg("hbm_write_bytes"),
-            "source": [os.path.relpath(p, ROOT) for p in PMC_SUMMARIES], "l2_hit": avg("l2_hit"),
+            "source": [os.path.relpath(p, ROOT) for p in paths], "l2_hit": avg("l2_hit"),
             "mfma_busy": avg("mfma_busy"), "clock_ghz": avg("clock_ghz"),
             "per_kind": {s.get("kind", str(i)): {k: s.get(k) for k in ("hbm_bytes", "l2_hit", "mfma_busy", "clock_ghz",
                                                                         "launch_s")}
@@ -362,7 +388,7 @@ def main():
     if world > 1:
         dist.barrier()
     tag = "p2p_d_model8_fwd" if p2p else "resblock_conv_fwd"
-    timer = ops.KernelTimer([tag])
+    timer = ops.KernelTimer([tag] + ([] if p2p or cycle else ["resblock_conv_dgrad", "resblock_conv_wgrad"]))
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     with timer:
@@ -382,7 +408,8 @@ def main():
     nprod = {"f16x3": 3, "fwd_f16x3": 3, "bf16x6": 6, "fwd_x6": 6}.get(math)
     peak = BF16_MFMA_PEAK_TFLOPS / nprod if nprod else FP32_MFMA_PEAK_TFLOPS
     fwd_x6 = nprod is not None
-    durs = timer.durations_ms()[tag]
+    all_durs = timer.durations_ms()
+    durs = all_durs[tag]
     avg_ms = sum(durs) / max(len(durs), 1)
     if p2p:
         # the discriminator's model.8 conv (256 -> 512, 4x4 s1): per step one 2B-image launch (D step) and
@@ -435,7 +462,8 @@ def main():
                                         if fwd_x6 else "fp32 MFMA dense peak"),
                          "frac": round(achieved / peak, 4),
                          "traffic": (None if p2p else
-                                     pmc_traffic("conv_fwd_f3_kernel<256,256,...,STATS>" if nprod == 3 else None)),
+                                     pmc_traffic("conv_fwd_f3_kernel<256,256,...,STATS>" if nprod == 3 else None,
+                                                 RESBLOCK_KINDS[tag]["pmc"])),
                          "avg_launch_ms": round(avg_ms, 4), "launches": len(durs),
                          "flop_per_launch": flops},
             "step_tflops": (None if cycle else
@@ -454,6 +482,25 @@ def main():
         if tr:
             tr["over_algorithmic"] = round(tr["bytes_per_launch"] / resblock_conv_bytes(B, R), 3)
             tr["algorithmic_bytes"] = resblock_conv_bytes(B, R)
+        if not (p2p or cycle) and nprod == 3:
+            # every resblock conv kind with its own live launch average, fraction and counter pass
+            kinds = {}
+            for k, spec in RESBLOCK_KINDS.items():
+                d = all_durs.get(k) or []
+                if not d:
+                    continue
+                ms = sum(d) / len(d)
+                ach = resblock_conv_flops(B, R) / (ms * 1e-3) / 1e12
+                alg = spec["bytes"](B, R)
+                t = pmc_traffic(spec["kernel"], spec["pmc"])
+                if t:
+                    t["over_algorithmic"] = round(t["bytes_per_launch"] / alg, 3)
+                kinds[k] = {"kernel": spec["kernel"], "achieved": round(ach, 2), "peak": round(peak, 2),
+                            "unit": "TFLOP/s", "frac": round(ach / peak, 4), "avg_launch_ms": round(ms, 4),
+                            "launches": len(d), "flop_per_launch": resblock_conv_flops(B, R),
+                            "algorithmic_bytes": alg, "achieved_algorithmic_GBs": round(alg / (ms * 1e-3) / 1e9, 1),
+                            "traffic": t}
+            out["roofline"]["per_kind"] = kinds
         if world == 1 and not args.no_cpu_baseline:
             threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", 0)) or len(os.sched_getaffinity(0))
             out["cpu_baseline"] = cpu_baseline(R, threads, steps=1 if cycle or p2p else 3, workload=args.workload,

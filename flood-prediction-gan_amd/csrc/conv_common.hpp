@@ -118,4 +118,9 @@ bool f3_stats_ok(const fg_conv_problem* probs, int nprob, int max_n);
 // Pipelined f16x3 weight-gradient kernel (conv_wgrad_f3.hip), same contract.
 int launch_wgrad_f3(const fg_wgrad_problem& p, hipStream_t stream, int* rc);
 
+// The generator stem's weight gradient (conv_stem.hip: 7x7, 9 -> 64 channels, 64-px strips of m_chunk / 64
+// rows per split), same contract; stem_wgrad_rows = its rows per split, or 0 when it does not apply.
+int stem_wgrad_rows(const fg_wgrad_problem& p);
+int launch_wgrad_stem(const fg_wgrad_problem& p, hipStream_t stream, int* rc);
+
 }  // namespace fgc

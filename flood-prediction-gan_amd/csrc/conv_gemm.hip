@@ -1456,6 +1456,7 @@ FG_API int fg_conv_wgrad(const fg_wgrad_problem* prob, hipStream_t stream) {
             if (!p.p_absmax || !p.x_absmax)
                 return fg::fail(FG_ERR_INVALID, "fg_conv_wgrad: the f16x3 math needs p_absmax and x_absmax");
             int rc = 0;
+            if (g_wgrad_tile < 0 && fgc::launch_wgrad_stem(p, stream, &rc)) return rc; // conv_stem.hip
             if (g_wgrad_tile < 0 && fgc::launch_wgrad_f3(p, stream, &rc)) return rc;   // conv_wgrad_f3.hip
             if (p.p_presplit || p.x_presplit)
                 return fg::fail(FG_ERR_INVALID, "fg_conv_wgrad: pre-split operands need the pipelined kernel");

@@ -1,0 +1,238 @@
+// The generator stem's weight gradient: the 7x7 conv over the reflect-padded 9-channel input with 64
+// output channels (models/model_architectures.py:312, :342-343; convolution_backward's weight gradient):
+//
+//   out[split][a][r*63 + j] = sum over the split's output pixels (y, x) of  gy[y][x][a] * xpad[y + r][9 x + j]
+//
+// with j = s*9 + c, so that for one kernel row r the 63 k-columns of an output pixel are the 63 CONTIGUOUS
+// values of the padded input row starting at its own 9 channels.  A workgroup owns a 64-px column strip of
+// `rows` output rows of one image and walks down it: each step stages ONE new input row of the strip (70 px x 9
+// channels, split once into the scaled fp16 pieces h, l) into a ring of 8 LDS rows -- the 7 kernel rows read
+// the ring, so the input is fetched once per strip instead of once per tap -- and the gradient row (64 px x 64
+// channels, split once).  v_mfma_f32_16x16x32_f16 with the reduction over 32 consecutive pixels: the gradient
+// operand is a transposed read (ds_read_b64_tr_b16) of its [px][channel] image; the input operand a
+// transposed read of the flat input row, 8 B aligned through four copies of each row shifted by 0..3
+// elements (a lane reading pixel q of its group uses copy (4 - q) & 3).  The 64 x 448 (63 per r, one padding
+// column) product of a step is split over 8 waves: waves 0-3 own 4 column blocks of 16, waves 4-7 three, each
+// all 64 output channels, so every SIMD carries 7 blocks.  One fp32 partial slab per workgroup
+// (fg_wgrad_reduce sums them).  Replaces conv_wgrad_x6 for this shape (2x its algorithmic bytes).
+#include "conv_common.hpp"
+
+namespace {
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+constexpr int ST_C = 9, ST_J = 63, ST_K = 7 * ST_J, ST_N = 64;
+constexpr int ST_PX = 64;                        // output pixels per strip (two reductions of 32)
+constexpr int ST_FLAT = (ST_PX + 6) * ST_C;      // 630 flat input values per strip row
+constexpr int ST_COPY = 640;                     // fp16 per shifted copy (>= 630 + 3 + the 4 of the last read)
+constexpr int ST_COPYB = ST_COPY * 2;
+constexpr int ST_PIECE = 4 * ST_COPYB;           // the four shifted copies of one piece
+constexpr int ST_XROW = 2 * ST_PIECE;            // h, l
+constexpr int ST_RING = 8;                       // 7 rows in use + the one being staged
+constexpr int ST_GIMG = ST_PX * ST_N * 2;        // gradient row image per piece: [64 px][64 ch] fp16
+constexpr int ST_GBUF = 2 * ST_GIMG;
+constexpr int ST_LDS = ST_RING * ST_XROW + 2 * ST_GBUF;   // 114688 B
+constexpr int kOOB = 0x7fffffff;
+
+// 32-B column-pair swizzle of the gradient image (conv_wgrad_f3.hip): the 8 pixel rows a 32-lane half of a
+// transposed read touches land on distinct bank groups
+__device__ __forceinline__ int swz_tr(int row) { return ((row & 3) | (((row >> 3) & 1) << 2)) << 1; }
+__device__ __forceinline__ int gimg_off(int row, int col) {
+    return row * (ST_N * 2) + (((col >> 3) ^ (swz_tr(row) & 7)) << 4) + ((col & 7) << 1);
+}
+
+__device__ __forceinline__ f16x8 tr_frag(const char* base, int a0, int a1) {
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + a0));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + a1));
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(f16x8, v);
+}
+
+__device__ __forceinline__ void split4(const f32x4& v, float s, f16x4& h, f16x4& l) {
+    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+    u32x2 hu, lu;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+        unsigned a, b;
+        fgc::split_pair_mix(v[2 * e], v[2 * e + 1], s, a, b);
+        hu[e] = a;
+        lu[e] = b;
+    }
+    h = __builtin_bit_cast(f16x4, hu);
+    l = __builtin_bit_cast(f16x4, lu);
+}
+
+__global__ void __launch_bounds__(512, 1) stem_wgrad_kernel(const fg_wgrad_problem P, int rows) {
+    __shared__ __attribute__((aligned(1024))) char smem[ST_LDS];
+    char* const xring = smem;
+    char* const gbuf = smem + ST_RING * ST_XROW;
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int strips = P.m_b / ST_PX, groups = P.m_a / rows;
+    const int split = blockIdx.x;
+    const int img = split / (strips * groups);
+    const int rem = split - img * strips * groups;
+    const int grp = rem / strips, strip = rem - grp * strips;      // neighbouring blocks: neighbouring strips
+    const int a0 = grp * rows, b0 = strip * ST_PX;
+    const int nsteps = rows + 6;
+
+    const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc((void*)P.p, 0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)P.x, 0, 0x7fffffff, 0x00020000);
+    const float sp = fgc::pow2_scale(P.p_absmax);
+    const float sx = fgc::pow2_scale(P.x_absmax);
+
+    // the shifted copies' unwritten heads / tails read as zeros
+    for (int i = tid; i < ST_RING * ST_XROW / 16; i += 512) reinterpret_cast<f32x4*>(xring)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // ---- staging: flat input values e = tid, tid + 512 (< 630) of row a0 + li; gradient float4 slots
+    // (px = tid / 16 + 32 i, channels 4 (tid % 16) ..) of output row a0 + li - 6
+    const int gpx = tid >> 4, gch = (tid & 15) * 4;
+    const bool x2 = tid + 512 < ST_FLAT;
+    const int xbase = img * (int)P.sxn + b0 * ST_C;
+    const int gbase = img * (int)P.spn + b0 * (int)P.spb + gch;
+    float rx0 = 0.f, rx1 = 0.f;
+    f32x4 rg0 = {0.f, 0.f, 0.f, 0.f}, rg1 = rg0;
+    auto load = [&](int li) {
+        const bool ok = li < nsteps;
+        const int xo = xbase + (a0 + li) * (int)P.sxr + tid;
+        rx0 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, ok ? xo * 4 : kOOB, 0, 0));
+        rx1 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, ok && x2 ? (xo + 512) * 4 : kOOB, 0, 0));
+        const bool gok = ok && li >= 6;
+        const int go = gbase + (a0 + li - 6) * (int)P.spa + gpx * (int)P.spb;
+        rg0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(pr, gok ? go * 4 : kOOB, 0, 0));
+        rg1 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            pr, gok ? (go + 32 * (int)P.spb) * 4 : kOOB, 0, 0));
+    };
+    auto put_x = [&](char* xs, int e, float v) {
+        const float vs = v * sx;
+        const _Float16 h = (_Float16)vs;
+        const _Float16 l = (_Float16)(vs - (float)h);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            *reinterpret_cast<_Float16*>(xs + t * ST_COPYB + 2 * (e + t)) = h;
+            *reinterpret_cast<_Float16*>(xs + ST_PIECE + t * ST_COPYB + 2 * (e + t)) = l;
+        }
+    };
+    auto store = [&](int li) {
+        char* xs = xring + (li & (ST_RING - 1)) * ST_XROW;
+        put_x(xs, tid, rx0);
+        if (x2) put_x(xs, tid + 512, rx1);
+        if (li >= 6) {
+            char* gb = gbuf + (li & 1) * ST_GBUF;
+            f16x4 h, l;
+            split4(rg0, sp, h, l);
+            *reinterpret_cast<f16x4*>(gb + gimg_off(gpx, gch)) = h;
+            *reinterpret_cast<f16x4*>(gb + ST_GIMG + gimg_off(gpx, gch)) = l;
+            split4(rg1, sp, h, l);
+            *reinterpret_cast<f16x4*>(gb + gimg_off(gpx + 32, gch)) = h;
+            *reinterpret_cast<f16x4*>(gb + ST_GIMG + gimg_off(gpx + 32, gch)) = l;
+        }
+    };
+
+    // ---- column blocks: t = 4 r + ct (ct: columns 16 ct .. of kernel row r); waves 0-3 own t = 4w .. 4w+3,
+    // waves 4-7 own t = 16 + 3 (w - 4) .. +2
+    const int t0 = wave < 4 ? 4 * wave : 16 + 3 * (wave - 4);
+    const int g = lane >> 4, q = (lane >> 2) & 3, p4 = (lane & 3) * 4;
+    const int cp = (4 - q) & 3;                     // the shifted copy that makes this lane's read 8-B aligned
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[mt][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    auto compute = [&](int k, auto NTW) {
+        constexpr int NT = decltype(NTW)::value;
+        const char* gb = gbuf + (k & 1) * ST_GBUF;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            f16x8 ah[4], al[4];
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) {
+                const int c = mt * 16 + p4;
+                const int o0 = gimg_off(32 * kk + 8 * g + q, c), o1 = gimg_off(32 * kk + 8 * g + 4 + q, c);
+                ah[mt] = tr_frag(gb, o0, o1);
+                al[mt] = tr_frag(gb + ST_GIMG, o0, o1);
+            }
+            const int f0 = 9 * (32 * kk + 8 * g + q) + p4 + cp;
+#pragma unroll
+            for (int i = 0; i < NT; ++i) {
+                const int t = t0 + i, r = t >> 2, ct = t & 3;
+                const char* xs = xring + ((k - 6 + r) & (ST_RING - 1)) * ST_XROW + cp * ST_COPYB;
+                const int ad = 2 * (f0 + 16 * ct);
+                const f16x8 bh = tr_frag(xs, ad, ad + 72);
+                const f16x8 bl = tr_frag(xs + ST_PIECE, ad, ad + 72);
+#pragma unroll
+                for (int mt = 0; mt < 4; ++mt) {
+                    acc[mt][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[mt], bh, acc[mt][i], 0, 0, 0);
+                    acc[mt][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[mt], bl, acc[mt][i], 0, 0, 0);
+                    acc[mt][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[mt], bh, acc[mt][i], 0, 0, 0);
+                }
+            }
+        }
+    };
+
+    // ---- write-after-barrier pipeline: step k stores step k+1's registers (ring slot (k+1) & 7 and gradient
+    // buffer (k+1) & 1 are not read by step k), refills them with step k+2 and reduces output row k - 6
+    __syncthreads();
+    load(0);
+    store(0);
+    load(1);
+    __syncthreads();
+    for (int k = 0; k < nsteps; ++k) {
+        if (k + 1 < nsteps) store(k + 1);
+        load(k + 2);
+        if (k >= 6) {
+            if (wave < 4)
+                compute(k, std::integral_constant<int, 4>{});
+            else
+                compute(k, std::integral_constant<int, 3>{});
+        }
+        __syncthreads();
+    }
+
+    // ---- epilogue: scaled fp32 slab rows a (output channels), columns r*63 + j
+    float* out = P.out + (size_t)split * ST_N * ST_K;
+    const float osc = 1.f / (sp * sx);
+    const int fr = lane & 15;
+    const int ntw = wave < 4 ? 4 : 3;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        if (i >= ntw) break;
+        const int t = t0 + i, r = t >> 2, j = 16 * (t & 3) + fr;
+        if (j >= ST_J) continue;
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+            for (int reg = 0; reg < 4; ++reg)
+                out[(size_t)(mt * 16 + 4 * g + reg) * ST_K + r * ST_J + j] = acc[mt][i][reg] * osc;
+    }
+}
+
+}  // namespace
+
+namespace fgc {
+
+int stem_wgrad_rows(const fg_wgrad_problem& p) {
+    // rows per split encoded as m_chunk = 64 * rows (a 64-px strip of `rows` output rows per workgroup)
+    if (p.n_a != ST_N || p.kh != 7 || p.j_valid != ST_J || p.sxb != ST_C || p.sxr != p.sxa || p.m_b % ST_PX ||
+        p.m_chunk % ST_PX || p.p_presplit || p.x_presplit || !p.p_absmax || !p.x_absmax || ((uintptr_t)p.p & 15) ||
+        (p.spn | p.spa | p.spb) % 4 || p.spb < ST_N)
+        return 0;
+    const int rows = p.m_chunk / ST_PX;
+    if (rows < 1 || p.m_a % rows || (long long)p.splits != (long long)p.m_img * (p.m_b / ST_PX) * (p.m_a / rows))
+        return 0;
+    return rows;
+}
+
+// Returns 1 when the stem kernel took the problem (status in *rc), 0 when it does not apply.
+int launch_wgrad_stem(const fg_wgrad_problem& p, hipStream_t stream, int* rc) {
+    const int rows = stem_wgrad_rows(p);
+    if (!rows) return 0;
+    hipLaunchKernelGGL(stem_wgrad_kernel, dim3(p.splits), dim3(512), 0, stream, p, rows);
+    *rc = fg::launched("stem_wgrad");
+    return 1;
+}
+
+}  // namespace fgc

@@ -277,10 +277,184 @@ __global__ void __launch_bounds__(NW * 64, 1) conv_win_kernel(const WinArgs args
     }
 }
 
+// Register-staged form: one kernel row per barrier pair instead of one tap per barrier.  The whole row's
+// weights (KW taps, [s][pc][NR][C]) and its input strip sit in LDS together (single-buffered: 68.6 + 57.3 KB at
+// C 64); the next row's strip and weights are loaded into registers (16-B buffer loads, the same bytes the DMA
+// form copies) while the KW taps of the current row run -- 168 MFMAs per wave between barriers instead of 24 --
+// and written over the current ones after a barrier.
+template <int C, int KW, int TN, int NW>
+__global__ void __launch_bounds__(NW * 64, 1) conv_win_rs_kernel(const WinArgs args) {
+    constexpr int NT = NW * 64;
+    constexpr int BM = 256, WM = BM / NW, TM = WM / 16;
+    constexpr int PB = 4 * C;                                   // strip bytes per pixel (h | l)
+    constexpr int NR = TN * 16;                                 // weight rows staged
+    constexpr int STRIP_BYTES = (BM + 2 * (KW - 1)) * PB;
+    constexpr int SCH = (STRIP_BYTES / 16 + NT - 1) / NT;       // strip 16-B chunks per thread
+    constexpr int W_TAP = 2 * NR * C * 2;                       // [pc][NR][C] fp16 per tap
+    constexpr int TAP_CH = W_TAP / 16;
+    constexpr int WCH = KW * TAP_CH / NT;                       // weight 16-B chunks per thread per kernel row
+    static_assert((KW * TAP_CH) % NT == 0, "weight row is not a whole number of chunks per thread");
+    constexpr int W_OFF = (STRIP_BYTES + 1023) / 1024 * 1024;
+    __shared__ __attribute__((aligned(1024))) char smem[W_OFF + KW * W_TAP];
+
+    const fg_conv_problem& P = args.P;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wid = fg::xcd_remap(blockIdx.x, gridDim.x);
+    const int img = wid / args.tiles_per_img;
+    const int p0 = (wid - img * args.tiles_per_img) * BM;
+    const int mab = P.m_a * P.m_b;
+    const int a0 = p0 / P.m_b, b0 = p0 - (p0 / P.m_b) * P.m_b;
+    const int len0 = min(BM, min(P.m_b - b0, mab - p0));
+    const int len1 = (a0 + 1 < P.m_a) ? min(BM - len0, P.m_b) : 0;
+    const int s0pix = len0 + KW - 1;
+    const int strip_bytes = (len0 + len1 + 2 * (KW - 1)) * PB;
+    const int wp = args.wp;
+    constexpr int kOOB = 0x7fffffff;
+
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)args.xs, 0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)P.w, 0, 0x7fffffff, 0x00020000);
+
+    // strip chunk o = (tid + i NT) * 16 of the LDS strip <- its source byte (row offset r * wp * PB added per row)
+    const int seg0_pix = img * (int)(P.sxn / C) + a0 * wp + b0;
+    const int seg1_pix = img * (int)(P.sxn / C) + (a0 + 1) * wp;
+    int s_src[SCH];
+#pragma unroll
+    for (int i = 0; i < SCH; ++i) {
+        const int o = (tid + i * NT) * 16;
+        s_src[i] = o >= strip_bytes ? -1 : o < s0pix * PB ? seg0_pix * PB + o : seg1_pix * PB + (o - s0pix * PB);
+    }
+    // weight chunk F = tid + i NT of the row image [s][pc][NR][C]: tap s = F / TAP_CH, in-tap chunk f
+    int w_src[WCH];
+#pragma unroll
+    for (int i = 0; i < WCH; ++i) {
+        const int F = tid + i * NT, s = F / TAP_CH, f = F - s * TAP_CH;
+        const int pc = f / (NR * C / 8);
+        const int rem = f - pc * (NR * C / 8);
+        const int n = rem / (C / 8);
+        const int ch = (rem - n * (C / 8)) ^ swz_wrow<C>(n);
+        w_src[i] = (min(n, P.n_out - 1) * (P.ldw / 8) + ch) * 32 + pc * 16 + ((s * C) / 8) * 32;
+    }
+    f32x4 rs[SCH], rw[WCH];
+    auto load = [&](int r) {
+        const int soff = r * wp * PB, woff = ((r * P.jp) / 8) * 32;
+#pragma unroll
+        for (int i = 0; i < SCH; ++i)
+            rs[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, s_src[i] >= 0 ? s_src[i] + soff : kOOB, 0, 0));
+#pragma unroll
+        for (int i = 0; i < WCH; ++i)
+            rw[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(wr, w_src[i] + woff, 0, 0));
+    };
+    auto store = [&]() {
+#pragma unroll
+        for (int i = 0; i < SCH; ++i)
+            if (s_src[i] >= 0) *reinterpret_cast<f32x4*>(smem + (tid + i * NT) * 16) = rs[i];
+#pragma unroll
+        for (int i = 0; i < WCH; ++i) *reinterpret_cast<f32x4*>(smem + W_OFF + (tid + i * NT) * 16) = rw[i];
+    };
+
+    const float sa = fgc::pow2_scale(P.x_absmax);
+    const float sb = fgc::pow2_scale(P.w_absmax);
+    const float out_scale = 1.f / (sa * sb);
+
+    const int fr = lane & 15, g = lane >> 4;
+    int q0[TM], x0[TM];
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) {
+        const int i = wave * WM + tm * 16 + fr;
+        q0[tm] = i < len0 ? i : i + KW - 1;
+        x0[tm] = i < len0 ? b0 + i : i - len0;
+    }
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    constexpr int CC = C / 32;
+    auto tap = [&](int s) {
+        f16x8 ah[CC][TM], al[CC][TM];
+#pragma unroll
+        for (int cc = 0; cc < CC; ++cc)
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm) {
+                const char* px = smem + (q0[tm] + s) * PB;
+                const int sw = swz_strip<C>(x0[tm] + s);
+                ah[cc][tm] = *reinterpret_cast<const f16x8*>(px + ((cc * 4 + g) ^ sw) * 16);
+                al[cc][tm] = *reinterpret_cast<const f16x8*>(px + ((C / 8 + cc * 4 + g) ^ sw) * 16);
+            }
+        const char* wb = smem + W_OFF + s * W_TAP;
+#pragma unroll
+        for (int cc = 0; cc < CC; ++cc) {
+            f16x8 bh[TN], bl[TN];
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) {
+                const int n = tn * 16 + fr;
+                const char* row = wb + n * (2 * C) + ((cc * 4 + g) ^ swz_wrow<C>(n)) * 16;
+                bh[tn] = *reinterpret_cast<const f16x8*>(row);
+                bl[tn] = *reinterpret_cast<const f16x8*>(row + NR * 2 * C);
+            }
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                for (int tn = 0; tn < TN; ++tn) {
+                    acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[cc][tm], bh[tn], acc[tm][tn], 0, 0, 0);
+                    acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[cc][tm], bl[tn], acc[tm][tn], 0, 0, 0);
+                    acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[cc][tm], bh[tn], acc[tm][tn], 0, 0, 0);
+                }
+        }
+    };
+
+    const int KH = P.kh;
+    load(0);
+    store();
+    __syncthreads();
+    for (int r = 0; r < KH; ++r) {
+        if (r + 1 < KH) load(r + 1);
+#pragma unroll
+        for (int s = 0; s < KW; ++s) tap(s);
+        if (r + 1 < KH) {
+            __syncthreads();
+            store();
+            __syncthreads();
+        }
+    }
+
+    // ---- epilogue
+    const int act = P.act;
+    const bool accum = P.accumulate != 0;
+    float bias_v[TN];
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) bias_v[tn] = P.bias ? P.bias[min(tn * 16 + fr, P.n_out - 1)] : 0.f;
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) {
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {
+            const int i = wave * WM + tm * 16 + 4 * g + reg;
+            if (i >= len0 + len1) continue;
+            const int a = i < len0 ? a0 : a0 + 1, b = i < len0 ? b0 + i : i - len0;
+            float* yrow = P.y + img * P.syn + a * P.sya + b * P.syb;
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) {
+                const int n = tn * 16 + fr;
+                if (n >= P.n_out) continue;
+                float v = fg::act_fwd(acc[tm][tn][reg] * out_scale + bias_v[tn], act);
+                float* dst = yrow + n * P.syc;
+                if (accum) v += *dst;
+                *dst = v;
+            }
+        }
+    }
+}
+
 // waves per workgroup: 4 (one per SIMD, 64 rows each) or 8 (two per SIMD, 32 rows each: a partner wave's
 // MFMAs cover each wave's fragment-read latency); FLOODGAN_WIN_WAVES selects (A/B)
 template <int C, int KW, int TN>
 int launch_win(const WinArgs& a, int tiles, hipStream_t stream) {
+    const char* rs = getenv("FLOODGAN_WIN_RS");
+    if (rs && atoi(rs)) {
+        hipLaunchKernelGGL((conv_win_rs_kernel<C, KW, TN, 8>), dim3(tiles), dim3(512), 0, stream, a);
+        return fg::launched("conv_win_rs");
+    }
     const char* e = getenv("FLOODGAN_WIN_WAVES");
     const int nw = e ? atoi(e) : g_win_waves;
     const char* ea = getenv("FLOODGAN_WIN_APF");

@@ -6,6 +6,7 @@
 
 namespace {
 thread_local char g_err[1024] = "";
+thread_local const char* g_last = "";
 }
 
 namespace fg {
@@ -19,6 +20,7 @@ int fail(int code, const char* fmt, ...) {
 }
 
 int launched(const char* what) {
+    g_last = what;
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail((int)e, "%s: launch failed: %s", what, hipGetErrorString(e));
     return 0;
@@ -41,6 +43,8 @@ int num_cus() {
 }  // namespace fg
 
 FG_API const char* fg_last_error(void) { return g_err; }
+
+FG_API const char* fg_last_launch(void) { return g_last; }
 
 FG_API int fg_version(void) { return 1; }
 

@@ -89,6 +89,7 @@ class fg_tile_batch(C.Structure):
 # (name, argtypes) of every exported symbol; tests check the library exports all of them
 SIGNATURES = {
     "fg_last_error": [],
+    "fg_last_launch": [],
     "fg_version": [],
     "fg_device_ok": [],
     "fg_conv_fwd": [C.POINTER(fg_conv_problem), C.c_int, C.c_void_p],
@@ -181,7 +182,7 @@ SIGNATURES = {
     "fg_tiff_read": [C.c_char_p, C.c_void_p, C.c_longlong],
     "fg_tile_transform": [C.POINTER(fg_tile_batch), C.c_void_p],
 }
-RESTYPES = {"fg_last_error": C.c_char_p, "fg_in_workspace_doubles": C.c_longlong, "fg_bn_workspace_doubles": C.c_longlong,
+RESTYPES = {"fg_last_error": C.c_char_p, "fg_last_launch": C.c_char_p, "fg_in_workspace_doubles": C.c_longlong, "fg_bn_workspace_doubles": C.c_longlong,
             "fg_ssim_workspace_doubles": C.c_longlong, "fg_sq_err_workspace_doubles": C.c_longlong,
             "fg_channel_sum_workspace_doubles": C.c_longlong,
             "fg_in_partials_workspace_doubles": C.c_longlong, "fg_conv1x1_wgrad_workspace_floats": C.c_longlong}
@@ -285,3 +286,8 @@ def require_device(t, what="tensor"):
     if not (t.is_cuda and t.dtype == torch.float32):
         raise RuntimeError(f"floodgan: {what} must be a float32 tensor on a HIP device "
                            f"(got {t.dtype} on {t.device}); there is no CPU path")
+
+
+def last_launch():
+    """the kernel family the most recent fg_* call on this thread launched (fg_last_launch)"""
+    return load().fg_last_launch().decode()

@@ -53,7 +53,8 @@ def paired_attention_generator_backward(x: torch.Tensor, params: List[torch.Tens
     P = dict(zip(GEN_KEYS, params))
     _, _, S = X.gen_forward(P, x, save=True)
     gx = torch.empty(x.shape, dtype=torch.float32, device=x.device)
-    grads = X.gen_backward(P, S, g_out.contiguous(), input_grad=gx, g_mask=g_mask)
+    # an empty g_mask: no loss term reads the mask (the caller passes none)
+    grads = X.gen_backward(P, S, g_out.contiguous(), input_grad=gx, g_mask=g_mask if g_mask.numel() else None)
     return gx, [grads[k] for k in GEN_KEYS]
 
 
@@ -64,7 +65,12 @@ def _(x, params, g_out, g_mask):
 
 def _gen_backward(ctx, g_out, g_mask):
     x, *params = ctx.saved_tensors
-    # autograd materialises the gradient of an unused output as zeros: the mask's term is then a no-op add
+    # autograd materialises the gradient of an unused output as zeros (the mask's term is then a no-op add); with
+    # materialize_grads off it arrives as None, passed on as an empty tensor (the operator's schema takes a Tensor)
+    if g_mask is None:
+        g_mask = g_out.new_empty(0)
+    if g_out is None:
+        g_out = torch.zeros((x.shape[0], 3) + tuple(x.shape[2:]), dtype=x.dtype, device=x.device)
     return torch.ops.floodgan.paired_attention_generator_backward(x, params, g_out, g_mask)
 
 

@@ -105,8 +105,8 @@ class _Grads:
         for b in bufs:
             b.t.record_stream(self.side)
 
-    def wgrad(self, prob, wmap, name, bufs):
-        self.off_path(lambda: ops.wgrad(prob, wmap, self.get(name), accumulate=self.acc), bufs, (name,),
+    def wgrad(self, prob, wmap, name, bufs, tag=None):
+        self.off_path(lambda: ops.wgrad(prob, wmap, self.get(name), accumulate=self.acc, tag=tag), bufs, (name,),
                       prepare=lambda: ops.prepare_wgrad(prob))
 
     def ready(self, ready, name):
@@ -148,6 +148,8 @@ def _norm(c, act, pad, mode, residual=None, stats=None, presplit=False, ps_copy=
     out = Buf.empty(c.n, c.h, c.w, c.c, pad, c.t.device)
     ps = (Buf.empty(c.n, c.h, c.w, c.c, pad, c.t.device)
           if ps_copy and ops.presplit_on() and ops.PRESPLIT_RESID else None)
+    if ps is not None and not ops.presplit_fits(ps):
+        ps = None                  # beyond what the pre-split consumers take (ops.PRESPLIT_MAX_BYTES)
     ops.in_apply(c, mean, rstd, act, residual, out, mode, presplit=presplit, ps_copy=ps)
     return (mean, rstd, out, ps) if ps_copy else (mean, rstd, out)
 
@@ -270,12 +272,13 @@ def _block_bwd(P, pre, b, grad, G):
     ps = ops.presplit_on()
     ops.in_bwd(gsrc, fold, gadd, cb2, b["mb2"], b["rb2"], FG_ACT_NONE, g_cb2, G.get(pre + "conv2.bias"), G.acc,
                gsum=g_h if lazy else None, presplit=ps)
-    _wgrad_conv(P, G, pre + "conv2", g_cb2, b["rb"], 1, 3, 1)
+    _wgrad_conv(P, G, pre + "conv2", g_cb2, b["rb"], 1, 3, 1, tag="resblock_conv_wgrad")
     g_rbp = _dgrad_s1_padded(P, pre + "conv2", g_cb2)  # gradient w.r.t. the reflect-padded relu output
     g_cb1 = Buf.empty(N, Hh, Ww, Cc, 2, dev)
     ops.in_bwd(g_rbp, 1, None, b["cb1"], b["mb1"], b["rb1"], FG_ACT_RELU, g_cb1, G.get(pre + "conv1.bias"), G.acc,
                presplit=ps)
-    _wgrad_conv(P, G, pre + "conv1", g_cb1, b["h"] if b.get("h_ps") is None else b["h_ps"], 1, 3, 1)
+    _wgrad_conv(P, G, pre + "conv1", g_cb1, b["h"] if b.get("h_ps") is None else b["h_ps"], 1, 3, 1,
+                tag="resblock_conv_wgrad")
     g_hp = _dgrad_s1_padded(P, pre + "conv1", g_cb1)
     return g_hp, 1, g_h                               # reflect-pad adjoint + residual path, summed lazily
 
@@ -294,7 +297,7 @@ def _dgrad_s1_padded(P, name, gy):
     m = PL.wmap_conv_dgrad_s1(w.shape, gy.c)
     wp = ops.pack_weight(w, m)
     out = Buf.empty(N, Hh, Ww, Cc, 1, gy.t.device)     # interior = padded rows / cols 1..H
-    ops.conv([PL.conv_problem(gy, 1, 3, 1, wp, m, out)])
+    ops.conv([PL.conv_problem(gy, 1, 3, 1, wp, m, out)], tag="resblock_conv_dgrad")
     # padded-domain position p reads gy rows / cols p-2 .. p (relative to gy's interior; rows -2, -1 and
     # H, H+1 are zero); out's interior origin is padded position 1.  Row strips: one row of the full
     # pack (gather row r at pack row r); column strips: packs of their single kernel column.
@@ -337,10 +340,10 @@ def block_backward_nchw(S, g, need_input=True):
     return (_to_nchw(g_new) if need_input else None), grads
 
 
-def _wgrad_conv(P, G, name, gy, X, pad, k, stride):
+def _wgrad_conv(P, G, name, gy, X, pad, k, stride, tag=None):
     w = P[name + ".weight"]
     G.wgrad(PL.wgrad_conv(gy, X, pad, k, stride, w.shape[0]), PL.wmap_wgrad(w.shape, True, X.c, k), name + ".weight",
-            (gy, X))
+            (gy, X), tag=tag)
 
 
 def _dgrad_s1(P, name, gyp, pad_used, k, Y):

@@ -8,7 +8,7 @@ import os
 import torch
 
 from . import _lib as L
-from .plans import Buf, Slice, f3_wgrad_eligible, packed_numel, slab_numel, wgrad_splits
+from .plans import Buf, Slice, f3_wgrad_eligible, packed_numel, slab_numel, stem_wgrad_layout, wgrad_splits
 
 EPS = 1e-5
 
@@ -116,6 +116,17 @@ PRESPLIT_RESID = os.environ.get("FLOODGAN_PRESPLIT_RESID", "1") != "0"
 
 def presplit_on():
     return PRESPLIT and L.fwd_f16x3() and L.wgrad_f16x3() and L.wgrad_f3_on()
+
+
+# Only the pipelined kernels read FG_PRESPLIT operands, and they address their outputs with 31-bit byte offsets
+# (conv_f3.hip f3_takes): a consumer of a larger operand would produce an output the kernel declines.  Producers
+# therefore write a buffer beyond this size in fp32 (every kernel reads that) -- at bs 8, 512^2 the largest
+# pre-split buffer (64 channels at 512^2) is 0.55 GB.
+PRESPLIT_MAX_BYTES = (1 << 31) - (1 << 24)
+
+
+def presplit_fits(buf):
+    return buf is not None and 4 * _tensor(buf).numel() <= PRESPLIT_MAX_BYTES
 
 
 def is_presplit(obj):
@@ -326,6 +337,19 @@ class KernelTimer:
 _TIMER = None
 
 
+def _timed(tag, fn):
+    """run fn (one launch on the current stream), bracketed by HIP events when the active KernelTimer
+    collects `tag`"""
+    if _TIMER is None or tag not in _TIMER.tags:
+        return fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    out = fn()
+    e.record()
+    _TIMER.events[tag].append((s, e))
+    return out
+
+
 USE_WIN = True   # route eligible single convs to the row-strip kernel (fg_conv_win)
 
 
@@ -341,18 +365,11 @@ def conv(probs, tag=None, in_stats=False):
     statistics partials and conv returns (mean, rstd) per (image, channel), else None."""
     if USE_WIN and len(probs) == 1 and win_eligible(probs[0]):
         return conv_win(probs[0], tag)
-    if _TIMER is not None and tag in _TIMER.tags:
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
-        stats = _conv(probs, in_stats)
-        e.record()
-        _TIMER.events[tag].append((s, e))
-    else:
-        stats = _conv(probs, in_stats)
+    stats = _conv(probs, in_stats, tag)
     return None if stats is None else _merge_stats(len(probs), *stats)
 
 
-def _conv(probs, in_stats=False):
+def _conv(probs, in_stats=False, tag=None):
     arr = (L.fg_conv_problem * len(probs))()
     f16 = L.fwd_f16x3()
     keep = {}
@@ -384,7 +401,7 @@ def _conv(probs, in_stats=False):
             if CHECK_SCALES and wt.dtype == torch.float32:
                 check_scale(wt, wa, "fp32 weight")
     stats = _stats_partials(probs, arr) if (in_stats and FUSED_IN_STATS) else None
-    L.check(_lib().fg_conv_fwd(arr, len(probs), L.stream_handle()), "conv_fwd")
+    _timed(tag, lambda: L.check(_lib().fg_conv_fwd(arr, len(probs), L.stream_handle()), "conv_fwd"))
     _wrote(*[p["y"][0] for p in probs])
     return stats
 
@@ -479,16 +496,7 @@ def conv_win(prob, tag=None):
     s.x_absmax = xs.absmax.data_ptr()
     s.w_absmax = prob["w"][0].absmax.data_ptr()
 
-    def run():
-        L.check(_lib().fg_conv_win(arr, L.ptr(xs), off // X.c, L.stream_handle()), "conv_win")
-    if _TIMER is not None and tag in _TIMER.tags:
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        ev0.record()
-        run()
-        ev1.record()
-        _TIMER.events[tag].append((ev0, ev1))
-    else:
-        run()
+    _timed(tag, lambda: L.check(_lib().fg_conv_win(arr, L.ptr(xs), off // X.c, L.stream_handle()), "conv_win"))
     _wrote(prob["y"][0])
 
 
@@ -528,6 +536,8 @@ def _wgrad_win(prob, wmap, dw, accumulate):
             "wgrad_reduce")
 
 
+LAST_WGRAD_KERNEL = None   # the kernel family the last wgrad() launch ran (fg_last_launch; tests)
+
 _WG_FIELDS = ("spn", "spa", "spb", "sxn", "sxa", "sxb", "sxr", "m_img", "m_a", "m_b", "n_a", "kh", "j_valid",
               "splits", "m_chunk")
 
@@ -545,12 +555,17 @@ def prepare_wgrad(prob):
         absmax(prob["x"][0])
 
 
-def wgrad(prob, wmap, dw, accumulate=False):
-    """weight gradient into the PyTorch-layout tensor dw (overwritten, or += if accumulate)"""
+def wgrad(prob, wmap, dw, accumulate=False, tag=None):
+    """weight gradient into the PyTorch-layout tensor dw (overwritten, or += if accumulate); `tag` times the
+    weight-gradient launch itself (not the split reduction) under a KernelTimer"""
     dev = _dev(prob["p"][0])
     if USE_WIN and L.wgrad_f16x3() and wgrad_win_eligible(prob):
         return _wgrad_win(prob, wmap, dw, accumulate)
-    if L.wgrad_f16x3() and L.wgrad_f3_on() and f3_wgrad_eligible(prob):
+    stem = stem_wgrad_layout(prob) if L.wgrad_f16x3() else None
+    if stem is not None and not (is_presplit(prob["p"][0]) or is_presplit(prob["x"][0])):
+        # the stem's strip kernel (conv_stem.hip) defines its own splits: 64-px strips of m_chunk / 64 rows
+        prob = dict(prob, splits=stem[0], m_chunk=stem[1])
+    elif L.wgrad_f16x3() and L.wgrad_f3_on() and f3_wgrad_eligible(prob):
         # re-split the pixel range for the pipelined kernel's tiles (one workgroup per CU)
         splits, chunk = wgrad_splits(prob["n_a"], prob["kh"] * prob["j_valid"],
                                      prob["m_img"] * prob["m_a"] * prob["m_b"], f3=True)
@@ -568,7 +583,9 @@ def wgrad(prob, wmap, dw, accumulate=False):
             check_scale(prob["x"][0], xa, "wgrad input")
     s.p_presplit, s.x_presplit = int(is_presplit(prob["p"][0])), int(is_presplit(prob["x"][0]))
     st = L.stream_handle()
-    L.check(_lib().fg_conv_wgrad(C.byref(s), st), "conv_wgrad")
+    _timed(tag, lambda: L.check(_lib().fg_conv_wgrad(C.byref(s), st), "conv_wgrad"))
+    global LAST_WGRAD_KERNEL
+    LAST_WGRAD_KERNEL = L.last_launch()
     m = wmap_struct(wmap)
     L.check(_lib().fg_wgrad_reduce(L.ptr(slab), int(prob["splits"]), C.byref(m), L.ptr(dw), int(accumulate), st),
             "wgrad_reduce")
@@ -683,7 +700,9 @@ def in_stats(src):
 def in_apply(src, mean, rstd, act, residual, dst, pad_mode, presplit=False, ps_copy=None):
     """presplit: dst is written in the FG_PRESPLIT format (no residual; the f16x3 math).  ps_copy (Buf of dst's
     geometry): dst in fp32 AND a FG_PRESPLIT copy there (fg_in_apply_dual)"""
+    presplit = presplit and presplit_fits(dst)
     if ps_copy is not None:
+        assert presplit_fits(ps_copy), "pre-split copy beyond PRESPLIT_MAX_BYTES (the caller checks presplit_fits)"
         assert not presplit and L.fwd_f16x3()
         ra = absmax(residual) if residual is not None else None
         slot, ps_slot = _amax_out(dst), _amax_out(ps_copy)
@@ -710,7 +729,7 @@ def in_bwd(gsrc, fold_pad, gadd, src, mean, rstd, act, dst, bias_grad=None, bias
     presplit: dst is written in the FG_PRESPLIT format (the f16x3 math)."""
     work = _work(src.n, src.c, src.t.device)
     _wrote(gsum)
-    if presplit:
+    if presplit and presplit_fits(dst):
         assert L.fwd_f16x3()
         slot = _amax_out(dst)
         L.check(_lib().fg_in_bwd_presplit(view(gsrc), fold_pad, view(gadd), view(src), L.ptr(mean), L.ptr(rstd), act,

@@ -301,6 +301,26 @@ def wgrad_splits(n_a, K, M, f3=False):
     return splits, chunk
 
 
+STEM_PX = 64        # conv_stem.hip: output pixels per strip
+STEM_SPLITS = 256   # about one workgroup per CU
+
+
+def stem_wgrad_layout(prob):
+    """(splits, m_chunk) for the stem weight-gradient kernel (conv_stem.hip: the 7x7 conv over the 9-channel input
+    with 64 outputs) -- one workgroup per 64-px column strip of `rows` output rows, m_chunk = 64 * rows -- or None
+    when the kernel does not take the problem (fgc::stem_wgrad_rows, the same conditions)"""
+    if not (prob["n_a"] == 64 and prob["kh"] == 7 and prob["j_valid"] == 63 and prob["sxb"] == 9
+            and prob["sxr"] == prob["sxa"] and prob["m_b"] % STEM_PX == 0 and prob["spb"] >= 64
+            and (prob["spn"] | prob["spa"] | prob["spb"]) % 4 == 0):
+        return None
+    strips = prob["m_img"] * (prob["m_b"] // STEM_PX)
+    m_a = prob["m_a"]
+    # the most rows per split that still gives about STEM_SPLITS workgroups (a divisor of m_a)
+    want = max(1, -(-strips * m_a // STEM_SPLITS))
+    rows = next((r for r in range(want, m_a + 1) if m_a % r == 0), m_a)
+    return strips * (m_a // rows), STEM_PX * rows
+
+
 def f3_wgrad_eligible(prob):
     """the shapes the pipelined f16x3 weight-gradient kernel takes (conv_wgrad_f3.hip)"""
     return prob["n_a"] >= 64 and prob["kh"] * prob["j_valid"] >= 256 and prob["n_a"] % 4 == 0 \

@@ -152,6 +152,9 @@ typedef struct fg_weight_map {
 /* library                                                                                   */
 /* ---------------------------------------------------------------------------------------- */
 const char* fg_last_error(void);
+/* Name of the kernel family this thread's most recent fg_* call launched (e.g. "stem_wgrad", "conv_wgrad_f3"):
+ * lets tests assert which kernel a dispatch chose. */
+const char* fg_last_launch(void);
 int fg_version(void);
 int fg_device_ok(void);   /* 0 if a gfx950 device is current, else an error code */
 

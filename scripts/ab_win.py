@@ -1,7 +1,7 @@
-"""A/B (GPU) of the row-strip window kernel's workgroup shape (FLOODGAN_WIN_WAVES 4 or 8 waves) and strip-fragment
-prefetch (FLOODGAN_WIN_APF 0/1) on the content
-head's forward (7x7 64 -> 27 at 512^2) and input gradient (7x7 27(32) -> 64 over 518^2), bs 8; outputs compared.
-  python scripts/diag_win_waves.py"""
+"""A/B (GPU) of the row-strip window kernel forms on the content head's forward (7x7 64 -> 27 at 512^2) and input
+gradient (7x7 27(32) -> 64 over 518^2), bs 8, interleaved; outputs compared: FLOODGAN_WIN_RS=1 (register-staged,
+one barrier pair per kernel row) against the LDS-DMA form (one barrier per tap).
+  python scripts/ab_win.py"""
 import os
 import sys
 
@@ -36,19 +36,17 @@ def main():
     for name, prob, out, flops in (("content fwd 7x7 64->27 @512", fwd, cl, 2.0 * N * 512 * 512 * 27 * 64 * 49),
                                    ("content dgrad 7x7 27->64 @518", dgr, Y, 2.0 * N * 518 * 518 * 64 * 27 * 49)):
         res = {}
-        for nw, apf in (("8", "0"), ("8", "1"), ("4", "1"), ("8", "0"), ("8", "1"), ("4", "1")):
-            os.environ["FLOODGAN_WIN_WAVES"] = nw
-            os.environ["FLOODGAN_WIN_APF"] = apf
+        for rs in ("0", "1", "0", "1"):
+            os.environ["FLOODGAN_WIN_RS"] = rs
             out.t.zero_()
             ops.conv_win(prob)
             torch.cuda.synchronize()
-            res[nw + apf] = out.t.clone()
+            res[rs] = out.t.clone()
             ms = min(time_it(lambda: ops.conv_win(prob)) for _ in range(3))
-            d = float((res[nw + apf] - res["80"]).norm() / res["80"].norm())
-            print(f"{name:32s} waves {nw} apf {apf} {ms * 1e3:8.1f} us {flops / ms / 1e9:7.1f} TFLOP/s  "
-                  f"rel diff vs 8/0 {d:.1e}", flush=True)
-    os.environ.pop("FLOODGAN_WIN_WAVES")
-    os.environ.pop("FLOODGAN_WIN_APF")
+            d = float((res[rs] - res["0"]).norm() / res["0"].norm())
+            print(f"{name:32s} rs {rs} {ms * 1e3:8.1f} us {flops / ms / 1e9:7.1f} TFLOP/s  rel diff vs dma {d:.1e}",
+                  flush=True)
+    os.environ.pop("FLOODGAN_WIN_RS")
 
 
 if __name__ == "__main__":

@@ -1,7 +1,10 @@
 """Run one conv-engine launch shape repeatedly (for rocprofv3 counter passes).
-  python scripts/conv_one.py [fwd|fwd_stats|fwd_stats_ps|wgrad] [reps]  -- resblock 3x3 256->256 @128, bs 8
+  python scripts/conv_one.py [fwd|fwd_stats|fwd_stats_ps|wgrad|dgrad_ps|wgrad_ps] [reps]
+  -- resblock 3x3 256->256 @128, bs 8
   (fwd_stats: with the InstanceNorm statistics epilogue, as the step's conv1 runs; fwd_stats_ps: on a FG_PRESPLIT
-  operand written by the norm pass, as the step's conv2 runs)"""
+  operand written by the norm pass, as the step's conv2 runs; dgrad_ps: the input-gradient interior launch of
+  executor._dgrad_s1_padded over a pre-split conv-output gradient with its zero border 2; wgrad_ps: the step's
+  weight gradient with both operands pre-split, gradient border 2, input reflect border 1)"""
 import os
 import sys
 
@@ -31,7 +34,27 @@ def main():
         c.t.normal_()
         mean, rstd = ops.in_stats(c)
         ops.in_apply(c, mean, rstd, 1, None, X, 1, presplit=True)      # relu(IN(c)) with the reflect border
-    if kind in ("fwd", "fwd_stats", "fwd_stats_ps"):
+    if kind in ("dgrad_ps", "wgrad_ps"):
+        c = Buf.empty(N, H, H, C, 0, dev)
+        c.t.normal_()
+        mean, rstd = ops.in_stats(c)
+        G = Buf.empty(N, H, H, C, 2, dev)
+        ops.in_apply(c, mean, rstd, 0, None, G, 0, presplit=True)      # a pre-split gradient, zero border 2
+        if kind == "dgrad_ps":
+            md = PL.wmap_conv_dgrad_s1(w.shape, C)
+            out = Buf.empty(N, H, H, C, 1, dev)
+            prob = PL.conv_problem(G, 1, k, 1, ops.pack_weight(w, md), md, out)
+            fn = lambda: ops.conv([prob])  # noqa: E731
+        else:
+            c2 = Buf.empty(N, H, H, C, 0, dev)
+            c2.t.normal_()
+            m2, r2 = ops.in_stats(c2)
+            ops.in_apply(c2, m2, r2, 1, None, X, 1, presplit=True)     # relu(IN(.)) with the reflect border
+            wprob = PL.wgrad_conv(G, X, 1, k, 1, C)
+            dw = torch.empty_like(w)
+            wm = PL.wmap_wgrad(w.shape, True, X.c, k)
+            fn = lambda: ops.wgrad(wprob, wm, dw)  # noqa: E731
+    elif kind in ("fwd", "fwd_stats", "fwd_stats_ps"):
         prob = PL.conv_problem(X, 1, k, 1, ops.pack_weight(w, m), m, Y, bias=torch.zeros(C, device=dev))
         fn = lambda: ops.conv([prob], in_stats=kind != "fwd")  # noqa: E731
     else:

@@ -19,6 +19,8 @@ if [ -n "$DP2" ]; then
 fi
 scripts/gpu_profile.sh $TAG > /dev/null 2>&1 || { echo "profile failed"; exit 1; }
 if [ -n "$PMC" ]; then
-  scripts/gpu_pmc.sh ${TAG}_fwd > /dev/null && KIND=wgrad scripts/gpu_pmc.sh ${TAG}_wgrad > /dev/null || { echo "pmc failed"; exit 1; }
+  for k in fwd_stats_ps dgrad_ps wgrad_ps; do
+    KIND=$k scripts/gpu_pmc.sh ${TAG}_$k > /dev/null || { echo "pmc $k failed"; exit 1; }
+  done
 fi
 echo "round done"

@@ -66,3 +66,21 @@ def test_compile_traces_through_custom_ops():
 
     got = torch.compile(f, backend="aot_eager", fullgraph=True)(x, gp)
     assert torch.allclose(got, f(x, gp))
+
+
+def test_backward_without_materialized_mask_grad():
+    """the generator operator's backward formula with dL/dmask = None (autograd with materialize_grads off)
+    equals the one with a zero mask gradient (an empty tensor is passed to the Tensor-typed schema)"""
+    from types import SimpleNamespace
+
+    from floodgan import custom_ops
+    from floodgan.model_architectures import GEN_KEYS
+    m = _model()
+    gp = [m.generator.param_dict()[k] for k in GEN_KEYS]
+    g = torch.Generator().manual_seed(5)
+    x = (torch.rand((1, 9, 32, 32), generator=g) * 2 - 1).to(DEV)
+    g_out = torch.rand((1, 3, 32, 32), generator=g).to(DEV)
+    ctx = SimpleNamespace(saved_tensors=(x, *gp))
+    gx0, gp0 = custom_ops._gen_backward(ctx, g_out, None)
+    gx1, gp1 = custom_ops._gen_backward(ctx, g_out, torch.zeros((1, 32, 32), device=DEV))
+    assert torch.equal(gx0, gx1) and all(torch.equal(a, b) for a, b in zip(gp0, gp1))

@@ -283,13 +283,46 @@ def test_wgrad_window(splits, H, W):
         L.set_conv_math(prev)
 
 
+@pytest.mark.parametrize("H,N,splits", [(64, 2, None), (128, 2, None), (128, 1, 4), (192, 1, 3)])
+def test_stem_wgrad_strips(H, N, splits):
+    """the stem's weight-gradient kernel (conv_stem.hip: 7x7 over the reflect-padded 9-channel input, 64
+    outputs; 64-px strips of `rows` output rows per workgroup walking an 8-row LDS ring) against fp64 at
+    1 .. 192 rows per split, 1 .. 3 strips per image (models/model_architectures.py:312, :342-343)"""
+    from floodgan import _lib as L, ops, plans as PL
+    prev, prev_s = L.get_conv_math(), PL.STEM_SPLITS
+    L.set_conv_math("f16x3")
+    try:
+        if splits is not None:
+            PL.STEM_SPLITS = splits
+        torch.manual_seed(11)
+        x = torch.randn(N, 9, H, H, dtype=torch.float64)
+        gy = torch.randn(N, 64, H, H, dtype=torch.float64) * 1e-3
+        w = torch.zeros(64, 9, 7, 7, dtype=torch.float64)
+        gw_ref = torch.nn.grad.conv2d_weight(F.pad(x, (3,) * 4, mode="reflect"), w.shape, gy)
+        X = buf_from(x, 3, "reflect")
+        GY = buf_from(gy, 0, "constant")
+        prob = PL.wgrad_conv(GY, X, 3, 7, 1, 64)
+        layout = PL.stem_wgrad_layout(prob)
+        assert layout is not None and (splits is None or layout[0] == splits)
+        dw = torch.empty(w.shape, dtype=torch.float32, device=DEV)
+        ops.wgrad(prob, PL.wmap_wgrad(w.shape, True, X.c, 7), dw)
+        assert ops.LAST_WGRAD_KERNEL == "stem_wgrad", ops.LAST_WGRAD_KERNEL
+        torch.cuda.synchronize()
+        assert nrel(dw, gw_ref) < KTOL
+    finally:
+        PL.STEM_SPLITS = prev_s
+        L.set_conv_math(prev)
+
+
+@pytest.mark.parametrize("rs", ["0", "1"])
 @pytest.mark.parametrize("case", ["content_fwd", "content_dgrad"])
-def test_conv_window(case):
+def test_conv_window(case, rs, monkeypatch):
     """the row-strip window kernel (fg_conv_win) on the content-head geometries -- 7x7 over 64
     channels -> 27, and its input gradient 27(32) -> 64 over the 6-bordered gradient -- with
     output rows of 256+ px (two-segment tiles, ragged last tile) against fp64"""
     from floodgan import _lib as L, ops, plans as PL
     from floodgan.plans import Buf
+    monkeypatch.setenv("FLOODGAN_WIN_RS", rs)     # 1: the register-staged form (one barrier pair per kernel row)
     prev = L.get_conv_math()
     L.set_conv_math("f16x3")
     try:
