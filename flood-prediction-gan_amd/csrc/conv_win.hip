@@ -451,6 +451,10 @@ __global__ void __launch_bounds__(NW * 64, 1) conv_win_rs_kernel(const WinArgs a
 template <int C, int KW, int TN>
 int launch_win(const WinArgs& a, int tiles, hipStream_t stream) {
     const char* rs = getenv("FLOODGAN_WIN_RS");
+    if (rs && atoi(rs) == 4) {
+        hipLaunchKernelGGL((conv_win_rs_kernel<C, KW, TN, 4>), dim3(tiles), dim3(256), 0, stream, a);
+        return fg::launched("conv_win_rs");
+    }
     if (rs && atoi(rs)) {
         hipLaunchKernelGGL((conv_win_rs_kernel<C, KW, TN, 8>), dim3(tiles), dim3(512), 0, stream, a);
         return fg::launched("conv_win_rs");

@@ -882,67 +882,6 @@ __global__ void in_partials_finalize(const double* __restrict__ work, int nprob,
     }
 }
 
-// One launch for the whole merge: block (image, 64-channel group) of 64 channels x 16 slices walks every 32-row
-// block of the image (coalesced 512-B rows of f32x2, fp64 sums), a fixed-order tree over the slices, then mean and
-// rstd.  Replaces in_partials_reduce + in_partials_finalize (two launches of ~7 + 5 us, latency-bound, 28 per
-// step at bs 8); the workspace is no longer used.
-constexpr int kMergeSlices = 16;
-
-__global__ void __launch_bounds__(64 * kMergeSlices) in_partials_merge(const float* __restrict__ part, int nprob,
-                                                                       int n_img, int rb_per_img, int c, float eps,
-                                                                       float* __restrict__ mean,
-                                                                       float* __restrict__ rstd) {
-    const int img = blockIdx.x, cl = threadIdx.x % 64, sl = threadIdx.x / 64;
-    const int ch = blockIdx.y * 64 + cl;
-    const size_t prob_stride = (size_t)n_img * rb_per_img * c * 2;
-    const int K = nprob * rb_per_img;
-    double s1 = 0, s2 = 0;
-    if (ch < c) {
-        int k = sl;
-        for (; k + 3 * kMergeSlices < K; k += 4 * kMergeSlices) {      // four blocks' loads in flight
-            f32x2 q[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int kk = k + u * kMergeSlices, pr = kk / rb_per_img, rb = img * rb_per_img + (kk - pr * rb_per_img);
-                q[u] = *reinterpret_cast<const f32x2*>(part + pr * prob_stride + ((size_t)rb * c + ch) * 2);
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const double m = q[u][0];
-                s1 += 32.0 * m;
-                s2 += (double)q[u][1] + 32.0 * m * m;
-            }
-        }
-        for (; k < K; k += kMergeSlices) {
-            const int pr = k / rb_per_img, rb = img * rb_per_img + (k - pr * rb_per_img);
-            const f32x2 q = *reinterpret_cast<const f32x2*>(part + pr * prob_stride + ((size_t)rb * c + ch) * 2);
-            const double m = q[0];
-            s1 += 32.0 * m;
-            s2 += (double)q[1] + 32.0 * m * m;
-        }
-    }
-    __shared__ double red[kMergeSlices][64][2];
-    red[sl][cl][0] = s1;
-    red[sl][cl][1] = s2;
-#pragma unroll
-    for (int st = kMergeSlices / 2; st > 0; st >>= 1) {
-        __syncthreads();
-        if (sl < st) {
-            red[sl][cl][0] += red[sl + st][cl][0];
-            red[sl][cl][1] += red[sl + st][cl][1];
-        }
-    }
-    __syncthreads();
-    if (sl == 0 && ch < c) {
-        const double n = 32.0 * K;
-        const double mu = red[0][cl][0] / n;
-        double var = red[0][cl][1] / n - mu * mu;
-        if (var < 0) var = 0;
-        mean[img * c + ch] = (float)mu;
-        rstd[img * c + ch] = (float)(1.0 / sqrt(var + (double)eps));
-    }
-}
-
 }  // namespace
 
 FG_API long long fg_in_partials_workspace_doubles(int n_img, int c) {
@@ -954,12 +893,6 @@ FG_API int fg_in_stats_partials(const float* partials, int nprob, int n_img, int
     if (!partials || !mean || !rstd || !work || nprob < 1 || nprob > 4 || n_img < 1 || rb_per_img < 1 || c < 1)
         return fg::fail(FG_ERR_INVALID, "fg_in_stats_partials: bad args");
     const int cg = (c + 63) / 64, K = nprob * rb_per_img;
-    const char* e1 = getenv("FLOODGAN_IN_MERGE1");     // A/B: 0 = the two-launch reduce + finalize
-    if (!e1 || atoi(e1)) {
-        hipLaunchKernelGGL(in_partials_merge, dim3(n_img, cg), dim3(64 * kMergeSlices), 0, stream, partials, nprob,
-                           n_img, rb_per_img, c, eps, mean, rstd);
-        return fg::launched("in_partials_merge");
-    }
     // ~1024 blocks over the chip, each thread at least ~4 of the image's 32-row blocks
     const int splits = std::max(1, std::min({kPartialSplitsMax, (1024 + n_img * cg - 1) / (n_img * cg), K / 16}));
     hipLaunchKernelGGL(in_partials_reduce, dim3(n_img, cg, splits), dim3(256), 0, stream, partials, nprob, n_img,

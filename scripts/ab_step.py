@@ -1,7 +1,7 @@
 """A/B of engine switches on the full bs-8 512^2 training step, interleaved in ONE process (device
 clocks and boxes differ by several percent, so separate bench runs cannot resolve small gains).
   python scripts/ab_step.py f3_persistent [rounds] [steps] [values, default 0,1]
-Switches: f3_persistent, f3_sched, f3_order, f3_fill, f3_interleave, head_1x1, win_waves (values 4,8), wgrad_f3, use_win, in_rows, presplit, ps_wide (values 4,5), ps_resid, stem_pad4, stem_wgrad, win_rs, in_merge1."""
+Switches: f3_persistent, f3_sched, f3_order, f3_fill, f3_interleave, head_1x1, win_waves (values 4,8), wgrad_f3, use_win, in_rows, presplit, ps_wide (values 4,5), ps_resid, stem_pad4, stem_wgrad, win_rs."""
 import os
 import sys
 import time
@@ -51,8 +51,7 @@ def switch(name, on):
         ops.STEM_WGRAD = bool(on)
     elif name == "win_rs":
         os.environ["FLOODGAN_WIN_RS"] = str(int(on))
-    elif name == "in_merge1":
-        os.environ["FLOODGAN_IN_MERGE1"] = str(int(on))
+
     else:
         raise SystemExit(f"unknown switch {name}")
 

@@ -1,6 +1,7 @@
 """A/B (GPU) of the row-strip window kernel forms on the content head's forward (7x7 64 -> 27 at 512^2) and input
 gradient (7x7 27(32) -> 64 over 518^2), bs 8, interleaved; outputs compared: FLOODGAN_WIN_RS=1 (register-staged,
-one barrier pair per kernel row) against the LDS-DMA form (one barrier per tap).
+one barrier pair per kernel row; 4: its 4-wave form, 64 rows per wave) against the LDS-DMA form (one barrier per
+tap).
   python scripts/ab_win.py"""
 import os
 import sys
@@ -36,7 +37,7 @@ def main():
     for name, prob, out, flops in (("content fwd 7x7 64->27 @512", fwd, cl, 2.0 * N * 512 * 512 * 27 * 64 * 49),
                                    ("content dgrad 7x7 27->64 @518", dgr, Y, 2.0 * N * 518 * 518 * 64 * 27 * 49)):
         res = {}
-        for rs in ("0", "1", "0", "1"):
+        for rs in ("0", "1", "4", "0", "1", "4"):
             os.environ["FLOODGAN_WIN_RS"] = rs
             out.t.zero_()
             ops.conv_win(prob)
