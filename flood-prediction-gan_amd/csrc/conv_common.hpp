@@ -122,5 +122,9 @@ int launch_wgrad_f3(const fg_wgrad_problem& p, hipStream_t stream, int* rc);
 // rows per split), same contract; stem_wgrad_rows = its rows per split, or 0 when it does not apply.
 int stem_wgrad_rows(const fg_wgrad_problem& p);
 int launch_wgrad_stem(const fg_wgrad_problem& p, hipStream_t stream, int* rc);
+// The stem's forward (conv_stem.hip), same contract; stem_fwd_rows = its rows per workgroup, or 0 when it does not
+// apply.  It also honours fg_conv_problem.in_stats.
+int stem_fwd_rows(const fg_conv_problem& p);
+int launch_fwd_stem(const fg_conv_problem& p, hipStream_t stream, int* rc);
 
 }  // namespace fgc

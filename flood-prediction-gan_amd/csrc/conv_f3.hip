@@ -731,9 +731,20 @@ int g_f3_ps_wide = 5;  // fg_set_f3_ps_wide: the N > 128 tile of pre-split opera
                        // 0.371 -> 0.348 ms, profiles/round3/r3v_f3_presplit_cfg.log.  4 waves of 128 x 128 with the
                        // accumulators in AGPRs ran 3.26 ms: not kept)
 
+// Narrow-N wave tiles (A/B, FLOODGAN_F3_NARROW=1): the 32 x 64 / 32 x 128 wave tiles of cfg 7 / 6 read 512 / 427 B of
+// LDS fragments per MFMA -- at the LDS port's 128 B per clock that is at or beyond what the four SIMDs' MFMAs consume
+// -- where 64 x 64 wave tiles read 341 (the resblock's 64 x 128: 256): cfg 10 = 512 x 64 as 8 waves of 64 x 64,
+// cfg 11 = 256 x 128 as 4 x 2 waves of 64 x 64
+static bool narrow_on() { const char* e = getenv("FLOODGAN_F3_NARROW"); return e && atoi(e) != 0; }
+
 int auto_cfg(const fg_conv_problem* p, int nprob, int max_n) {
     int cfg = f3_config(max_n);
     if (g_f3_tile >= 0 || cfg < 0) return cfg;
+    if (narrow_on() && (cfg == 6 || cfg == 7)) {
+        const int alt = cfg == 7 ? 10 : 11;
+        const int bm = alt == 10 ? 512 : 256, bn = alt == 10 ? 64 : 128;
+        if (2 * batch_tiles(p, nprob, bm, bn) > fg::num_cus()) return alt;
+    }
     if (cfg == 4 && p[0].x_presplit && 2 * batch_tiles(p, nprob, 256, 256) > fg::num_cus()) return g_f3_ps_wide;
     if (!g_f3_fill) return cfg;
     const int cus = fg::num_cus();
@@ -801,6 +812,8 @@ int launch_fwd_f3(const ConvBatch& b, int nprob, int max_n, hipStream_t stream, 
         case 7: *rc = launch_cfg<256, 64, 32, 64, 3>(b, nprob, stream); return 1;
         case 8: *rc = launch_cfg<256, 64, 64, 64, 3>(b, nprob, stream); return 1;
         case 9: *rc = launch_cfg<128, 64, 32, 64, 3>(b, nprob, stream); return 1;
+        case 10: *rc = launch_cfg<512, 64, 64, 64, 2>(b, nprob, stream); return 1;
+        case 11: *rc = launch_cfg<256, 128, 64, 64, 3>(b, nprob, stream); return 1;
         default: return 0;
     }
 }
@@ -808,7 +821,7 @@ int launch_fwd_f3(const ConvBatch& b, int nprob, int max_n, hipStream_t stream, 
 }  // namespace fgc
 
 FG_API int fg_set_f3_tile(int cfg) {
-    if (cfg < -2 || cfg > 9) return fg::fail(FG_ERR_INVALID, "fg_set_f3_tile: %d", cfg);
+    if (cfg < -2 || cfg > 11) return fg::fail(FG_ERR_INVALID, "fg_set_f3_tile: %d", cfg);
     g_f3_tile = cfg;
     return 0;
 }

@@ -1277,6 +1277,8 @@ int launch_wgrad(const fg_wgrad_problem& p, bool vx, bool vp, hipStream_t stream
 }
 
 int g_fwd_tile = -1;   // tuning hook (fg_set_fwd_tile): force one bf16x6 forward tile config
+// A/B (FLOODGAN_STEM_FWD=0: the register-staged x6 kernel): the stem forward on its strip kernel
+static bool stem_fwd_on() { const char* e = getenv("FLOODGAN_STEM_FWD"); return !e || atoi(e) != 0; }
 
 // split-math forward tile configs {BM, BN, wave tile, waves/SIMD, prefetch distance, LDS swizzle}
 template <class SM>
@@ -1332,6 +1334,11 @@ FG_API int fg_conv_fwd(const fg_conv_problem* probs, int nprob, hipStream_t stre
     const bool x6 = f16 || (g_conv_math & FG_MATH_FWD_X6) != 0;   // a split-math kernel
     bool stats = false;
     for (int i = 0; i < nprob; ++i) stats |= probs[i].in_stats != nullptr;
+    // the generator stem (7x7 over 9 channels -> 64): its strip kernel, epilogue statistics included (conv_stem.hip)
+    if (f16 && nprob == 1 && ws == 2 && g_fwd_tile < 0 && stem_fwd_on()) {
+        int rc = 0;
+        if (fgc::launch_fwd_stem(probs[0], stream, &rc)) return rc;
+    }
     if (stats && !(f16 && vec && ws == 2 && g_fwd_tile < 0 && fgc::f3_stats_ok(probs, nprob, max_n)))
         return fg::fail(FG_ERR_INVALID, "fg_conv_fwd: in_stats needs the pipelined f16x3 kernel (see fg_conv_stats_ok)");
     if ((ws == 1 && (!x6 || f16)) || (ws == 2 && !f16))
@@ -1410,6 +1417,7 @@ FG_API int fg_conv_fwd(const fg_conv_problem* probs, int nprob, hipStream_t stre
 FG_API int fg_conv_stats_ok(const fg_conv_problem* probs, int nprob) {
     if (!probs || nprob < 1 || nprob > 4) return 0;
     if (!(g_conv_math & FG_MATH_FWD_F16X3) || g_fwd_tile >= 0) return 0;
+    if (nprob == 1 && stem_fwd_on() && fgc::stem_fwd_rows(probs[0]) && probs[0].m_b % 32 == 0) return 1;
     int max_n = 0;
     for (int i = 0; i < nprob; ++i) {
         const fg_conv_problem& p = probs[i];

@@ -15,6 +15,8 @@
 // column) product of a step is split over 8 waves: waves 0-3 own 4 column blocks of 16, waves 4-7 three, each
 // all 64 output channels, so every SIMD carries 7 blocks.  One fp32 partial slab per workgroup
 // (fg_wgrad_reduce sums them).  Replaces conv_wgrad_x6 for this shape (2x its algorithmic bytes).
+#include <algorithm>
+
 #include "conv_common.hpp"
 
 namespace {
@@ -210,9 +212,197 @@ __global__ void __launch_bounds__(512, 1) stem_wgrad_kernel(const fg_wgrad_probl
     }
 }
 
+// ---- the stem's forward: y[px][n] = bias[n] + sum_r sum_{j<63} xpad[a + r][9 px + j] * w[n][r*64 + j]
+// 4 waves (one per SIMD) over a 64-px strip walking down `rows` output rows with the same 8-row input ring.  The
+// weights (64 x 448, pre-split fp16) stay in REGISTERS for the whole launch: wave w holds output channels
+// 32 (w & 1) .. +31 (two 16-row MFMA blocks x 14 reductions of 32 x 2 pieces = 224 VGPRs) and computes pixels
+// 32 (w >> 1) .. +31 of every row, as C^T[channel][pixel] = W[channel][k] X^T[k][pixel] on v_mfma_f32_16x16x32_f16.
+// The input operand (8 consecutive flat values per lane) comes from the shifted copies with two 8-B aligned
+// reads (copy (4 - px % 4) % 4).  A lane's accumulator holds 4 consecutive channels of one pixel: one 16-B store,
+// and each wave's 32 pixels are one InstanceNorm statistics block (mean, M2 per channel) of the epilogue.
+__global__ void __launch_bounds__(256, 1) stem_fwd_kernel(const fg_conv_problem P, int rows) {
+    __shared__ __attribute__((aligned(1024))) char xring[ST_RING * ST_XROW];
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int nh = wave & 1, ph = wave >> 1;
+    const int strips = P.m_b / ST_PX, groups = P.m_a / rows;
+    const int split = blockIdx.x;
+    const int img = split / (strips * groups);
+    const int rem = split - img * strips * groups;
+    const int grp = rem / strips, strip = rem - grp * strips;
+    const int a0 = grp * rows, b0 = strip * ST_PX;
+    const int nsteps = rows + 6;
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)P.x, 0, 0x7fffffff, 0x00020000);
+    const float sx = fgc::pow2_scale(P.x_absmax);
+    const float sw = fgc::pow2_scale(P.w_absmax);
+    const float osc = 1.f / (sx * sw);
+    const int g = lane >> 4, fr = lane & 15;
+
+    for (int i = tid; i < ST_RING * ST_XROW / 16; i += 256) reinterpret_cast<f32x4*>(xring)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // weights: fragment (reduction ks, block nt, piece) = the lane's 8 k of output channel 32 nh + 16 nt + fr
+    f16x8 wf[14][2][2];
+    {
+        const f16x8* wp = reinterpret_cast<const f16x8*>(P.w);
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+            const int n = 32 * nh + 16 * nt + fr;
+#pragma unroll
+            for (int ks = 0; ks < 14; ++ks) {
+                const int q = n * (P.ldw / 8) + ks * 4 + g;
+                wf[ks][nt][0] = wp[q * 2];
+                wf[ks][nt][1] = wp[q * 2 + 1];
+            }
+        }
+    }
+    float bias[2][4];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) bias[nt][i] = P.bias ? P.bias[32 * nh + 16 * nt + 4 * g + i] : 0.f;
+
+    // staging: flat values e = tid + 256 i (< 630) of input row a0 + li
+    float rx[3];
+    const int xbase = img * (int)P.sxn + b0 * ST_C + tid;
+    auto load = [&](int li) {
+        const bool ok = li < nsteps;
+        const int xo = xbase + (a0 + li) * (int)P.sxr;
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+            rx[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                  xr, ok && tid + 256 * i < ST_FLAT ? (xo + 256 * i) * 4 : kOOB, 0, 0));
+    };
+    auto store = [&](int li) {
+        char* xs = xring + (li & (ST_RING - 1)) * ST_XROW;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const int e = tid + 256 * i;
+            if (e >= ST_FLAT) continue;
+            const float vs = rx[i] * sx;
+            const _Float16 h = (_Float16)vs;
+            const _Float16 l = (_Float16)(vs - (float)h);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                *reinterpret_cast<_Float16*>(xs + t * ST_COPYB + 2 * (e + t)) = h;
+                *reinterpret_cast<_Float16*>(xs + ST_PIECE + t * ST_COPYB + 2 * (e + t)) = l;
+            }
+        }
+    };
+
+    const int cp = (4 - (lane & 3)) & 3;             // px % 4 == lane % 4 (strip and block origins are x 16)
+    const int mab = P.m_a * P.m_b;
+    auto compute_row = [&](int k) {
+        f32x4 acc[2][2];
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+            for (int pt = 0; pt < 2; ++pt) acc[nt][pt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int r = 0; r < 7; ++r) {
+            const char* xs = xring + ((k - 6 + r) & (ST_RING - 1)) * ST_XROW + cp * ST_COPYB;
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+                for (int pt = 0; pt < 2; ++pt) {
+                    const int px = 32 * ph + 16 * pt + fr;
+                    const int ad = 2 * (9 * px + 32 * kk + 8 * g + cp);
+                    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+                    const u32x2 h0 = *reinterpret_cast<const u32x2*>(xs + ad);
+                    const u32x2 h1 = *reinterpret_cast<const u32x2*>(xs + ad + 8);
+                    const u32x2 l0 = *reinterpret_cast<const u32x2*>(xs + ST_PIECE + ad);
+                    const u32x2 l1 = *reinterpret_cast<const u32x2*>(xs + ST_PIECE + ad + 8);
+                    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+                    const f16x8 bh = __builtin_bit_cast(f16x8, u32x4{h0[0], h0[1], h1[0], h1[1]});
+                    const f16x8 bl = __builtin_bit_cast(f16x8, u32x4{l0[0], l0[1], l1[0], l1[1]});
+#pragma unroll
+                    for (int nt = 0; nt < 2; ++nt) {
+                        const int ks = 2 * r + kk;
+                        acc[nt][pt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[ks][nt][1], bh, acc[nt][pt], 0, 0, 0);
+                        acc[nt][pt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[ks][nt][0], bl, acc[nt][pt], 0, 0, 0);
+                        acc[nt][pt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[ks][nt][0], bh, acc[nt][pt], 0, 0, 0);
+                    }
+                }
+            }
+        }
+        // epilogue: output row a, this wave's 32 pixels x 32 channels; lane = 4 channels of one pixel
+        const int a = a0 + k - 6;
+        float* yrow = P.y + img * P.syn + a * P.sya + (b0 + 32 * ph) * P.syb;
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+            for (int pt = 0; pt < 2; ++pt) {
+                f32x4 v;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) v[i] = acc[nt][pt][i] * osc + bias[nt][i];
+                *reinterpret_cast<f32x4*>(yrow + (16 * pt + fr) * P.syb + 32 * nh + 16 * nt + 4 * g) = v;
+            }
+        if (P.in_stats) {
+            // (mean, M2) of each channel over the 32 pixels (16 lanes x 2 blocks), from the raw accumulators
+            const int rb = (img * mab + a * P.m_b + b0 + 32 * ph) / 32;
+            float* dst = P.in_stats + (size_t)rb * P.n_out * 2;
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    float s = acc[nt][0][i] + acc[nt][1][i];
+#pragma unroll
+                    for (int off = 1; off < 16; off <<= 1) s += __shfl_xor(s, off);
+                    const float mu = s * (1.f / 32);
+                    const float d0 = acc[nt][0][i] - mu, d1 = acc[nt][1][i] - mu;
+                    float q = d0 * d0 + d1 * d1;
+#pragma unroll
+                    for (int off = 1; off < 16; off <<= 1) q += __shfl_xor(q, off);
+                    if (fr == 0) {
+                        const int ch = 32 * nh + 16 * nt + 4 * g + i;
+                        *reinterpret_cast<float2*>(dst + ch * 2) = make_float2(mu * osc + bias[nt][i], q * (osc * osc));
+                    }
+                }
+        }
+    };
+
+    __syncthreads();
+    load(0);
+    store(0);
+    load(1);
+    __syncthreads();
+    for (int k = 0; k < nsteps; ++k) {
+        if (k + 1 < nsteps) store(k + 1);
+        load(k + 2);
+        if (k >= 6) compute_row(k);
+        __syncthreads();
+    }
+}
+
 }  // namespace
 
 namespace fgc {
+
+// rows per workgroup of the stem forward (conv_stem.hip), or 0 when it does not take the problem: the 7x7 conv over a
+// 9-channel reflect-padded input with 64 f16x3 outputs written NHWC (bias, no activation / accumulation), 64-px
+// strips; about one workgroup per CU
+int stem_fwd_rows(const fg_conv_problem& p) {
+    if (p.kh != 7 || p.j_valid != ST_J || p.jp != 64 || p.ldw != 448 || p.sxb != ST_C || p.sxa != p.sxr ||
+        p.n_out != ST_N || p.w_split != 2 || p.x_presplit || p.act || p.accumulate || p.syc != 1 || p.syb % 4 ||
+        (p.sya | p.syn) % 4 || ((uintptr_t)p.y & 15) || ((uintptr_t)p.w & 15) || !p.x_absmax || !p.w_absmax ||
+        p.m_b % ST_PX || p.m_a < 1 || p.m_img < 1)
+        return 0;
+    const long long xext = 4 * ((long long)(p.m_img - 1) * p.sxn + (long long)(p.m_a + 6) * p.sxr + p.m_b * ST_C + 64);
+    const long long yext = 4 * ((long long)(p.m_img - 1) * p.syn + (long long)p.m_a * p.sya + (long long)p.m_b * p.syb);
+    if (xext >= (1LL << 31) || yext >= (1LL << 31) || p.sxn < 0 || p.syn < 0) return 0;
+    const long long strips = (long long)p.m_img * (p.m_b / ST_PX);
+    const int want = (int)std::max(1LL, (strips * p.m_a + 255) / 256);
+    for (int r = want; r <= p.m_a; ++r)
+        if (p.m_a % r == 0) return r;
+    return p.m_a;
+}
+
+int launch_fwd_stem(const fg_conv_problem& p, hipStream_t stream, int* rc) {
+    const int rows = stem_fwd_rows(p);
+    if (!rows) return 0;
+    const int grid = p.m_img * (p.m_b / ST_PX) * (p.m_a / rows);
+    hipLaunchKernelGGL(stem_fwd_kernel, dim3(grid), dim3(256), 0, stream, p, rows);
+    *rc = fg::launched("stem_fwd");
+    return 1;
+}
 
 int stem_wgrad_rows(const fg_wgrad_problem& p) {
     // rows per split encoded as m_chunk = 64 * rows (a 64-px strip of `rows` output rows per workgroup)

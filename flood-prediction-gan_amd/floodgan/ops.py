@@ -357,6 +357,9 @@ USE_WIN = True   # route eligible single convs to the row-strip kernel (fg_conv_
 FUSED_IN_STATS = os.environ.get("FLOODGAN_FUSED_IN_STATS", "1") != "0"
 
 
+LAST_CONV_KERNEL = None    # the kernel family the last conv() launch ran (fg_last_launch; tests)
+
+
 def conv(probs, tag=None, in_stats=False):
     """Launch 1-4 fg_conv_problem dicts (plans.conv_problem / phase_problems) in one kernel
     (the row-strip window kernel for a lone eligible 7x7 conv, see win_eligible).  in_stats=True:
@@ -402,6 +405,8 @@ def _conv(probs, in_stats=False, tag=None):
                 check_scale(wt, wa, "fp32 weight")
     stats = _stats_partials(probs, arr) if (in_stats and FUSED_IN_STATS) else None
     _timed(tag, lambda: L.check(_lib().fg_conv_fwd(arr, len(probs), L.stream_handle()), "conv_fwd"))
+    global LAST_CONV_KERNEL
+    LAST_CONV_KERNEL = L.last_launch()
     _wrote(*[p["y"][0] for p in probs])
     return stats
 

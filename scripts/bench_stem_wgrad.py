@@ -1,6 +1,7 @@
-"""The stem's weight gradient (7x7 over the packed 9-channel input -> 64, bs 8, 512^2), interleaved A/B: the strip
-kernel (conv_stem.hip, its own 256 splits) against the register-staged x6 kernel (forced with fg_set_wgrad_tile 2 and
-the generic split layout); outputs compared, and both against an fp64 reference of one image's weight gradient.
+"""The stem (7x7 over the packed 9-channel input -> 64, bs 8, 512^2), interleaved A/B of the strip kernels
+(conv_stem.hip) against the register-staged x6 kernels: the weight gradient (the strip kernel's own 256 splits vs the x6
+kernel forced with fg_set_wgrad_tile 2 on the generic split layout) and the forward with the statistics epilogue
+(FLOODGAN_STEM_FWD 1 / 0); outputs compared, and the weight gradients against fp64.
   python scripts/bench_stem_wgrad.py"""
 import os
 import sys
@@ -40,6 +41,24 @@ def main():
             print(f"stem wgrad {kind:4s} ({ops.LAST_WGRAD_KERNEL}): {ms * 1e3:8.1f} us per wgrad + reduce, "
                   f"{2 * N * H * H * 64 * 441 / ms / 1e9:7.1f} TFLOP/s", flush=True)
     L.load().fg_set_wgrad_tile(-1)
+    # forward (+ statistics epilogue; the x6 path computes the statistics in a separate pass)
+    w = torch.randn(64, 9, 7, 7, device="cuda") * 0.05
+    m = PL.wmap_conv_fwd(w.shape, 9)
+    Y = Buf.empty(N, H, H, 64, 0, "cuda")
+    fprob = PL.conv_problem(X0, 3, 7, 1, ops.pack_weight(w, m), m, Y, bias=torch.zeros(64, device="cuda"))
+    fout = {}
+    for rep in range(2):
+        for on in ("1", "0"):
+            os.environ["FLOODGAN_STEM_FWD"] = on
+            def run():
+                st = ops.conv([fprob], in_stats=True)
+                return st if st is not None else ops.in_stats(Y)
+            ms = time_it(run, reps=5)
+            fout[on] = Y.t.clone()
+            print(f"stem fwd + stats, strip kernel {on} ({ops.LAST_CONV_KERNEL}): {ms * 1e3:8.1f} us, "
+                  f"{2 * N * H * H * 64 * 441 / ms / 1e9:7.1f} TFLOP/s", flush=True)
+    os.environ.pop("FLOODGAN_STEM_FWD")
+    print(f"stem fwd strip vs x6 rel diff {float((fout['1'] - fout['0']).norm() / fout['0'].norm()):.2e}", flush=True)
     # fp64 reference over the whole batch
     gy = gc1.interior().permute(0, 3, 1, 2).double().cpu()
     ref = torch.nn.grad.conv2d_weight(F.pad(x.double().cpu(), (3,) * 4, mode="reflect"), dw.shape, gy)

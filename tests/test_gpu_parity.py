@@ -166,7 +166,7 @@ def test_convT(cin, cout, H, conv_math):
 
 @pytest.mark.parametrize("persistent,sched,order", [(0, 2, 3), (1, 2, 3), (1, 1, 3), (1, 0, 3), (1, 1, 2),
                                                     (1, 1, 1), (1, 1, 0), (1, 1, 7), (1, 3, 7), (0, 3, 7)])
-@pytest.mark.parametrize("cfg", [-2, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("cfg", [-2, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11])
 @pytest.mark.parametrize("case", [(256, 256, 3, 1, 1, "reflect", 20), (128, 256, 4, 2, 1, "constant", 22),
                                   (64, 128, 3, 2, 1, "constant", 30), (256, 512, 4, 1, 1, "constant", 11),
                                   (128, 64, 3, 1, 1, "constant", 21)])
@@ -311,6 +311,41 @@ def test_stem_wgrad_strips(H, N, splits):
         assert nrel(dw, gw_ref) < KTOL
     finally:
         PL.STEM_SPLITS = prev_s
+        L.set_conv_math(prev)
+
+
+@pytest.mark.parametrize("H,N", [(64, 2), (128, 2), (192, 1)])
+def test_stem_fwd_strips(H, N):
+    """the stem's forward kernel (conv_stem.hip: 7x7 over the reflect-padded 9-channel input, 64 outputs + bias,
+    weights resident in registers, 64-px strips over an 8-row LDS ring) against fp64, with and without the
+    InstanceNorm statistics epilogue (models/model_architectures.py:312, :342-343)"""
+    from floodgan import _lib as L, ops, plans as PL
+    from floodgan.plans import Buf
+    prev = L.get_conv_math()
+    L.set_conv_math("f16x3")
+    try:
+        torch.manual_seed(12)
+        x = torch.rand(N, 9, H, H, dtype=torch.float64) * 2 - 1
+        w = torch.randn(64, 9, 7, 7, dtype=torch.float64) * 0.05
+        b = torch.randn(64, dtype=torch.float64) * 0.1
+        ref = F.conv2d(F.pad(x, (3,) * 4, mode="reflect"), w, b)
+        X = buf_from(x, 3, "reflect")
+        wd = w.float().to(DEV)
+        m = PL.wmap_conv_fwd(wd.shape, X.c)
+        for stats in (False, True):
+            Y = Buf.empty(N, H, H, 64, 0, DEV)
+            st = ops.conv([PL.conv_problem(X, 3, 7, 1, ops.pack_weight(wd, m), m, Y, bias=b.float().to(DEV))],
+                          in_stats=stats)
+            assert ops.LAST_CONV_KERNEL == "stem_fwd", ops.LAST_CONV_KERNEL
+            torch.cuda.synchronize()
+            assert nrel(nchw(Y), ref) < KTOL
+            if stats:
+                assert st is not None
+                mu = ref.mean(dim=(2, 3))
+                var = ref.var(dim=(2, 3), unbiased=False)
+                assert nrel(st[0].view(N, 64), mu) < KTOL
+                assert nrel(st[1].view(N, 64), (var + 1e-5).rsqrt()) < KTOL
+    finally:
         L.set_conv_math(prev)
 
 
@@ -707,7 +742,7 @@ def test_presplit_resblock_convs(N, H):
 
 
 @pytest.mark.parametrize("persistent", [1, 3])
-@pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11])
 @pytest.mark.parametrize("case", [(256, 256, 3, 1, 1, 20), (128, 64, 3, 2, 1, 24), (64, 128, 3, 1, 1, 17)])
 def test_presplit_f3_tiles_and_stats(case, cfg, persistent):
     """every pipelined tile config (and the automatic choice, -1) on a FG_PRESPLIT operand, with and without the
