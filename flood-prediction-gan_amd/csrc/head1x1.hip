@@ -9,6 +9,8 @@
 //   input gradient: thread = (pixel, group of 16 input channels), writes 4 float4 of the 64-channel row;
 //   weight + bias:  thread = (output o, channel quad), sums over the block's pixels; per-block partials are
 //                   reduced over blocks in fp64 in a fixed order (deterministic).
+#include <algorithm>
+
 #include "fg_common.hpp"
 
 namespace {
@@ -40,68 +42,113 @@ __device__ __forceinline__ void stage(const fg_view& v, int q4, int p0, int P, f
 
 __global__ void __launch_bounds__(256) conv1x1_fwd_kernel(fg_view x, const float* __restrict__ w,
                                                           const float* __restrict__ b, int n_out, fg_view y) {
-    __shared__ __attribute__((aligned(16))) float xs[TP * XS];
+    __shared__ __attribute__((aligned(16))) float xs[2][TP * XS];
     __shared__ __attribute__((aligned(16))) float ws[NO * XS];
-    const int P = x.n * x.h * x.w, p0 = blockIdx.x * TP;
+    const int P = x.n * x.h * x.w, ntiles = (P + TP - 1) / TP;
+    // persistent: the weights are staged once per block, the block walks tiles blockIdx.x, + gridDim.x, ...
+    // with the next tile's loads in flight (registers) while the current one is computed
     for (int i = threadIdx.x; i < NO * CI; i += 256) {
         const int o = i / CI, c = i - o * CI;
         ws[o * XS + c] = o < n_out ? w[i] : 0.f;
     }
-    stage(x, CI / 4, p0, P, xs, XS);
+    const int px = threadIdx.x >> 2, og = threadIdx.x & 3;
+    float bias[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bias[j] = (b && 4 * og + j < n_out) ? b[4 * og + j] : 0.f;
+    // staging: thread t loads quads t, t + 256, t + 512, t + 768 of the tile (pixel i / 16, quad i % 16)
+    f32x4 rv[4];
+    auto load = [&](int t) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int i = threadIdx.x + 256 * k, pp = i >> 4, q = i & 15, p = t * TP + pp;
+            rv[k] = (t < ntiles && p < P) ? ld4(x.ptr + pix_off(x, p) + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+    };
+    auto store = [&](float* dst) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int i = threadIdx.x + 256 * k;
+            st4(dst + (i >> 4) * XS + 4 * (i & 15), rv[k]);
+        }
+    };
+    int t = blockIdx.x, buf = 0;
+    load(t);
+    store(xs[0]);
+    load(t + gridDim.x);
     __syncthreads();
-    const int px = threadIdx.x >> 2, og = threadIdx.x & 3, p = p0 + px;
-    float acc[4];
+    for (; t < ntiles; t += gridDim.x, buf ^= 1) {
+        if (t + gridDim.x < ntiles) store(xs[buf ^ 1]);
+        load(t + 2 * gridDim.x);
+        const int p = t * TP + px;
+        float acc[4] = {bias[0], bias[1], bias[2], bias[3]};
+        if (4 * og < n_out) {
+            const float* xr = xs[buf] + px * XS;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[j] = (b && 4 * og + j < n_out) ? b[4 * og + j] : 0.f;
-    if (4 * og < n_out) {
-        const float* xr = xs + px * XS;
+            for (int q = 0; q < CI / 4; ++q) {
+                const f32x4 v = ld4(xr + 4 * q);
 #pragma unroll
-        for (int q = 0; q < CI / 4; ++q) {
-            const f32x4 v = ld4(xr + 4 * q);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const f32x4 wv = ld4(ws + (4 * og + j) * XS + 4 * q);
-                acc[j] = fmaf(v[0], wv[0], acc[j]);
-                acc[j] = fmaf(v[1], wv[1], acc[j]);
-                acc[j] = fmaf(v[2], wv[2], acc[j]);
-                acc[j] = fmaf(v[3], wv[3], acc[j]);
+                for (int j = 0; j < 4; ++j) {
+                    const f32x4 wv = ld4(ws + (4 * og + j) * XS + 4 * q);
+                    acc[j] = fmaf(v[0], wv[0], acc[j]);
+                    acc[j] = fmaf(v[1], wv[1], acc[j]);
+                    acc[j] = fmaf(v[2], wv[2], acc[j]);
+                    acc[j] = fmaf(v[3], wv[3], acc[j]);
+                }
             }
         }
+        if (p < P && 4 * og < y.c_alloc) st4(y.ptr + pix_off(y, p) + 4 * og, f32x4{acc[0], acc[1], acc[2], acc[3]});
+        __syncthreads();
     }
-    if (p < P && 4 * og < y.c_alloc) st4(y.ptr + pix_off(y, p) + 4 * og, f32x4{acc[0], acc[1], acc[2], acc[3]});
 }
 
 __global__ void __launch_bounds__(256) conv1x1_dgrad_kernel(fg_view gy, const float* __restrict__ w, int n_out,
                                                             fg_view gx) {
-    __shared__ __attribute__((aligned(16))) float gs[TP * GS];
+    __shared__ __attribute__((aligned(16))) float gs[2][TP * GS];
     __shared__ __attribute__((aligned(16))) float ws[NO * XS];
-    const int P = gx.n * gx.h * gx.w, p0 = blockIdx.x * TP;
+    const int P = gx.n * gx.h * gx.w, ntiles = (P + TP - 1) / TP;
+    const int q4 = (n_out + 3) / 4;                    // gradient quads per pixel (<= 4)
+    // persistent like the forward: weights once per block, the next tile's gradient rows in registers
     for (int i = threadIdx.x; i < NO * CI; i += 256) {
         const int o = i / CI, c = i - o * CI;
         ws[o * XS + c] = o < n_out ? w[i] : 0.f;
     }
-    stage(gy, (n_out + 3) / 4, p0, P, gs, GS);
+    const int px = threadIdx.x >> 2, cg = threadIdx.x & 3;   // channels 16 cg .. 16 cg + 15
+    f32x4 rv;                                          // thread t: pixel t / 4, quad t % 4 of the tile
+    auto load = [&](int t) {
+        const int pp = threadIdx.x >> 2, q = threadIdx.x & 3, p = t * TP + pp;
+        rv = (t < ntiles && p < P && q < q4) ? ld4(gy.ptr + pix_off(gy, p) + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+    };
+    auto store = [&](float* dst) { st4(dst + (threadIdx.x >> 2) * GS + 4 * (threadIdx.x & 3), rv); };
+    int t = blockIdx.x, buf = 0;
+    load(t);
+    store(gs[0]);
+    load(t + gridDim.x);
     __syncthreads();
-    const int px = threadIdx.x >> 2, cg = threadIdx.x & 3, p = p0 + px;   // channels 16 cg .. 16 cg + 15
-    f32x4 a[4];
+    for (; t < ntiles; t += gridDim.x, buf ^= 1) {
+        if (t + gridDim.x < ntiles) store(gs[buf ^ 1]);
+        load(t + 2 * gridDim.x);
+        const int p = t * TP + px;
+        f32x4 a[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) a[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const float* gr = gs + px * GS;
-    for (int o = 0; o < n_out; ++o) {
-        const float g = gr[o];
+        for (int k = 0; k < 4; ++k) a[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const float* gr = gs[buf] + px * GS;
+        for (int o = 0; o < n_out; ++o) {
+            const float g = gr[o];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const f32x4 wv = ld4(ws + o * XS + 16 * cg + 4 * k);
-            a[k][0] = fmaf(g, wv[0], a[k][0]);
-            a[k][1] = fmaf(g, wv[1], a[k][1]);
-            a[k][2] = fmaf(g, wv[2], a[k][2]);
-            a[k][3] = fmaf(g, wv[3], a[k][3]);
+            for (int k = 0; k < 4; ++k) {
+                const f32x4 wv = ld4(ws + o * XS + 16 * cg + 4 * k);
+                a[k][0] = fmaf(g, wv[0], a[k][0]);
+                a[k][1] = fmaf(g, wv[1], a[k][1]);
+                a[k][2] = fmaf(g, wv[2], a[k][2]);
+                a[k][3] = fmaf(g, wv[3], a[k][3]);
+            }
         }
-    }
-    if (p < P) {
-        float* dst = gx.ptr + pix_off(gx, p) + 16 * cg;
+        if (p < P) {
+            float* dst = gx.ptr + pix_off(gx, p) + 16 * cg;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) st4(dst + 4 * k, a[k]);
+            for (int k = 0; k < 4; ++k) st4(dst + 4 * k, a[k]);
+        }
+        __syncthreads();
     }
 }
 
@@ -182,7 +229,9 @@ FG_API int fg_conv1x1_fwd(fg_view x, const float* w, const float* bias, int n_ou
         return fg::fail(FG_ERR_INVALID, "fg_conv1x1_fwd: bad args (c_in %d, n_out %d, y.c_alloc %d)", x.c_alloc, n_out,
                         y.c_alloc);
     const int P = x.n * x.h * x.w;
-    hipLaunchKernelGGL(conv1x1_fwd_kernel, dim3((P + TP - 1) / TP), dim3(256), 0, stream, x, w, bias, n_out, y);
+    const int ntiles = (P + TP - 1) / TP;
+    hipLaunchKernelGGL(conv1x1_fwd_kernel, dim3(std::min(ntiles, 4 * fg::num_cus())), dim3(256), 0, stream, x, w, bias,
+                       n_out, y);
     return fg::launched("conv1x1_fwd");
 }
 
@@ -191,7 +240,9 @@ FG_API int fg_conv1x1_dgrad(fg_view gy, const float* w, int n_out, fg_view gx, h
         return fg::fail(FG_ERR_INVALID, "fg_conv1x1_dgrad: bad args (n_out %d, gy.c_alloc %d, gx.c_alloc %d)", n_out,
                         gy.c_alloc, gx.c_alloc);
     const int P = gx.n * gx.h * gx.w;
-    hipLaunchKernelGGL(conv1x1_dgrad_kernel, dim3((P + TP - 1) / TP), dim3(256), 0, stream, gy, w, n_out, gx);
+    const int ntiles = (P + TP - 1) / TP;
+    hipLaunchKernelGGL(conv1x1_dgrad_kernel, dim3(std::min(ntiles, 4 * fg::num_cus())), dim3(256), 0, stream, gy, w,
+                       n_out, gx);
     return fg::launched("conv1x1_dgrad");
 }
 

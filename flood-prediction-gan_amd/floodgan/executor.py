@@ -154,12 +154,6 @@ def _norm(c, act, pad, mode, residual=None, stats=None, presplit=False, ps_copy=
     return (mean, rstd, out, ps) if ps_copy else (mean, rstd, out)
 
 
-# FLOODGAN_STEM_PAD4=1: the generator input buffer's channels padded to a multiple of 4.  The stem's weight gradient
-# then takes the pipelined kernel (its 64-row tile), but the stem forward pays for the zero channels: step A/B 47.97
-# (off) vs 48.24 ms (on), profiles/round3/r3af_ab_stem_pad4.log -- off by default
-STEM_PAD4 = os.environ.get("FLOODGAN_STEM_PAD4", "0") == "1"
-
-
 def has_attention(P):
     """PairedAttention / AttentionGAN generators carry the attention head; CycleGAN's does not"""
     return "deconv3_attention.weight" in P
@@ -183,8 +177,7 @@ def gen_forward(P, x, save=True, x_extra=None):
         raise RuntimeError(f"PairedAttentionGenerator needs H, W divisible by 4 and >= 8 (got {H}x{W})")
     dev = x.device
     S = {}
-    # STEM_PAD4: 9-channel inputs padded to 12 zero-filled channels (16-B rows; see STEM_PAD4)
-    X0 = Buf.empty(N, H, W, PL.rup(Cin + Ce, 4) if STEM_PAD4 and Cin + Ce > 8 else Cin + Ce, 3, dev)
+    X0 = Buf.empty(N, H, W, Cin + Ce, 3, dev)
     ops.pack_input(x, Cin, x_extra, Ce, X0, 0, N, FG_PAD_REFLECT)             # F.pad(input, 3, reflect)
     c1 = Buf.empty(N, H, W, 64, 0, dev)
     st = _conv_fwd(P, "conv1", X0, 3, 7, 1, c1, in_stats=True)

@@ -541,7 +541,6 @@ def _wgrad_win(prob, wmap, dw, accumulate):
             "wgrad_reduce")
 
 
-STEM_WGRAD = True          # the stem's strip kernel (conv_stem.hip); False: the generic split layout (x6 kernel)
 LAST_WGRAD_KERNEL = None   # the kernel family the last wgrad() launch ran (fg_last_launch; tests)
 
 _WG_FIELDS = ("spn", "spa", "spb", "sxn", "sxa", "sxb", "sxr", "m_img", "m_a", "m_b", "n_a", "kh", "j_valid",
@@ -567,7 +566,7 @@ def wgrad(prob, wmap, dw, accumulate=False, tag=None):
     dev = _dev(prob["p"][0])
     if USE_WIN and L.wgrad_f16x3() and wgrad_win_eligible(prob):
         return _wgrad_win(prob, wmap, dw, accumulate)
-    stem = stem_wgrad_layout(prob) if STEM_WGRAD and L.wgrad_f16x3() else None
+    stem = stem_wgrad_layout(prob) if L.wgrad_f16x3() else None
     if stem is not None and not (is_presplit(prob["p"][0]) or is_presplit(prob["x"][0])):
         # the stem's strip kernel (conv_stem.hip) defines its own splits: 64-px strips of m_chunk / 64 rows
         prob = dict(prob, splits=stem[0], m_chunk=stem[1])

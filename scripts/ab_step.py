@@ -1,7 +1,7 @@
 """A/B of engine switches on the full bs-8 512^2 training step, interleaved in ONE process (device
 clocks and boxes differ by several percent, so separate bench runs cannot resolve small gains).
   python scripts/ab_step.py f3_persistent [rounds] [steps] [values, default 0,1]
-Switches: f3_persistent, f3_sched, f3_order, f3_fill, f3_interleave, head_1x1, win_waves (values 4,8), wgrad_f3, use_win, in_rows, presplit, ps_wide (values 4,5), ps_resid, stem_pad4, stem_wgrad, stem_fwd, win_rs, f3_narrow."""
+Switches: f3_persistent, f3_sched, f3_order, f3_fill, f3_interleave, head_1x1, wgrad_f3, use_win, in_rows, presplit, ps_wide (values 4,5), ps_resid, stem_fwd, f3_narrow."""
 import os
 import sys
 import time
@@ -29,9 +29,6 @@ def switch(name, on):
         lib.fg_set_f3_fill(int(on))
     elif name == "presplit":
         ops.PRESPLIT = bool(on)
-    elif name == "stem_pad4":
-        from floodgan import executor
-        executor.STEM_PAD4 = bool(on)
     elif name == "ps_resid":
         ops.PRESPLIT_RESID = bool(on)
     elif name == "ps_wide":
@@ -43,18 +40,12 @@ def switch(name, on):
     elif name == "head_1x1":
         from floodgan import executor
         executor.HEAD_1X1 = bool(on)
-    elif name == "win_waves":
-        os.environ["FLOODGAN_WIN_WAVES"] = str(int(on))
     elif name == "use_win":
         ops.USE_WIN = bool(on)
-    elif name == "stem_wgrad":
-        ops.STEM_WGRAD = bool(on)
     elif name == "stem_fwd":
         os.environ["FLOODGAN_STEM_FWD"] = str(int(on))
     elif name == "f3_narrow":
         os.environ["FLOODGAN_F3_NARROW"] = str(int(on))
-    elif name == "win_rs":
-        os.environ["FLOODGAN_WIN_RS"] = str(int(on))
 
     else:
         raise SystemExit(f"unknown switch {name}")

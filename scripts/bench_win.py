@@ -1,7 +1,6 @@
-"""A/B (GPU) of the row-strip window kernel forms on the content head's forward (7x7 64 -> 27 at 512^2) and input
-gradient (7x7 27(32) -> 64 over 518^2), bs 8, interleaved; outputs compared: FLOODGAN_WIN_RS=1 (register-staged,
-one barrier pair per kernel row; 4: its 4-wave form, 64 rows per wave) against the LDS-DMA form (one barrier per
-tap).
+"""Timing (GPU) of the row-strip window kernel on the content head's forward (7x7 64 -> 27 at 512^2) and input
+gradient (7x7 27(32) -> 64 over 518^2), bs 8 (round 4: its LDS-DMA form, one barrier per tap, was replaced by the
+register-staged one, profiles/round4/r4c_ab_win.log).
   python scripts/ab_win.py"""
 import os
 import sys
@@ -36,18 +35,10 @@ def main():
     dgr = PL.conv_problem(gcl, 6, 7, 1, ops.pack_weight(w, md), md, Y)
     for name, prob, out, flops in (("content fwd 7x7 64->27 @512", fwd, cl, 2.0 * N * 512 * 512 * 27 * 64 * 49),
                                    ("content dgrad 7x7 27->64 @518", dgr, Y, 2.0 * N * 518 * 518 * 64 * 27 * 49)):
-        res = {}
-        for rs in ("0", "1", "4", "0", "1", "4"):
-            os.environ["FLOODGAN_WIN_RS"] = rs
+        for _ in range(3):
             out.t.zero_()
-            ops.conv_win(prob)
-            torch.cuda.synchronize()
-            res[rs] = out.t.clone()
             ms = min(time_it(lambda: ops.conv_win(prob)) for _ in range(3))
-            d = float((res[rs] - res["0"]).norm() / res["0"].norm())
-            print(f"{name:32s} rs {rs} {ms * 1e3:8.1f} us {flops / ms / 1e9:7.1f} TFLOP/s  rel diff vs dma {d:.1e}",
-                  flush=True)
-    os.environ.pop("FLOODGAN_WIN_RS")
+            print(f"{name:32s} {ms * 1e3:8.1f} us {flops / ms / 1e9:7.1f} TFLOP/s", flush=True)
 
 
 if __name__ == "__main__":

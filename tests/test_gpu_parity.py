@@ -349,15 +349,13 @@ def test_stem_fwd_strips(H, N):
         L.set_conv_math(prev)
 
 
-@pytest.mark.parametrize("rs", ["0", "1"])
 @pytest.mark.parametrize("case", ["content_fwd", "content_dgrad"])
-def test_conv_window(case, rs, monkeypatch):
+def test_conv_window(case):
     """the row-strip window kernel (fg_conv_win) on the content-head geometries -- 7x7 over 64
     channels -> 27, and its input gradient 27(32) -> 64 over the 6-bordered gradient -- with
     output rows of 256+ px (two-segment tiles, ragged last tile) against fp64"""
     from floodgan import _lib as L, ops, plans as PL
     from floodgan.plans import Buf
-    monkeypatch.setenv("FLOODGAN_WIN_RS", rs)     # 1: the register-staged form (one barrier pair per kernel row)
     prev = L.get_conv_math()
     L.set_conv_math("f16x3")
     try:
