@@ -213,17 +213,21 @@ __global__ void __launch_bounds__(512, 1) stem_wgrad_kernel(const fg_wgrad_probl
 }
 
 // ---- the stem's forward: y[px][n] = bias[n] + sum_r sum_{j<63} xpad[a + r][9 px + j] * w[n][r*64 + j]
-// 4 waves (one per SIMD) over a 64-px strip walking down `rows` output rows with the same 8-row input ring.  The
-// weights (64 x 448, pre-split fp16) stay in REGISTERS for the whole launch: wave w holds output channels
-// 32 (w & 1) .. +31 (two 16-row MFMA blocks x 14 reductions of 32 x 2 pieces = 224 VGPRs) and computes pixels
-// 32 (w >> 1) .. +31 of every row, as C^T[channel][pixel] = W[channel][k] X^T[k][pixel] on v_mfma_f32_16x16x32_f16.
-// The input operand (8 consecutive flat values per lane) comes from the shifted copies with two 8-B aligned
-// reads (copy (4 - px % 4) % 4).  A lane's accumulator holds 4 consecutive channels of one pixel: one 16-B store,
-// and each wave's 32 pixels are one InstanceNorm statistics block (mean, M2 per channel) of the epilogue.
-__global__ void __launch_bounds__(256, 1) stem_fwd_kernel(const fg_conv_problem P, int rows) {
-    __shared__ __attribute__((aligned(1024))) char xring[ST_RING * ST_XROW];
+// 8 waves (two per SIMD) over a 64-px strip walking down `rows` output rows with the same 8-row input ring.  The
+// weights (64 x 448, pre-split fp16) stay in REGISTERS for the whole launch: wave (nh, ph, kh) holds output channels
+// 32 nh .. +31 for reductions 7 kh .. 7 kh + 6 of 14 (two 16-row MFMA blocks x 7 reductions of 32 x 2 pieces = 112
+// VGPRs) and computes pixels 32 ph .. +31 of every row, as C^T[channel][pixel] = W[channel][k] X^T[k][pixel] on
+// v_mfma_f32_16x16x32_f16; the K halves meet in LDS (double-buffered 16 KB) and the kh = 0 waves finish the row.
+// The input operand (8 consecutive flat values per lane) comes from the shifted copies with two 8-B aligned reads
+// (copy (4 - px % 4) % 4).  A lane's accumulator holds 4 consecutive channels of one pixel: one 16-B store, and
+// each wave's 32 pixels are one InstanceNorm statistics block (mean, M2 per channel) of the epilogue.
+__global__ void __launch_bounds__(512, 1) stem_fwd_kernel(const fg_conv_problem P, int rows) {
+    constexpr int RED = 4 * 64 * 16 * 4;            // the kh = 1 partials of one row: 4 waves x 64 lanes x 16 floats
+    __shared__ __attribute__((aligned(1024))) char smem[ST_RING * ST_XROW + 2 * RED];
+    char* const xring = smem;
+    float* const red = reinterpret_cast<float*>(smem + ST_RING * ST_XROW);
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int nh = wave & 1, ph = wave >> 1;
+    const int nh = wave & 1, ph = (wave >> 1) & 1, kh = wave >> 2;
     const int strips = P.m_b / ST_PX, groups = P.m_a / rows;
     const int split = blockIdx.x;
     const int img = split / (strips * groups);
@@ -237,20 +241,20 @@ __global__ void __launch_bounds__(256, 1) stem_fwd_kernel(const fg_conv_problem 
     const float osc = 1.f / (sx * sw);
     const int g = lane >> 4, fr = lane & 15;
 
-    for (int i = tid; i < ST_RING * ST_XROW / 16; i += 256) reinterpret_cast<f32x4*>(xring)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = tid; i < ST_RING * ST_XROW / 16; i += 512) reinterpret_cast<f32x4*>(xring)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    // weights: fragment (reduction ks, block nt, piece) = the lane's 8 k of output channel 32 nh + 16 nt + fr
-    f16x8 wf[14][2][2];
+    // weights: fragment (reduction 7 kh + i, block nt, piece) = the lane's 8 k of output channel 32 nh + 16 nt + fr
+    f16x8 wf[7][2][2];
     {
         const f16x8* wp = reinterpret_cast<const f16x8*>(P.w);
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) {
             const int n = 32 * nh + 16 * nt + fr;
 #pragma unroll
-            for (int ks = 0; ks < 14; ++ks) {
-                const int q = n * (P.ldw / 8) + ks * 4 + g;
-                wf[ks][nt][0] = wp[q * 2];
-                wf[ks][nt][1] = wp[q * 2 + 1];
+            for (int i = 0; i < 7; ++i) {
+                const int q = n * (P.ldw / 8) + (7 * kh + i) * 4 + g;
+                wf[i][nt][0] = wp[q * 2];
+                wf[i][nt][1] = wp[q * 2 + 1];
             }
         }
     }
@@ -260,22 +264,22 @@ __global__ void __launch_bounds__(256, 1) stem_fwd_kernel(const fg_conv_problem 
 #pragma unroll
         for (int i = 0; i < 4; ++i) bias[nt][i] = P.bias ? P.bias[32 * nh + 16 * nt + 4 * g + i] : 0.f;
 
-    // staging: flat values e = tid + 256 i (< 630) of input row a0 + li
-    float rx[3];
+    // staging: flat values e = tid, tid + 512 (< 630) of input row a0 + li
+    float rx[2];
     const int xbase = img * (int)P.sxn + b0 * ST_C + tid;
     auto load = [&](int li) {
         const bool ok = li < nsteps;
         const int xo = xbase + (a0 + li) * (int)P.sxr;
 #pragma unroll
-        for (int i = 0; i < 3; ++i)
+        for (int i = 0; i < 2; ++i)
             rx[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                  xr, ok && tid + 256 * i < ST_FLAT ? (xo + 256 * i) * 4 : kOOB, 0, 0));
+                                                  xr, ok && tid + 512 * i < ST_FLAT ? (xo + 512 * i) * 4 : kOOB, 0, 0));
     };
     auto store = [&](int li) {
         char* xs = xring + (li & (ST_RING - 1)) * ST_XROW;
 #pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            const int e = tid + 256 * i;
+        for (int i = 0; i < 2; ++i) {
+            const int e = tid + 512 * i;
             if (e >= ST_FLAT) continue;
             const float vs = rx[i] * sx;
             const _Float16 h = (_Float16)vs;
@@ -290,40 +294,44 @@ __global__ void __launch_bounds__(256, 1) stem_fwd_kernel(const fg_conv_problem 
 
     const int cp = (4 - (lane & 3)) & 3;             // px % 4 == lane % 4 (strip and block origins are x 16)
     const int mab = P.m_a * P.m_b;
+    f32x4 acc[2][2];
     auto compute_row = [&](int k) {
-        f32x4 acc[2][2];
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
             for (int pt = 0; pt < 2; ++pt) acc[nt][pt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int r = 0; r < 7; ++r) {
+        for (int i = 0; i < 7; ++i) {
+            const int ks = 7 * kh + i, r = ks >> 1, kk = ks & 1;
             const char* xs = xring + ((k - 6 + r) & (ST_RING - 1)) * ST_XROW + cp * ST_COPYB;
 #pragma unroll
-            for (int kk = 0; kk < 2; ++kk) {
+            for (int pt = 0; pt < 2; ++pt) {
+                const int px = 32 * ph + 16 * pt + fr;
+                const int ad = 2 * (9 * px + 32 * kk + 8 * g + cp);
+                typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+                typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+                const u32x2 h0 = *reinterpret_cast<const u32x2*>(xs + ad);
+                const u32x2 h1 = *reinterpret_cast<const u32x2*>(xs + ad + 8);
+                const u32x2 l0 = *reinterpret_cast<const u32x2*>(xs + ST_PIECE + ad);
+                const u32x2 l1 = *reinterpret_cast<const u32x2*>(xs + ST_PIECE + ad + 8);
+                const f16x8 bh = __builtin_bit_cast(f16x8, u32x4{h0[0], h0[1], h1[0], h1[1]});
+                const f16x8 bl = __builtin_bit_cast(f16x8, u32x4{l0[0], l0[1], l1[0], l1[1]});
 #pragma unroll
-                for (int pt = 0; pt < 2; ++pt) {
-                    const int px = 32 * ph + 16 * pt + fr;
-                    const int ad = 2 * (9 * px + 32 * kk + 8 * g + cp);
-                    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-                    const u32x2 h0 = *reinterpret_cast<const u32x2*>(xs + ad);
-                    const u32x2 h1 = *reinterpret_cast<const u32x2*>(xs + ad + 8);
-                    const u32x2 l0 = *reinterpret_cast<const u32x2*>(xs + ST_PIECE + ad);
-                    const u32x2 l1 = *reinterpret_cast<const u32x2*>(xs + ST_PIECE + ad + 8);
-                    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-                    const f16x8 bh = __builtin_bit_cast(f16x8, u32x4{h0[0], h0[1], h1[0], h1[1]});
-                    const f16x8 bl = __builtin_bit_cast(f16x8, u32x4{l0[0], l0[1], l1[0], l1[1]});
-#pragma unroll
-                    for (int nt = 0; nt < 2; ++nt) {
-                        const int ks = 2 * r + kk;
-                        acc[nt][pt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[ks][nt][1], bh, acc[nt][pt], 0, 0, 0);
-                        acc[nt][pt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[ks][nt][0], bl, acc[nt][pt], 0, 0, 0);
-                        acc[nt][pt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[ks][nt][0], bh, acc[nt][pt], 0, 0, 0);
-                    }
+                for (int nt = 0; nt < 2; ++nt) {
+                    acc[nt][pt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[i][nt][1], bh, acc[nt][pt], 0, 0, 0);
+                    acc[nt][pt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[i][nt][0], bl, acc[nt][pt], 0, 0, 0);
+                    acc[nt][pt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[i][nt][0], bh, acc[nt][pt], 0, 0, 0);
                 }
             }
         }
-        // epilogue: output row a, this wave's 32 pixels x 32 channels; lane = 4 channels of one pixel
+    };
+    // the kh = 0 wave of (nh, ph): add the kh = 1 partials, store the row and its statistics
+    auto finish_row = [&](int k) {
+        const float* rb_ = red + ((k & 1) * 4 + (wave & 3)) * 64 * 16 + lane * 4;
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+            for (int pt = 0; pt < 2; ++pt) acc[nt][pt] += *reinterpret_cast<const f32x4*>(rb_ + (nt * 2 + pt) * 256);
         const int a = a0 + k - 6;
         float* yrow = P.y + img * P.syn + a * P.sya + (b0 + 32 * ph) * P.syb;
 #pragma unroll
@@ -359,6 +367,9 @@ __global__ void __launch_bounds__(256, 1) stem_fwd_kernel(const fg_conv_problem 
         }
     };
 
+    // step k: store input row k + 1 (ring slot (k+1) & 7, not read by row k - 6), load row k + 2, reduce output row
+    // k - 6 (rows k-6 .. k); the kh = 1 waves leave their partials in red[k & 1] (red[(k+1) & 1] is still being read
+    // by the kh = 0 waves of the previous row -- they passed this step's barrier only after reading it)
     __syncthreads();
     load(0);
     store(0);
@@ -367,8 +378,18 @@ __global__ void __launch_bounds__(256, 1) stem_fwd_kernel(const fg_conv_problem 
     for (int k = 0; k < nsteps; ++k) {
         if (k + 1 < nsteps) store(k + 1);
         load(k + 2);
-        if (k >= 6) compute_row(k);
+        if (k >= 6) {
+            compute_row(k);
+            if (kh) {
+                float* rb_ = red + ((k & 1) * 4 + (wave & 3)) * 64 * 16 + lane * 4;
+#pragma unroll
+                for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+                    for (int pt = 0; pt < 2; ++pt) *reinterpret_cast<f32x4*>(rb_ + (nt * 2 + pt) * 256) = acc[nt][pt];
+            }
+        }
         __syncthreads();
+        if (k >= 6 && !kh) finish_row(k);
     }
 }
 
@@ -399,7 +420,7 @@ int launch_fwd_stem(const fg_conv_problem& p, hipStream_t stream, int* rc) {
     const int rows = stem_fwd_rows(p);
     if (!rows) return 0;
     const int grid = p.m_img * (p.m_b / ST_PX) * (p.m_a / rows);
-    hipLaunchKernelGGL(stem_fwd_kernel, dim3(grid), dim3(256), 0, stream, p, rows);
+    hipLaunchKernelGGL(stem_fwd_kernel, dim3(grid), dim3(512), 0, stream, p, rows);
     *rc = fg::launched("stem_fwd");
     return 1;
 }

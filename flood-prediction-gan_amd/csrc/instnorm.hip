@@ -187,6 +187,32 @@ __device__ __forceinline__ void store_presplit(float* p, const f32x4& o, float s
     *reinterpret_cast<i32x4*>(p) = out;
 }
 
+// fg_split_pixels-layout store (the window convs' operand, conv_win.hip) of this lane's 4 channels o (scaled by s):
+// per pixel [h(C) | l(C)] in 16-B chunks, chunk k stored at k ^ swz_pixel(x) for the pixel's padded column x;
+// lanes 2q, 2q+1 hold channels 8q..8q+7 of the pixel at byte base px: after the same 8-byte swap as
+// store_presplit the even lane stores h of group q (chunk q), the odd lane l (chunk C/8 + q)
+template <int C>
+__device__ __forceinline__ void store_splitpix(char* px, const f32x4& o, float s, int c4, int x) {
+    f16x4 h, l;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const float v = o[e] * s;
+        h[e] = (_Float16)v;
+        l[e] = (_Float16)(v - (float)h[e]);
+    }
+    const int odd = c4 & 1, q = c4 >> 1;
+    typedef int i32x2 __attribute__((ext_vector_type(2)));
+    const i32x2 hv = __builtin_bit_cast(i32x2, h), lv = __builtin_bit_cast(i32x2, l);
+    const i32x2 send = odd ? hv : lv;
+    i32x2 recv;
+    recv[0] = __builtin_amdgcn_update_dpp(0, send[0], 0xB1, 0xF, 0xF, false);
+    recv[1] = __builtin_amdgcn_update_dpp(0, send[1], 0xB1, 0xF, 0xF, false);
+    typedef int i32x4 __attribute__((ext_vector_type(4)));
+    const i32x4 out = odd ? i32x4{recv[0], recv[1], lv[0], lv[1]} : i32x4{hv[0], hv[1], recv[0], recv[1]};
+    const int k = odd ? C / 8 + q : q;
+    *reinterpret_cast<i32x4*>(px + ((k ^ fgc::swz_pixel<C>(x)) << 4)) = out;
+}
+
 // Row form of the apply pass (channel quads dividing the block: C/4 | 256): block = one padded output
 // row (n, yp), thread = (pixel lane gi, channel quad c4); mean / rstd read once per thread, U pixels'
 // loads issued before any of them is used (the grid-stride form above re-derived (n, y, x, c) with
@@ -198,7 +224,7 @@ __global__ void __launch_bounds__(NT) in_apply_rows_kernel(fg_view src, const fl
                                                            fg_view dst, int pad_mode, int lshift,
                                                            unsigned* __restrict__ amax, float* __restrict__ split_slot,
                                                            float* __restrict__ ps_ptr, float* __restrict__ ps_slot,
-                                                           const float* __restrict__ res_amax) {
+                                                           const float* __restrict__ res_amax, int splitpix) {
     const int L = 1 << lshift, PG = NT >> lshift;
     const int C = dst.c_alloc, h = dst.h, w = dst.w, pad = dst.pad;
     const int hp = h + 2 * pad, wp = w + 2 * pad;
@@ -261,7 +287,11 @@ __global__ void __launch_bounds__(NT) in_apply_rows_kernel(fg_view src, const fl
                     for (int e = 0; e < 4; ++e) o[e] = fg::act_fwd(o[e], act);
                     o += rv[k];
                 }
-                if (split_slot) {
+                if (split_slot && splitpix) {
+                    char* pxb = reinterpret_cast<char*>(drow - 4 * c4 + (size_t)xp * C);
+                    if (C == 64) store_splitpix<64>(pxb, o, ss, c4, xp);
+                    else store_splitpix<32>(pxb, o, ss, c4, xp);
+                } else if (split_slot) {
                     store_presplit(drow + (size_t)xp * C, o, ss, c4 & 1);
                 } else {
                     am = max(am, absbits4(o));
@@ -938,7 +968,7 @@ FG_API int fg_in_stats(fg_view src, float eps, float* mean, float* rstd, double*
 namespace {
 int in_apply_impl(fg_view src, const float* mean, const float* rstd, int act, fg_view residual, fg_view dst,
                   int pad_mode, float* absmax, float* split_slot, hipStream_t stream, float* ps_ptr = nullptr,
-                  float* ps_slot = nullptr, const float* res_amax = nullptr);
+                  float* ps_slot = nullptr, const float* res_amax = nullptr, int splitpix = 0);
 int in_bwd_impl(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, const float* mean, const float* rstd, int act,
                 fg_view dst, float* bias_grad, int bias_accumulate, fg_view gsum, double* work, float* absmax,
                 float* split_slot, hipStream_t stream);
@@ -969,10 +999,19 @@ FG_API int fg_in_apply_presplit(fg_view src, const float* mean, const float* rst
                          stream);
 }
 
+FG_API int fg_in_apply_splitpix(fg_view src, const float* mean, const float* rstd, int act, fg_view dst, int pad_mode,
+                                 float* scale_slot, hipStream_t stream) {
+    if (!scale_slot || (dst.c_alloc != 32 && dst.c_alloc != 64) || ((uintptr_t)dst.ptr & 31))
+        return fg::fail(FG_ERR_INVALID, "fg_in_apply_splitpix: needs a zeroed scale slot, C 32 or 64, a 32-B aligned dst "
+                                        "(C=%d)", dst.c_alloc);
+    return in_apply_impl(src, mean, rstd, act, fg_view{nullptr, 0, 0, 0, 0, 0}, dst, pad_mode, nullptr, scale_slot,
+                         stream, nullptr, nullptr, nullptr, 1);
+}
+
 namespace {
 int in_apply_impl(fg_view src, const float* mean, const float* rstd, int act, fg_view residual, fg_view dst,
                   int pad_mode, float* absmax, float* split_slot, hipStream_t stream, float* ps_ptr, float* ps_slot,
-                  const float* res_amax) {
+                  const float* res_amax, int splitpix) {
     if (!ok_view(src) || !ok_view(dst) || !mean || !rstd || src.c_alloc % 4 || dst.c_alloc != src.c_alloc ||
         dst.h != src.h || dst.w != src.w || dst.n != src.n)
         return fg::fail(FG_ERR_INVALID, "fg_in_apply: bad args");
@@ -984,7 +1023,7 @@ int in_apply_impl(fg_view src, const float* mean, const float* rstd, int act, fg
     if ((g_in_rows || split_slot || ps_ptr) && NT % C4 == 0) {
         hipLaunchKernelGGL(in_apply_rows_kernel, dim3(dst.n * (dst.h + 2 * dst.pad)), dim3(NT), 0, stream, src, mean,
                            rstd, act, residual, dst, pad_mode, ilog2(C4), reinterpret_cast<unsigned*>(absmax),
-                           split_slot, ps_ptr, ps_slot, res_amax);
+                           split_slot, ps_ptr, ps_slot, res_amax, splitpix);
         return fg::launched("in_apply_rows");
     }
     const long long total = (long long)dst.n * (dst.h + 2 * dst.pad) * (dst.w + 2 * dst.pad) * (dst.c_alloc / 4);

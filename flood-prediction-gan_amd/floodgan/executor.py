@@ -140,7 +140,7 @@ def _convT_fwd(P, name, X, Y):
     return ops.conv(PL.phase_problems(X, w.shape, 3, 1, Y, wps, maps, bias=P[name + ".bias"]), in_stats=True)
 
 
-def _norm(c, act, pad, mode, residual=None, stats=None, presplit=False, ps_copy=False):
+def _norm(c, act, pad, mode, residual=None, stats=None, presplit=False, ps_copy=False, splitpix=False):
     """InstanceNorm + activation of conv output c; stats = (mean, rstd) from the conv's epilogue, or
     computed here.  presplit: the output is written in the FG_PRESPLIT format (read only by convs).  ps_copy: also a
     FG_PRESPLIT copy of the fp32 output (returned as a 4th value, None when the f16x3 pre-split path is off)"""
@@ -150,8 +150,13 @@ def _norm(c, act, pad, mode, residual=None, stats=None, presplit=False, ps_copy=
           if ps_copy and ops.presplit_on() and ops.PRESPLIT_RESID else None)
     if ps is not None and not ops.presplit_fits(ps):
         ps = None                  # beyond what the pre-split consumers take (ops.PRESPLIT_MAX_BYTES)
-    ops.in_apply(c, mean, rstd, act, residual, out, mode, presplit=presplit, ps_copy=ps)
+    ops.in_apply(c, mean, rstd, act, residual, out, mode, presplit=presplit, ps_copy=ps, splitpix=splitpix)
     return (mean, rstd, out, ps) if ps_copy else (mean, rstd, out)
+
+
+# the content head's input written in the window kernels' split layout by its norm pass (FLOODGAN_SPLITPIX=0: fp32 +
+# a fg_split_pixels pass, A/B)
+SPLITPIX = os.environ.get("FLOODGAN_SPLITPIX", "1") != "0"
 
 
 def has_attention(P):
@@ -206,7 +211,11 @@ def gen_forward(P, x, save=True, x_extra=None):
         md1, rd1, ad1 = _norm(d1, FG_ACT_RELU, 1, FG_PAD_ZERO, stats=st, presplit=ps)
         d2 = Buf.empty(N, H, W, 64, 0, dev)
         st = _convT_fwd(P, f"deconv2_{tag}", ad1, d2)
-        md2, rd2, ad2 = _norm(d2, FG_ACT_RELU, pad2, mode2, stats=st)
+        # the content head's ad2 is read only by the window conv and its weight gradient: written in their split
+        # layout directly (no fp32 copy, no fg_split_pixels pass)
+        # (when the window kernels take the head: output rows of >= 256 px, a multiple of 32; ops.win_eligible)
+        spx = tag == "content" and ps and SPLITPIX and ops.USE_WIN and W >= 256 and W % 32 == 0
+        md2, rd2, ad2 = _norm(d2, FG_ACT_RELU, pad2, mode2, stats=st, splitpix=spx)
         heads[tag] = dict(d1=d1, md1=md1, rd1=rd1, ad1=ad1, d2=d2, md2=md2, rd2=rd2, ad2=ad2)
     cl = Buf.empty(N, H, W, CONTENT_ALLOC, 0, dev)
     _conv_fwd(P, "deconv3_content", heads["content"]["ad2"], 3, 7, 1, cl)
@@ -481,7 +490,7 @@ def _decided(B, lo=0, hi=None, pre=None, mean=None):
     LeakyReLU): NCHW bool on the host.  A pre-split output (FG_PRESPLIT) is decided from the norm's input
     `pre` and `mean` instead: act((c - mean) * rstd) > 0 <=> c > mean (rstd > 0; fp32 subtraction keeps the
     sign)."""
-    if ops.is_presplit(B):
+    if ops.is_presplit(B) or ops.is_splitpix(B):
         d = pre.interior() > mean.view(pre.n, 1, 1, pre.c)
         return d[lo:hi].permute(0, 3, 1, 2).contiguous().cpu()
     return (B.interior()[lo:hi] > 0).permute(0, 3, 1, 2).contiguous().cpu()
@@ -496,7 +505,7 @@ def gen_act_decisions(S):
         out[f"block{i}"] = _decided(b["rb"], pre=b["cb1"], mean=b["mb1"])
     for tag, hd in S["heads"].items():
         out[f"deconv1_{tag}"] = _decided(hd["ad1"], pre=hd["d1"], mean=hd["md1"])
-        out[f"deconv2_{tag}"] = _decided(hd["ad2"])
+        out[f"deconv2_{tag}"] = _decided(hd["ad2"], pre=hd["d2"], mean=hd["md2"])
     return out
 
 

@@ -101,6 +101,8 @@ def _wrote(*objs):
                 t._fg_split = None
             if getattr(t, "_fg_presplit", False):
                 t._fg_presplit = False
+            if getattr(t, "_fg_splitpix", False):
+                t._fg_splitpix = False
 
 
 # Pre-split operands (FG_PRESPLIT, include/floodgan.h): the norm passes that feed a resblock conv write its
@@ -135,6 +137,16 @@ def is_presplit(obj):
         return False
     if getattr(t, "_fg_presplit_ver", None) != t._version:
         raise RuntimeError("a pre-split (FG_PRESPLIT) buffer was written by torch since its producer ran")
+    return True
+
+
+def is_splitpix(obj):
+    """the buffer holds the fg_split_pixels layout written by its producer (in_apply(splitpix=True)), not fp32"""
+    t = _tensor(obj)
+    if not getattr(t, "_fg_splitpix", False):
+        return False
+    if getattr(t, "_fg_splitpix_ver", None) != t._version:
+        raise RuntimeError("a split-pixels buffer was written by torch since its producer ran")
     return True
 
 
@@ -188,6 +200,8 @@ def absmax(t):
     tensor or of a Buf (border and padding channels included: everything a gather can read);
     cached on the tensor until an op writes it."""
     t = _tensor(t)
+    if getattr(t, "_fg_splitpix", False) and getattr(t, "_fg_splitpix_ver", None) == t._version:
+        raise RuntimeError("absmax of a split-pixels buffer (it holds fp16 pieces, read only by the window kernels)")
     if getattr(t, "_fg_presplit", False) and getattr(t, "_fg_presplit_ver", None) == t._version:
         # the producer's scale slot is the only valid scale source of a pre-split buffer
         if getattr(t, "_fg_amax", None) is None or getattr(t, "_fg_amax_ver", None) != t._version:
@@ -448,6 +462,8 @@ def split_pixels(X):
     t = X.t
     if is_presplit(X):
         raise RuntimeError("split_pixels of a pre-split buffer")
+    if is_splitpix(X):
+        return t._fg_split              # the producer wrote the split layout itself (in_apply(splitpix=True))
     cached = getattr(t, "_fg_split", None)
     if cached is not None and getattr(t, "_fg_split_ver", None) == t._version:
         if CHECK_SCALES:
@@ -702,9 +718,21 @@ def in_stats(src):
     return mean, rstd
 
 
-def in_apply(src, mean, rstd, act, residual, dst, pad_mode, presplit=False, ps_copy=None):
+def in_apply(src, mean, rstd, act, residual, dst, pad_mode, presplit=False, ps_copy=None, splitpix=False):
     """presplit: dst is written in the FG_PRESPLIT format (no residual; the f16x3 math).  ps_copy (Buf of dst's
-    geometry): dst in fp32 AND a FG_PRESPLIT copy there (fg_in_apply_dual)"""
+    geometry): dst in fp32 AND a FG_PRESPLIT copy there (fg_in_apply_dual).  splitpix: dst (C 32 / 64) is written
+    in the fg_split_pixels layout the window kernels read (split_pixels(dst) then returns it; no fp32 values)"""
+    if splitpix:
+        assert residual is None and not presplit and ps_copy is None and L.fwd_f16x3() and L.wgrad_f16x3()
+        slot = _amax_out(dst)
+        L.check(_lib().fg_in_apply_splitpix(view(src), L.ptr(mean), L.ptr(rstd), act, view(dst), pad_mode,
+                                            L.ptr(slot), L.stream_handle()), "in_apply_splitpix")
+        t = _tensor(dst)
+        split = t.view(torch.float16)
+        split.absmax = slot
+        t._fg_split, t._fg_split_ver = split, t._version
+        t._fg_splitpix, t._fg_splitpix_ver = True, t._version
+        return
     presplit = presplit and presplit_fits(dst)
     if ps_copy is not None:
         assert presplit_fits(ps_copy), "pre-split copy beyond PRESPLIT_MAX_BYTES (the caller checks presplit_fits)"

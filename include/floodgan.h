@@ -372,6 +372,12 @@ int fg_in_bwd(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, const float
  * x_absmax.  Saves the consumer's on-the-fly split (a resblock's conv1 -> conv2 hop). */
 int fg_in_apply_presplit(fg_view src, const float* mean, const float* rstd, int act, fg_view dst, int pad_mode,
                          float* scale_slot, hipStream_t stream);
+/* The same pass writing dst (C = 32 or 64) in the fg_split_pixels layout -- per pixel the fp16 pieces [h(C) | l(C)]
+ * of the scaled values, 16-B chunk k at k ^ swizzle(padded column) -- the operand of fg_conv_win / fg_conv_wgrad_win
+ * (no fp32 copy and no separate fg_split_pixels pass): the content head's input relu(IN(deconv2_content)),
+ * models/model_architectures.py:351-353.  Scale bound and slot as fg_in_apply_presplit. */
+int fg_in_apply_splitpix(fg_view src, const float* mean, const float* rstd, int act, fg_view dst, int pad_mode,
+                         float* scale_slot, hipStream_t stream);
 
 /* fg_in_apply writing dst in fp32 (absmax raised as there) AND a FG_PRESPLIT copy into ps_dst (same geometry, 32-B
  * aligned) at the scale of the bound sqrt(HW - 1) + max|residual| (residual_absmax: the residual's absmax slot,
