@@ -549,6 +549,9 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
     // wait for stage `done`'s own DMAs: the VMEM operations younger than them are the stages issued after it
     // and, when stage `done` was issued before the last epilogue, that epilogue's NST stores (vmcnt counts
     // loads, LDS-DMA and stores together, in issue order).  Any smaller count is safe (it waits for more).
+    // NST is the trip count of the epilogue's store loop (tm < TM, reg < 4, tn < TN: one raw_buffer_store_b32
+    // each, never predicated off); tests/test_isa_cpu.py checks every instantiation's code object issues exactly
+    // that many single-dword buffer stores and no merged wider ones.
     constexpr int D = A_GL + B_GL, NST = TM * 4 * TN;
     constexpr int W1 = D < 63 ? D : 63, WS = NST < 63 ? NST : 63, WSD = NST + D < 63 ? NST + D : 63;
     auto wait_stage = [&]() {
@@ -731,11 +734,15 @@ int g_f3_ps_wide = 5;  // fg_set_f3_ps_wide: the N > 128 tile of pre-split opera
                        // 0.371 -> 0.348 ms, profiles/round3/r3v_f3_presplit_cfg.log.  4 waves of 128 x 128 with the
                        // accumulators in AGPRs ran 3.26 ms: not kept)
 
-// Narrow-N wave tiles (A/B, FLOODGAN_F3_NARROW=1): the 32 x 64 / 32 x 128 wave tiles of cfg 7 / 6 read 512 / 427 B of
-// LDS fragments per MFMA -- at the LDS port's 128 B per clock that is at or beyond what the four SIMDs' MFMAs consume
-// -- where 64 x 64 wave tiles read 341 (the resblock's 64 x 128: 256): cfg 10 = 512 x 64 as 8 waves of 64 x 64,
-// cfg 11 = 256 x 128 as 4 x 2 waves of 64 x 64
-static bool narrow_on() { const char* e = getenv("FLOODGAN_F3_NARROW"); return e && atoi(e) != 0; }
+// Narrow-N wave tiles: the 32 x 64 / 32 x 128 wave tiles of cfg 7 / 6 read 512 / 427 B of LDS fragments per MFMA --
+// at the LDS port's 128 B per clock that is at or beyond what the four SIMDs' MFMAs consume -- where 64 x 64 wave
+// tiles read 341 (the resblock's 64 x 128: 256): cfg 10 = 512 x 64 as 8 waves of 64 x 64, cfg 11 = 256 x 128 as
+// 4 x 2 waves of 64 x 64.  Taken whenever the launch still fills half the CUs on them: the step 46.16 -> 46.02 ms
+// (interleaved A/B, profiles/round4/r4e_ab_f3_narrow.log); FLOODGAN_F3_NARROW=0 keeps cfg 7 / 6
+static bool narrow_on() {
+    static const bool on = [] { const char* e = getenv("FLOODGAN_F3_NARROW"); return !e || atoi(e) != 0; }();
+    return on;
+}
 
 int auto_cfg(const fg_conv_problem* p, int nprob, int max_n) {
     int cfg = f3_config(max_n);

@@ -1277,7 +1277,8 @@ int launch_wgrad(const fg_wgrad_problem& p, bool vx, bool vp, hipStream_t stream
 }
 
 int g_fwd_tile = -1;   // tuning hook (fg_set_fwd_tile): force one bf16x6 forward tile config
-// A/B (FLOODGAN_STEM_FWD=0: the register-staged x6 kernel): the stem forward on its strip kernel
+// the stem forward on its strip kernel (step 46.31 -> 46.16 ms, profiles/round4/r4e_ab_stem_fwd.log); read per call
+// so that scripts/bench_stem_wgrad.py can interleave it with the register-staged x6 kernel (FLOODGAN_STEM_FWD=0)
 static bool stem_fwd_on() { const char* e = getenv("FLOODGAN_STEM_FWD"); return !e || atoi(e) != 0; }
 
 // split-math forward tile configs {BM, BN, wave tile, waves/SIMD, prefetch distance, LDS swizzle}

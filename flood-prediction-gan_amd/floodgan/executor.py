@@ -154,8 +154,8 @@ def _norm(c, act, pad, mode, residual=None, stats=None, presplit=False, ps_copy=
     return (mean, rstd, out, ps) if ps_copy else (mean, rstd, out)
 
 
-# the content head's input written in the window kernels' split layout by its norm pass (FLOODGAN_SPLITPIX=0: fp32 +
-# a fg_split_pixels pass, A/B)
+# the content head's input written in the window kernels' split layout by its norm pass (step 46.39 -> 46.19 ms,
+# profiles/round4/r4e_ab_splitpix.log; FLOODGAN_SPLITPIX=0: fp32 + a fg_split_pixels pass)
 SPLITPIX = os.environ.get("FLOODGAN_SPLITPIX", "1") != "0"
 
 

@@ -123,7 +123,11 @@ def presplit_on():
 # Only the pipelined kernels read FG_PRESPLIT operands, and they address their outputs with 31-bit byte offsets
 # (conv_f3.hip f3_takes): a consumer of a larger operand would produce an output the kernel declines.  Producers
 # therefore write a buffer beyond this size in fp32 (every kernel reads that) -- at bs 8, 512^2 the largest
-# pre-split buffer (64 channels at 512^2) is 0.55 GB.
+# pre-split buffer (64 channels at 512^2) is 0.55 GB.  The other geometry the pipelined kernels need (packed row
+# run jp % 32 == 0, channel groups of 8, more than 32 output channels -- conv_f3.hip f3_takes / presplit_ok) holds
+# at every producer call site for any batch size and resolution: each pre-split buffer has 64..512 channels and
+# feeds only 3x3 / 4x4 convs and weight gradients with 64..512 outputs.  A consumer that still declines a pre-split
+# operand fails with FG_ERR_INVALID (it never reads it as fp32).
 PRESPLIT_MAX_BYTES = (1 << 31) - (1 << 24)
 
 

@@ -207,6 +207,47 @@ def test_conv_f3_tiles(case, cfg, persistent, sched, order):
         L.set_conv_math(prev)
 
 
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11])
+@pytest.mark.parametrize("case", [(32, 128, 1, 1, 0, "constant", 40),    # K = 32: one k chunk per tile (nkt < NS)
+                                  (64, 64, 1, 1, 0, "constant", 37),     # K = 64: two chunks, ragged M
+                                  (32, 256, 3, 1, 1, "reflect", 24)])    # K = 288: several chunks per tile
+def test_conv_f3_persistent_bit_exact(case, cfg):
+    """the tile-crossing stream of the persistent conv_f3 kernel (a few workgroups each walk many tiles: the next
+    tile's stages are issued over the previous tile's epilogue stores, and wait_stage counts those NST stores into
+    its vmcnt) gives output bit-identical to one workgroup per tile -- short-K convs (one k chunk per tile, fewer
+    than the ring depth) are where a too-loose stage wait would read a stage before its DMA landed"""
+    from floodgan import _lib as L, ops, plans as PL
+    from floodgan.plans import Buf
+    cin, cout, k, s, p, mode, H = case
+    prev = L.get_conv_math()
+    L.set_conv_math("f16x3")
+    try:
+        L.set_f3_tile(cfg)
+        torch.manual_seed(17)
+        x = torch.randn(3, cin, H, H, dtype=torch.float64)
+        w = torch.randn(cout, cin, k, k, dtype=torch.float64) * 0.1
+        X = buf_from(x, p, mode)
+        wd = w.float().to(DEV)
+        m = PL.wmap_conv_fwd(wd.shape, X.c)
+        Ho = PL.out_size(H, k, s, p)
+        out = {}
+        for persistent in (0, 2, 3, 7):
+            L.load().fg_set_f3_persistent(persistent)
+            Y = Buf.empty(3, Ho, Ho, cout, 0, DEV)
+            Y.t.fill_(float("nan"))
+            ops.conv([PL.conv_problem(X, p, k, s, ops.pack_weight(wd, m), m, Y, bias=torch.ones(cout, device=DEV))])
+            assert ops.LAST_CONV_KERNEL == "conv_fwd_f3", ops.LAST_CONV_KERNEL
+            out[persistent] = Y.t.clone()
+        torch.cuda.synchronize()
+        assert not torch.isnan(out[0]).any()
+        for persistent in (2, 3, 7):
+            assert torch.equal(out[persistent], out[0]), persistent
+    finally:
+        L.set_f3_tile(-1)
+        L.load().fg_set_f3_persistent(1)
+        L.set_conv_math(prev)
+
+
 @pytest.mark.parametrize("on", [0, 1, 2, 3])
 @pytest.mark.parametrize("case", [(256, 256, 3, 1, 1, "reflect", 40), (128, 256, 4, 2, 1, "constant", 34),
                                   (256, 512, 4, 1, 1, "constant", 17), (64, 128, 3, 2, 1, "constant", 36),
