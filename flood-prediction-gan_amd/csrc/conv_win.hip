@@ -62,10 +62,16 @@ struct WinArgs {
 // One kernel row per barrier pair: the whole row's weights (KW taps, [s][pc][NR][C]) and its input strip sit in LDS
 // together (68.6 + 57.3 KB at C 64); the next row's strip and weights are loaded into registers (16-B buffer loads)
 // while the KW taps of the current row run, and written over the current ones after a barrier.
-template <int C, int KW, int TN, int NW>
+//
+// BM = 512 (C = 32, the input gradient): 64-row waves over all 64 output columns, 8 A + 8 B fragments per 48 MFMAs
+// (341 LDS bytes per MFMA instead of 512); the 32-channel strip of 524 pixels (67 KB) and the row's weights (57 KB)
+// still fit in LDS.  Needs output rows of >= BM pixels (a tile spans at most two row segments): 1141 -> 1071 us at
+// bs 8 (profiles/round4/r4j_bench_win.log).  The forward's analogue (64-row waves paired over the two 32-channel
+// halves, 683 -> 512 LDS bytes per MFMA) ran 1.5 % slower and was dropped.
+template <int C, int KW, int TN, int NW, int BM = 256>
 __global__ void __launch_bounds__(NW * 64, 1) conv_win_kernel(const WinArgs args) {
     constexpr int NT = NW * 64;
-    constexpr int BM = 256, WM = BM / NW, TM = WM / 16;
+    constexpr int WM = BM / NW, TM = WM / 16;
     constexpr int PB = 4 * C;                                   // strip bytes per pixel (h | l)
     constexpr int NR = TN * 16;                                 // weight rows staged
     constexpr int STRIP_BYTES = (BM + 2 * (KW - 1)) * PB;
@@ -230,6 +236,16 @@ __global__ void __launch_bounds__(NW * 64, 1) conv_win_kernel(const WinArgs args
 // rows ran 1.31 ms on both geometries, profiles/round4/r4c_ab_win.log)
 template <int C, int KW, int TN>
 int launch_win(const WinArgs& a, int tiles, hipStream_t stream) {
+    if constexpr (C == 32) {
+        const char* e = getenv("FLOODGAN_WIN_BM");      // A/B: 256 = 32-row waves
+        if (a.P.m_b >= 512 && !(e && atoi(e) == 256)) {
+            WinArgs b = a;
+            b.tiles_per_img = (a.P.m_a * a.P.m_b + 511) / 512;
+            hipLaunchKernelGGL((conv_win_kernel<C, KW, TN, 8, 512>), dim3(b.tiles_per_img * a.P.m_img), dim3(512), 0,
+                               stream, b);
+            return fg::launched("conv_win");
+        }
+    }
     hipLaunchKernelGGL((conv_win_kernel<C, KW, TN, 8>), dim3(tiles), dim3(512), 0, stream, a);
     return fg::launched("conv_win");
 }

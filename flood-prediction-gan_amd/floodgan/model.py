@@ -45,7 +45,8 @@ class PairedStep:
         self.last_mask = None
         self.last_output = None
         # test instrumentation: when True, each call stores the activation decisions of its three
-        # networks' passes in self.decisions ({"G": [...], "D": [fake, real, G-step]}, oracle order)
+        # networks' passes in self.decisions ({"G": [...], "D": [fake, real, G-step]}, oracle order) and the
+        # L1 term's sign decisions ({"L1": [{"l1": sign(fake - y)}]})
         self.record_decisions = False
         self.decisions = None
 
@@ -85,6 +86,7 @@ class PairedStep:
                         input_grad_accumulate=True)
         if rec is not None:
             rec["D"].append(X.disc_act_decisions(dS))
+            rec["L1"] = [{"l1": torch.sign(fake.detach() - y)}]   # the L1 term's sign decisions (-1 / 0 / +1)
             self.decisions = rec
         del dS, dinp
         self.gflat.begin(self.group)

@@ -144,6 +144,25 @@ def _act(h, slope, name, forced):
     return torch.where(m, h, h * slope)
 
 
+def _l1(fake, y, decisions):
+    """F.l1_loss(fake, y) (models/model.py:643); with decisions holding an "L1" entry (tests only) each element's
+    gradient sign is the implementation's, sign(fake - y) in {-1, 0, +1} (0 where its fp32 fake equals y exactly, as
+    torch's own l1 backward gives): an element within rounding of fake == y can be decided differently by two
+    evaluations, and one flip moves the G output gradient by ~2 / sqrt(elements) of its norm.  Disagreements are
+    logged like the activation kinks (|fake - y| / rms)."""
+    t = decisions.take("L1") if decisions is not None else None
+    if t is None:
+        return F.l1_loss(fake, y)
+    (masks, net), d = t, fake - y
+    s = masks["l1"].to(d.device, d.dtype).contiguous()
+    dd = d.detach()
+    dis = torch.sign(dd) != s
+    n = int(dis.sum())
+    rms = float(dd.pow(2).mean().sqrt()) or 1.0
+    decisions.log.append((net, "l1", n, float(dd[dis].abs().max()) / rms if n else 0.0))
+    return (s * d).mean()
+
+
 def _forced(decisions, net):
     """(masks, net, log) for the next call of `net`, or None"""
     if decisions is None:
@@ -279,7 +298,7 @@ class PairedStepOracle:
         self.opt_g.zero_grad()
         pred = discriminator_forward(self.D, cat_fake, _forced(decisions, "D"))
         l_g = F.mse_loss(pred, torch.ones_like(pred))
-        l1 = F.l1_loss(fake, y)
+        l1 = _l1(fake, y, decisions)
         (l_g + l1 * 100).backward()
         if record is not None:
             record["g_grads"] = OrderedDict((k, v.grad.detach().clone()) for k, v in self.G.items())

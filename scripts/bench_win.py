@@ -35,10 +35,18 @@ def main():
     dgr = PL.conv_problem(gcl, 6, 7, 1, ops.pack_weight(w, md), md, Y)
     for name, prob, out, flops in (("content fwd 7x7 64->27 @512", fwd, cl, 2.0 * N * 512 * 512 * 27 * 64 * 49),
                                    ("content dgrad 7x7 27->64 @518", dgr, Y, 2.0 * N * 518 * 518 * 64 * 27 * 49)):
-        for _ in range(3):
-            out.t.zero_()
-            ms = min(time_it(lambda: ops.conv_win(prob)) for _ in range(3))
-            print(f"{name:32s} {ms * 1e3:8.1f} us {flops / ms / 1e9:7.1f} TFLOP/s", flush=True)
+        ref = None
+        for _ in range(2):
+            for bm in ("512", "256"):      # the input gradient's tile rows (FLOODGAN_WIN_BM; the forward: 256)
+                os.environ["FLOODGAN_WIN_BM"] = bm
+                out.t.zero_()
+                ms = min(time_it(lambda: ops.conv_win(prob)) for _ in range(3))
+                if ref is None:
+                    ref = out.t.clone()
+                d = float((out.t - ref).norm() / ref.norm())
+                print(f"{name:32s} bm={bm} {ms * 1e3:8.1f} us {flops / ms / 1e9:7.1f} TFLOP/s  rel diff {d:.1e}",
+                      flush=True)
+        os.environ.pop("FLOODGAN_WIN_BM")
 
 
 if __name__ == "__main__":

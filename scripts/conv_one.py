@@ -1,6 +1,6 @@
 """Run one conv-engine launch shape repeatedly (for rocprofv3 counter passes).
-  python scripts/conv_one.py [fwd|fwd_stats|fwd_stats_ps|wgrad|dgrad_ps|wgrad_ps] [reps]
-  -- resblock 3x3 256->256 @128, bs 8
+  python scripts/conv_one.py [fwd|fwd_stats|fwd_stats_ps|wgrad|dgrad_ps|wgrad_ps|stem_fwd|stem_wgrad] [reps]
+  -- resblock 3x3 256->256 @128, bs 8 (stem_*: the generator stem 7x7 9->64 @512, bs 8, on its strip kernels)
   (fwd_stats: with the InstanceNorm statistics epilogue, as the step's conv1 runs; fwd_stats_ps: on a FG_PRESPLIT
   operand written by the norm pass, as the step's conv2 runs; dgrad_ps: the input-gradient interior launch of
   executor._dgrad_s1_padded over a pre-split conv-output gradient with its zero border 2; wgrad_ps: the step's
@@ -17,11 +17,41 @@ from floodgan import _lib as L, ops, plans as PL  # noqa: E402
 from floodgan.plans import Buf  # noqa: E402
 
 
+def stem(kind, dev):
+    """the stem launch as the step runs it: the packed input (reflect border 3), forward with the statistics
+    epilogue, or the weight gradient against a 64-channel conv-output gradient"""
+    from floodgan._lib import FG_PAD_REFLECT
+    L.set_conv_math("f16x3")
+    N, H = 8, 512
+    x = torch.rand(N, 9, H, H, device=dev) * 2 - 1
+    X0 = Buf.empty(N, H, H, 9, 3, dev)
+    ops.pack_input(x, 9, None, 0, X0, 0, N, FG_PAD_REFLECT)
+    if kind == "stem_wgrad":
+        gy = Buf.empty(N, H, H, 64, 0, dev)
+        gy.t.normal_()
+        prob = PL.wgrad_conv(gy, X0, 3, 7, 1, 64)
+        dw = torch.empty(64, 9, 7, 7, device=dev)
+        wm = PL.wmap_wgrad(dw.shape, True, 9, 7)
+        return lambda: ops.wgrad(prob, wm, dw)
+    w = torch.randn(64, 9, 7, 7, device=dev) * 0.05
+    m = PL.wmap_conv_fwd(w.shape, 9)
+    Y = Buf.empty(N, H, H, 64, 0, dev)
+    prob = PL.conv_problem(X0, 3, 7, 1, ops.pack_weight(w, m), m, Y, bias=torch.zeros(64, device=dev))
+    return lambda: ops.conv([prob], in_stats=True)
+
+
 def main():
     kind = sys.argv[1] if len(sys.argv) > 1 else "fwd"
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
     L.load()
     dev = "cuda"
+    if kind.startswith("stem_"):
+        fn = stem(kind, dev)
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        print("done", kind, reps)
+        return
     N, H, C, k = 8, 128, 256, 3
     X = Buf.empty(N, H, H, C, 1, dev)
     X.t.uniform_(-1, 1)

@@ -1,0 +1,21 @@
+#!/bin/bash
+# Counter passes for the kernels bench.py's roofline names (the three resblock conv kinds) and the stem strip
+# kernels, each summarised into profiles/<round>/<tag>_pmc_*.json; stops at the first failing pass.
+#   scripts/gpu_pmc_all.sh r4 round4 ["fwd_stats_ps dgrad_ps wgrad_ps stem_wgrad stem_fwd"]
+cd "$(dirname "$0")/.." || exit 1
+TAG=${1:-r4}; RD=${2:-round4}; KINDS=${3:-"fwd_stats_ps dgrad_ps wgrad_ps stem_wgrad stem_fwd"}
+mkdir -p "profiles/$RD"
+for k in $KINDS; do
+  case $k in
+    fwd_stats_ps) key=conv_fwd_f3; ktag="conv_fwd_f3_kernel<256,256,...,STATS>"; name=resblock_fwd_stats_ps;;
+    dgrad_ps) key=conv_fwd_f3; ktag="conv_fwd_f3_kernel<256,256,...> (input-gradient interior)"; name=resblock_dgrad_ps;;
+    wgrad_ps) key=conv_wgrad_f3; ktag="conv_wgrad_f3_kernel<256,0,3>"; name=resblock_wgrad_ps;;
+    stem_wgrad) key=stem_wgrad_kernel; ktag="stem_wgrad_kernel"; name=stem_wgrad;;
+    stem_fwd) key=stem_fwd_kernel; ktag="stem_fwd_kernel"; name=stem_fwd;;
+    *) echo "unknown kind $k"; exit 1;;
+  esac
+  KIND=$k scripts/gpu_pmc.sh "${TAG}_$k" || { echo "pmc $k failed"; exit 1; }
+  python scripts/pmc_summary.py "gpurun_out/pmc_${TAG}_$k" "$key" "$ktag" "$k" > "profiles/$RD/${TAG}_pmc_$name.json" \
+    || { echo "summary $k failed"; exit 1; }
+  cat "profiles/$RD/${TAG}_pmc_$name.json"
+done

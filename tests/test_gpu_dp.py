@@ -146,7 +146,7 @@ def test_two_rank_paired_f16x3_vs_fp64(tmp_path, report):
         assert torch.equal(v, ranks[1]["state"][k]), k              # replicas stay identical
     merged = {net: [{k: torch.cat((a[k], b[k]), 0) for k in a} for a, b in zip(ranks[0]["decisions"][net],
                                                                              ranks[1]["decisions"][net])]
-              for net in ("G", "D")}
+              for net in ("G", "D", "L1") if net in ranks[0]["decisions"]}
     dec = O.ActDecisions(merged)
     x, y = W.global_batch("paired", n, res)
     st = O.PairedStepOracle(dtype=torch.float64)

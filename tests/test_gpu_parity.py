@@ -390,13 +390,17 @@ def test_stem_fwd_strips(H, N):
         L.set_conv_math(prev)
 
 
-@pytest.mark.parametrize("case", ["content_fwd", "content_dgrad"])
-def test_conv_window(case):
+@pytest.mark.parametrize("case,env", [("content_fwd", {}), ("content_dgrad", {}), ("content_dgrad_512", {}),
+                                      ("content_dgrad_512", {"FLOODGAN_WIN_BM": "256"})])
+def test_conv_window(case, env, monkeypatch):
     """the row-strip window kernel (fg_conv_win) on the content-head geometries -- 7x7 over 64
     channels -> 27, and its input gradient 27(32) -> 64 over the 6-bordered gradient -- with
-    output rows of 256+ px (two-segment tiles, ragged last tile) against fp64"""
+    output rows of 256+ px (two-segment tiles, ragged last tile) against fp64; the input gradient on 512-row
+    tiles where its output rows allow (>= 512 px, the default) and on 256-row ones (FLOODGAN_WIN_BM=256)"""
     from floodgan import _lib as L, ops, plans as PL
     from floodgan.plans import Buf
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
     prev = L.get_conv_math()
     L.set_conv_math("f16x3")
     try:
@@ -414,7 +418,8 @@ def test_conv_window(case):
             prob = PL.conv_problem(X, 3, 7, 1, ops.pack_weight(wd, m), m, Y, bias=b.float().to(DEV))
             ref = y
         else:
-            cin, cout, H, W = 64, 27, 5, 290       # dgrad: gy has 27 (alloc 32) channels, output 64
+            # dgrad: gy has 27 (alloc 32) channels, output 64 over the 6-wider padded domain
+            cin, cout, H, W = (64, 27, 5, 290) if case == "content_dgrad" else (64, 27, 3, 515)
             gy = torch.randn(2, cout, H, W, dtype=torch.float64) * 1e-6
             w = torch.randn(cout, cin, 7, 7, dtype=torch.float64) * 0.05
             # gradient w.r.t. the 3-padded input = full correlation of gy with the flipped kernel
@@ -445,7 +450,7 @@ def test_conv_window(case):
 def test_conv1x1_head(N, H, W, n_out, xpad):
     """the attention head's 1x1 conv in fp32 FMA (fg_conv1x1_*): forward (pad channels written as 0), input
     gradient, weight + bias gradients (written and accumulated) against fp64, ragged last tiles"""
-    from floodgan import ops
+    from floodgan import _lib as L, ops
     from floodgan.plans import Buf
     torch.manual_seed(21)
     x = torch.randn(N, 64, H, W, dtype=torch.float64)
