@@ -212,6 +212,14 @@ __global__ void __launch_bounds__(512, 1) stem_wgrad_kernel(const fg_wgrad_probl
     }
 }
 
+// The forward's ring: copies 1-3 of each piece start 8 B past their 1280-B slot, so that the 32 lanes of a fragment
+// read (16 pixels x 2 k groups, each lane on the copy of its pixel's alignment) hit 64 distinct banks -- with the
+// copies 320 dwords (0 mod 64) apart the reads were 3-way conflicted (half of the kernel's LDS cycles were
+// SQ_LDS_BANK_CONFLICT, profiles/round4/r4_pmc_stem_fwd.json)
+constexpr int SF_PIECE = 4 * ST_COPYB + 16;
+constexpr int SF_XROW = 2 * SF_PIECE;
+__device__ __forceinline__ int sf_copy(int t) { return t * ST_COPYB + (t ? 8 : 0); }
+
 // ---- the stem's forward: y[px][n] = bias[n] + sum_r sum_{j<63} xpad[a + r][9 px + j] * w[n][r*64 + j]
 // 8 waves (two per SIMD) over a 64-px strip walking down `rows` output rows with the same 8-row input ring.  The
 // weights (64 x 448, pre-split fp16) stay in REGISTERS for the whole launch: wave (nh, ph, kh) holds output channels
@@ -223,9 +231,9 @@ __global__ void __launch_bounds__(512, 1) stem_wgrad_kernel(const fg_wgrad_probl
 // each wave's 32 pixels are one InstanceNorm statistics block (mean, M2 per channel) of the epilogue.
 __global__ void __launch_bounds__(512, 1) stem_fwd_kernel(const fg_conv_problem P, int rows) {
     constexpr int RED = 4 * 64 * 16 * 4;            // the kh = 1 partials of one row: 4 waves x 64 lanes x 16 floats
-    __shared__ __attribute__((aligned(1024))) char smem[ST_RING * ST_XROW + 2 * RED];
+    __shared__ __attribute__((aligned(1024))) char smem[ST_RING * SF_XROW + 2 * RED];
     char* const xring = smem;
-    float* const red = reinterpret_cast<float*>(smem + ST_RING * ST_XROW);
+    float* const red = reinterpret_cast<float*>(smem + ST_RING * SF_XROW);
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nh = wave & 1, ph = (wave >> 1) & 1, kh = wave >> 2;
     const int strips = P.m_b / ST_PX, groups = P.m_a / rows;
@@ -241,7 +249,7 @@ __global__ void __launch_bounds__(512, 1) stem_fwd_kernel(const fg_conv_problem 
     const float osc = 1.f / (sx * sw);
     const int g = lane >> 4, fr = lane & 15;
 
-    for (int i = tid; i < ST_RING * ST_XROW / 16; i += 512) reinterpret_cast<f32x4*>(xring)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = tid; i < ST_RING * SF_XROW / 16; i += 512) reinterpret_cast<f32x4*>(xring)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     // weights: fragment (reduction 7 kh + i, block nt, piece) = the lane's 8 k of output channel 32 nh + 16 nt + fr
     f16x8 wf[7][2][2];
@@ -276,7 +284,7 @@ __global__ void __launch_bounds__(512, 1) stem_fwd_kernel(const fg_conv_problem 
                                                   xr, ok && tid + 512 * i < ST_FLAT ? (xo + 512 * i) * 4 : kOOB, 0, 0));
     };
     auto store = [&](int li) {
-        char* xs = xring + (li & (ST_RING - 1)) * ST_XROW;
+        char* xs = xring + (li & (ST_RING - 1)) * SF_XROW;
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             const int e = tid + 512 * i;
@@ -286,8 +294,8 @@ __global__ void __launch_bounds__(512, 1) stem_fwd_kernel(const fg_conv_problem 
             const _Float16 l = (_Float16)(vs - (float)h);
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
-                *reinterpret_cast<_Float16*>(xs + t * ST_COPYB + 2 * (e + t)) = h;
-                *reinterpret_cast<_Float16*>(xs + ST_PIECE + t * ST_COPYB + 2 * (e + t)) = l;
+                *reinterpret_cast<_Float16*>(xs + sf_copy(t) + 2 * (e + t)) = h;
+                *reinterpret_cast<_Float16*>(xs + SF_PIECE + sf_copy(t) + 2 * (e + t)) = l;
             }
         }
     };
@@ -303,7 +311,7 @@ __global__ void __launch_bounds__(512, 1) stem_fwd_kernel(const fg_conv_problem 
 #pragma unroll
         for (int i = 0; i < 7; ++i) {
             const int ks = 7 * kh + i, r = ks >> 1, kk = ks & 1;
-            const char* xs = xring + ((k - 6 + r) & (ST_RING - 1)) * ST_XROW + cp * ST_COPYB;
+            const char* xs = xring + ((k - 6 + r) & (ST_RING - 1)) * SF_XROW + sf_copy(cp);
 #pragma unroll
             for (int pt = 0; pt < 2; ++pt) {
                 const int px = 32 * ph + 16 * pt + fr;
@@ -312,8 +320,8 @@ __global__ void __launch_bounds__(512, 1) stem_fwd_kernel(const fg_conv_problem 
                 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
                 const u32x2 h0 = *reinterpret_cast<const u32x2*>(xs + ad);
                 const u32x2 h1 = *reinterpret_cast<const u32x2*>(xs + ad + 8);
-                const u32x2 l0 = *reinterpret_cast<const u32x2*>(xs + ST_PIECE + ad);
-                const u32x2 l1 = *reinterpret_cast<const u32x2*>(xs + ST_PIECE + ad + 8);
+                const u32x2 l0 = *reinterpret_cast<const u32x2*>(xs + SF_PIECE + ad);
+                const u32x2 l1 = *reinterpret_cast<const u32x2*>(xs + SF_PIECE + ad + 8);
                 const f16x8 bh = __builtin_bit_cast(f16x8, u32x4{h0[0], h0[1], h1[0], h1[1]});
                 const f16x8 bl = __builtin_bit_cast(f16x8, u32x4{l0[0], l0[1], l1[0], l1[1]});
 #pragma unroll

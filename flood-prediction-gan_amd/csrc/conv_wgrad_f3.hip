@@ -69,7 +69,10 @@ conv_wgrad_f3_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
     constexpr int NT = 512, NWA = TA / 64, NWK = 8 / NWA, WK = TK / NWK, TM = 4, TN = WK / 16;
     constexpr int SPT = BR * TK / 4 / NT;           // float4 slots per thread per operand per stage (4)
     constexpr int IMGP = BR * TA * 2, IMGX = BR * TK * 2;   // bytes per piece image
-    constexpr int BUF = 2 * IMGP + 2 * IMGX;
+    // piece images at PH = 0, PL, XH, XL: each l image 64 B past its h image's bank phase, so that the pre-split
+    // staging's lane pairs (an 8-channel group's h and l halves, one 16-B store each) hit different banks
+    constexpr int PL = IMGP + 64, XH = 2 * IMGP + 128, XL = XH + IMGX + 64;
+    constexpr int BUF = XL + IMGX + 64;
     constexpr int kOOB = 0x7fffffff;
     __shared__ __attribute__((aligned(1024))) char smem[2 * BUF];   // [buf][P h, P l, X h, X l]
 
@@ -145,23 +148,23 @@ conv_wgrad_f3_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
             f16x4 h, l;
             if (p_slot) {
                 if constexpr (PS & 1) {
-                    const int op = img_off<TA>(prow0 + 8 * i, col & ~7) + ((col & 4) ? IMGP : 0);
+                    const int op = img_off<TA>(prow0 + 8 * i, col & ~7) + ((col & 4) ? PL : 0);
                     *reinterpret_cast<f16x8*>(b + op) = __builtin_bit_cast(f16x8, rp[i]);
                 } else {
                     const int op = img_off<TA>(prow0 + 8 * i, col);
                     split4(rp[i], sp, h, l);
                     *reinterpret_cast<f16x4*>(b + op) = h;
-                    *reinterpret_cast<f16x4*>(b + IMGP + op) = l;
+                    *reinterpret_cast<f16x4*>(b + PL + op) = l;
                 }
             }
             if constexpr (PS & 2) {
-                const int ox = img_off<TK>(prow0 + 8 * i, col & ~7) + ((col & 4) ? IMGX : 0);
-                *reinterpret_cast<f16x8*>(b + 2 * IMGP + ox) = __builtin_bit_cast(f16x8, rx[i]);
+                const int ox = img_off<TK>(prow0 + 8 * i, col & ~7) + ((col & 4) ? XL : XH);
+                *reinterpret_cast<f16x8*>(b + ox) = __builtin_bit_cast(f16x8, rx[i]);
             } else {
                 const int ox = img_off<TK>(prow0 + 8 * i, col);
                 split4(rx[i], sx, h, l);
-                *reinterpret_cast<f16x4*>(b + 2 * IMGP + ox) = h;
-                *reinterpret_cast<f16x4*>(b + 2 * IMGP + IMGX + ox) = l;
+                *reinterpret_cast<f16x4*>(b + XH + ox) = h;
+                *reinterpret_cast<f16x4*>(b + XL + ox) = l;
             }
         }
     };
@@ -189,7 +192,7 @@ conv_wgrad_f3_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
             const int c = wa * 64 + tm * 16 + p4;
             const int o0 = img_off<TA>(8 * g + q, c), o1 = img_off<TA>(8 * g + 4 + q, c);
             ah[tm] = tr_frag(b, o0, o1);
-            al[tm] = tr_frag(b + IMGP, o0, o1);
+            al[tm] = tr_frag(b + PL, o0, o1);
         }
 #pragma unroll
         for (int t0 = 0; t0 < TN; t0 += TG) {
@@ -198,8 +201,8 @@ conv_wgrad_f3_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
             for (int t = 0; t < TG; ++t) {
                 const int c = wk * WK + (t0 + t) * 16 + p4;
                 const int o0 = img_off<TK>(8 * g + q, c), o1 = img_off<TK>(8 * g + 4 + q, c);
-                bh[t] = tr_frag(b + 2 * IMGP, o0, o1);
-                bl[t] = tr_frag(b + 2 * IMGP + IMGX, o0, o1);
+                bh[t] = tr_frag(b + XH, o0, o1);
+                bl[t] = tr_frag(b + XL, o0, o1);
             }
             if constexpr (SCH == 1) {
                 // this group's staging slot: split + write the registers of the next stage into the

@@ -102,6 +102,83 @@ __global__ void __launch_bounds__(256) n1_wgrad_kernel(const float* __restrict__
         for (int t = 0; t < KT; ++t) out[(t >> 2) * 4 * C + (t & 3) * C + c0 + e] = acc[e][t];
 }
 
+
+// ---- the PatchGAN's input gradient restricted to a few input channels (model.0, Conv2d(C+3, 64, 4, 2, 1),
+// models/model_architectures.py:424): the G step needs dL/d(fake) = the gradient w.r.t. D's last 3 input
+// channels only (models/model.py:640-646).  As a transposed conv it is 3 outputs x 4 taps x 64 channels per pixel:
+// 0.6 GMAC at bs 8, 512^2, against 136 MB of gradient to read -- memory-bound, far below the MFMA ridge (the engine
+// ran it as 4 phases of a 32-column tile with 29 idle columns, ~0.29 ms).  Exact fp32 FMA here:
+//   block = (image, output rows 2 t0 .. 2 t0 + 1, output columns 2 u0 .. 2 u0 + 127); the gradient rows t0 - 1 ..
+//   t0 + 1 x columns u0 - 1 .. u0 + 64 (64 channels) are staged into LDS with coalesced 16-B loads; wave
+//   (py, px) computes the 64 pixels of one (row, column) parity -- each uses the same 2 x 2 taps, whose weights sit in
+//   the lanes' registers: lane = (pixel group pg, channel quad cq), a 16-lane reduction per pixel.
+//   y[n][j][Y][X] (+)= sum_{a,b} sum_ch g[n][a][b][ch] * w[ch][c0 + j][Y + 1 - 2a][X + 1 - 2b]
+constexpr int D0C = 64, D0U = 64, D0COLS = D0U + 2;
+
+template <int CN>
+__global__ void __launch_bounds__(256) d0_input_grad_kernel(fg_view g, const float* __restrict__ w, int ctot, int c0,
+                                                            float* __restrict__ y, int yc, int H, int W, int accumulate,
+                                                            int ublocks) {
+    __shared__ f32x4 gs[3][D0COLS][D0C / 4];
+    __shared__ float os[CN][2][2 * D0U];
+    const int Ho = H / 2, Wo = W / 2;
+    const int ub = blockIdx.x % ublocks, t0 = (blockIdx.x / ublocks) % Ho, n = blockIdx.x / (ublocks * Ho);
+    const int u0 = ub * D0U;
+    const int tid = threadIdx.x;
+    for (int i = tid; i < 3 * D0COLS * (D0C / 4); i += 256) {
+        const int row = i / (D0COLS * (D0C / 4)), rem = i - row * (D0COLS * (D0C / 4));
+        const int col = rem / (D0C / 4), q = rem - col * (D0C / 4);
+        const int a = t0 - 1 + row, b = u0 - 1 + col;      // a in [-1, Ho]: inside the zero border
+        gs[row][col][q] = b <= Wo ? *reinterpret_cast<const f32x4*>(g.ptr + fg::vidx(g, n, a, b) + 4 * q)
+                                  : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    const int wave = tid >> 6, lane = tid & 63, py = wave >> 1, px = wave & 1, pg = lane >> 4, cq = lane & 15;
+    // output row 2 t0 (py 1): taps r = 1 (gradient row t0 -> LDS row 1), 3 (t0 - 1 -> 0);
+    // row 2 t0 + 1 (py 0): r = 0 (t0 + 1 -> 2), 2 (t0 -> 1).  Columns likewise with px, s and LDS column offsets.
+    const int r0 = py ? 1 : 0, r1 = r0 + 2, lr0 = py ? 1 : 2, lr1 = lr0 - 1;
+    const int s0 = px ? 1 : 0, s1 = s0 + 2, lc0 = px ? 1 : 2, lc1 = lc0 - 1;
+    f32x4 wt[4][CN];          // taps (r0,s0) (r0,s1) (r1,s0) (r1,s1) x outputs: this lane's 4 channels
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const int r = t < 2 ? r0 : r1, sc = (t & 1) ? s1 : s0;
+#pragma unroll
+        for (int j = 0; j < CN; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) wt[t][j][e] = w[((size_t)(4 * cq + e) * ctot + c0 + j) * 16 + r * 4 + sc];
+    }
+    __syncthreads();
+    for (int jj = pg; jj < D0U; jj += 4) {
+        float acc[CN];
+#pragma unroll
+        for (int j = 0; j < CN; ++j) acc[j] = 0.f;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const f32x4 v = gs[t < 2 ? lr0 : lr1][jj + ((t & 1) ? lc1 : lc0)][cq];
+#pragma unroll
+            for (int j = 0; j < CN; ++j) {
+                acc[j] = fmaf(v[0], wt[t][j][0], acc[j]);
+                acc[j] = fmaf(v[1], wt[t][j][1], acc[j]);
+                acc[j] = fmaf(v[2], wt[t][j][2], acc[j]);
+                acc[j] = fmaf(v[3], wt[t][j][3], acc[j]);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < CN; ++j)
+#pragma unroll
+            for (int off = 1; off < 16; off <<= 1) acc[j] += __shfl_xor(acc[j], off);
+        if (cq == 0)
+#pragma unroll
+            for (int j = 0; j < CN; ++j) os[j][1 - py][2 * jj + 1 - px] = acc[j];
+    }
+    __syncthreads();
+    for (int i = tid; i < CN * 2 * 2 * D0U; i += 256) {
+        const int j = i / (4 * D0U), rr = (i / (2 * D0U)) & 1, xl = i & (2 * D0U - 1);
+        const int Y = 2 * t0 + rr, X = 2 * u0 + xl;
+        if (X >= W) continue;
+        float* dst = y + (((size_t)n * yc + j) * H + Y) * W + X;
+        *dst = accumulate ? *dst + os[j][rr][xl] : os[j][rr][xl];
+    }
+}
 }  // namespace
 
 FG_API int fg_conv_n1_fwd(const float* x, int nimg, int hp, int wp, int c, const float* w, const float* bias,
@@ -129,4 +206,21 @@ FG_API int fg_conv_n1_wgrad(const float* x, int nimg, int hp, int wp, int c, con
     hipLaunchKernelGGL(n1_wgrad_kernel, dim3(fg_conv_n1_wgrad_blocks(nimg, hp, rows_per_block)), dim3(256), 0, stream,
                        x, hp, wp, gp, ghp, gwp, nimg, rows_per_block, slabs);
     return fg::launched("conv_n1_wgrad");
+}
+
+FG_API int fg_d0_input_grad(fg_view g, const float* w, int ctot, int c0, int cn, float* y, int yc, int H, int W,
+                            int accumulate, hipStream_t stream) {
+    if (!g.ptr || !w || !y || g.c_alloc != D0C || g.pad < 1 || (H & 1) || (W & 1) || g.h != H / 2 || g.w != W / 2 ||
+        cn < 1 || cn > 4 || c0 < 0 || c0 + cn > ctot || yc < cn || ((uintptr_t)g.ptr & 15))
+        return fg::fail(FG_ERR_INVALID, "fg_d0_input_grad: needs the 64-channel gradient of a 4x4 stride-2 pad-1 conv "
+                                        "(zero border >= 1, H and W even) and 1..4 input channels (cn=%d)", cn);
+    const int ublocks = (W / 2 + D0U - 1) / D0U;
+    const dim3 grid((unsigned)(g.n * (H / 2) * ublocks));
+    switch (cn) {
+        case 1: hipLaunchKernelGGL(d0_input_grad_kernel<1>, grid, dim3(256), 0, stream, g, w, ctot, c0, y, yc, H, W, accumulate, ublocks); break;
+        case 2: hipLaunchKernelGGL(d0_input_grad_kernel<2>, grid, dim3(256), 0, stream, g, w, ctot, c0, y, yc, H, W, accumulate, ublocks); break;
+        case 3: hipLaunchKernelGGL(d0_input_grad_kernel<3>, grid, dim3(256), 0, stream, g, w, ctot, c0, y, yc, H, W, accumulate, ublocks); break;
+        default: hipLaunchKernelGGL(d0_input_grad_kernel<4>, grid, dim3(256), 0, stream, g, w, ctot, c0, y, yc, H, W, accumulate, ublocks); break;
+    }
+    return fg::launched("d0_input_grad");
 }

@@ -119,6 +119,8 @@ SIGNATURES = {
     "fg_conv_n1_wgrad_blocks": [C.c_int, C.c_int, C.c_int],
     "fg_conv_n1_wgrad": [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int,
                          C.c_void_p, C.c_void_p],
+    "fg_d0_input_grad": [fg_view, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int,
+                         C.c_int, C.c_void_p],
     "fg_split_pixels": [C.c_void_p, C.c_longlong, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p],
     "fg_conv_win": [C.POINTER(fg_conv_problem), C.c_void_p, C.c_longlong, C.c_void_p],
     "fg_conv_wgrad_win": [C.POINTER(fg_wgrad_problem), C.c_void_p, C.c_longlong, C.c_int, C.c_int, C.c_void_p,

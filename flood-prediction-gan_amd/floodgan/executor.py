@@ -39,6 +39,10 @@ def generator_param_names():
 
 DISC_LAYERS = ["model.0", "model.2", "model.5", "model.8", "model.11"]
 
+# D's input gradient restricted to a few channels (the G step's dL/d(fake)) on its fp32 kernel (fg_d0_input_grad);
+# FLOODGAN_D0_DGRAD=0: the restricted 4-phase transposed conv on the engine
+D0_DGRAD = os.environ.get("FLOODGAN_D0_DGRAD", "1") != "0"
+
 
 def disc_bucket_names():
     """the discriminator's gradient buckets (one per layer) in the order disc_backward completes them"""
@@ -519,13 +523,24 @@ def disc_act_decisions(S, lo=0, hi=None):
 # discriminator
 # ======================================================================================
 
+# D's input buffer with 9 < channels < 16 allocated as 16 zero-filled channels: model.0's packed row run (4 taps x C)
+# is then a multiple of 32 and its forward / weight gradient run on the pipelined kernels instead of the register-
+# staged ones (FLOODGAN_DISC_C16=0: C channels)
+DISC_C16 = os.environ.get("FLOODGAN_DISC_C16", "0") != "0"
+
+
+def disc_alloc(c_in_total):
+    return 16 if DISC_C16 and 8 < c_in_total < 16 else c_in_total
+
+
 def disc_pack(pairs, c_in_total):
     """Stack (a [N,Ca,H,W], b [N,Cb,H,W] or None) pairs along the batch into one zero-padded
-    NHWC input buffer (torch.cat((a, b), 1) of models/model.py:616-617, fused)."""
+    NHWC input buffer (torch.cat((a, b), 1) of models/model.py:616-617, fused); channels past c_in_total (up to
+    disc_alloc) are zeros."""
     a0 = pairs[0][0]
     N = sum(a.shape[0] for a, _ in pairs)
     H, W = a0.shape[2], a0.shape[3]
-    buf = Buf.empty(N, H, W, c_in_total, 1, a0.device)
+    buf = Buf.empty(N, H, W, disc_alloc(c_in_total), 1, a0.device)
     slot = ops.amax_slot(buf) if len(pairs) > 1 else None      # the parts raise one shared absmax slot
     img0 = 0
     for a, b in pairs:
@@ -631,7 +646,10 @@ def disc_backward(P, S, g_pred, param_grads=True, grads_into=None, input_grad=No
         c0, cn = input_grad_channels
         # input_grad: contiguous [N, Ctot, H, W]; D-input channels c0 .. c0+cn land in its channels 0 .. cn
         assert input_grad.is_contiguous() and input_grad.shape[1] >= cn
-        _dgrad_s2(P, "model.0", g_e0, 4, y_nchw=(input_grad.view(-1), input_grad.shape[1], inp.h, inp.w), n_base=c0,
-                  n_out=cn, accumulate=int(input_grad_accumulate))
+        if D0_DGRAD and ops.d0_input_grad_ok(g_e0, c0, cn, inp.h, inp.w):
+            ops.d0_input_grad(g_e0, P["model.0.weight"], c0, cn, input_grad, input_grad_accumulate)
+        else:
+            _dgrad_s2(P, "model.0", g_e0, 4, y_nchw=(input_grad.view(-1), input_grad.shape[1], inp.h, inp.w),
+                      n_base=c0, n_out=cn, accumulate=int(input_grad_accumulate))
     G.join()
     return G.out

@@ -639,6 +639,19 @@ def conv_n1_wgrad(X, G, wmap, dw):
     L.check(_lib().fg_wgrad_reduce(L.ptr(slab), blocks, C.byref(m), L.ptr(dw), 0, st), "wgrad_reduce")
 
 
+def d0_input_grad_ok(G, c0, cn, H, W):
+    return G.c == 64 and G.pad >= 1 and H % 2 == 0 and W % 2 == 0 and G.h == H // 2 and G.w == W // 2 and 1 <= cn <= 4
+
+
+def d0_input_grad(G, w, c0, cn, y, accumulate):
+    """dL/d(D input channels c0 .. c0+cn-1) of model.0 (4x4 s2 p1, 64 outputs) from its output gradient G (Buf, 64 ch,
+    zero border >= 1) into y [N, >= cn, H, W] contiguous NCHW channels 0 .. cn-1 (fg_d0_input_grad, exact fp32)"""
+    assert y.is_contiguous() and w.is_contiguous()
+    _wrote(y)
+    L.check(_lib().fg_d0_input_grad(view(G), L.ptr(w), w.shape[1], c0, cn, L.ptr(y), y.shape[1], y.shape[2],
+                                    y.shape[3], int(accumulate), L.stream_handle()), "d0_input_grad")
+
+
 # ------------------------------------------------------------------ layout
 
 def pack_input(a, ca, b, cb, dst, img0, nimg, pad_mode, amax=None):

@@ -300,6 +300,14 @@ int fg_conv_n1_wgrad_blocks(int nimg, int hp, int rows_per_block);
 int fg_conv_n1_wgrad(const float* x, int nimg, int hp, int wp, int c, const float* gp, int ghp, int gwp,
                      int rows_per_block, float* slabs, hipStream_t stream);
 
+/* The PatchGAN model.0 input gradient (Conv2d(ctot, 64, 4, 2, 1), models/model_architectures.py:424) for input
+ * channels c0 .. c0 + cn - 1 only (cn <= 4: the G step's dL/d(fake), models/model.py:640-646), in exact fp32:
+ * g = dL/d(model.0 output) as an NHWC view of 64 channels at H/2 x W/2 with a zero border >= 1, w = model.0.weight
+ * [64][ctot][4][4]; y = NCHW [N][yc][H][W] whose channels 0 .. cn - 1 receive it (accumulate: added).  Replaces the
+ * restricted 4-phase transposed conv the engine ran (ops._dgrad_s2 with n_base / n_out). */
+int fg_d0_input_grad(fg_view g, const float* w, int ctot, int c0, int cn, float* y, int yc, int H, int W,
+                     int accumulate, hipStream_t stream);
+
 /* Raise the absmax slot `out` (FG_AMAX_SHARDS floats, initialised by the caller) to bound
  * max |x[i]| over n contiguous floats (bitwise max of |x|; NaN-propagating).  The operand-
  * scale source of the f16x3 math. */

@@ -27,23 +27,25 @@ def case(N, H, cin, cout):
     wps = [ops.pack_weight(w, m) for m, _, _ in maps]
     probs = PL.phase_problems(X, w.shape, 3, 1, Y, wps, maps, bias=torch.zeros(cout, device="cuda"))
     flops = 2.0 * N * (2 * H) ** 2 * cout * cin * 9 / 4
-    return (lambda: ops.conv(probs, in_stats=True)), flops, (X, w, Y, c)
+    return (lambda st=True: ops.conv(probs, in_stats=st)), flops, (X, w, Y, c)
 
 
 def main():
     lib = L.load()
-    cases = {"deconv2 128->64 (N=64)": (case(8, 256, 128, 64), [-1, 7, 8, 9, 6, 3]),
-             "deconv1 256->128 (N=128)": (case(8, 128, 256, 128), [-1, 6, 1, 2, 3, 0, 5, 4])}
+    cases = {"deconv2 128->64 (N=64)": (case(8, 256, 128, 64), [-1, 7, 10, 9, 6]),
+             "deconv1 256->128 (N=128)": (case(8, 128, 256, 128), [-1, 6, 11, 4, 5])}
     for name, ((fn, flops, keep), cfgs) in cases.items():
         res = {}
         for _ in range(3):
             for cfg in cfgs:
                 L.set_f3_tile(cfg)
-                res.setdefault(cfg, []).append(time_it(fn, reps=10))
+                for st in (True, False):
+                    res.setdefault((cfg, st), []).append(time_it(lambda: fn(st), reps=10))
         L.set_f3_tile(-1)
         for cfg in cfgs:
-            ms = min(res[cfg])
-            print(f"{name:28s} cfg {cfg:3d}: {ms:.4f} ms  {flops / ms / 1e9:6.1f} TFLOP/s", flush=True)
+            for st in (True, False):
+                ms = min(res[(cfg, st)])
+                print(f"{name:28s} cfg {cfg:3d} stats {int(st)}: {ms:.4f} ms  {flops / ms / 1e9:6.1f} TFLOP/s", flush=True)
 
 
 if __name__ == "__main__":

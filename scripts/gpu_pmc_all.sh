@@ -1,6 +1,6 @@
 #!/bin/bash
 # Counter passes for the kernels bench.py's roofline names (the three resblock conv kinds) and the stem strip
-# kernels, each summarised into profiles/<round>/<tag>_pmc_*.json; stops at the first failing pass.
+# kernels, each summarised into gpurun_out/<tag>_pmc_*.json (copy into profiles/<round>/); stops at the first failing pass.
 #   scripts/gpu_pmc_all.sh r4 round4 ["fwd_stats_ps dgrad_ps wgrad_ps stem_wgrad stem_fwd"]
 cd "$(dirname "$0")/.." || exit 1
 TAG=${1:-r4}; RD=${2:-round4}; KINDS=${3:-"fwd_stats_ps dgrad_ps wgrad_ps stem_wgrad stem_fwd"}
@@ -15,7 +15,7 @@ for k in $KINDS; do
     *) echo "unknown kind $k"; exit 1;;
   esac
   KIND=$k scripts/gpu_pmc.sh "${TAG}_$k" || { echo "pmc $k failed"; exit 1; }
-  python scripts/pmc_summary.py "gpurun_out/pmc_${TAG}_$k" "$key" "$ktag" "$k" > "profiles/$RD/${TAG}_pmc_$name.json" \
+  python scripts/pmc_summary.py "gpurun_out/pmc_${TAG}_$k" "$key" "$ktag" "$k" > "gpurun_out/${TAG}_pmc_$name.json" \
     || { echo "summary $k failed"; exit 1; }
-  cat "profiles/$RD/${TAG}_pmc_$name.json"
+  cat "gpurun_out/${TAG}_pmc_$name.json"
 done

@@ -446,6 +446,37 @@ def test_conv_window(case, env, monkeypatch):
         L.set_conv_math(prev)
 
 
+@pytest.mark.parametrize("ctot,c0,cn,H,W,acc", [(12, 9, 3, 64, 64, True), (12, 9, 3, 256, 130, False),
+                                               (4, 0, 4, 34, 200, True), (6, 2, 1, 18, 18, False)])
+def test_d0_input_grad(ctot, c0, cn, H, W, acc):
+    """the PatchGAN model.0 input gradient restricted to input channels c0 .. c0+cn-1 (fg_d0_input_grad, exact fp32;
+    the G step's dL/d(fake)) against fp64 autograd of Conv2d(ctot, 64, 4, 2, 1), written and accumulated into an
+    NCHW tensor, partial 64-column blocks included, and against the engine's restricted transposed conv"""
+    from floodgan import executor as X, ops
+    torch.manual_seed(31)
+    N = 2
+    x = torch.randn(N, ctot, H, W, dtype=torch.float64, requires_grad=True)
+    w = torch.randn(64, ctot, 4, 4, dtype=torch.float64) * 0.05
+    e = F.conv2d(x, w, stride=2, padding=1)
+    gy = torch.randn_like(e)
+    (gx,) = torch.autograd.grad(e, x, gy)
+    G = buf_from(gy, 1, "constant")
+    base = torch.randn(N, cn + 1, H, W, device=DEV)
+    y = base.clone()
+    wd = w.float().to(DEV).contiguous()
+    ops.d0_input_grad(G, wd, c0, cn, y, acc)
+    torch.cuda.synchronize()
+    ref = gx[:, c0:c0 + cn] + (base[:, :cn].double().cpu() if acc else 0)
+    assert nrel(y[:, :cn].double().cpu(), ref) < 1e-6
+    assert torch.equal(y[:, cn:], base[:, cn:])               # channels past cn untouched
+    # the engine's restricted 4-phase transposed conv of the same gradient (the FLOODGAN_D0_DGRAD=0 path)
+    y2 = base.clone()
+    X._dgrad_s2({"model.0.weight": wd}, "model.0", G, 4, y_nchw=(y2.view(-1), y2.shape[1], H, W), n_base=c0, n_out=cn,
+                accumulate=int(acc))
+    torch.cuda.synchronize()
+    assert nrel(y2[:, :cn].double().cpu(), ref) < KTOL
+
+
 @pytest.mark.parametrize("N,H,W,n_out,xpad", [(2, 20, 37, 10, 0), (3, 9, 64, 10, 1), (1, 5, 7, 16, 0), (2, 96, 96, 3, 0)])
 def test_conv1x1_head(N, H, W, n_out, xpad):
     """the attention head's 1x1 conv in fp32 FMA (fg_conv1x1_*): forward (pad channels written as 0), input
