@@ -468,9 +468,7 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
                         sm[u] = s2[0] + s2[1];
                     }
 #pragma unroll
-                    for (int u = 0; u < SG; ++u) sm[u] += __shfl_xor(sm[u], 16);
-#pragma unroll
-                    for (int u = 0; u < SG; ++u) sm[u] += __shfl_xor(sm[u], 32);
+                    for (int u = 0; u < SG; ++u) sm[u] = fg::rows_sum4(sm[u]);     // lanes l, l^16, l^32, l^48
 #pragma unroll
                     for (int u = 0; u < SG; ++u) {
                         const float mu = sm[u] * (1.f / 32);
@@ -486,9 +484,7 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
                         sq[u] = q2[0] + q2[1];
                     }
 #pragma unroll
-                    for (int u = 0; u < SG; ++u) sq[u] += __shfl_xor(sq[u], 16);
-#pragma unroll
-                    for (int u = 0; u < SG; ++u) sq[u] += __shfl_xor(sq[u], 32);
+                    for (int u = 0; u < SG; ++u) sq[u] = fg::rows_sum4(sq[u]);     // lanes l, l^16, l^32, l^48
                     if (g == 0) {
 #pragma unroll
                         for (int u = 0; u < SG; ++u)

@@ -334,7 +334,7 @@ __global__ void __launch_bounds__(512, 1) stem_fwd_kernel(const fg_conv_problem 
         }
     };
     // the kh = 0 wave of (nh, ph): add the kh = 1 partials, store the row and its statistics
-    auto finish_row = [&](int k) {
+    auto finish_row = [&](int k, f32x4 (&acc)[2][2]) {
         const float* rb_ = red + ((k & 1) * 4 + (wave & 3)) * 64 * 16 + lane * 4;
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt)
@@ -360,13 +360,11 @@ __global__ void __launch_bounds__(512, 1) stem_fwd_kernel(const fg_conv_problem 
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     float s = acc[nt][0][i] + acc[nt][1][i];
-#pragma unroll
-                    for (int off = 1; off < 16; off <<= 1) s += __shfl_xor(s, off);
+                    s = fg::row_sum16(s);
                     const float mu = s * (1.f / 32);
                     const float d0 = acc[nt][0][i] - mu, d1 = acc[nt][1][i] - mu;
                     float q = d0 * d0 + d1 * d1;
-#pragma unroll
-                    for (int off = 1; off < 16; off <<= 1) q += __shfl_xor(q, off);
+                    q = fg::row_sum16(q);
                     if (fr == 0) {
                         const int ch = 32 * nh + 16 * nt + 4 * g + i;
                         *reinterpret_cast<float2*>(dst + ch * 2) = make_float2(mu * osc + bias[nt][i], q * (osc * osc));
@@ -375,30 +373,39 @@ __global__ void __launch_bounds__(512, 1) stem_fwd_kernel(const fg_conv_problem 
         }
     };
 
-    // step k: store input row k + 1 (ring slot (k+1) & 7, not read by row k - 6), load row k + 2, reduce output row
-    // k - 6 (rows k-6 .. k); the kh = 1 waves leave their partials in red[k & 1] (red[(k+1) & 1] is still being read
-    // by the kh = 0 waves of the previous row -- they passed this step's barrier only after reading it)
+    // step k: the MFMAs of output row k - 6 (ring rows k-6 .. k) are issued first; behind them, while they run, input row
+    // k + 1 is stored (ring slot (k+1) & 7, not read by row k - 6), row k + 2 loaded and -- in the kh = 0 waves -- the
+    // PREVIOUS row finished (its kh = 1 partials in red[(k-1) & 1], its own accumulators saved in accp), so the
+    // epilogue no longer sits between two barriers with the kh = 1 waves idle.  The kh = 1 waves leave this row's
+    // partials in red[k & 1] (red[(k+1) & 1] was read before this step's barrier).
     __syncthreads();
     load(0);
     store(0);
     load(1);
     __syncthreads();
+    f32x4 accp[2][2];
     for (int k = 0; k < nsteps; ++k) {
+        if (k >= 6) compute_row(k);
         if (k + 1 < nsteps) store(k + 1);
         load(k + 2);
+        if (k >= 7 && !kh) finish_row(k - 1, accp);
         if (k >= 6) {
-            compute_row(k);
             if (kh) {
                 float* rb_ = red + ((k & 1) * 4 + (wave & 3)) * 64 * 16 + lane * 4;
 #pragma unroll
                 for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
                     for (int pt = 0; pt < 2; ++pt) *reinterpret_cast<f32x4*>(rb_ + (nt * 2 + pt) * 256) = acc[nt][pt];
+            } else {
+#pragma unroll
+                for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+                    for (int pt = 0; pt < 2; ++pt) accp[nt][pt] = acc[nt][pt];
             }
         }
         __syncthreads();
-        if (k >= 6 && !kh) finish_row(k);
     }
+    if (!kh && nsteps > 6) finish_row(nsteps - 1, accp);
 }
 
 }  // namespace

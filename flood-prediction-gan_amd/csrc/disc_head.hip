@@ -163,9 +163,7 @@ __global__ void __launch_bounds__(256) d0_input_grad_kernel(fg_view g, const flo
             }
         }
 #pragma unroll
-        for (int j = 0; j < CN; ++j)
-#pragma unroll
-            for (int off = 1; off < 16; off <<= 1) acc[j] += __shfl_xor(acc[j], off);
+        for (int j = 0; j < CN; ++j) acc[j] = fg::row_sum16(acc[j]);
         if (cq == 0)
 #pragma unroll
             for (int j = 0; j < CN; ++j) os[j][1 - py][2 * jj + 1 - px] = acc[j];

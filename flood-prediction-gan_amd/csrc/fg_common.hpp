@@ -59,6 +59,28 @@ inline size_t view_elems(const fg_view& v) {
     return (size_t)v.n * (v.h + 2 * v.pad) * (v.w + 2 * v.pad) * v.c_alloc;
 }
 
+// Cross-lane sums on the VALU (DPP / gfx950 permlane swaps) instead of ds_bpermute (__shfl_xor goes through the LDS
+// crossbar): the same pairings as the xor butterflies they replace, so the results are bit-identical.
+// row_sum16: every lane gets the sum over its row of 16 lanes (xor 1, 2, then the quad / half-row mirrors = xor 4, 8)
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row_sum16(float v) {
+    v += dpp<0xB1>(v);      // quad_perm [1,0,3,2]
+    v += dpp<0x4E>(v);      // quad_perm [2,3,0,1]
+    v += dpp<0x141>(v);     // row_half_mirror: quad q <-> the other quad of the half-row
+    v += dpp<0x140>(v);     // row_mirror: half-row <-> half-row
+    return v;
+}
+// rows_sum4: every lane gets the sum of the value over lanes l, l^16, l^32, l^48 ((x0 + x1) + (x2 + x3) by row)
+__device__ __forceinline__ float rows_sum4(float v) {
+    const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+    const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
 inline int blocks_for(long long work, int per_block, int cap = 1 << 20) {
     long long b = (work + per_block - 1) / per_block;
     if (b < 1) b = 1;
