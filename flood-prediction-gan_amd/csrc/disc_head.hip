@@ -8,6 +8,8 @@
 //   weight gradient: input-pixel-centric -- each thread owns 2 channels x 16 taps of dW and adds
 //            g[y-r][x-s] * a[y][x][c] for the 16 output pixels that read input pixel (y, x), so
 //            every input pixel is read once; per-block partial sums go to fg_wgrad_reduce slabs.
+#include <algorithm>
+
 #include "fg_common.hpp"
 
 namespace {
@@ -108,34 +110,50 @@ __global__ void __launch_bounds__(256) n1_wgrad_kernel(const float* __restrict__
 // channels only (models/model.py:640-646).  As a transposed conv it is 3 outputs x 4 taps x 64 channels per pixel:
 // 0.6 GMAC at bs 8, 512^2, against 136 MB of gradient to read -- memory-bound, far below the MFMA ridge (the engine
 // ran it as 4 phases of a 32-column tile with 29 idle columns, ~0.29 ms).  Exact fp32 FMA here:
-//   block = (image, output rows 2 t0 .. 2 t0 + 1, output columns 2 u0 .. 2 u0 + 127); the gradient rows t0 - 1 ..
-//   t0 + 1 x columns u0 - 1 .. u0 + 64 (64 channels) are staged into LDS with coalesced 16-B loads; wave
-//   (py, px) computes the 64 pixels of one (row, column) parity -- each uses the same 2 x 2 taps, whose weights sit in
-//   the lanes' registers: lane = (pixel group pg, channel quad cq), a 16-lane reduction per pixel.
+//   block = (image, 64-column block u0 .. u0 + 63 of the gradient, a run of gradient rows t0): per row t0 it
+//   produces output rows 2 t0, 2 t0 + 1 x columns 2 u0 .. 2 u0 + 127 from gradient rows t0 - 1 .. t0 + 1, kept in a
+//   3-row LDS ring (66 columns x 64 channels; each row staged once with coalesced 16-B loads, the next one in
+//   flight in registers while the current pair of output rows is computed).  Wave (py, px) computes the 64 pixels of
+//   one (row, column) parity, which all use the same 2 x 2 taps: their weights are loaded into the lanes' registers
+//   ONCE per block; lane = (pixel group pg, channel quad cq), a 16-lane DPP reduction per pixel; the outputs go out
+//   through LDS as whole rows.
 //   y[n][j][Y][X] (+)= sum_{a,b} sum_ch g[n][a][b][ch] * w[ch][c0 + j][Y + 1 - 2a][X + 1 - 2b]
-constexpr int D0C = 64, D0U = 64, D0COLS = D0U + 2;
+constexpr int D0C = 64, D0U = 64, D0COLS = D0U + 2, D0Q = D0C / 4;
+constexpr int D0LD = (D0COLS * D0Q + 255) / 256;          // 16-B loads per thread per staged row
 
 template <int CN>
 __global__ void __launch_bounds__(256) d0_input_grad_kernel(fg_view g, const float* __restrict__ w, int ctot, int c0,
                                                             float* __restrict__ y, int yc, int H, int W, int accumulate,
-                                                            int ublocks) {
-    __shared__ f32x4 gs[3][D0COLS][D0C / 4];
+                                                            int ublocks, int rows_per_block) {
+    __shared__ f32x4 gs[3][D0COLS][D0Q];
     __shared__ float os[CN][2][2 * D0U];
     const int Ho = H / 2, Wo = W / 2;
-    const int ub = blockIdx.x % ublocks, t0 = (blockIdx.x / ublocks) % Ho, n = blockIdx.x / (ublocks * Ho);
-    const int u0 = ub * D0U;
+    const int nsplit = (Ho + rows_per_block - 1) / rows_per_block;
+    const int ub = blockIdx.x % ublocks, sp = (blockIdx.x / ublocks) % nsplit, n = blockIdx.x / (ublocks * nsplit);
+    const int u0 = ub * D0U, tb = sp * rows_per_block, te = min(Ho, tb + rows_per_block);
     const int tid = threadIdx.x;
-    for (int i = tid; i < 3 * D0COLS * (D0C / 4); i += 256) {
-        const int row = i / (D0COLS * (D0C / 4)), rem = i - row * (D0COLS * (D0C / 4));
-        const int col = rem / (D0C / 4), q = rem - col * (D0C / 4);
-        const int a = t0 - 1 + row, b = u0 - 1 + col;      // a in [-1, Ho]: inside the zero border
-        gs[row][col][q] = b <= Wo ? *reinterpret_cast<const f32x4*>(g.ptr + fg::vidx(g, n, a, b) + 4 * q)
-                                  : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
+    f32x4 rg[D0LD];
+    auto load_row = [&](int a) {        // gradient row a (-1 .. Ho: the zero border included) into registers
+#pragma unroll
+        for (int k = 0; k < D0LD; ++k) {
+            const int i = tid + 256 * k, col = i / D0Q, q = i - col * D0Q, b = u0 - 1 + col;
+            rg[k] = (i < D0COLS * D0Q && b <= Wo && a <= Ho)
+                        ? *reinterpret_cast<const f32x4*>(g.ptr + fg::vidx(g, n, a, b) + 4 * q)
+                        : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+    };
+    auto store_row = [&](int a) {
+        f32x4* dst = &gs[(a + 3) % 3][0][0];
+#pragma unroll
+        for (int k = 0; k < D0LD; ++k) {
+            const int i = tid + 256 * k;
+            if (i < D0COLS * D0Q) dst[i] = rg[k];
+        }
+    };
     const int wave = tid >> 6, lane = tid & 63, py = wave >> 1, px = wave & 1, pg = lane >> 4, cq = lane & 15;
-    // output row 2 t0 (py 1): taps r = 1 (gradient row t0 -> LDS row 1), 3 (t0 - 1 -> 0);
-    // row 2 t0 + 1 (py 0): r = 0 (t0 + 1 -> 2), 2 (t0 -> 1).  Columns likewise with px, s and LDS column offsets.
-    const int r0 = py ? 1 : 0, r1 = r0 + 2, lr0 = py ? 1 : 2, lr1 = lr0 - 1;
+    // output row 2 t0 (py 1): taps r = 1 (gradient row t0), 3 (t0 - 1); row 2 t0 + 1 (py 0): r = 0 (t0 + 1), 2 (t0).
+    // Columns likewise with px, s and the LDS column offsets.
+    const int r0 = py ? 1 : 0, r1 = r0 + 2, dr0 = py ? 0 : 1, dr1 = dr0 - 1;
     const int s0 = px ? 1 : 0, s1 = s0 + 2, lc0 = px ? 1 : 2, lc1 = lc0 - 1;
     f32x4 wt[4][CN];          // taps (r0,s0) (r0,s1) (r1,s0) (r1,s1) x outputs: this lane's 4 channels
 #pragma unroll
@@ -146,37 +164,50 @@ __global__ void __launch_bounds__(256) d0_input_grad_kernel(fg_view g, const flo
 #pragma unroll
             for (int e = 0; e < 4; ++e) wt[t][j][e] = w[((size_t)(4 * cq + e) * ctot + c0 + j) * 16 + r * 4 + sc];
     }
-    __syncthreads();
-    for (int jj = pg; jj < D0U; jj += 4) {
-        float acc[CN];
+    if (tb >= te) return;
+    load_row(tb - 1);
+    store_row(tb - 1);
+    load_row(tb);
+    store_row(tb);
+    load_row(tb + 1);
+    for (int t0 = tb; t0 < te; ++t0) {
+        store_row(t0 + 1);                       // slot (t0 + 1) % 3 = (t0 - 2) % 3, last read at t0 - 1
+        __syncthreads();
+        if (t0 + 1 < te) load_row(t0 + 2);       // in flight during this row pair
+        const f32x4(*rw0)[D0Q] = gs[(t0 + dr0 + 3) % 3];
+        const f32x4(*rw1)[D0Q] = gs[(t0 + dr1 + 3) % 3];
+        for (int jj = pg; jj < D0U; jj += 4) {
+            float acc[CN];
 #pragma unroll
-        for (int j = 0; j < CN; ++j) acc[j] = 0.f;
+            for (int j = 0; j < CN; ++j) acc[j] = 0.f;
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const f32x4 v = gs[t < 2 ? lr0 : lr1][jj + ((t & 1) ? lc1 : lc0)][cq];
+            for (int t = 0; t < 4; ++t) {
+                const f32x4 v = (t < 2 ? rw0 : rw1)[jj + ((t & 1) ? lc1 : lc0)][cq];
 #pragma unroll
-            for (int j = 0; j < CN; ++j) {
-                acc[j] = fmaf(v[0], wt[t][j][0], acc[j]);
-                acc[j] = fmaf(v[1], wt[t][j][1], acc[j]);
-                acc[j] = fmaf(v[2], wt[t][j][2], acc[j]);
-                acc[j] = fmaf(v[3], wt[t][j][3], acc[j]);
+                for (int j = 0; j < CN; ++j) {
+                    acc[j] = fmaf(v[0], wt[t][j][0], acc[j]);
+                    acc[j] = fmaf(v[1], wt[t][j][1], acc[j]);
+                    acc[j] = fmaf(v[2], wt[t][j][2], acc[j]);
+                    acc[j] = fmaf(v[3], wt[t][j][3], acc[j]);
+                }
             }
+#pragma unroll
+            for (int j = 0; j < CN; ++j) acc[j] = fg::row_sum16(acc[j]);
+            if (cq == 0)
+#pragma unroll
+                for (int j = 0; j < CN; ++j) os[j][1 - py][2 * jj + 1 - px] = acc[j];
         }
-#pragma unroll
-        for (int j = 0; j < CN; ++j) acc[j] = fg::row_sum16(acc[j]);
-        if (cq == 0)
-#pragma unroll
-            for (int j = 0; j < CN; ++j) os[j][1 - py][2 * jj + 1 - px] = acc[j];
-    }
-    __syncthreads();
-    for (int i = tid; i < CN * 2 * 2 * D0U; i += 256) {
-        const int j = i / (4 * D0U), rr = (i / (2 * D0U)) & 1, xl = i & (2 * D0U - 1);
-        const int Y = 2 * t0 + rr, X = 2 * u0 + xl;
-        if (X >= W) continue;
-        float* dst = y + (((size_t)n * yc + j) * H + Y) * W + X;
-        *dst = accumulate ? *dst + os[j][rr][xl] : os[j][rr][xl];
+        __syncthreads();
+        for (int i = tid; i < CN * 2 * 2 * D0U; i += 256) {
+            const int j = i / (4 * D0U), rr = (i / (2 * D0U)) & 1, xl = i & (2 * D0U - 1);
+            const int Y = 2 * t0 + rr, X = 2 * u0 + xl;
+            if (X >= W) continue;
+            float* dst = y + (((size_t)n * yc + j) * H + Y) * W + X;
+            *dst = accumulate ? *dst + os[j][rr][xl] : os[j][rr][xl];
+        }
     }
 }
+
 }  // namespace
 
 FG_API int fg_conv_n1_fwd(const float* x, int nimg, int hp, int wp, int c, const float* w, const float* bias,
@@ -212,13 +243,16 @@ FG_API int fg_d0_input_grad(fg_view g, const float* w, int ctot, int c0, int cn,
         cn < 1 || cn > 4 || c0 < 0 || c0 + cn > ctot || yc < cn || ((uintptr_t)g.ptr & 15))
         return fg::fail(FG_ERR_INVALID, "fg_d0_input_grad: needs the 64-channel gradient of a 4x4 stride-2 pad-1 conv "
                                         "(zero border >= 1, H and W even) and 1..4 input channels (cn=%d)", cn);
-    const int ublocks = (W / 2 + D0U - 1) / D0U;
-    const dim3 grid((unsigned)(g.n * (H / 2) * ublocks));
+    const int ublocks = (W / 2 + D0U - 1) / D0U, Ho = H / 2;
+    // ~2 blocks per CU, each walking a run of gradient rows (its weights loaded once, each gradient row staged once)
+    const int want = std::max(1, 2 * fg::num_cus() / (g.n * ublocks));
+    const int rows = std::max(1, (Ho + want - 1) / want);
+    const dim3 grid((unsigned)(g.n * ublocks * ((Ho + rows - 1) / rows)));
     switch (cn) {
-        case 1: hipLaunchKernelGGL(d0_input_grad_kernel<1>, grid, dim3(256), 0, stream, g, w, ctot, c0, y, yc, H, W, accumulate, ublocks); break;
-        case 2: hipLaunchKernelGGL(d0_input_grad_kernel<2>, grid, dim3(256), 0, stream, g, w, ctot, c0, y, yc, H, W, accumulate, ublocks); break;
-        case 3: hipLaunchKernelGGL(d0_input_grad_kernel<3>, grid, dim3(256), 0, stream, g, w, ctot, c0, y, yc, H, W, accumulate, ublocks); break;
-        default: hipLaunchKernelGGL(d0_input_grad_kernel<4>, grid, dim3(256), 0, stream, g, w, ctot, c0, y, yc, H, W, accumulate, ublocks); break;
+        case 1: hipLaunchKernelGGL(d0_input_grad_kernel<1>, grid, dim3(256), 0, stream, g, w, ctot, c0, y, yc, H, W, accumulate, ublocks, rows); break;
+        case 2: hipLaunchKernelGGL(d0_input_grad_kernel<2>, grid, dim3(256), 0, stream, g, w, ctot, c0, y, yc, H, W, accumulate, ublocks, rows); break;
+        case 3: hipLaunchKernelGGL(d0_input_grad_kernel<3>, grid, dim3(256), 0, stream, g, w, ctot, c0, y, yc, H, W, accumulate, ublocks, rows); break;
+        default: hipLaunchKernelGGL(d0_input_grad_kernel<4>, grid, dim3(256), 0, stream, g, w, ctot, c0, y, yc, H, W, accumulate, ublocks, rows); break;
     }
     return fg::launched("d0_input_grad");
 }

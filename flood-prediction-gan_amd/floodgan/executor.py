@@ -523,24 +523,13 @@ def disc_act_decisions(S, lo=0, hi=None):
 # discriminator
 # ======================================================================================
 
-# D's input buffer with 9 < channels < 16 allocated as 16 zero-filled channels: model.0's packed row run (4 taps x C)
-# is then a multiple of 32 and its forward / weight gradient run on the pipelined kernels instead of the register-
-# staged ones (FLOODGAN_DISC_C16=0: C channels)
-DISC_C16 = os.environ.get("FLOODGAN_DISC_C16", "0") != "0"
-
-
-def disc_alloc(c_in_total):
-    return 16 if DISC_C16 and 8 < c_in_total < 16 else c_in_total
-
-
 def disc_pack(pairs, c_in_total):
     """Stack (a [N,Ca,H,W], b [N,Cb,H,W] or None) pairs along the batch into one zero-padded
-    NHWC input buffer (torch.cat((a, b), 1) of models/model.py:616-617, fused); channels past c_in_total (up to
-    disc_alloc) are zeros."""
+    NHWC input buffer (torch.cat((a, b), 1) of models/model.py:616-617, fused)."""
     a0 = pairs[0][0]
     N = sum(a.shape[0] for a, _ in pairs)
     H, W = a0.shape[2], a0.shape[3]
-    buf = Buf.empty(N, H, W, disc_alloc(c_in_total), 1, a0.device)
+    buf = Buf.empty(N, H, W, c_in_total, 1, a0.device)
     slot = ops.amax_slot(buf) if len(pairs) > 1 else None      # the parts raise one shared absmax slot
     img0 = 0
     for a, b in pairs:
