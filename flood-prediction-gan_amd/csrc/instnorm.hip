@@ -40,6 +40,11 @@ int choose_chunks(int n, long long hw, int target = 2048) {
 }
 
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+// non-temporal (streaming) load: for bytes read for the last time, so they do not displace reused ones from the
+// Infinity Cache
+__device__ __forceinline__ f32x4 ld4_nt(const float* p) {
+    return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+}
 
 __global__ void in_stats_kernel(fg_view src, int chunks, double* __restrict__ work) {
     const int C = src.c_alloc, L = C / 4, PG = NT / L;
@@ -346,7 +351,10 @@ __device__ __forceinline__ f32x4 fold_extra(f32x4 v, const fg_view& g, int fp, i
 }
 
 // statistics pass with kRowU pixels' loads in flight per thread (same chunking / work layout and the same
-// fp32 accumulation order per thread as in_bwd_stats_kernel: results are bit-identical)
+// fp32 accumulation order per thread as in_bwd_stats_kernel: results are bit-identical).  NTG: the gradient and gadd
+// are read non-temporally -- with gsum the apply pass reads the gathered sum instead of them, so they are dead after
+// this pass, and src + gsum (268 MB at the resblock shape) can stay in the 256-MB Infinity Cache for the apply pass
+template <bool NTG>
 __global__ void __launch_bounds__(NT) in_bwd_stats_u_kernel(fg_view g, int fp, fg_view gadd, fg_view src,
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ rstd, int act, int chunks,
@@ -374,9 +382,10 @@ __global__ void __launch_bounds__(NT) in_bwd_stats_u_kernel(fg_view g, int fp, f
                 xs[k] = x;
                 const bool ok = p + k * PG < p1;
                 sv[k] = ok ? ld4(src.ptr + fg::vidx(src, n, y, x) + 4 * c4) : f32x4{0.f, 0.f, 0.f, 0.f};
-                gv[k] = ok ? ld4(g.ptr + fg::vidx(g, n, y + fp, x + fp) + 4 * c4) : f32x4{0.f, 0.f, 0.f, 0.f};
-                av[k] = (ok && gadd.ptr) ? ld4(gadd.ptr + fg::vidx(gadd, n, y, x) + 4 * c4)
-                                         : f32x4{0.f, 0.f, 0.f, 0.f};
+                const float* gp = g.ptr + fg::vidx(g, n, y + fp, x + fp) + 4 * c4;
+                gv[k] = ok ? (NTG ? ld4_nt(gp) : ld4(gp)) : f32x4{0.f, 0.f, 0.f, 0.f};
+                const float* ap = gadd.ptr + fg::vidx(gadd, n, y, x) + 4 * c4;
+                av[k] = (ok && gadd.ptr) ? (NTG ? ld4_nt(ap) : ld4(ap)) : f32x4{0.f, 0.f, 0.f, 0.f};
                 x += PG;
                 while (x >= w) {
                     x -= w;
@@ -1073,9 +1082,15 @@ int in_bwd_impl(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, const flo
     float* coef = reinterpret_cast<float*>(work + (size_t)src.n * C * MAX_CHUNKS * 3);
     double* bpart = work + (size_t)src.n * C * MAX_CHUNKS * 3 + (size_t)src.n * C;
     float* gmax_part = split_slot ? reinterpret_cast<float*>(bpart + (size_t)src.n * C) : nullptr;
-    if (g_in_rows || split_slot)
-        hipLaunchKernelGGL(in_bwd_stats_u_kernel, dim3(chunks, src.n), dim3(NT), 0, stream, gsrc, fold_pad, gadd, src,
-                           mean, rstd, act, chunks, work, gsum, gmax_part);
+    static const bool nt_env = [] { const char* e = getenv("FLOODGAN_IN_NT"); return !e || atoi(e) != 0; }();
+    const char* nte = getenv("FLOODGAN_IN_NT_AB");          // A/B hook read per call (scripts/ab_step.py in_nt)
+    const bool ntg = gsum.ptr && (nte ? atoi(nte) != 0 : nt_env);
+    if ((g_in_rows || split_slot) && ntg)
+        hipLaunchKernelGGL(in_bwd_stats_u_kernel<true>, dim3(chunks, src.n), dim3(NT), 0, stream, gsrc, fold_pad, gadd,
+                           src, mean, rstd, act, chunks, work, gsum, gmax_part);
+    else if (g_in_rows || split_slot)
+        hipLaunchKernelGGL(in_bwd_stats_u_kernel<false>, dim3(chunks, src.n), dim3(NT), 0, stream, gsrc, fold_pad, gadd,
+                           src, mean, rstd, act, chunks, work, gsum, gmax_part);
     else
         hipLaunchKernelGGL(in_bwd_stats_kernel, dim3(chunks, src.n), dim3(NT), 0, stream, gsrc, fold_pad, gadd, src,
                            mean, rstd, act, chunks, work, gsum);

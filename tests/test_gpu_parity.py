@@ -478,11 +478,14 @@ def test_d0_input_grad(ctot, c0, cn, H, W, acc):
 
 
 @pytest.mark.parametrize("N,H,W,n_out,xpad", [(2, 20, 37, 10, 0), (3, 9, 64, 10, 1), (1, 5, 7, 16, 0), (2, 96, 96, 3, 0)])
-def test_conv1x1_head(N, H, W, n_out, xpad):
+@pytest.mark.parametrize("lanes", ["1", "0"])
+def test_conv1x1_head(N, H, W, n_out, xpad, lanes, monkeypatch):
     """the attention head's 1x1 conv in fp32 FMA (fg_conv1x1_*): forward (pad channels written as 0), input
-    gradient, weight + bias gradients (written and accumulated) against fp64, ragged last tiles"""
+    gradient (the gradient's padding channels NaN: never read), weight + bias gradients (written and accumulated)
+    against fp64, ragged last tiles; the lane forms (FLOODGAN_HEAD_LANES=1, the default) and the LDS-tile forms"""
     from floodgan import _lib as L, ops
     from floodgan.plans import Buf
+    monkeypatch.setenv("FLOODGAN_HEAD_LANES", lanes)
     torch.manual_seed(21)
     x = torch.randn(N, 64, H, W, dtype=torch.float64)
     w = (torch.randn(n_out, 64, 1, 1, dtype=torch.float64) * 0.1).requires_grad_(True)
@@ -501,6 +504,8 @@ def test_conv1x1_head(N, H, W, n_out, xpad):
     if n_out < 16:
         assert float(Y.nhwc()[..., n_out:].abs().max()) == 0.0
     GY = buf_from(gy, 0, "constant", c_alloc=16)
+    if n_out < 16:
+        GY.nhwc()[..., n_out:] = float("nan")
     GX = Buf.empty(N, H, W, 64, 0, DEV)
     ops.conv1x1_dgrad(GY, wd, n_out, GX)
     dw = torch.full(w.shape, 3.0, device=DEV)
