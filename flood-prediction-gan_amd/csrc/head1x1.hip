@@ -152,12 +152,13 @@ __global__ void __launch_bounds__(256) conv1x1_dgrad_kernel(fg_view gy, const fl
     }
 }
 
-// ---- lane forms (round 4): no LDS staging.  A wave takes 4 pixels per step, lane = (pixel group pg, channel quad
-// cq): the 16 lanes of a pixel read its 64 channels as one contiguous 256-B segment (forward) or the 16 lanes share
-// one 64-B gradient row (input gradient: identical addresses, one fetch); the weights sit in registers for the whole
-// launch; LU steps' loads are in flight together.  Forward: each lane forms the 16 outputs' partial dot products over
-// its 4 channels and a DPP reduce-scatter over the 16 lanes (4 exchange steps, halving the vector each time) leaves
-// output cq's sum in lane cq -- 64 B of logits written contiguously per pixel.
+// ---- the forward's lane form (round 4): no LDS staging.  A wave takes 4 pixels per step, lane = (pixel group pg,
+// channel quad cq): the 16 lanes of a pixel read its 64 channels as one contiguous 256-B segment; the weights sit in
+// registers for the whole launch; LU steps' loads are in flight together.  Each lane forms the 16 outputs' partial
+// dot products over its 4 channels and a DPP reduce-scatter over the 16 lanes (4 exchange steps, halving the vector
+// each time) leaves output cq's sum in lane cq -- 64 B of logits written contiguously per pixel: 176 -> 131 us at
+// bs 8, 512^2 (profiles/round4/r4p_kernel_stats_timed.csv).  The same form for the input gradient (the 16 lanes of a
+// pixel sharing its 64-B gradient row) ran 229 us against the LDS-tile kernel's 206 and was not kept.
 constexpr int LU = 4;
 
 template <int CTRL>
@@ -204,41 +205,7 @@ __global__ void __launch_bounds__(256) conv1x1_fwd_lanes(fg_view x, const float*
     }
 }
 
-__global__ void __launch_bounds__(256) conv1x1_dgrad_lanes(fg_view gy, const float* __restrict__ w, int n_out,
-                                                           fg_view gx) {
-    const long long P = (long long)gx.n * gx.h * gx.w;
-    const int lane = threadIdx.x & 63, pg = lane >> 4, cq = lane & 15;
-    const long long gw = (long long)blockIdx.x * 4 + (threadIdx.x >> 6), nw = (long long)gridDim.x * 4;
-    f32x4 wr[NO];
-#pragma unroll
-    for (int o = 0; o < NO; ++o) wr[o] = o < n_out ? ld4(w + o * CI + 4 * cq) : f32x4{0.f, 0.f, 0.f, 0.f};
-    const int q4 = (n_out + 3) / 4;
-    for (long long base = gw * 4 * LU; base < P; base += nw * 4 * LU) {
-        f32x4 g[LU][NO / 4];
-#pragma unroll
-        for (int u = 0; u < LU; ++u) {
-            const long long p = base + u * 4 + pg;
-            const float* gp = gy.ptr + (p < P ? pix_off_fast(gy, p) : 0);
-#pragma unroll
-            for (int q = 0; q < NO / 4; ++q) g[u][q] = (p < P && q < q4) ? ld4(gp + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-#pragma unroll
-        for (int u = 0; u < LU; ++u) {
-            f32x4 a = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int o = 0; o < NO; ++o) {
-                const float gv = o < n_out ? g[u][o / 4][o % 4] : 0.f;     // padding channels may hold anything
-                a[0] = fmaf(gv, wr[o][0], a[0]);
-                a[1] = fmaf(gv, wr[o][1], a[1]);
-                a[2] = fmaf(gv, wr[o][2], a[2]);
-                a[3] = fmaf(gv, wr[o][3], a[3]);
-            }
-            const long long p = base + u * 4 + pg;
-            if (p < P) st4(gx.ptr + pix_off_fast(gx, p) + 4 * cq, a);
-        }
-    }
-}
-
+// A/B and test hook: FLOODGAN_HEAD_LANES=0 runs the forward's LDS-tile kernel
 static bool lanes_on() { const char* e = getenv("FLOODGAN_HEAD_LANES"); return !e || atoi(e) != 0; }
 
 // block: pixels [blockIdx.x * per, +per) in tiles of TP; thread (o = t / 16, channel quad cq = t % 16)
@@ -335,12 +302,6 @@ FG_API int fg_conv1x1_dgrad(fg_view gy, const float* w, int n_out, fg_view gx, h
         return fg::fail(FG_ERR_INVALID, "fg_conv1x1_dgrad: bad args (n_out %d, gy.c_alloc %d, gx.c_alloc %d)", n_out,
                         gy.c_alloc, gx.c_alloc);
     const int P = gx.n * gx.h * gx.w;
-    if (lanes_on()) {
-        const long long steps = ((long long)P + 4 * LU - 1) / (4 * LU);
-        hipLaunchKernelGGL(conv1x1_dgrad_lanes, dim3((unsigned)std::min<long long>((steps + 3) / 4, 8 * fg::num_cus())),
-                           dim3(256), 0, stream, gy, w, n_out, gx);
-        return fg::launched("conv1x1_dgrad");
-    }
     const int ntiles = (P + TP - 1) / TP;
     hipLaunchKernelGGL(conv1x1_dgrad_kernel, dim3(std::min(ntiles, 4 * fg::num_cus())), dim3(256), 0, stream, gy, w,
                        n_out, gx);

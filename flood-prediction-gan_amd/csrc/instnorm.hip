@@ -45,6 +45,15 @@ __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<
 __device__ __forceinline__ f32x4 ld4_nt(const float* p) {
     return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
 }
+template <bool NTL>
+__device__ __forceinline__ f32x4 ldx(const float* p) { return NTL ? ld4_nt(p) : ld4(p); }
+// the apply passes' last reads of their inputs (the conv output, the residual / gradient): non-temporal A/B
+// (FLOODGAN_IN_NT2; FLOODGAN_IN_NT2_AB per call)
+bool in_nt2_on() {
+    static const bool env = [] { const char* e = getenv("FLOODGAN_IN_NT2"); return e && atoi(e) != 0; }();
+    const char* ab = getenv("FLOODGAN_IN_NT2_AB");
+    return ab ? atoi(ab) != 0 : env;
+}
 
 __global__ void in_stats_kernel(fg_view src, int chunks, double* __restrict__ work) {
     const int C = src.c_alloc, L = C / 4, PG = NT / L;
@@ -224,6 +233,7 @@ __device__ __forceinline__ void store_splitpix(char* px, const f32x4& o, float s
 // 64-bit divisions per element and held one load in flight: 5.0 TB/s).
 constexpr int kRowU = 4;
 
+template <bool NTL>
 __global__ void __launch_bounds__(NT) in_apply_rows_kernel(fg_view src, const float* __restrict__ mean,
                                                            const float* __restrict__ rstd, int act, fg_view res,
                                                            fg_view dst, int pad_mode, int lshift,
@@ -278,8 +288,8 @@ __global__ void __launch_bounds__(NT) in_apply_rows_kernel(fg_view src, const fl
                 const bool inside = x >= 0 && x < w;
                 ok[k] = xp < wp && (inside || reflect);
                 x = ok[k] ? fg::reflect_idx(x, w) : 0;
-                v[k] = ok[k] ? ld4(srow + (size_t)x * C) : f32x4{0.f, 0.f, 0.f, 0.f};
-                rv[k] = (ok[k] && rrow) ? ld4(rrow + (size_t)x * C) : f32x4{0.f, 0.f, 0.f, 0.f};
+                v[k] = ok[k] ? ldx<NTL>(srow + (size_t)x * C) : f32x4{0.f, 0.f, 0.f, 0.f};
+                rv[k] = (ok[k] && rrow) ? ldx<NTL>(rrow + (size_t)x * C) : f32x4{0.f, 0.f, 0.f, 0.f};
             }
 #pragma unroll
             for (int k = 0; k < kRowU; ++k) {
@@ -628,6 +638,7 @@ __global__ void in_bwd_apply_kernel(fg_view g, int fp, fg_view gadd, fg_view src
 }
 
 // row form of the backward apply (C/4 | 256): block = one padded output row, kRowU pixels' loads in flight
+template <bool NTL>
 __global__ void __launch_bounds__(NT) in_bwd_apply_rows_kernel(fg_view g, int fp, fg_view gadd, fg_view src,
                                                                const float* __restrict__ mean,
                                                                const float* __restrict__ rstd,
@@ -672,9 +683,9 @@ __global__ void __launch_bounds__(NT) in_bwd_apply_rows_kernel(fg_view g, int fp
             for (int k = 0; k < kRowU; ++k) {
                 const int x = xp0 + k * PG - pad;
                 ok[k] = x >= 0 && x < w;
-                sv[k] = ok[k] ? ld4(srow + (size_t)x * C) : z;
-                gv[k] = ok[k] ? ld4(grow + (size_t)x * C) : z;
-                av[k] = (ok[k] && arow) ? ld4(arow + (size_t)x * C) : z;
+                sv[k] = ok[k] ? ldx<NTL>(srow + (size_t)x * C) : z;
+                gv[k] = ok[k] ? ldx<NTL>(grow + (size_t)x * C) : z;
+                av[k] = (ok[k] && arow) ? ldx<NTL>(arow + (size_t)x * C) : z;
             }
 #pragma unroll
             for (int k = 0; k < kRowU; ++k) {
@@ -1030,7 +1041,8 @@ int in_apply_impl(fg_view src, const float* mean, const float* rstd, int act, fg
         return fg::fail(FG_ERR_INVALID, "fg_in_apply: reflect pad too large");
     const int C4 = dst.c_alloc / 4;
     if ((g_in_rows || split_slot || ps_ptr) && NT % C4 == 0) {
-        hipLaunchKernelGGL(in_apply_rows_kernel, dim3(dst.n * (dst.h + 2 * dst.pad)), dim3(NT), 0, stream, src, mean,
+        auto kern = in_nt2_on() ? in_apply_rows_kernel<true> : in_apply_rows_kernel<false>;
+        hipLaunchKernelGGL(kern, dim3(dst.n * (dst.h + 2 * dst.pad)), dim3(NT), 0, stream, src, mean,
                            rstd, act, residual, dst, pad_mode, ilog2(C4), reinterpret_cast<unsigned*>(absmax),
                            split_slot, ps_ptr, ps_slot, res_amax, splitpix);
         return fg::launched("in_apply_rows");
@@ -1104,7 +1116,8 @@ int in_bwd_impl(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, const flo
     // with gsum the apply pass reads the gathered gradient the statistics pass wrote (one read, no fold)
     const fg_view none = {nullptr, 0, 0, 0, 0, 0};
     if (g_in_rows || split_slot) {
-        hipLaunchKernelGGL(in_bwd_apply_rows_kernel, dim3(dst.n * (dst.h + 2 * dst.pad)), dim3(NT), 0, stream,
+        auto kern = in_nt2_on() ? in_bwd_apply_rows_kernel<true> : in_bwd_apply_rows_kernel<false>;
+        hipLaunchKernelGGL(kern, dim3(dst.n * (dst.h + 2 * dst.pad)), dim3(NT), 0, stream,
                            gsum.ptr ? gsum : gsrc, gsum.ptr ? 0 : fold_pad, gsum.ptr ? none : gadd, src, mean, rstd,
                            coef, act, dst, reinterpret_cast<unsigned*>(absmax), bpart, bias_grad, bias_accumulate,
                            ilog2(C / 4), split_slot);

@@ -482,7 +482,7 @@ def test_d0_input_grad(ctot, c0, cn, H, W, acc):
 def test_conv1x1_head(N, H, W, n_out, xpad, lanes, monkeypatch):
     """the attention head's 1x1 conv in fp32 FMA (fg_conv1x1_*): forward (pad channels written as 0), input
     gradient (the gradient's padding channels NaN: never read), weight + bias gradients (written and accumulated)
-    against fp64, ragged last tiles; the lane forms (FLOODGAN_HEAD_LANES=1, the default) and the LDS-tile forms"""
+    against fp64, ragged last tiles; the forward's lane form (FLOODGAN_HEAD_LANES=1, the default) and its LDS-tile form"""
     from floodgan import _lib as L, ops
     from floodgan.plans import Buf
     monkeypatch.setenv("FLOODGAN_HEAD_LANES", lanes)
