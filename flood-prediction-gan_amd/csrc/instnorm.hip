@@ -47,10 +47,11 @@ __device__ __forceinline__ f32x4 ld4_nt(const float* p) {
 }
 template <bool NTL>
 __device__ __forceinline__ f32x4 ldx(const float* p) { return NTL ? ld4_nt(p) : ld4(p); }
-// the apply passes' last reads of their inputs (the conv output, the residual / gradient): non-temporal A/B
-// (FLOODGAN_IN_NT2; FLOODGAN_IN_NT2_AB per call)
+// the apply passes' last reads of their inputs (the conv output, the residual / gradient) are non-temporal: the
+// Infinity Cache then keeps the output the next conv reads instead of bytes never read again -- step 46.08 -> 45.60
+// ms (profiles/round4/r4q_ab_in_nt2.log); FLOODGAN_IN_NT2=0 turns it off, FLOODGAN_IN_NT2_AB is read per call (A/B)
 bool in_nt2_on() {
-    static const bool env = [] { const char* e = getenv("FLOODGAN_IN_NT2"); return e && atoi(e) != 0; }();
+    static const bool env = [] { const char* e = getenv("FLOODGAN_IN_NT2"); return !e || atoi(e) != 0; }();
     const char* ab = getenv("FLOODGAN_IN_NT2_AB");
     return ab ? atoi(ab) != 0 : env;
 }
