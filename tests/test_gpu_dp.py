@@ -89,11 +89,13 @@ def test_two_rank_step_equals_single_rank(kind, n, res, tmp_path, report):
         skip = {k: (O.cancelled_biases()[0] if "generator" in k else O.cancelled_biases()[1])
                 for k in W.nets(m, kind)}
     worst, same = ("", 0.0), True
-    # after updates, an element whose gradient sits at rounding level may take either Adam direction (a sign-like step
-    # of up to lr per iteration in either run): such elements may differ by up to 2 lr per iteration; everything
-    # else agrees to rounding.  Asserted: no element beyond that bound, at most 1 % of a tensor's elements at it
+    # after updates the two runs' parameters can differ element-wise by at most two opposite Adam steps per iteration
+    # (|step| <= lr at step 1, <= 1.054 lr at step 2 for these betas): an element whose gradient sits at rounding level may take either
+    # sign-like direction, and Adam's normalisation amplifies rounding-level gradient differences up to that bound.
+    # Asserted: no element beyond it (a DP bug -- a missing / doubled bucket, a stale replica -- shows in the
+    # iteration-0 gradients above, which must agree to 1e-5)
     lr = max(g["lr"] for o in (m.optimizer_generator, m.optimizer_discriminator) for g in o.param_groups)
-    step_bound = 2 * lr * iters * 1.01
+    step_bound = 2 * lr * iters * 1.1      # |Adam step| <= 1.054 lr at step 2 for betas (0.5, 0.999) (Cauchy-Schwarz)
     worst_flip = ("", 0.0)
     # the all-reduced iteration-0 gradients equal the whole-batch gradients up to summation order;
     # the paired G step already sees Adam(D), whose elements with rounding-level gradients (undecided
@@ -113,13 +115,13 @@ def test_two_rank_step_equals_single_rank(kind, n, res, tmp_path, report):
             if e > worst[1]:
                 worst = (f"{net}/{k}", e)
             if a.is_floating_point():
-                d = (a.double() - v.double().cpu()).abs()
-                assert float(d.max()) <= step_bound, (f"{net}/{k}", float(d.max()), step_bound)
-                frac = float((d > 1e-5 * (v.double().cpu().abs() + 1e-3)).double().mean())
-                if frac > worst_flip[1]:
-                    worst_flip = (f"{net}/{k}", frac)
+                d = float((a.double() - v.double().cpu()).abs().max())
+                assert d <= step_bound, (f"{net}/{k}", d, step_bound)
+                if d > worst_flip[1]:
+                    worst_flip = (f"{net}/{k}", d)
     report("dp_two_rank_vs_single", kind=kind, n=n, res=res, loss_rel=lrel.tolist(), worst_param=worst,
-           worst_flip_fraction=worst_flip, worst_grad_it0=gworst, worst_grad_it0_after_adam_d=gworst_post,
+           worst_element_diff=worst_flip, step_bound=step_bound, worst_grad_it0=gworst,
+           worst_grad_it0_after_adam_d=gworst_post,
            replicas_identical=bool(same))
     assert same
     assert gworst[1] < 1e-5 and gworst_post[1] < 1e-4, (gworst, gworst_post)
@@ -127,10 +129,9 @@ def test_two_rank_step_equals_single_rank(kind, n, res, tmp_path, report):
     # G loss [2] already sees Adam(D): P3 like everything after an update)
     pre = [0, 1, 3] if kind == "paired" else list(range(lrel.shape[1]))
     assert lrel[0][pre].max() < 1e-5, lrel
-    # after updates: the iteration-0 gradients agree to summation order (above), so only elements whose
-    # gradient is at rounding level can take a different Adam direction: at most 2 lr per iteration each (asserted
-    # element-wise above) and few of them; the losses stay within the P3 bound
-    assert lrel.max() < 1e-3 and worst_flip[1] < 0.01, (lrel, worst, worst_flip)
+    # after updates: every element within two Adam steps per iteration (asserted above); the losses stay within the
+    # P3 bound
+    assert lrel.max() < 1e-3, (lrel, worst, worst_flip)
 
 
 def test_two_rank_paired_f16x3_vs_fp64(tmp_path, report):
