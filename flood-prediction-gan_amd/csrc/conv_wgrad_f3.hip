@@ -61,9 +61,7 @@ __device__ __forceinline__ void split4(const f32x4& v, float s, f16x4& h, f16x4&
 // the partner wave's MFMAs instead of stalling the SIMD at the top of every stage).
 // PS bit 0 / bit 1: P / X arrive in the FG_PRESPLIT format (include/floodgan.h): a float4 slot then holds
 // the h (col % 8 == 0) or the l (col % 8 == 4) piece of its 8-channel group, written to its image as it stands
-// XNT: the X operand (the layer's saved input, read here for the last time) is loaded non-temporally, so the Infinity
-// Cache keeps the output gradient P that the input-gradient conv reads next
-template <int TA, int SCH, int PS = 0, bool XNT = false>
+template <int TA, int SCH, int PS = 0>
 __global__ void __launch_bounds__(512, 1)
 conv_wgrad_f3_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
     // 8 waves as NWA (a) x NWK (k); wave tile 64 (a) x WK (k): TA 256 -> 4 x 2, 64 x 128; TA 128 -> 2 x 4, 64 x 64;
@@ -128,8 +126,7 @@ conv_wgrad_f3_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
             const int pb = wi[i] * (int)P.spn + wa_[i] * (int)P.spa + wb[i] * (int)P.spb + a0 + col;
             const int xb = wi[i] * (int)P.sxn + wa_[i] * (int)P.sxa + wb[i] * (int)P.sxb + x_koff;
             rp[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(pr, ok && p_col_ok ? pb * 4 : kOOB, 0, 0));
-            rx[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, ok && x_koff >= 0 ? xb * 4 : kOOB, 0,
-                                                                                     XNT ? 2 : 0));   // 2: nt
+            rx[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, ok && x_koff >= 0 ? xb * 4 : kOOB, 0, 0));
             // advance by BR pixels
             wm[i] += BR;
             wb[i] += b32;
@@ -273,13 +270,6 @@ int g_wgrad_f3 = 2;   // fg_set_wgrad_f3 (A/B hook): 0 off, 1 stage schedule 0, 
 
 namespace fgc {
 
-// A/B (FLOODGAN_WG_XNT; FLOODGAN_WG_XNT_AB per call): non-temporal X loads in the resblock weight gradient
-static bool wg_xnt_on() {
-    static const bool env = [] { const char* e = getenv("FLOODGAN_WG_XNT"); return e && atoi(e) != 0; }();
-    const char* ab = getenv("FLOODGAN_WG_XNT_AB");
-    return ab ? atoi(ab) != 0 : env;
-}
-
 // Returns 1 when the pipelined kernel took the problem (status in *rc), 0 when it does not apply.
 int launch_wgrad_f3(const fg_wgrad_problem& p, hipStream_t stream, int* rc) {
     // (K >= 256: D model.0's K = 192 ran 199 us here against 185 on the register-staged kernel, r3ae)
@@ -308,8 +298,6 @@ int launch_wgrad_f3(const fg_wgrad_problem& p, hipStream_t stream, int* rc) {
                 hipLaunchKernelGGL((conv_wgrad_f3_kernel<256, 0, 1>), grid, dim3(512), 0, stream, p, ta, tk);
             else if (ps == 2)
                 hipLaunchKernelGGL((conv_wgrad_f3_kernel<256, 0, 2>), grid, dim3(512), 0, stream, p, ta, tk);
-            else if (wg_xnt_on())
-                hipLaunchKernelGGL((conv_wgrad_f3_kernel<256, 0, 3, true>), grid, dim3(512), 0, stream, p, ta, tk);
             else
                 hipLaunchKernelGGL((conv_wgrad_f3_kernel<256, 0, 3>), grid, dim3(512), 0, stream, p, ta, tk);
         } else {

@@ -50,12 +50,6 @@ __device__ __forceinline__ f32x4 ldx(const float* p) { return NTL ? ld4_nt(p) : 
 // the apply passes' last reads of their inputs (the conv output, the residual / gradient) are non-temporal: the
 // Infinity Cache then keeps the output the next conv reads instead of bytes never read again -- step 46.08 -> 45.60
 // ms (profiles/round4/r4q_ab_in_nt2.log); FLOODGAN_IN_NT2=0 turns it off, FLOODGAN_IN_NT2_AB is read per call (A/B)
-// A/B (FLOODGAN_IN_NTS; FLOODGAN_IN_NTS_AB per call): the dual apply's fp32 output stored non-temporally
-bool in_nts_on() {
-    static const bool env = [] { const char* e = getenv("FLOODGAN_IN_NTS"); return e && atoi(e) != 0; }();
-    const char* ab = getenv("FLOODGAN_IN_NTS_AB");
-    return ab ? atoi(ab) != 0 : env;
-}
 bool in_nt2_on() {
     static const bool env = [] { const char* e = getenv("FLOODGAN_IN_NT2"); return !e || atoi(e) != 0; }();
     const char* ab = getenv("FLOODGAN_IN_NT2_AB");
@@ -240,7 +234,7 @@ __device__ __forceinline__ void store_splitpix(char* px, const f32x4& o, float s
 // 64-bit divisions per element and held one load in flight: 5.0 TB/s).
 constexpr int kRowU = 4;
 
-template <bool NTL, bool NTS>
+template <bool NTL>
 __global__ void __launch_bounds__(NT) in_apply_rows_kernel(fg_view src, const float* __restrict__ mean,
                                                            const float* __restrict__ rstd, int act, fg_view res,
                                                            fg_view dst, int pad_mode, int lshift,
@@ -317,13 +311,7 @@ __global__ void __launch_bounds__(NT) in_apply_rows_kernel(fg_view src, const fl
                     store_presplit(drow + (size_t)xp * C, o, ss, c4 & 1);
                 } else {
                     am = max(am, absbits4(o));
-                    // dual output: the fp32 residual stream is next read three launches later (the next block's
-                    // residual add, by then out of the cache anyway) -- streamed past the Infinity Cache (NTS), which
-                    // keeps the pre-split copy conv1 reads next
-                    if (NTS && psrow)
-                        __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(drow + (size_t)xp * C));
-                    else
-                        *reinterpret_cast<f32x4*>(drow + (size_t)xp * C) = o;
+                    *reinterpret_cast<f32x4*>(drow + (size_t)xp * C) = o;
                     if (psrow) store_presplit(psrow + (size_t)xp * C, o, ss, c4 & 1);
                 }
             }
@@ -1054,9 +1042,7 @@ int in_apply_impl(fg_view src, const float* mean, const float* rstd, int act, fg
         return fg::fail(FG_ERR_INVALID, "fg_in_apply: reflect pad too large");
     const int C4 = dst.c_alloc / 4;
     if ((g_in_rows || split_slot || ps_ptr) && NT % C4 == 0) {
-        const bool nts = in_nts_on() && ps_ptr;
-        auto kern = in_nt2_on() ? (nts ? in_apply_rows_kernel<true, true> : in_apply_rows_kernel<true, false>)
-                                : (nts ? in_apply_rows_kernel<false, true> : in_apply_rows_kernel<false, false>);
+        auto kern = in_nt2_on() ? in_apply_rows_kernel<true> : in_apply_rows_kernel<false>;
         hipLaunchKernelGGL(kern, dim3(dst.n * (dst.h + 2 * dst.pad)), dim3(NT), 0, stream, src, mean,
                            rstd, act, residual, dst, pad_mode, ilog2(C4), reinterpret_cast<unsigned*>(absmax),
                            split_slot, ps_ptr, ps_slot, res_amax, splitpix);

@@ -1,7 +1,7 @@
 """A/B of engine switches on the full bs-8 512^2 training step, interleaved in ONE process (device
 clocks and boxes differ by several percent, so separate bench runs cannot resolve small gains).
   python scripts/ab_step.py f3_persistent [rounds] [steps] [values, default 0,1]
-Switches: f3_persistent, f3_sched, f3_order, f3_fill, f3_interleave, head_1x1, wgrad_f3, use_win, in_rows, presplit, ps_wide (values 4,5), ps_resid, stem_fwd, splitpix, d0_dgrad, in_nt, in_nt2, head_lanes, wg_xnt, in_nts."""
+Switches: f3_persistent, f3_sched, f3_order, f3_fill, f3_interleave, head_1x1, wgrad_f3, use_win, in_rows, presplit, ps_wide (values 4,5), ps_resid, stem_fwd, splitpix, d0_dgrad, in_nt, in_nt2, head_lanes."""
 import os
 import sys
 import time
@@ -46,10 +46,6 @@ def switch(name, on):
         os.environ["FLOODGAN_STEM_FWD"] = str(int(on))
     elif name == "head_lanes":
         os.environ["FLOODGAN_HEAD_LANES"] = str(int(on))
-    elif name == "in_nts":
-        os.environ["FLOODGAN_IN_NTS_AB"] = str(int(on))
-    elif name == "wg_xnt":
-        os.environ["FLOODGAN_WG_XNT_AB"] = str(int(on))
     elif name == "in_nt2":
         os.environ["FLOODGAN_IN_NT2_AB"] = str(int(on))
     elif name == "in_nt":
