@@ -884,14 +884,17 @@ def test_fused_in_stats_declined():
 
 # ------------------------------------------------------------------ tail, losses, adam
 
-def test_tail():
+@pytest.mark.parametrize("H,W", [(16, 16), (19, 300)])
+def test_tail(H, W):
+    """Generator tail forward / backward; (19, 300): the 256-pixel blocks of the LDS-staged kernels
+    straddle rows, images and g_content's zero border."""
     from floodgan import ops
     from floodgan.plans import Buf
     torch.manual_seed(4)
-    N, H = 2, 16
-    cl = torch.randn(N, 27, H, H, dtype=torch.float64, requires_grad=True)
-    al = torch.randn(N, 10, H, H, dtype=torch.float64, requires_grad=True)
-    x = torch.randn(N, 9, H, H, dtype=torch.float64)
+    N = 2
+    cl = torch.randn(N, 27, H, W, dtype=torch.float64, requires_grad=True)
+    al = torch.randn(N, 10, H, W, dtype=torch.float64, requires_grad=True)
+    x = torch.randn(N, 9, H, W, dtype=torch.float64)
     t = torch.tanh(cl)
     a = torch.softmax(al, 1)
     out = sum(t[:, 3 * i:3 * i + 3] * a[:, i:i + 1] for i in range(9)) + x[:, :3] * a[:, 9:10]
@@ -900,12 +903,14 @@ def test_tail():
     CL = buf_from(cl.detach(), 0, "constant", 32)
     AL = buf_from(al.detach(), 0, "constant", 16)
     xd = x.float().to(DEV)
-    o = torch.empty(N, 3, H, H, device=DEV)
-    mk = torch.empty(N, H, H, device=DEV)
+    o = torch.empty(N, 3, H, W, device=DEV)
+    mk = torch.empty(N, H, W, device=DEV)
     ops.tail_fwd(CL, AL, xd, o, mk)
     assert nrel(o, out) < KTOL and nrel(mk, a[:, 9]) < KTOL
-    GC = Buf.empty(N, H, H, 32, 6, DEV)
-    GA = Buf.empty(N, H, H, 16, 0, DEV)
+    GC = Buf.empty(N, H, W, 32, 6, DEV)
+    GA = Buf.empty(N, H, W, 16, 0, DEV)
+    GC.t.fill_(float("nan"))
+    GA.t.fill_(float("nan"))
     ops.tail_bwd(CL, AL, xd, g.float().to(DEV), GC, GA)
     torch.cuda.synchronize()
     assert nrel(nchw(GC, 27), gcl_ref) < KTOL and nrel(nchw(GA, 10), gal_ref) < KTOL
@@ -917,7 +922,7 @@ def test_tail():
         assert float(GA.t._fg_amax.max()) == float(GA.t.abs().max())
         assert ops.absmax(GC) is GC.t._fg_amax          # cached: no separate pass
     # a loss on last_attention_mask (attention10) as well: its gradient joins attention channel 9's
-    gm = torch.randn(N, H, H, dtype=torch.float64)
+    gm = torch.randn(N, H, W, dtype=torch.float64)
     gcl_ref2, gal_ref2 = torch.autograd.grad((out, a[:, 9]), (cl, al), (g, gm))
     gm_d = gm.float().to(DEV).permute(1, 2, 0).contiguous().permute(2, 0, 1)     # a strided [N, H, W] view
     ops.tail_bwd(CL, AL, xd, g.float().to(DEV), GC, GA, g_mask=gm_d)
