@@ -232,6 +232,190 @@ __global__ void __launch_bounds__(NW * 64, 1) conv_win_kernel(const WinArgs args
     }
 }
 
+// C = 64 forward, two workgroups per CU: a workgroup of 4 waves x 64 rows walks 14 "phases" -- one kernel row's
+// 32-channel half each: the strip's half pixels (268 px x 128 B, in the 32-channel chunk swizzle) and that half of
+// the row's 7 taps of weights (28 KB), 63 KB of LDS -- so two workgroups share a CU and one's copy / barriers run
+// under the other's MFMAs (the 8-wave kernel above holds 123 KB: one workgroup per CU, every wave idle during each
+// row's copy).  Per tap and wave: 8 A + 4 B fragment reads for 24 MFMAs (512 LDS bytes per MFMA, was 683), the
+// next tap's fragments read ahead of the current MFMAs.
+template <int KW>
+__global__ void __launch_bounds__(256, 2) conv_win2_kernel(const WinArgs args) {
+    constexpr int C = 64, CH = 32, NT = 256, BM = 256, TN = 2, TM = 4, WM = 64;
+    constexpr int PB = 2 * CH * 2;                              // LDS strip bytes per pixel: h | l of the half
+    constexpr int NR = TN * 16;
+    constexpr int STRIP_PIX = BM + 2 * (KW - 1);
+    constexpr int STRIP_CH = STRIP_PIX * PB / 16;               // 16-B chunks
+    constexpr int SCH = (STRIP_CH + NT - 1) / NT;
+    constexpr int W_TAP = 2 * NR * CH * 2;                      // [pc][NR][CH] fp16 per tap
+    constexpr int TAP_CH = W_TAP / 16;
+    constexpr int W_CH = KW * TAP_CH;
+    constexpr int WCH = (W_CH + NT - 1) / NT;
+    constexpr int W_OFF = (STRIP_PIX * PB + 1023) / 1024 * 1024;
+    __shared__ __attribute__((aligned(1024))) char smem[W_OFF + KW * W_TAP];
+
+    const fg_conv_problem& P = args.P;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wid = fg::xcd_remap(blockIdx.x, gridDim.x);
+    const int img = wid / args.tiles_per_img;
+    const int p0 = (wid - img * args.tiles_per_img) * BM;
+    const int mab = P.m_a * P.m_b;
+    const int a0 = p0 / P.m_b, b0 = p0 - (p0 / P.m_b) * P.m_b;
+    const int len0 = min(BM, min(P.m_b - b0, mab - p0));
+    const int len1 = (a0 + 1 < P.m_a) ? min(BM - len0, P.m_b) : 0;
+    const int s0pix = len0 + KW - 1;
+    const int npix = len0 + len1 + 2 * (KW - 1);
+    const int wp = args.wp;
+    constexpr int kOOB = 0x7fffffff;
+
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)args.xs, 0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)P.w, 0, 0x7fffffff, 0x00020000);
+
+    // LDS strip chunk o (pixel q = o / 8, slot j): slot j holds the half's logical chunk L = j ^ swz_pixel<32>(x)
+    // (0..3: h of channels 8L.., 4..7: l), which sits in the 64-channel split pixel at chunk g ^ swz_pixel<64>(x),
+    // g = 4 hc + L (h) or 8 + 4 hc + L - 4 (l)
+    const int seg0_pix = img * (int)(P.sxn / C) + a0 * wp + b0;
+    const int seg1_pix = img * (int)(P.sxn / C) + (a0 + 1) * wp;
+    int s_src0[SCH], s_src1[SCH];
+#pragma unroll
+    for (int i = 0; i < SCH; ++i) {
+        const int o = tid + i * NT, q = o >> 3, j = o & 7;
+        const bool live = o < STRIP_CH && q < npix;
+        const int x = q < s0pix ? b0 + q : q - s0pix;          // padded column of the strip pixel
+        const int pix = q < s0pix ? seg0_pix + q : seg1_pix + (q - s0pix);
+        const int L = j ^ fgc::swz_pixel<CH>(x);
+        const int sw = fgc::swz_pixel<C>(x);
+        const int g0 = L < 4 ? L : 4 + L, g1 = g0 + 4;          // logical chunk in half 0 / half 1
+        s_src0[i] = live ? pix * (4 * C) + ((g0 ^ sw) << 4) : -1;
+        s_src1[i] = live ? pix * (4 * C) + ((g1 ^ sw) << 4) : -1;
+    }
+    // weight chunk F of the half-row image [s][pc][NR][CH] (chunk slots swizzled as swz_wrow<32>)
+    int w_src[WCH];
+#pragma unroll
+    for (int i = 0; i < WCH; ++i) {
+        const int F = tid + i * NT, s = F / TAP_CH, f = F - s * TAP_CH;
+        const int pc = f / (NR * CH / 8);
+        const int rem = f - pc * (NR * CH / 8);
+        const int n = rem / (CH / 8);
+        const int ch = (rem - n * (CH / 8)) ^ swz_wrow<CH>(n);
+        w_src[i] = F >= W_CH ? -1 : (min(n, P.n_out - 1) * (P.ldw / 8) + ch) * 32 + pc * 16 + ((s * C) / 8) * 32;
+    }
+    f32x4 rs[SCH], rw[WCH];
+    auto load = [&](int ph) {
+        const int r = ph >> 1, hc = ph & 1;
+        const int soff = r * wp * (4 * C), woff = ((r * P.jp) / 8) * 32 + hc * (CH / 8) * 32;
+#pragma unroll
+        for (int i = 0; i < SCH; ++i) {
+            const int src = hc ? s_src1[i] : s_src0[i];
+            rs[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, src >= 0 ? src + soff : kOOB, 0, 0));
+        }
+#pragma unroll
+        for (int i = 0; i < WCH; ++i)
+            rw[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(wr, w_src[i] >= 0 ? w_src[i] + woff : kOOB, 0, 0));
+    };
+    auto store = [&]() {
+#pragma unroll
+        for (int i = 0; i < SCH; ++i)
+            if (s_src0[i] >= 0) *reinterpret_cast<f32x4*>(smem + (tid + i * NT) * 16) = rs[i];
+#pragma unroll
+        for (int i = 0; i < WCH; ++i)
+            if (w_src[i] >= 0) *reinterpret_cast<f32x4*>(smem + W_OFF + (tid + i * NT) * 16) = rw[i];
+    };
+
+    const float sa = fgc::pow2_scale(P.x_absmax);
+    const float sb = fgc::pow2_scale(P.w_absmax);
+    const float out_scale = 1.f / (sa * sb);
+
+    const int fr = lane & 15, g = lane >> 4;
+    int q0[TM], x0[TM];
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) {
+        const int i = wave * WM + tm * 16 + fr;
+        q0[tm] = i < len0 ? i : i + KW - 1;
+        x0[tm] = i < len0 ? b0 + i : i - len0;
+    }
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    struct Frags {
+        f16x8 ah[TM], al[TM], bh[TN], bl[TN];
+    };
+    auto read = [&](int s, Frags& f) {
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) {
+            const char* px = smem + (q0[tm] + s) * PB;
+            const int sw = fgc::swz_pixel<CH>(x0[tm] + s);
+            f.ah[tm] = *reinterpret_cast<const f16x8*>(px + (g ^ sw) * 16);
+            f.al[tm] = *reinterpret_cast<const f16x8*>(px + ((4 + g) ^ sw) * 16);
+        }
+        const char* wb = smem + W_OFF + s * W_TAP;
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+            const int n = tn * 16 + fr;
+            const char* row = wb + n * (2 * CH) + (g ^ swz_wrow<CH>(n)) * 16;
+            f.bh[tn] = *reinterpret_cast<const f16x8*>(row);
+            f.bl[tn] = *reinterpret_cast<const f16x8*>(row + NR * 2 * CH);
+        }
+    };
+    auto mma = [&](const Frags& f) {
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) {
+                acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f.al[tm], f.bh[tn], acc[tm][tn], 0, 0, 0);
+                acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f.ah[tm], f.bl[tn], acc[tm][tn], 0, 0, 0);
+                acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f.ah[tm], f.bh[tn], acc[tm][tn], 0, 0, 0);
+            }
+    };
+
+    const int NPH = 2 * P.kh;
+    load(0);
+    store();
+    __syncthreads();
+    for (int ph = 0; ph < NPH; ++ph) {
+        if (ph + 1 < NPH) load(ph + 1);
+#pragma unroll
+        for (int s = 0; s < KW; ++s) {
+            Frags f;
+            read(s, f);
+            mma(f);
+        }
+        if (ph + 1 < NPH) {
+            __syncthreads();
+            store();
+            __syncthreads();
+        }
+    }
+
+    // ---- epilogue (as conv_win_kernel)
+    const int act = P.act;
+    const bool accum = P.accumulate != 0;
+    float bias_v[TN];
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) bias_v[tn] = P.bias ? P.bias[min(tn * 16 + fr, P.n_out - 1)] : 0.f;
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) {
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {
+            const int i = wave * WM + tm * 16 + 4 * g + reg;
+            if (i >= len0 + len1) continue;
+            const int a = i < len0 ? a0 : a0 + 1, b = i < len0 ? b0 + i : i - len0;
+            float* yrow = P.y + img * P.syn + a * P.sya + b * P.syb;
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) {
+                const int n = tn * 16 + fr;
+                if (n >= P.n_out) continue;
+                float v = fg::act_fwd(acc[tm][tn][reg] * out_scale + bias_v[tn], act);
+                float* dst = yrow + n * P.syc;
+                if (accum) v += *dst;
+                *dst = v;
+            }
+        }
+    }
+}
+
 // 8 waves (two per SIMD, 32 rows each: a partner wave's MFMAs cover each wave's fragment-read latency; 4 waves of 64
 // rows ran 1.31 ms on both geometries, profiles/round4/r4c_ab_win.log)
 template <int C, int KW, int TN>
@@ -244,6 +428,15 @@ int launch_win(const WinArgs& a, int tiles, hipStream_t stream) {
             hipLaunchKernelGGL((conv_win_kernel<C, KW, TN, 8, 512>), dim3(b.tiles_per_img * a.P.m_img), dim3(512), 0,
                                stream, b);
             return fg::launched("conv_win");
+        }
+    }
+    if constexpr (C == 64) {
+        // the forward on two 4-wave workgroups per CU (1201 -> 1078 us, profiles/round4/r4z_bench_win.log;
+        // A/B: FLOODGAN_WIN_2WG=0 runs the 8-wave kernel)
+        const char* e = getenv("FLOODGAN_WIN_2WG");
+        if (!(e && atoi(e) == 0)) {
+            hipLaunchKernelGGL((conv_win2_kernel<KW>), dim3(tiles), dim3(256), 0, stream, a);
+            return fg::launched("conv_win2");
         }
     }
     hipLaunchKernelGGL((conv_win_kernel<C, KW, TN, 8>), dim3(tiles), dim3(512), 0, stream, a);

@@ -36,17 +36,20 @@ def main():
     for name, prob, out, flops in (("content fwd 7x7 64->27 @512", fwd, cl, 2.0 * N * 512 * 512 * 27 * 64 * 49),
                                    ("content dgrad 7x7 27->64 @518", dgr, Y, 2.0 * N * 518 * 518 * 64 * 27 * 49)):
         ref = None
+        # the input gradient's tile rows (FLOODGAN_WIN_BM); the forward's kernel (FLOODGAN_WIN_2WG: 1 = two 4-wave
+        # workgroups per CU over channel-half phases, the default; 0 = one 8-wave workgroup per CU)
+        var = ("FLOODGAN_WIN_BM", ("512", "256")) if "dgrad" in name else ("FLOODGAN_WIN_2WG", ("0", "1"))
         for _ in range(2):
-            for bm in ("512", "256"):      # the input gradient's tile rows (FLOODGAN_WIN_BM; the forward: 256)
-                os.environ["FLOODGAN_WIN_BM"] = bm
+            for v in var[1]:
+                os.environ[var[0]] = v
                 out.t.zero_()
                 ms = min(time_it(lambda: ops.conv_win(prob)) for _ in range(3))
                 if ref is None:
                     ref = out.t.clone()
                 d = float((out.t - ref).norm() / ref.norm())
-                print(f"{name:32s} bm={bm} {ms * 1e3:8.1f} us {flops / ms / 1e9:7.1f} TFLOP/s  rel diff {d:.1e}",
+                print(f"{name:32s} {var[0][9:]}={v} {ms * 1e3:8.1f} us {flops / ms / 1e9:7.1f} TFLOP/s  rel diff {d:.1e}",
                       flush=True)
-        os.environ.pop("FLOODGAN_WIN_BM")
+        os.environ.pop(var[0])
 
 
 if __name__ == "__main__":

@@ -1,5 +1,5 @@
 """Run one conv-engine launch shape repeatedly (for rocprofv3 counter passes).
-  python scripts/conv_one.py [fwd|fwd_stats|fwd_stats_ps|wgrad|dgrad_ps|wgrad_ps|stem_fwd|stem_wgrad] [reps]
+  python scripts/conv_one.py [fwd|fwd_stats|fwd_stats_ps|wgrad|dgrad_ps|wgrad_ps|stem_fwd|stem_wgrad|win_fwd] [reps]
   -- resblock 3x3 256->256 @128, bs 8 (stem_*: the generator stem 7x7 9->64 @512, bs 8, on its strip kernels)
   (fwd_stats: with the InstanceNorm statistics epilogue, as the step's conv1 runs; fwd_stats_ps: on a FG_PRESPLIT
   operand written by the norm pass, as the step's conv2 runs; dgrad_ps: the input-gradient interior launch of
@@ -40,13 +40,26 @@ def stem(kind, dev):
     return lambda: ops.conv([prob], in_stats=True)
 
 
+def win_fwd(dev):
+    """the content head's 7x7 64 -> 27 forward on the row-strip window kernel (bs 8, 512^2), as bench_win.py"""
+    L.set_conv_math("f16x3")
+    N = 8
+    ad2 = Buf.empty(N, 512, 512, 64, 3, dev)
+    ad2.t.uniform_(-1, 1)
+    w = torch.randn(27, 64, 7, 7, device=dev) * 0.02
+    m = PL.wmap_conv_fwd(w.shape, 64)
+    cl = Buf.empty(N, 512, 512, 32, 0, dev)
+    prob = PL.conv_problem(ad2, 3, 7, 1, ops.pack_weight(w, m), m, cl)
+    return lambda: ops.conv_win(prob)
+
+
 def main():
     kind = sys.argv[1] if len(sys.argv) > 1 else "fwd"
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
     L.load()
     dev = "cuda"
-    if kind.startswith("stem_"):
-        fn = stem(kind, dev)
+    if kind.startswith("stem_") or kind == "win_fwd":
+        fn = stem(kind, dev) if kind != "win_fwd" else win_fwd(dev)
         for _ in range(reps):
             fn()
         torch.cuda.synchronize()

@@ -12,6 +12,7 @@ for k in $KINDS; do
     wgrad_ps) key=conv_wgrad_f3; ktag="conv_wgrad_f3_kernel<256,0,3>"; name=resblock_wgrad_ps;;
     stem_wgrad) key=stem_wgrad_kernel; ktag="stem_wgrad_kernel"; name=stem_wgrad;;
     stem_fwd) key=stem_fwd_kernel; ktag="stem_fwd_kernel"; name=stem_fwd;;
+    win_fwd) key=conv_win2_kernel; ktag="conv_win2_kernel<7>"; name=win_fwd;;
     *) echo "unknown kind $k"; exit 1;;
   esac
   KIND=$k scripts/gpu_pmc.sh "${TAG}_$k" || { echo "pmc $k failed"; exit 1; }
