@@ -416,11 +416,177 @@ __global__ void __launch_bounds__(256, 2) conv_win2_kernel(const WinArgs args) {
     }
 }
 
+typedef __attribute__((address_space(3))) void lds_void;
+
+// C = 32 (the content head's input gradient, N <= 64), two workgroups per CU: 4 waves x 64 rows x 64 outputs per
+// workgroup of 256 output pixels.  Each kernel row runs as two phases that share one staged strip (268 px x 128 B):
+// the weights of taps 0..3, then of taps 4..6 (32 / 24 KB), so a workgroup holds 66 KB of LDS and two share a CU.
+// Operands arrive by LDS-DMA (16-B buffer loads into LDS, no staging registers: the accumulators and fragments
+// need them); one workgroup's copy latency and barriers run under the other's MFMAs.  Per tap and wave: 8 A + 8 B
+// fragment reads for 48 MFMAs (341 LDS bytes per MFMA, as the 8-wave 512-row kernel).
+template <int KW>
+__global__ void __launch_bounds__(256, 2) conv_win2_dgrad_kernel(const WinArgs args) {
+    constexpr int C = 32, NT = 256, BM = 256, TN = 4, TM = 4, WM = 64;
+    constexpr int PB = 4 * C;                                   // strip bytes per pixel (h | l)
+    constexpr int NR = TN * 16;
+    constexpr int STRIP_PIX = BM + 2 * (KW - 1);
+    constexpr int STRIP_CH = STRIP_PIX * PB / 16;
+    constexpr int W_TAP = 2 * NR * C * 2;                       // [pc][NR][C] fp16 per tap
+    constexpr int TAP_CH = W_TAP / 16;
+    constexpr int G0 = (KW + 1) / 2;                            // taps of the first phase
+    constexpr int W_OFF = (STRIP_PIX * PB + 1023) / 1024 * 1024;
+    __shared__ __attribute__((aligned(1024))) char smem[W_OFF + G0 * W_TAP];
+    static_assert((G0 * TAP_CH) % NT == 0 && ((KW - G0) * TAP_CH) % NT == 0, "weight phases are whole wave copies");
+
+    const fg_conv_problem& P = args.P;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wid = fg::xcd_remap(blockIdx.x, gridDim.x);
+    const int img = wid / args.tiles_per_img;
+    const int p0 = (wid - img * args.tiles_per_img) * BM;
+    const int mab = P.m_a * P.m_b;
+    const int a0 = p0 / P.m_b, b0 = p0 - (p0 / P.m_b) * P.m_b;
+    const int len0 = min(BM, min(P.m_b - b0, mab - p0));
+    const int len1 = (a0 + 1 < P.m_a) ? min(BM - len0, P.m_b) : 0;
+    const int s0pix = len0 + KW - 1;
+    const int strip_bytes = (len0 + len1 + 2 * (KW - 1)) * PB;
+    const int wp = args.wp;
+    constexpr int kOOB = 0x7fffffff;
+
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)args.xs, 0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)P.w, 0, 0x7fffffff, 0x00020000);
+    const int seg0_pix = img * (int)(P.sxn / C) + a0 * wp + b0;
+    const int seg1_pix = img * (int)(P.sxn / C) + (a0 + 1) * wp;
+
+    // strip: wave-instruction i of this wave copies chunks o = (i*4 + wave)*64 + lane (waves whose chunks start past
+    // the strip skip it; a partial one ends inside the pad before W_OFF)
+    auto dma_strip = [&](int r) {
+        const int soff = r * wp * PB;
+#pragma unroll
+        for (int i = 0; i < (STRIP_CH + NT - 1) / NT; ++i) {
+            const int ob = (i * 4 + wave) * 64;
+            if (ob >= STRIP_CH) continue;
+            const int o = (ob + lane) * 16;
+            const int src = o >= strip_bytes ? kOOB : (o < s0pix * PB ? seg0_pix * PB + o : seg1_pix * PB + (o - s0pix * PB)) + soff;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_void*)(smem + ob * 16), 16, src, 0, 0, 0);
+        }
+    };
+    // weights of taps t0 .. t0 + nt - 1 of kernel row r: chunk F of the image [s][pc][NR][C]
+    auto dma_w = [&](int r, int t0, int nt) {
+        const int woff = ((r * P.jp) / 8) * 32;
+        for (int i = 0; i < nt * TAP_CH / NT; ++i) {
+            const int Fb = (i * 4 + wave) * 64, F = Fb + lane;
+            const int sl = F / TAP_CH, f = F - sl * TAP_CH;
+            const int pc = f / (NR * C / 8);
+            const int rem = f - pc * (NR * C / 8);
+            const int n = rem / (C / 8);
+            const int ch = (rem - n * (C / 8)) ^ swz_wrow<C>(n);
+            const int src = (min(n, P.n_out - 1) * (P.ldw / 8) + ch) * 32 + pc * 16 + (((t0 + sl) * C) / 8) * 32 + woff;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (lds_void*)(smem + W_OFF + Fb * 16), 16, src, 0, 0, 0);
+        }
+    };
+
+    const float sa = fgc::pow2_scale(P.x_absmax);
+    const float sb = fgc::pow2_scale(P.w_absmax);
+    const float out_scale = 1.f / (sa * sb);
+
+    const int fr = lane & 15, g = lane >> 4;
+    int q0[TM], x0[TM];
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) {
+        const int i = wave * WM + tm * 16 + fr;
+        q0[tm] = i < len0 ? i : i + KW - 1;
+        x0[tm] = i < len0 ? b0 + i : i - len0;
+    }
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // tap s of the strip with the staged weight slot sl
+    auto tap = [&](int s, int sl) {
+        f16x8 ah[TM], al[TM];
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) {
+            const char* px = smem + (q0[tm] + s) * PB;
+            const int sw = swz_strip<C>(x0[tm] + s);
+            ah[tm] = *reinterpret_cast<const f16x8*>(px + (g ^ sw) * 16);
+            al[tm] = *reinterpret_cast<const f16x8*>(px + ((C / 8 + g) ^ sw) * 16);
+        }
+        const char* wb = smem + W_OFF + sl * W_TAP;
+        f16x8 bh[TN], bl[TN];
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+            const int n = tn * 16 + fr;
+            const char* row = wb + n * (2 * C) + (g ^ swz_wrow<C>(n)) * 16;
+            bh[tn] = *reinterpret_cast<const f16x8*>(row);
+            bl[tn] = *reinterpret_cast<const f16x8*>(row + NR * 2 * C);
+        }
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) {
+                acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[tm], bh[tn], acc[tm][tn], 0, 0, 0);
+                acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[tm], bl[tn], acc[tm][tn], 0, 0, 0);
+                acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[tm], bh[tn], acc[tm][tn], 0, 0, 0);
+            }
+    };
+
+    for (int r = 0; r < P.kh; ++r) {
+        __syncthreads();                              // the previous phase's reads are done
+        dma_strip(r);
+        dma_w(r, 0, G0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+#pragma unroll
+        for (int s = 0; s < G0; ++s) tap(s, s);
+        __syncthreads();
+        dma_w(r, G0, KW - G0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+#pragma unroll
+        for (int s = G0; s < KW; ++s) tap(s, s - G0);
+    }
+
+    // ---- epilogue (as conv_win_kernel)
+    const int act = P.act;
+    const bool accum = P.accumulate != 0;
+    float bias_v[TN];
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) bias_v[tn] = P.bias ? P.bias[min(tn * 16 + fr, P.n_out - 1)] : 0.f;
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) {
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {
+            const int i = wave * WM + tm * 16 + 4 * g + reg;
+            if (i >= len0 + len1) continue;
+            const int a = i < len0 ? a0 : a0 + 1, b = i < len0 ? b0 + i : i - len0;
+            float* yrow = P.y + img * P.syn + a * P.sya + b * P.syb;
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) {
+                const int n = tn * 16 + fr;
+                if (n >= P.n_out) continue;
+                float v = fg::act_fwd(acc[tm][tn][reg] * out_scale + bias_v[tn], act);
+                float* dst = yrow + n * P.syc;
+                if (accum) v += *dst;
+                *dst = v;
+            }
+        }
+    }
+}
+
 // 8 waves (two per SIMD, 32 rows each: a partner wave's MFMAs cover each wave's fragment-read latency; 4 waves of 64
 // rows ran 1.31 ms on both geometries, profiles/round4/r4c_ab_win.log)
 template <int C, int KW, int TN>
 int launch_win(const WinArgs& a, int tiles, hipStream_t stream) {
     if constexpr (C == 32) {
+        // the input gradient on two 4-wave workgroups per CU (1071 -> 952 us, profiles/round4/r4zb_bench_win.log;
+        // A/B: FLOODGAN_WIN_2WG=0 runs the 8-wave kernels, 512-row tiles unless FLOODGAN_WIN_BM=256)
+        const char* e2 = getenv("FLOODGAN_WIN_2WG");
+        if (!(e2 && atoi(e2) == 0)) {
+            hipLaunchKernelGGL((conv_win2_dgrad_kernel<KW>), dim3(tiles), dim3(256), 0, stream, a);
+            return fg::launched("conv_win2_dgrad");
+        }
         const char* e = getenv("FLOODGAN_WIN_BM");      // A/B: 256 = 32-row waves
         if (a.P.m_b >= 512 && !(e && atoi(e) == 256)) {
             WinArgs b = a;

@@ -36,9 +36,9 @@ def main():
     for name, prob, out, flops in (("content fwd 7x7 64->27 @512", fwd, cl, 2.0 * N * 512 * 512 * 27 * 64 * 49),
                                    ("content dgrad 7x7 27->64 @518", dgr, Y, 2.0 * N * 518 * 518 * 64 * 27 * 49)):
         ref = None
-        # the input gradient's tile rows (FLOODGAN_WIN_BM); the forward's kernel (FLOODGAN_WIN_2WG: 1 = two 4-wave
-        # workgroups per CU over channel-half phases, the default; 0 = one 8-wave workgroup per CU)
-        var = ("FLOODGAN_WIN_BM", ("512", "256")) if "dgrad" in name else ("FLOODGAN_WIN_2WG", ("0", "1"))
+        # FLOODGAN_WIN_2WG: 1 = two 4-wave workgroups per CU (the default), 0 = one 8-wave workgroup per CU
+        # (the input gradient's two-workgroup kernel uses LDS-DMA phases)
+        var = ("FLOODGAN_WIN_2WG", ("0", "1"))
         for _ in range(2):
             for v in var[1]:
                 os.environ[var[0]] = v

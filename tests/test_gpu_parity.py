@@ -392,13 +392,16 @@ def test_stem_fwd_strips(H, N):
 
 @pytest.mark.parametrize("case,env", [("content_fwd", {}), ("content_fwd", {"FLOODGAN_WIN_2WG": "0"}),
                                       ("content_dgrad", {}), ("content_dgrad_512", {}),
-                                      ("content_dgrad_512", {"FLOODGAN_WIN_BM": "256"})])
+                                      ("content_dgrad", {"FLOODGAN_WIN_2WG": "0"}),
+                                      ("content_dgrad_512", {"FLOODGAN_WIN_2WG": "0"}),
+                                      ("content_dgrad_512", {"FLOODGAN_WIN_2WG": "0", "FLOODGAN_WIN_BM": "256"})])
 def test_conv_window(case, env, monkeypatch):
     """the row-strip window kernel (fg_conv_win) on the content-head geometries -- 7x7 over 64
     channels -> 27, and its input gradient 27(32) -> 64 over the 6-bordered gradient -- with
     output rows of 256+ px (two-segment tiles, ragged last tile) against fp64; the forward on its two-workgroup
-    channel-half kernel (the default) and the 8-wave one (FLOODGAN_WIN_2WG=0); the input gradient on 512-row
-    tiles where its output rows allow (>= 512 px, the default) and on 256-row ones (FLOODGAN_WIN_BM=256)"""
+    channel-half kernel (the default) and the 8-wave one (FLOODGAN_WIN_2WG=0); the input gradient on its
+    two-workgroup LDS-DMA kernel (the default) and, with FLOODGAN_WIN_2WG=0, the 8-wave ones: 512-row tiles where
+    its output rows allow (>= 512 px) and 256-row ones (FLOODGAN_WIN_BM=256)"""
     from floodgan import _lib as L, ops, plans as PL
     from floodgan.plans import Buf
     for k, v in env.items():
