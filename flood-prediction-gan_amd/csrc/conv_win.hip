@@ -232,12 +232,25 @@ __global__ void __launch_bounds__(NW * 64, 1) conv_win_kernel(const WinArgs args
     }
 }
 
+typedef __attribute__((address_space(3))) void lds_void;
+
+// nothing is scheduled across it
+__device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0); }
+// one 16-B LDS-DMA per lane: lane i's bytes land at lds + 16 i (lds wave-uniform).  A device function: the builtin
+// named in a lambda of the forward kernel's body left that kernel's host-side launch stub undefined.
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, int voff) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds, 16, voff, 0, 0, 0);
+}
+
 // C = 64 forward, two workgroups per CU: a workgroup of 4 waves x 64 rows walks 14 "phases" -- one kernel row's
 // 32-channel half each: the strip's half pixels (268 px x 128 B, in the 32-channel chunk swizzle) and that half of
 // the row's 7 taps of weights (28 KB), 63 KB of LDS -- so two workgroups share a CU and one's copy / barriers run
 // under the other's MFMAs (the 8-wave kernel above holds 123 KB: one workgroup per CU, every wave idle during each
-// row's copy).  Per tap and wave: 8 A + 4 B fragment reads for 24 MFMAs (512 LDS bytes per MFMA, was 683), the
-// next tap's fragments read ahead of the current MFMAs.
+// row's copy).  A phase's operands arrive by LDS-DMA (16-B buffer loads straight into LDS; the other workgroup's
+// MFMAs cover the latency), and the registers that frees hold the next tap's fragments, read ahead of the current
+// tap's MFMAs (sched_barrier keeps that order).  Per tap and wave: 8 A + 4 B fragment reads for 24 MFMAs (512 LDS
+// bytes per MFMA, was 683).  Register-staged copies instead of DMA, without the read-ahead: 1.5-2.5 % slower
+// (profiles/round4/r4ze_bench_win.log).
 template <int KW>
 __global__ void __launch_bounds__(256, 2) conv_win2_kernel(const WinArgs args) {
     constexpr int C = 64, CH = 32, NT = 256, BM = 256, TN = 2, TM = 4, WM = 64;
@@ -299,28 +312,6 @@ __global__ void __launch_bounds__(256, 2) conv_win2_kernel(const WinArgs args) {
         const int ch = (rem - n * (CH / 8)) ^ swz_wrow<CH>(n);
         w_src[i] = F >= W_CH ? -1 : (min(n, P.n_out - 1) * (P.ldw / 8) + ch) * 32 + pc * 16 + ((s * C) / 8) * 32;
     }
-    f32x4 rs[SCH], rw[WCH];
-    auto load = [&](int ph) {
-        const int r = ph >> 1, hc = ph & 1;
-        const int soff = r * wp * (4 * C), woff = ((r * P.jp) / 8) * 32 + hc * (CH / 8) * 32;
-#pragma unroll
-        for (int i = 0; i < SCH; ++i) {
-            const int src = hc ? s_src1[i] : s_src0[i];
-            rs[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, src >= 0 ? src + soff : kOOB, 0, 0));
-        }
-#pragma unroll
-        for (int i = 0; i < WCH; ++i)
-            rw[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(wr, w_src[i] >= 0 ? w_src[i] + woff : kOOB, 0, 0));
-    };
-    auto store = [&]() {
-#pragma unroll
-        for (int i = 0; i < SCH; ++i)
-            if (s_src0[i] >= 0) *reinterpret_cast<f32x4*>(smem + (tid + i * NT) * 16) = rs[i];
-#pragma unroll
-        for (int i = 0; i < WCH; ++i)
-            if (w_src[i] >= 0) *reinterpret_cast<f32x4*>(smem + W_OFF + (tid + i * NT) * 16) = rw[i];
-    };
-
     const float sa = fgc::pow2_scale(P.x_absmax);
     const float sb = fgc::pow2_scale(P.w_absmax);
     const float out_scale = 1.f / (sa * sb);
@@ -371,21 +362,42 @@ __global__ void __launch_bounds__(256, 2) conv_win2_kernel(const WinArgs args) {
     };
 
     const int NPH = 2 * P.kh;
-    load(0);
-    store();
-    __syncthreads();
-    for (int ph = 0; ph < NPH; ++ph) {
-        if (ph + 1 < NPH) load(ph + 1);
+    auto dma = [&](int ph) {
+        const int r = ph >> 1, hc = ph & 1;
+        const int soff = r * wp * (4 * C), woff = ((r * P.jp) / 8) * 32 + hc * (CH / 8) * 32;
 #pragma unroll
-        for (int s = 0; s < KW; ++s) {
-            Frags f;
-            read(s, f);
-            mma(f);
+        for (int i = 0; i < SCH; ++i) {
+            const int ob = i * NT + wave * 64;
+            if (ob >= STRIP_CH) continue;
+            const int src = hc ? s_src1[i] : s_src0[i];
+            dma16(xr, smem + ob * 16, src >= 0 ? src + soff : kOOB);
         }
-        if (ph + 1 < NPH) {
-            __syncthreads();
-            store();
-            __syncthreads();
+#pragma unroll
+        for (int i = 0; i < WCH; ++i) {
+            const int ob = i * NT + wave * 64;
+            if (ob >= W_CH) continue;
+            dma16(wr, smem + W_OFF + ob * 16, w_src[i] >= 0 ? w_src[i] + woff : kOOB);
+        }
+    };
+    for (int ph = 0; ph < NPH; ++ph) {
+        if (ph) __syncthreads();
+        dma(ph);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        Frags fa, fb;
+        read(0, fa);
+#pragma unroll
+        for (int s = 0; s < KW; s += 2) {
+            if (s + 1 < KW) read(s + 1, fb);
+            sched_fence();
+            mma(fa);
+            sched_fence();
+            if (s + 1 < KW) {
+                if (s + 2 < KW) read(s + 2, fa);
+                sched_fence();
+                mma(fb);
+                sched_fence();
+            }
         }
     }
 
@@ -415,8 +427,6 @@ __global__ void __launch_bounds__(256, 2) conv_win2_kernel(const WinArgs args) {
         }
     }
 }
-
-typedef __attribute__((address_space(3))) void lds_void;
 
 // C = 32 (the content head's input gradient, N <= 64), two workgroups per CU: 4 waves x 64 rows x 64 outputs per
 // workgroup of 256 output pixels.  Each kernel row runs as two phases that share one staged strip (268 px x 128 B):
@@ -467,7 +477,7 @@ __global__ void __launch_bounds__(256, 2) conv_win2_dgrad_kernel(const WinArgs a
             if (ob >= STRIP_CH) continue;
             const int o = (ob + lane) * 16;
             const int src = o >= strip_bytes ? kOOB : (o < s0pix * PB ? seg0_pix * PB + o : seg1_pix * PB + (o - s0pix * PB)) + soff;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_void*)(smem + ob * 16), 16, src, 0, 0, 0);
+            dma16(xr, smem + ob * 16, src);
         }
     };
     // weights of taps t0 .. t0 + nt - 1 of kernel row r: chunk F of the image [s][pc][NR][C]
@@ -481,7 +491,7 @@ __global__ void __launch_bounds__(256, 2) conv_win2_dgrad_kernel(const WinArgs a
             const int n = rem / (C / 8);
             const int ch = (rem - n * (C / 8)) ^ swz_wrow<C>(n);
             const int src = (min(n, P.n_out - 1) * (P.ldw / 8) + ch) * 32 + pc * 16 + (((t0 + sl) * C) / 8) * 32 + woff;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (lds_void*)(smem + W_OFF + Fb * 16), 16, src, 0, 0, 0);
+            dma16(wr, smem + W_OFF + Fb * 16, src);
         }
     };
 
