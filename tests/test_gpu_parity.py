@@ -441,6 +441,11 @@ def test_conv_window(case, env, monkeypatch):
         ops.conv_win(prob)
         torch.cuda.synchronize()
         assert nrel(nchw(Y, ref.shape[1]), ref) < KTOL
+        # the epilogue's accumulate and activation paths: Y += LeakyReLU(conv) over the first result
+        first = nchw(Y, ref.shape[1]).double()
+        ops.conv_win(dict(prob, accumulate=1, act=L.FG_ACT_LRELU))
+        torch.cuda.synchronize()
+        assert nrel(nchw(Y, ref.shape[1]), first + F.leaky_relu(ref, 0.2)) < KTOL
         ops.USE_WIN = False
         Y.t.zero_()
         ops.conv([prob])
