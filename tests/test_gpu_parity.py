@@ -529,12 +529,14 @@ def test_conv1x1_head(N, H, W, n_out, xpad, lanes, monkeypatch):
     assert nrel(dw, 2 * gw_ref) < KTOL and nrel(db, 2 * gb_ref) < KTOL
 
 
-def test_disc_head_n1():
-    """model.11 (Conv2d(512, 1, 4, 1, 1)): the fp32 FMA forward and weight-gradient kernels vs fp64"""
+@pytest.mark.parametrize("H", [11, 40])
+def test_disc_head_n1(H):
+    """model.11 (Conv2d(512, 1, 4, 1, 1)): the fp32 FMA forward and weight-gradient kernels vs fp64 (H 40: output
+    rows of 39 px, a ragged last quad)"""
     from floodgan import ops, plans as PL
     from floodgan.plans import Buf
     torch.manual_seed(7)
-    N, H = 3, 11
+    N = 3
     x = torch.randn(N, 512, H, H, dtype=torch.float64)
     w = torch.randn(1, 512, 4, 4, dtype=torch.float64) * 0.02
     b = torch.randn(1, dtype=torch.float64)
