@@ -231,6 +231,31 @@ def cpu_baseline(res, threads, steps=3, workload="paired", batches=(1, 8)):
                       f"batch-{batches[-1]} rate"}
 
 
+def fp32_math_arm(B, R, dev, x, y, steps=5, warmup=1):
+    """The same paired step under the exact-fp32 conv math (FLOODGAN_CONV_MATH=fp32: every conv product on
+    v_mfma_f32_32x32x2_f32, fp32 in / fp32 accumulate, as the reference's CPU convolutions compute) on a fresh
+    seed-47 model and the same batch: the price of exact fp32 arithmetic next to the f16x3 headline."""
+    from floodgan import _lib
+    from floodgan.model import Model
+    prev = _lib.get_conv_math()
+    _lib.set_conv_math("fp32")
+    try:
+        m = Model(model="PairedAttention", num_epochs=2, topography="all", device=dev)
+        for _ in range(warmup):
+            m.step_fn(x, y).cpu()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            m.step_fn(x, y).cpu()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+    finally:
+        _lib.set_conv_math(prev)
+    return {"conv_math": "fp32", "steps": steps, "warmup": warmup, "ms_per_step": round(1e3 * el / steps, 3),
+            "value": round(B * steps / el, 3), "unit": "img/s",
+            "note": "same step, batch and seed on a fresh model; every conv on the exact-fp32 MFMA (157.3 TFLOP/s peak)"}
+
+
 def rank_envs(n, port, base=None, backend="nccl"):
     """The environments of the N ranks `launch_ranks` starts: what torch.distributed.run would set
     (RANK, LOCAL_RANK, WORLD_SIZE, LOCAL_WORLD_SIZE, MASTER_ADDR / MASTER_PORT on 127.0.0.1) plus the
@@ -309,6 +334,10 @@ def main():
     ap.add_argument("--batch", type=int, default=8, help="images per GPU")
     ap.add_argument("--res", type=int, default=512)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-fp32-math", action="store_true",
+                    help="skip the fp32_math sub-record (5 steps of the same step under the exact-fp32 conv math)")
+    ap.add_argument("--timeout", type=float, default=0,
+                    help="N > 1 self-launch: seconds before hung ranks are terminated (rc 124); 0 = 900 + 30 s per step")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--workload", choices=["paired", "pix2pix", "attentiongan", "cyclegan"], default="paired")
     ap.add_argument("--data", choices=["resident", "tiles"], default="resident",
@@ -324,8 +353,10 @@ def main():
 
     backend = args.dist_backend or os.environ.get("FLOODGAN_DIST_BACKEND", "nccl")
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        # nothing has touched the GPU yet: start the N ranks as children and relay rank 0's line
-        sys.exit(launch_ranks(args.gpus, sys.argv[1:], backend=backend))
+        # nothing has touched the GPU yet: start the N ranks as children and relay rank 0's line; ranks that
+        # hang (a collective that never completes) are terminated after a generous limit, rc 124
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:], backend=backend,
+                              timeout=args.timeout or 900 + 30 * (args.steps + args.warmup)))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus:
         sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: refusing to report a "
@@ -408,6 +439,9 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
     math = _lib.get_conv_math()
+    fp32_rec = None
+    if world == 1 and not (cycle or p2p) and loader is None and not args.no_fp32_math and math != "fp32":
+        fp32_rec = fp32_math_arm(B, R, dev, x, y)
     # split maths execute several 16-bit MFMA products per fp32 multiply-add: the roof for fp32
     # work is the 16-bit dense MFMA peak / products (the fp32 MFMA path's roof is 157.3)
     nprod = {"f16x3": 3, "fwd_f16x3": 3, "bf16x6": 6, "fwd_x6": 6}.get(math)
@@ -508,6 +542,9 @@ def main():
                             "algorithmic_bytes": alg, "achieved_algorithmic_GBs": round(alg / (ms * 1e-3) / 1e9, 1),
                             "traffic": t}
             out["roofline"]["per_kind"] = kinds
+        if fp32_rec is not None:
+            fp32_rec["vs_headline"] = round(fp32_rec["value"] / img_s, 4)
+            out["fp32_math"] = fp32_rec
         if world == 1 and not args.no_cpu_baseline:
             threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", 0)) or len(os.sched_getaffinity(0))
             out["cpu_baseline"] = cpu_baseline(R, threads, steps=1 if cycle or p2p else 3, workload=args.workload,

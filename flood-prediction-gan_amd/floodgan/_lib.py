@@ -171,6 +171,9 @@ SIGNATURES = {
                   C.c_void_p, C.c_float, C.c_ulonglong, fg_view, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p,
                   C.c_void_p, C.c_void_p],
     "fg_dropout_mask": [C.c_ulonglong, C.c_float, C.c_longlong, C.c_void_p, C.c_void_p],
+    "fg_bernoulli_mt_workspace_words": [C.c_int],
+    "fg_bernoulli_mt": [C.c_void_p, C.c_longlong, C.c_longlong, C.c_void_p, C.c_int, C.c_longlong, C.c_int,
+                        C.POINTER(C.c_void_p), C.POINTER(C.c_longlong), C.c_double, C.c_void_p, C.c_void_p, C.c_void_p],
     "fg_unit_image": [fg_sview, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, fg_view, C.c_void_p],
     "fg_ssim_workspace_doubles": [C.c_int, C.c_int, C.c_int, C.c_int],
     "fg_ssim": [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_float, C.c_float,
@@ -185,7 +188,7 @@ SIGNATURES = {
     "fg_tiff_read": [C.c_char_p, C.c_void_p, C.c_longlong],
     "fg_tile_transform": [C.POINTER(fg_tile_batch), C.c_void_p],
 }
-RESTYPES = {"fg_last_error": C.c_char_p, "fg_last_launch": C.c_char_p, "fg_in_workspace_doubles": C.c_longlong, "fg_bn_workspace_doubles": C.c_longlong,
+RESTYPES = {"fg_bernoulli_mt_workspace_words": C.c_longlong, "fg_last_error": C.c_char_p, "fg_last_launch": C.c_char_p, "fg_in_workspace_doubles": C.c_longlong, "fg_bn_workspace_doubles": C.c_longlong,
             "fg_ssim_workspace_doubles": C.c_longlong, "fg_sq_err_workspace_doubles": C.c_longlong,
             "fg_channel_sum_workspace_doubles": C.c_longlong,
             "fg_in_partials_workspace_doubles": C.c_longlong, "fg_conv1x1_wgrad_workspace_floats": C.c_longlong}

@@ -49,41 +49,19 @@ def disc_bucket_names():
     return [[f"{layer}.{k}" for k in ("weight", "bias")] for layer in reversed(DISC_LAYERS)]
 
 
-# Off by default: measured at the bs-8 512^2 step (profiles/round2/r2m_*), the side-stream weight gradients
-# do run concurrently with the input-gradient chain, but every kernel then slows by the same factor (the
-# pipelined convs already hold every CU): 57.3 ms per step vs 56.6 on one stream.
-SIDE_STREAM = os.environ.get("FLOODGAN_SIDE_STREAM", "0") == "1"
-_SIDE_STREAMS = {}
-
-
-def _side_stream(device):
-    key = torch.device(device).index
-    if key not in _SIDE_STREAMS:
-        _SIDE_STREAMS[key] = torch.cuda.Stream(device=device)
-    return _SIDE_STREAMS[key]
-
-
 class _Grads:
     """Destination of parameter gradients: either fresh tensors (autograd path) or
     preallocated .grad tensors (fused step).
 
-    The weight gradients are off the backward's critical path -- nothing but the optimiser step
-    reads them -- so they run on a second HIP stream (side), overlapping the chain of input
-    gradients and norm backward passes that each next layer waits on.  A side launch waits for the
-    main stream's work so far; its operand buffers are recorded on the side stream (the caching
-    allocator then cannot hand their memory to a main-stream allocation while the side kernels still
-    read it) and their cached operand scales / split copies are computed on the main stream first
-    (a cache filled on the side stream could be read by a later main-stream kernel before it is
-    written).  join() makes the main stream wait for every side launch; ready() starts a gradient
-    bucket's all-reduce from the side stream, after both streams' writes to it."""
+    Every launch runs on the caller's (current) stream.  Weight gradients on a second stream beside the
+    input-gradient chain were measured slower (profiles/round2/r2m_*: 57.3 vs 56.6 ms per step; the
+    pipelined convs already hold every CU, so the overlapped kernels each slow down by the same factor)
+    and that path was removed in round 5."""
 
     def __init__(self, params, into=None, accumulate=False, device=None):
         self.params, self.into = params, into
         self.acc = accumulate       # raise existing gradients (a network used several times per step)
         self.out = {}
-        self.side = _side_stream(device) if SIDE_STREAM and device is not None and torch.device(device).type == "cuda" \
-            else None
-        self.main = torch.cuda.current_stream(device) if self.side is not None else None
 
     def get(self, name):
         if name not in self.out:
@@ -95,34 +73,20 @@ class _Grads:
         return self.out[name]
 
     def off_path(self, fn, bufs, names=(), prepare=None):
-        """run fn() (weight-gradient launches reading the Bufs `bufs`, writing the gradients `names`)
-        on the side stream; prepare() fills their operand caches on the main stream first"""
+        """run fn() (weight-gradient launches reading the Bufs `bufs`, writing the gradients `names`)"""
         for n in names:
-            self.get(n)                                   # allocated on the main stream
-        if self.side is None:
-            return fn()
-        if prepare is not None:
-            prepare()
-        self.side.wait_stream(self.main)
-        with torch.cuda.stream(self.side):
-            fn()
-        for b in bufs:
-            b.t.record_stream(self.side)
+            self.get(n)
+        return fn()
 
     def wgrad(self, prob, wmap, name, bufs, tag=None):
         self.off_path(lambda: ops.wgrad(prob, wmap, self.get(name), accumulate=self.acc, tag=tag), bufs, (name,),
                       prepare=lambda: ops.prepare_wgrad(prob))
 
     def ready(self, ready, name):
-        if self.side is None:
-            return ready(name)
-        self.side.wait_stream(self.main)
-        with torch.cuda.stream(self.side):
-            ready(name)
+        return ready(name)
 
     def join(self):
-        if self.side is not None:
-            self.main.wait_stream(self.side)
+        pass
 
 
 # ======================================================================================

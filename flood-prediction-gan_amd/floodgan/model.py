@@ -49,6 +49,11 @@ class PairedStep:
         # L1 term's sign decisions ({"L1": [{"l1": sign(fake - y)}]})
         self.record_decisions = False
         self.decisions = None
+        # test instrumentation (teacher forcing): discriminator parameters {name: tensor} that replace the
+        # result of Adam(D) before the G step, so that another implementation's G half can be compared on
+        # the same discriminator (the oracle's d_after); the step's own Adam(D) result is kept in d_after_own
+        self.d_after = None
+        self.d_after_own = None
 
     def __call__(self, x, y):
         ws, _ = world()
@@ -75,6 +80,11 @@ class PairedStep:
         del dS, dinp
         self.dflat.finish()
         self.opt_d.step()
+        if self.d_after is not None:
+            self.d_after_own = {k: p.detach().clone() for k, p in self.D.named_parameters()}
+            with torch.no_grad():
+                for k, p in self.D.named_parameters():
+                    p.copy_(self.d_after[k])
         # ---- generator step against the updated discriminator                 (:636-646)
         dinp = X.disc_pack([(x, fake)], C + 3)
         pred, dS = X.disc_forward(self.dp, dinp, save=True)
@@ -106,8 +116,8 @@ class Pix2PixStep(PairedStep):
     """The same iteration (models/model.py:611-651) for Pix2Pix: BatchNorm in training mode, so the D
     step's D(fake) and D(real) -- separate calls in the reference -- run as one 2N pass with two
     BatchNorm groups (per-half statistics, two running-stat updates in order), and the G step's D call
-    updates the discriminator's running statistics a third time.  The generator's Dropout masks are
-    drawn from torch's CPU generator in the reference's order (floodgan.pix2pix.draw_dropout_masks)."""
+    updates the discriminator's running statistics a third time.  With dropout_rng "host" the generator's Dropout
+    masks are torch's CPU stream in the reference's order, regenerated on the device (floodgan.torch_rng)."""
 
     def __init__(self, generator, discriminator, opt_g, opt_d, group=None):
         self.G, self.D = generator, discriminator
@@ -132,7 +142,13 @@ class Pix2PixStep(PairedStep):
         losses = torch.empty(4, dtype=torch.float32, device=dev)
         self.gflat.attach()
         self.dflat.attach()
-        masks = self.masks if self.masks is not None else P2P.draw_dropout(N, H, W, self.G.dropout_rng)
+        commit = None
+        if self.masks is not None:
+            masks = self.masks
+        elif self.G.dropout_rng == "host":
+            masks, commit = P2P.draw_dropout_deferred(N, H, W, dev)
+        else:
+            masks = P2P.draw_dropout(N, H, W, self.G.dropout_rng, dev)
         self.last_masks = masks
         fake, gS = P2P.gen_forward(self.gp, self.gb, x, masks=masks, training=True, save=True)
         dinp = X.disc_pack([(x, fake), (x, y)], C + 3)
@@ -167,6 +183,8 @@ class Pix2PixStep(PairedStep):
         self.gflat.finish()
         self.opt_g.step()
         self.last_output = fake
+        if commit is not None:             # torch's CPU generator advanced past this iteration's Dropout draws
+            commit()
         return losses
 
 

@@ -396,7 +396,8 @@ class Pix2PixGenerator(nn.Module):
     """models/model_architectures.py:9-22 -- U-Net-256: eight Pix2PixBlocks, innermost first.  The
     whole network is one autograd node on floodgan.pix2pix; BatchNorm running statistics are updated
     in place.  dropout_rng: "device" (default; hashed keep decisions seeded from torch's CPU generator)
-    or "host" (masks drawn exactly as the reference's CPU path draws them; see floodgan.pix2pix)."""
+    or "host" (the masks the reference's CPU path draws, bit for bit, generated on the device; see
+    floodgan.pix2pix and floodgan.torch_rng)."""
 
     dropout_rng = "device"
 
@@ -418,8 +419,8 @@ class Pix2PixGenerator(nn.Module):
         return dict(self.named_buffers())
 
     def forward(self, input):
-        masks = (P2P.draw_dropout(input.shape[0], input.shape[2], input.shape[3], self.dropout_rng) if self.training
-                 else None)
+        masks = (P2P.draw_dropout(input.shape[0], input.shape[2], input.shape[3], self.dropout_rng, input.device)
+                 if self.training else None)
         return _Pix2PixGeneratorFn.apply(self.buffer_dict(), self.training, masks, input,
                                          *self.param_dict().values())
 

@@ -21,10 +21,11 @@ BatchNorm apply / backward passes, its keep decisions either
   "device" (default): a counter-based hash of (seed, element) evaluated in the apply pass and
              recomputed in the backward -- no mask is drawn, stored or copied; one 62-bit seed per
              generator call comes from torch's CPU generator, so torch.manual_seed fixes the masks; or
-  "host":    0/1 masks drawn with torch's CPU generator exactly as the reference's CPU path draws them
-             (F.dropout: empty_like(x).bernoulli_(0.5), innermost level first: 7, 6, 5) and copied to
-             the device -- a seeded run then reproduces the reference's CPU run (the parity mode; a
-             512x512 batch of 8 costs ~0.1 s of host time per call).
+  "host":    the 0/1 masks torch's CPU generator gives the reference's CPU path (F.dropout:
+             empty_like(x).bernoulli_(0.5), innermost level first: 7, 6, 5), bit for bit -- a seeded run then
+             reproduces the reference's CPU run (the parity mode).  Round 5: the masks are no longer drawn on
+             the host; the device regenerates torch's MT19937 stream from the generator's state with chunked
+             jump-ahead (floodgan.torch_rng, csrc/mt19937.hip) and hands the advanced state back to torch.
 
 The discriminator's D(fake) and D(real) of the D step are separate BatchNorm calls in the
 reference (:624-628): one 2N-image pass with groups=2 (statistics per half, the running statistics
@@ -35,6 +36,7 @@ import torch
 from . import executor as X
 from . import ops
 from . import plans as PL
+from . import torch_rng
 from ._lib import FG_ACT_LRELU, FG_ACT_NONE, FG_ACT_RELU, FG_PAD_ZERO, require_device
 from .plans import Buf, Slice
 
@@ -120,10 +122,13 @@ def dropout_shapes(n, h, w):
     return {k: (n, 512, h >> (k - 1), w >> (k - 1)) for k in DROPOUT_LEVELS}
 
 
-def draw_dropout(n, h, w, mode="device"):
-    """One generator call's Dropout decisions: {level: host 0/1 mask} ("host") or {level: seed} ("device")"""
+def draw_dropout(n, h, w, mode="device", device="cuda"):
+    """One generator call's Dropout decisions: {level: device 0/1 mask} ("host": torch's CPU stream, regenerated
+    on the device; the generator advanced before returning) or {level: seed} ("device")"""
     if mode == "host":
-        return draw_dropout_masks(n, h, w)
+        masks, commit = draw_dropout_deferred(n, h, w, device)
+        commit()
+        return masks
     if mode != "device":
         raise ValueError(f"dropout mode must be 'device' or 'host' (got {mode!r})")
     base = int(torch.randint(1, 2 ** 62, (1,)).item())
@@ -137,6 +142,14 @@ def dropout_masks(drop, n, h, w, device="cuda"):
         d = drop[k]
         out[k] = ops.dropout_mask(d, shape, device) if isinstance(d, int) else d
     return out
+
+
+def draw_dropout_deferred(n, h, w, device="cuda"):
+    """"host" mode's masks as ({level: device 0/1 mask}, commit): commit() advances torch's CPU generator past
+    the draw (the fused step calls it at its end: nothing else in the iteration draws from that generator)"""
+    shapes = dropout_shapes(n, h, w)
+    outs, commit = torch_rng.draw(list(shapes.values()), 1 - DROP_P, device)
+    return dict(zip(shapes, outs)), commit
 
 
 def draw_dropout_masks(n, h, w):
@@ -195,7 +208,7 @@ def gen_forward(P, B, x, masks=None, training=True, save=True):
     check_input_size(H, W)
     dev = x.device
     if training and masks is None:
-        masks = draw_dropout(N, H, W)
+        masks = draw_dropout(N, H, W, device=x.device)
     dmask = {k: (m if isinstance(m, int) else m.to(dev)) for k, m in masks.items()} if training else {}
     ch = level_channels(Cin)
     S = dict(x=x, N=N, H=H, W=W, training=training, lv={})

@@ -507,6 +507,19 @@ int fg_bn_bwd(fg_view gA, int actA, fg_view gB, int actB, fg_view src, int group
 /* The 0/1 keep decisions of fg_bn_apply's hashed dropout for elements 0 .. total-1 (NCHW order of the
  * tensor the dropout applies to) into dst as floats (tests / host inspection). */
 int fg_dropout_mask(unsigned long long seed, float keep, long long total, float* dst, hipStream_t stream);
+/* torch's CPU Bernoulli stream on the device, bit for bit (replaces the host draws of the reference's
+ * nn.Dropout, models/model_architectures.py:52: F.dropout -> empty_like(x).bernoulli_(1 - p) per call):
+ * `elements` = sum(sizes) decisions drawn in order into the float 0/1 outputs outs[0..nout) (host array of
+ * device pointers, nout <= 4), element e keeping when the low 53 bits of (y(W[first + 2e]) << 32 |
+ * y(W[first + 2e + 1])) times 2^-53 are below p -- W the MT19937 word stream whose words 0..623 are `state`
+ * (device, the generator's 624 state words), first = 625 - the generator's `left`, y the tempering.
+ * jumps: device [njumps][624] words, x^(c * chunk) mod phi for c = 1..njumps (floodgan/data/mt19937_jumps.npz);
+ * final_state: the 624 words of the block holding the last word used (the state the draw leaves behind);
+ * work: fg_bernoulli_mt_workspace_words(chunks) device words, chunks = (last word - 1) / chunk + 1. */
+long long fg_bernoulli_mt_workspace_words(int nchunks);
+int fg_bernoulli_mt(const unsigned* state, long long first, long long elements, const unsigned* jumps, int njumps,
+                    long long chunk, int nout, float* const* outs, const long long* sizes, double p,
+                    unsigned* final_state, unsigned* work, hipStream_t stream);
 /* nn.MaxPool2d(2) over NHWC interiors (floor output size). */
 int fg_maxpool2(fg_view src, fg_view dst, hipStream_t stream);
 

@@ -47,6 +47,38 @@ def run(m, kind, x, y, iters):
     return [step(x.cuda(), y.cuda()).cpu() for _ in range(iters)]
 
 
+def optimizers(m):
+    return {"optimizer_generator": m.optimizer_generator, "optimizer_discriminator": m.optimizer_discriminator}
+
+
+def _cpu(o):
+    if isinstance(o, torch.Tensor):
+        return o.detach().cpu().clone()
+    if isinstance(o, dict):
+        return {k: _cpu(v) for k, v in o.items()}
+    if isinstance(o, (list, tuple)):
+        return type(o)(_cpu(v) for v in o)
+    return o
+
+
+def snapshot(m, kind):
+    """the full training state before an iteration: every network's parameters and both optimisers' state
+    dicts (torch.optim.Adam format; empty before the first step)"""
+    state = {f"{net}/{k}": v.detach().cpu().clone() for net, mod in nets(m, kind).items()
+             for k, v in mod.state_dict().items()}
+    return {"state": state, "optim": {k: _cpu(o.state_dict()) for k, o in optimizers(m).items()}}
+
+
+def load_snapshot(m, kind, snap):
+    """continue from another run's state (teacher forcing, tests only)"""
+    with torch.no_grad():
+        for net, mod in nets(m, kind).items():
+            mod.load_state_dict({k: snap["state"][f"{net}/{k}"] for k in mod.state_dict()})
+    for k, o in optimizers(m).items():
+        if snap["optim"][k]["state"]:
+            o.load_state_dict(snap["optim"][k])
+
+
 def main():
     out, kind, n, res, iters = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5])
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
@@ -65,18 +97,21 @@ def main():
         import random
         for pool in (m.cycle_step_fn.pre_pool, m.cycle_step_fn.post_pool):
             pool.rng = random.Random(5)
-    record = kind == "paired" and os.environ.get("FG_RECORD_DECISIONS") == "1"
+    step = m.step_fn if kind == "paired" else m.cycle_step_fn
+    record = os.environ.get("FG_RECORD_DECISIONS") == "1"
     if record:                     # the activation decisions of this rank's passes (teacher forcing, test only)
-        m.step_fn.record_decisions = True
-    losses = run(m, kind, xs, ys, 1)
-    grads0 = grads(m, kind)
-    dec = m.step_fn.decisions if record else None
-    losses += run(m, kind, xs, ys, iters - 1)
+        step.record_decisions = True
+    # per iteration: the state it started from (rank 0; the replicas are identical, checked at the end), the
+    # all-reduced gradients its optimiser steps used, and this rank's activation / L1-sign decisions
+    losses, its = [], []
+    for _ in range(iters):
+        pre = snapshot(m, kind) if rank == 0 else None
+        losses += run(m, kind, xs, ys, 1)
+        its.append({"pre": pre, "grads": grads(m, kind) if rank == 0 else None,
+                    "decisions": _cpu(step.decisions) if record else None})
     torch.cuda.synchronize()
     state = {f"{net}/{k}": v.detach().cpu() for net, mod in nets(m, kind).items() for k, v in mod.state_dict().items()}
-    out_d = {"losses": torch.stack(losses), "state": state, "grads0": grads0}
-    if dec is not None:
-        out_d["decisions"] = dec
+    out_d = {"losses": torch.stack(losses), "state": state, "iters": its}
     torch.save(out_d, f"{out}.rank{rank}")
     dist.barrier()
     dist.destroy_process_group()

@@ -1,9 +1,11 @@
 """Batch data parallelism of the REAL training steps (floodgan.parallel): two
 ranks, each a separate process holding its own replica on the one GPU of the test box, gloo on HIP
 tensors carrying the steps' bucketed asynchronous SUM all-reduces (the same FlatGrads / ready()
-path RCCL takes on an 8-GPU node).  Each rank trains on half of a global batch; the result must
-equal one process training on the whole batch: the per-rank losses average to the single-rank
-losses (equal shards, mean losses), and the parameters after two iterations agree.
+path RCCL takes on an 8-GPU node).  Each rank trains on half of a global batch; every iteration must
+equal one process training on the whole batch from the same state: the per-rank losses average to the
+single-process losses (equal shards, mean losses), the all-reduced gradients equal its gradients, and the
+updates meet the U criterion (decided elements move the same way and agree; tests/test_gpu_northstar.py).
+The production (f16x3) path is also pinned iteration by iteration against the fp64 oracle.
 
 What this pins: the 1/world pre-scaling folded into the loss gradients (model.py PairedStep,
 cycle.py CycleStep), the bucket layout and the ready() order of the executors' backward, and the
@@ -20,13 +22,12 @@ import socket
 import subprocess
 import sys
 
-import numpy as np
 import pytest
 import torch
 
-from oracle import attention_cycle as OC
 from oracle import paired_attention as O
-from test_gpu_parity import nrel
+from test_gpu_northstar import KINK, _update_agreement, u_compare, u_summary
+from test_gpu_parity import DEV, NTOL, nrel
 
 pytestmark = pytest.mark.gpu
 
@@ -47,108 +48,16 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("kind,n,res", [("paired", 4, 64), ("attentiongan", 2, 32)])
-def test_two_rank_step_equals_single_rank(kind, n, res, tmp_path, report):
-    iters = 2
-    out = str(tmp_path / "dp")
-    port = _free_port()
-    env = dict(os.environ, WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
-               OMP_NUM_THREADS="2", FLOODGAN_CONV_MATH="fp32")
-    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dp_worker.py"), out, kind, str(n), str(res),
-                               str(iters)], env=dict(env, RANK=str(r), LOCAL_RANK=str(r)))
-             for r in range(2)]
-    try:
-        rcs = [p.wait(timeout=240) for p in procs]
-    finally:
-        for p in procs:
-            if p.poll() is None:
-                p.kill()
-    assert rcs == [0, 0], rcs
-    ranks = [torch.load(f"{out}.rank{r}", weights_only=True) for r in range(2)]
-    # single process, whole batch
-    from floodgan import _lib as L
-    prev = L.get_conv_math()
-    L.set_conv_math("fp32")
-    try:
-        m = W.make_model(kind)
-        if kind != "paired":
-            import random
-            for pool in (m.cycle_step_fn.pre_pool, m.cycle_step_fn.post_pool):
-                pool.rng = random.Random(5)
-        x, y = W.global_batch(kind, n, res)
-        single = W.run(m, kind, x, y, 1)
-        grads0 = W.grads(m, kind)
-        single = torch.stack(single + W.run(m, kind, x, y, iters - 1)).double()
-    finally:
-        L.set_conv_math(prev)
-    mean = (ranks[0]["losses"].double() + ranks[1]["losses"].double()) / 2
-    lrel = ((mean - single).abs() / single.abs()).numpy()
-    if kind == "paired":
-        skip = {"generator": O.cancelled_biases()[0], "discriminator": O.cancelled_biases()[1]}
-    else:
-        skip = {k: (O.cancelled_biases()[0] if "generator" in k else O.cancelled_biases()[1])
-                for k in W.nets(m, kind)}
-    worst, same = ("", 0.0), True
-    # after updates the two runs' parameters can differ element-wise by at most two opposite Adam steps per iteration
-    # (|step| <= lr at step 1, <= 1.054 lr at step 2 for these betas): an element whose gradient sits at rounding level may take either
-    # sign-like direction, and Adam's normalisation amplifies rounding-level gradient differences up to that bound.
-    # Asserted: no element beyond it (a DP bug -- a missing / doubled bucket, a stale replica -- shows in the
-    # iteration-0 gradients above, which must agree to 1e-5)
-    lr = max(g["lr"] for o in (m.optimizer_generator, m.optimizer_discriminator) for g in o.param_groups)
-    step_bound = 2 * lr * iters * 1.1      # |Adam step| <= 1.054 lr at step 2 for betas (0.5, 0.999) (Cauchy-Schwarz)
-    worst_flip = ("", 0.0)
-    # the all-reduced iteration-0 gradients equal the whole-batch gradients up to summation order;
-    # the paired G step already sees Adam(D), whose elements with rounding-level gradients (undecided
-    # directions) may move differently: 1e-4 there, 1e-5 for every gradient of pre-update state
-    errs = [(k, nrel(ranks[0]["grads0"][k], v)) for k, v in grads0.items()
-            if k.split("/", 1)[1] not in skip[k.split("/", 1)[0]]]
-    post = [e for e in errs if kind == "paired" and e[0].startswith("generator/")]
-    gworst = max([e for e in errs if e not in post], key=lambda t: t[1])
-    gworst_post = max(post, key=lambda t: t[1]) if post else ("", 0.0)
-    for net, mod in W.nets(m, kind).items():
-        for k, v in mod.state_dict().items():
-            a, b = ranks[0]["state"][f"{net}/{k}"], ranks[1]["state"][f"{net}/{k}"]
-            same &= torch.equal(a, b)                       # replicas stay identical
-            if k in skip[net]:
-                continue
-            e = nrel(a, v)
-            if e > worst[1]:
-                worst = (f"{net}/{k}", e)
-            if a.is_floating_point():
-                d = float((a.double() - v.double().cpu()).abs().max())
-                assert d <= step_bound, (f"{net}/{k}", d, step_bound)
-                if d > worst_flip[1]:
-                    worst_flip = (f"{net}/{k}", d)
-    report("dp_two_rank_vs_single", kind=kind, n=n, res=res, loss_rel=lrel.tolist(), worst_param=worst,
-           worst_element_diff=worst_flip, step_bound=step_bound, worst_grad_it0=gworst,
-           worst_grad_it0_after_adam_d=gworst_post,
-           replicas_identical=bool(same))
-    assert same
-    assert gworst[1] < 1e-5 and gworst_post[1] < 1e-4, (gworst, gworst_post)
-    # iteration 0: the losses evaluated before any update agree to rounding (in the paired step the
-    # G loss [2] already sees Adam(D): P3 like everything after an update)
-    pre = [0, 1, 3] if kind == "paired" else list(range(lrel.shape[1]))
-    assert lrel[0][pre].max() < 1e-5, lrel
-    # after updates: every element within two Adam steps per iteration (asserted above); the losses stay within the
-    # P3 bound
-    assert lrel.max() < 1e-3, (lrel, worst, worst_flip)
-
-
-def test_two_rank_paired_f16x3_vs_fp64(tmp_path, report):
-    """The production DP path: the default f16x3 conv math, two ranks each on half of a global batch of 4
-    (64x64), bucketed asynchronous SUM all-reduces.  Iteration 0's all-reduced G and D gradients equal the fp64
-    oracle's whole-batch gradients (models/model.py:611-646) with the two ranks' activation decisions
-    teacher-forced (the per-rank operand scales differ from a whole batch's by powers of two, so kink
-    decisions may differ from any other evaluation): 1e-4 as P2, every differing decision at its kink, and the
-    replicas identical after the update."""
+def _launch(tmp_path, kind, n, res, iters, **env_extra):
+    """two dp_worker ranks (gloo on HIP tensors); their saved records"""
     out = str(tmp_path / "dp")
     port = _free_port()
     env = dict(os.environ, WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), OMP_NUM_THREADS="2",
                FG_RECORD_DECISIONS="1")
     env.pop("FLOODGAN_CONV_MATH", None)
-    n, res = 4, 64
-    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dp_worker.py"), out, "paired", str(n), str(res),
-                               "1"], env=dict(env, RANK=str(r), LOCAL_RANK=str(r))) for r in range(2)]
+    env.update(env_extra)
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dp_worker.py"), out, kind, str(n), str(res),
+                               str(iters)], env=dict(env, RANK=str(r), LOCAL_RANK=str(r))) for r in range(2)]
     try:
         rcs = [p.wait(timeout=240) for p in procs]
     finally:
@@ -158,22 +67,128 @@ def test_two_rank_paired_f16x3_vs_fp64(tmp_path, report):
     assert rcs == [0, 0], rcs
     ranks = [torch.load(f"{out}.rank{r}", weights_only=True) for r in range(2)]
     for k, v in ranks[0]["state"].items():
-        assert torch.equal(v, ranks[1]["state"][k]), k              # replicas stay identical
-    merged = {net: [{k: torch.cat((a[k], b[k]), 0) for k in a} for a, b in zip(ranks[0]["decisions"][net],
-                                                                             ranks[1]["decisions"][net])]
-              for net in ("G", "D", "L1") if net in ranks[0]["decisions"]}
-    dec = O.ActDecisions(merged)
-    x, y = W.global_batch("paired", n, res)
-    st = O.PairedStepOracle(dtype=torch.float64)
-    rec = {}
-    d_after = {k.split("/", 1)[1]: v for k, v in ranks[0]["state"].items() if k.startswith("discriminator/")}
-    st.step(x, y, record=rec, d_after=d_after, decisions=dec)
+        assert torch.equal(v, ranks[1]["state"][k]), k              # the replicas stay identical
+    return ranks
+
+
+def _merge(a, b):
+    """the two ranks' decisions of one iteration as one global batch (rank 0 holds the first half)"""
+    if isinstance(a, dict):
+        return {k: _merge(a[k], b[k]) for k in a}
+    if isinstance(a, list):
+        return [_merge(x, y) for x, y in zip(a, b)]
+    return torch.cat((a, b), 0)
+
+
+def _count_diff(a, b):
+    if isinstance(a, dict):
+        return sum(_count_diff(a[k], b[k]) for k in a)
+    if isinstance(a, list):
+        return sum(_count_diff(x, y) for x, y in zip(a, b))
+    return int((a.cpu() != b.cpu()).sum())
+
+
+def _post_state(ranks, it):
+    """the two-rank state after iteration `it`"""
+    its = ranks[0]["iters"]
+    return its[it + 1]["pre"]["state"] if it + 1 < len(its) else ranks[0]["state"]
+
+
+@pytest.mark.parametrize("kind,n,res", [("paired", 4, 64), ("attentiongan", 2, 32)])
+def test_two_rank_step_equals_single_rank(kind, n, res, tmp_path, report):
+    """Two ranks (exact-fp32 conv math) train two iterations on halves of a global batch.  For EACH iteration a
+    single process is loaded with the state the two ranks started it from (every network, both Adam states) and
+    runs the same iteration on the whole batch; in the paired step it also continues its G half on the two-rank
+    discriminator after Adam(D) (PairedStep.d_after), as the oracle comparisons do.  Asserted per iteration:
+      * the all-reduced gradients equal the single-process gradients: 1e-5 norm-relative (IN-cancelled biases
+        excluded, SURVEY.md §7.3) when both evaluations take the same activation / L1-sign decisions (counted);
+      * the losses: the two ranks' mean equals the single process's to 1e-5;
+      * the update (U criterion, tests/test_gpu_northstar.py): every element whose first moment is decided --
+        |m| above 10x the gradient's disagreement -- moves the same way (fraction 1.0) and the decided updates
+        agree to 1e-3; the undecided fraction is reported.
+    A DP defect -- a missing or doubled bucket, a stale replica, the 1/world scale applied twice -- moves the
+    gradients by O(1) and fails the first bound; rounding-level gradient noise that Adam's normalisation
+    amplifies only touches undecided elements."""
+    from floodgan import _lib as L
+    iters = 2
+    ranks = _launch(tmp_path, kind, n, res, iters, FLOODGAN_CONV_MATH="fp32")
+    x, y = W.global_batch(kind, n, res)
     skip_g, skip_d = O.cancelled_biases()
-    eg = max(((k, nrel(ranks[0]["grads0"]["generator/" + k], v)) for k, v in rec["g_grads"].items()
-              if k not in skip_g), key=lambda t: t[1])
-    ed = max(((k, nrel(ranks[0]["grads0"]["discriminator/" + k], v)) for k, v in rec["d_grads"].items()
-              if k not in skip_d), key=lambda t: t[1])
-    report("dp_two_rank_f16x3_vs_fp64", n=n, res=res, worst_G=eg, worst_D=ed,
-           decisions_differing=sum(c for _, _, c, _ in dec.log), worst_kink=dec.worst())
-    assert eg[1] < 1e-4 and ed[1] < 1e-4, (eg, ed)
-    assert dec.worst() < 1e-4, dec.worst()
+    prev = L.get_conv_math()
+    L.set_conv_math("fp32")
+    try:
+        for it in range(iters):
+            rec = ranks[0]["iters"][it]
+            post = _post_state(ranks, it)
+            m = W.make_model(kind)
+            if kind != "paired":
+                import random
+                for pool in (m.cycle_step_fn.pre_pool, m.cycle_step_fn.post_pool):
+                    pool.rng = random.Random(5)
+            W.load_snapshot(m, kind, rec["pre"])
+            step = m.step_fn if kind == "paired" else m.cycle_step_fn
+            step.record_decisions = True
+            if kind == "paired":
+                step.d_after = {k: post[f"discriminator/{k}"].to(DEV) for k, _ in m.discriminator.named_parameters()}
+            single = W.run(m, kind, x, y, 1)[0].double()
+            flips = _count_diff(_merge(rec["decisions"], ranks[1]["iters"][it]["decisions"]), step.decisions)
+            mean = (ranks[0]["losses"][it].double() + ranks[1]["losses"][it].double()) / 2
+            lrel = float(((mean - single).abs() / single.abs()).max())
+            opt_state = {}
+            for o in (m.optimizer_generator, m.optimizer_discriminator):
+                opt_state.update(o.state)
+            rows, bad = [], []
+            for net, mod in W.nets(m, kind).items():
+                skip = skip_g if "generator" in net else skip_d
+                for k, p in mod.named_parameters():
+                    if k in skip:
+                        continue
+                    key = f"{net}/{k}"
+                    ge = nrel(rec["grads"][key], p.grad)
+                    # the paired discriminator's own Adam(D) result (its parameters now hold d_after)
+                    p_single = step.d_after_own[k] if kind == "paired" and net == "discriminator" else p
+                    agree, uerr, frac, perr = _update_agreement(rec["pre"]["state"][key], post[key], p_single,
+                                                                rec["grads"][key], p.grad, opt_state[p]["exp_avg"])
+                    rows.append((net, k, ge, agree, uerr, frac, perr))
+                    if ge > (1e-5 if flips == 0 else 1e-3) or agree < 1.0 or uerr > NTOL:
+                        bad.append(rows[-1])
+            report("dp_two_rank_vs_single_continuation", kind=kind, n=n, res=res, it=it, decisions_differing=flips,
+                   loss_rel=lrel, **u_summary(rows), bad=bad)
+            assert flips <= 8, (it, flips)
+            assert not bad, (it, bad)
+            assert lrel < 1e-5, (it, mean, single)
+            del m
+    finally:
+        L.set_conv_math(prev)
+
+
+def test_two_rank_paired_f16x3_vs_fp64(tmp_path, report):
+    """The production DP path: the default f16x3 conv math, two ranks each on half of a global batch of 4
+    (64x64), bucketed asynchronous SUM all-reduces, two iterations.  For each iteration the fp64 oracle
+    continues from the state the ranks started it from (both networks, both Adam states), with the two ranks'
+    activation and L1-sign decisions teacher-forced and, for the G half, the two-rank discriminator after
+    Adam(D) (models/model.py:611-651, updates at :633 and :646).  Asserted per iteration: the all-reduced G / D
+    gradients vs fp64 to 1e-4 (P2), every differing decision at its kink, and the U criterion on the updates
+    (decided elements: direction 1.0, update 1e-3)."""
+    n, res, iters = 4, 64, 2
+    ranks = _launch(tmp_path, "paired", n, res, iters)
+    x, y = W.global_batch("paired", n, res)
+    for it in range(iters):
+        rec = ranks[0]["iters"][it]
+        pre, post = rec["pre"], _post_state(ranks, it)
+        dec = O.ActDecisions(_merge(rec["decisions"], ranks[1]["iters"][it]["decisions"]))
+        split = lambda st, net: {k.split("/", 1)[1]: v for k, v in st.items() if k.startswith(net + "/")}  # noqa: E731
+        g0, d0 = split(pre["state"], "generator"), split(pre["state"], "discriminator")
+        lr = pre["optim"]["optimizer_generator"]["param_groups"][0]["lr"]
+        st = O.PairedStepOracle(dtype=torch.float64, lr=lr)
+        st.load_state(g0, d0, pre["optim"]["optimizer_generator"] if it else None,
+                      pre["optim"]["optimizer_discriminator"] if it else None)
+        orec = {}
+        st.step(x, y, record=orec, d_after=split(post, "discriminator"), decisions=dec)
+        rows, bad = u_compare(st, orec, {"G": g0, "D": d0},
+                              {"G": split(post, "generator"), "D": split(post, "discriminator")},
+                              {"G": split(rec["grads"], "generator"), "D": split(rec["grads"], "discriminator")})
+        report("dp_two_rank_f16x3_vs_fp64", n=n, res=res, it=it, **u_summary(rows),
+               decisions_differing=sum(c for _, _, c, _ in dec.log), worst_kink=dec.worst(), bad=bad)
+        assert dec.worst() < KINK, (it, dec.worst())
+        assert not bad, (it, bad)

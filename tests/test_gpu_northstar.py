@@ -271,6 +271,7 @@ BETA1 = 0.5
 def _update_agreement(p0, p_hip, p_ref, g_hip, g_ref, m_ref):
     """(fraction of decided elements whose update direction agrees, norm-relative update error over
     the decided elements, fraction decided, norm-relative error of the whole updated tensor)"""
+    p0, p_hip, p_ref, g_hip, g_ref = (t.detach() for t in (p0, p_hip, p_ref, g_hip, g_ref))
     d_hip = (p_hip.double().cpu() - p0.double().cpu()).flatten()
     d_ref = (p_ref.double().cpu() - p0.double().cpu()).flatten()
     dg = (g_hip.double().cpu() - g_ref.double().cpu()).flatten()
@@ -288,13 +289,44 @@ def _update_agreement(p0, p_hip, p_ref, g_hip, g_ref, m_ref):
     return agree, err, n / d_ref.numel(), nrel(p_hip, p_ref)
 
 
+def u_compare(st, rec, P0, P_hip, g_hip):
+    """The U criterion for one iteration of a run against the fp64 oracle `st` that continued from the same
+    state (PairedStepOracle after step(..., record=rec, d_after=the run's D after Adam(D), decisions=...)).
+    P0 / P_hip / g_hip: {"G": {name: tensor}, "D": {...}} -- the run's parameters before and after the
+    iteration and the gradients its optimiser steps used.  Returns (rows, bad): per parameter (net, name,
+    gradient error, direction agreement of the decided elements, decided-update error, decided fraction,
+    whole-tensor error); bad = rows past the bounds (gradient 1e-4, agreement 1.0, decided update 1e-3).
+    IN-cancelled biases are skipped (their gradients are rounding noise)."""
+    skip_g, skip_d = O.cancelled_biases()
+    rows, bad = [], []
+    for net, grads, skip, opt_ref, params_ref, order in (
+            ("G", rec["g_grads"], skip_g, st.opt_g, st.G, list(st.G)),
+            ("D", rec["d_grads"], skip_d, st.opt_d, rec["d_after_own"], list(st.D))):
+        for k in order:
+            if k in skip:
+                continue
+            ge = nrel(g_hip[net][k], grads[k])
+            m_ref = opt_ref.state[opt_ref.param_groups[0]["params"][order.index(k)]]["exp_avg"]
+            agree, uerr, frac, perr = _update_agreement(P0[net][k], P_hip[net][k], params_ref[k], g_hip[net][k],
+                                                        grads[k], m_ref)
+            rows.append((net, k, ge, agree, uerr, frac, perr))
+            if ge > 1e-4 or agree < 1.0 or uerr > NTOL:
+                bad.append(rows[-1])
+    return rows, bad
+
+
+def u_summary(rows):
+    return dict(worst_grad=max(rows, key=lambda r: r[2])[1:3], min_agree=min(r[3] for r in rows),
+                worst_update=max(rows, key=lambda r: r[4])[1:5:3], min_decided=min(r[5] for r in rows),
+                worst_param_rel=max(rows, key=lambda r: r[6])[1:7:5])
+
+
 def _teacher_forced_iterations(m, batches, report, name, **tags):
     """Run the fused step over `batches` [(x, y, lr)], one iteration each.  Before each, the fp64 oracle is
     loaded with the HIP state (G, D, both Adam states) and runs the same iteration with the HIP path's
     activation decisions and, for the G half, the HIP discriminator after Adam(D).  Asserted per iteration:
     every G and D gradient within 1e-4, every differing decision at its kink, every decided element's update
     direction agrees and the decided updates agree to 1e-3 (models/model.py:633, :646)."""
-    skip_g, skip_d = O.cancelled_biases()
     G, D = m.generator, m.discriminator
     m.step_fn.record_decisions = True
     for it, (x, y, lr) in enumerate(batches):
@@ -312,28 +344,15 @@ def _teacher_forced_iterations(m, batches, report, name, **tags):
         dec = O.ActDecisions(m.step_fn.decisions)
         ref_losses = st.step(x, y, record=rec, d_after={k: v.detach().cpu() for k, v in D.named_parameters()},
                              decisions=dec)
-        rows, bad = [], []
-        for net, mod, P0, grads, skip, opt_ref in (("G", G, g0, rec["g_grads"], skip_g, st.opt_g),
-                                                   ("D", D, d0, rec["d_grads"], skip_d, st.opt_d)):
-            params_ref = st.G if net == "G" else rec["d_after_own"]
-            order = list(st.G if net == "G" else st.D)
-            for k, p in mod.named_parameters():
-                if k in skip:
-                    continue
-                ge = nrel(p.grad, grads[k])
-                m_ref = opt_ref.state[opt_ref.param_groups[0]["params"][order.index(k)]]["exp_avg"]
-                agree, uerr, frac, perr = _update_agreement(P0[k], p, params_ref[k], p.grad, grads[k], m_ref)
-                rows.append((net, k, ge, agree, uerr, frac, perr))
-                if ge > 1e-4 or agree < 1.0 or uerr > NTOL:
-                    bad.append(rows[-1])
+        rows, bad = u_compare(st, rec, {"G": g0, "D": d0}, {"G": dict(G.named_parameters()),
+                                                             "D": dict(D.named_parameters())},
+                              {"G": {k: p.grad for k, p in G.named_parameters()},
+                               "D": {k: p.grad for k, p in D.named_parameters()}})
         hl = losses.cpu().double().numpy()
         rl = np.array([float(v) for v in ref_losses])
         rl[3] *= 100
         lrel = float(np.max(np.abs(hl - rl) / np.abs(rl)))
-        report(name, it=it, **tags,
-               worst_grad=max(rows, key=lambda r: r[2])[1:3], min_agree=min(r[3] for r in rows),
-               worst_update=max(rows, key=lambda r: r[4])[1:5:3], min_decided=min(r[5] for r in rows),
-               worst_param_rel=max(rows, key=lambda r: r[6])[1:7:5], decisions_differing=sum(r[2] for r in dec.log),
+        report(name, it=it, **tags, **u_summary(rows), decisions_differing=sum(r[2] for r in dec.log),
                worst_kink=dec.worst(), loss_rel=lrel, bad=bad)
         assert np.isfinite(hl).all(), (it, hl)
         assert dec.worst() < KINK, (it, dec.worst())
@@ -363,6 +382,18 @@ def test_update_teacher_forced_10_iterations(R_, bs, report):
     lr = m.optimizer_generator.param_groups[0]["lr"]
     batches = [_inputs(bs, res=R_, seed=500 + it) + (lr,) for it in range(10)]
     _teacher_forced_iterations(m, batches, report, "update_teacher_forced_10it", R=R_, bs=bs)
+
+
+def test_update_teacher_forced_512(report):
+    """The U criterion at the bench resolution (512x512, batch 2, default switches: f16x3, pack cache, pre-split
+    operands, fused statistics): two consecutive iterations, each checked against the fp64 oracle continuing from
+    the HIP state with the HIP decisions teacher-forced (_teacher_forced_iterations; models/model.py:611-651,
+    updates at :633 and :646).  The second iteration runs on the packs, scale slots and Adam moments the first
+    one left behind."""
+    m = _model()
+    lr = m.optimizer_generator.param_groups[0]["lr"]
+    batches = [_inputs(2, seed=600 + it) + (lr,) for it in range(2)]
+    _teacher_forced_iterations(m, batches, report, "update_teacher_forced_512", R=R, bs=2)
 
 
 def test_check_scales_bench_loop_25_steps(report):
@@ -587,23 +618,17 @@ def test_f16x3_dynamic_range(case, report):
         assert a < max(KTOL, 4 * b), res
 
 
-def test_side_stream_weight_gradients_identical():
-    """FLOODGAN_SIDE_STREAM's schedule (weight gradients on a second stream) changes nothing but the
-    order of independent launches: two fused steps give bit-identical losses and parameters."""
-    from floodgan import executor as X
+def test_fused_step_deterministic():
+    """Run-to-run determinism of the fused step (every reduction in a fixed order, no atomics in the sums):
+    two fresh models trained two iterations on the same batches give bit-identical losses and parameters."""
     x, y = _inputs(2, res=64, seed=3)
     out = []
-    prev = X.SIDE_STREAM
-    try:
-        for side in (False, True):
-            X.SIDE_STREAM = side
-            m = _model()
-            ls = [m.step_fn(x.to(DEV), y.to(DEV)).cpu() for _ in range(2)]
-            torch.cuda.synchronize()
-            out.append((torch.stack(ls), [p.detach().cpu().clone() for p in m.generator.parameters()],
-                        [p.detach().cpu().clone() for p in m.discriminator.parameters()]))
-    finally:
-        X.SIDE_STREAM = prev
+    for _ in range(2):
+        m = _model()
+        ls = [m.step_fn(x.to(DEV), y.to(DEV)).cpu() for _ in range(2)]
+        torch.cuda.synchronize()
+        out.append((torch.stack(ls), [p.detach().cpu().clone() for p in m.generator.parameters()],
+                    [p.detach().cpu().clone() for p in m.discriminator.parameters()]))
     assert torch.equal(out[0][0], out[1][0])
     assert all(torch.equal(a, b) for a, b in zip(out[0][1], out[1][1]))
     assert all(torch.equal(a, b) for a, b in zip(out[0][2], out[1][2]))

@@ -230,3 +230,50 @@ def test_modules_autograd_and_eval_mode():
     F.mse_loss(pred, torch.ones_like(pred)).backward()
     assert all(p.grad is not None and torch.isfinite(p.grad).all() for p in G.parameters())
     assert all(p.grad is not None for p in D.parameters())
+
+
+@pytest.mark.parametrize("seed,pre,shapes,p", [
+    (47, 0, [(8, 512, 8, 8), (8, 512, 16, 16), (8, 512, 32, 32)], 0.5),   # Pix2Pix 512^2 batch 8: 69 chunks
+    (5, 3, [(2, 512, 4, 4), (2, 512, 8, 8), (2, 512, 16, 16)], 0.5),     # 256^2 batch 2: one chunk
+    (9, 623, [(1, 7, 3), (79872,), (79873,), (5,)], 0.3),                  # odd sizes across chunk boundaries
+    (0, 624, [(10_500_000,)], 0.5),                                        # past the committed jump table
+])
+def test_device_torch_stream_bit_exact(seed, pre, shapes, p):
+    """floodgan.torch_rng (csrc/mt19937.hip): the device-generated masks equal torch's CPU draws
+    torch.empty(shape).bernoulli_(p) -- the reference's nn.Dropout (models/model_architectures.py:52) -- element for
+    element, from the same generator state, and commit() leaves torch's generator exactly where those CPU draws
+    leave it."""
+    from floodgan import torch_rng
+    torch.manual_seed(seed)
+    if pre:
+        torch.randint(0, 2 ** 31, (pre,), dtype=torch.int64)
+    state = torch.get_rng_state()
+    outs, commit = torch_rng.draw(shapes, p, DEV)
+    commit()
+    after = torch.get_rng_state()
+    torch.set_rng_state(state)
+    ref = [torch.empty(s).bernoulli_(p) for s in shapes]
+    for o, r in zip(outs, ref):
+        assert o.shape == r.shape
+        assert torch.equal(o.cpu(), r), int((o.cpu() != r).sum())
+    assert torch.equal(after, torch.get_rng_state())
+
+
+def test_step_host_dropout_is_torch_stream(report):
+    """Pix2PixStep with dropout_rng = "host": the masks of each iteration are torch's CPU draws (levels 7, 6, 5, as
+    the reference's forward draws them) and, after the step, torch's generator stands where the CPU draws leave it
+    -- two iterations in a row at 256x256, batch 2."""
+    from floodgan import pix2pix as P2P
+    m = _model()
+    m.generator.dropout_rng = "host"
+    (x, y), _ = synth_inputs(N=2, C=9)
+    torch.manual_seed(123)
+    for it in range(2):
+        state = torch.get_rng_state()
+        m.step_fn(x.to(DEV), y.to(DEV)).cpu()
+        after = torch.get_rng_state()
+        torch.set_rng_state(state)
+        ref = P2P.draw_dropout_masks(2, R, R)
+        for k, v in ref.items():
+            assert torch.equal(m.step_fn.last_masks[k].cpu(), v), (it, k)
+        assert torch.equal(after, torch.get_rng_state()), it
