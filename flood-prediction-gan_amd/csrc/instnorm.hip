@@ -234,13 +234,86 @@ __device__ __forceinline__ void store_splitpix(char* px, const f32x4& o, float s
 // 64-bit divisions per element and held one load in flight: 5.0 TB/s).
 constexpr int kRowU = 4;
 
-template <bool NTL>
+// The attention head (Conv2d(64, 10, 1), models/model_architectures.py:334, :369) fused into the norm passes of its
+// 64-channel input (round 5): the 16 lanes of a pixel hold its 64 channels, four each.
+//   forward: the apply pass also forms the head's logits y[p][o] = b[o] + sum_c w[o][c] a[p][c] from the activation
+//            it just wrote -- the same per-lane fma chain and 16-lane DPP reduce-scatter as conv1x1_fwd_lanes
+//            (head1x1.hip), so the logits are bit-identical to that kernel's, without re-reading the 537-MB activation;
+//   backward: the statistics and apply passes read the 16-channel logits gradient instead of the 64-channel input
+//            gradient and form g[p][c] = sum_o w[o][c] gy[p][o] in registers, in conv1x1_dgrad_kernel's fma order
+//            (bit-identical): the dgrad launch and its 537-MB gradient (written once, read twice) are gone.
+constexpr int HEAD_CI = 64, HEAD_NO = 16;
+struct HeadArgs {
+    const float* w;     // [n_out][64]
+    const float* b;     // forward: [n_out] or null
+    int n_out;
+    fg_view y;          // forward: the logits (16-ch allocation, pad 0); backward: the logits gradient (16 ch)
+};
+
+template <int CTRL>
+__device__ __forceinline__ float head_dpp(float v) { return fg::dpp<CTRL>(v); }
+
+// forward: lane cq (of a pixel's 16) holds channels 4cq..4cq+3 in v and w[o][4cq..4cq+3] in wr[o]; returns output cq's
+// sum (conv1x1_fwd_lanes' order)
+__device__ __forceinline__ float head_logit(const f32x4& v, const f32x4 (&wr)[HEAD_NO], int cq) {
+    float acc[HEAD_NO];
+#pragma unroll
+    for (int o = 0; o < HEAD_NO; ++o)
+        acc[o] = fmaf(v[3], wr[o][3], fmaf(v[2], wr[o][2], fmaf(v[1], wr[o][1], v[0] * wr[o][0])));
+    const bool h3 = cq & 8, h2 = cq & 4, h1 = cq & 2, h0 = cq & 1;
+    float a8[8], a4[4], a2[2];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a8[k] = (h3 ? acc[8 + k] : acc[k]) + head_dpp<0x140>(h3 ? acc[k] : acc[8 + k]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) a4[k] = (h2 ? a8[4 + k] : a8[k]) + head_dpp<0x141>(h2 ? a8[k] : a8[4 + k]);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) a2[k] = (h1 ? a4[2 + k] : a4[k]) + head_dpp<0x1B>(h1 ? a4[k] : a4[2 + k]);
+    return (h0 ? a2[1] : a2[0]) + head_dpp<0xB1>(h0 ? a2[0] : a2[1]);
+}
+
+// backward: the logits gradient of pixel (n, y, x) (its first HEAD_NB channels: 3 quads, loaded in the load phase with
+// the other operands), then the 4 channels' input gradient from it in conv1x1_dgrad_kernel's fma order
+constexpr int HEAD_NB = 12;      // logits the fused backward takes (n_out <= 12)
+struct HeadG {
+    f32x4 q[HEAD_NB / 4];
+};
+__device__ __forceinline__ HeadG head_load(const fg_view& gy, int n, int y, int x) {
+    const float* gp = gy.ptr + fg::vidx(gy, n, y, x);
+    HeadG g;
+#pragma unroll
+    for (int q = 0; q < HEAD_NB / 4; ++q) g.q[q] = *reinterpret_cast<const f32x4*>(gp + 4 * q);
+    return g;
+}
+__device__ __forceinline__ f32x4 head_grad(const HeadG& g, const f32x4 (&wr)[HEAD_NB], int n_out) {
+    f32x4 a = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int o = 0; o < HEAD_NB; ++o) {
+        if (o < n_out) {
+            const float go = g.q[o / 4][o % 4];
+            a[0] = fmaf(go, wr[o][0], a[0]);
+            a[1] = fmaf(go, wr[o][1], a[1]);
+            a[2] = fmaf(go, wr[o][2], a[2]);
+            a[3] = fmaf(go, wr[o][3], a[3]);
+        }
+    }
+    return a;
+}
+
+template <int NO>
+__device__ __forceinline__ void head_weights(const HeadArgs& hd, int c4, f32x4 (&wr)[NO]) {
+#pragma unroll
+    for (int o = 0; o < NO; ++o)
+        wr[o] = o < hd.n_out ? *reinterpret_cast<const f32x4*>(hd.w + o * HEAD_CI + 4 * c4) : f32x4{0.f, 0.f, 0.f, 0.f};
+}
+
+template <bool NTL, bool HEAD = false>
 __global__ void __launch_bounds__(NT) in_apply_rows_kernel(fg_view src, const float* __restrict__ mean,
                                                            const float* __restrict__ rstd, int act, fg_view res,
                                                            fg_view dst, int pad_mode, int lshift,
                                                            unsigned* __restrict__ amax, float* __restrict__ split_slot,
                                                            float* __restrict__ ps_ptr, float* __restrict__ ps_slot,
-                                                           const float* __restrict__ res_amax, int splitpix) {
+                                                           const float* __restrict__ res_amax, int splitpix,
+                                                           HeadArgs hd = HeadArgs{}) {
     const int L = 1 << lshift, PG = NT >> lshift;
     const int C = dst.c_alloc, h = dst.h, w = dst.w, pad = dst.pad;
     const int hp = h + 2 * pad, wp = w + 2 * pad;
@@ -277,6 +350,12 @@ __global__ void __launch_bounds__(NT) in_apply_rows_kernel(fg_view src, const fl
     } else {
         y = fg::reflect_idx(y, h);
         const f32x4 m = ld4(mean + (size_t)n * C + 4 * c4), r = ld4(rstd + (size_t)n * C + 4 * c4);
+        f32x4 wr[HEAD ? HEAD_NO : 1];
+        float hb = 0.f;
+        if constexpr (HEAD) {
+            head_weights<HEAD_NO>(hd, c4, wr);
+            hb = (hd.b && c4 < hd.n_out) ? hd.b[c4] : 0.f;
+        }
         const float* srow = src.ptr + fg::vidx(src, n, y, 0) + 4 * c4;
         const float* rrow = res.ptr ? res.ptr + fg::vidx(res, n, y, 0) + 4 * c4 : nullptr;
         for (int xp0 = gi; xp0 < wp; xp0 += kRowU * PG) {
@@ -313,6 +392,10 @@ __global__ void __launch_bounds__(NT) in_apply_rows_kernel(fg_view src, const fl
                     am = max(am, absbits4(o));
                     *reinterpret_cast<f32x4*>(drow + (size_t)xp * C) = o;
                     if (psrow) store_presplit(psrow + (size_t)xp * C, o, ss, c4 & 1);
+                }
+                if constexpr (HEAD) {       // the interior (the head reads an unpadded activation: pad 0)
+                    const float lg = head_logit(o, wr, c4);
+                    if (c4 < hd.y.c_alloc) hd.y.ptr[fg::vidx(hd.y, n, y, xp - pad) + c4] = lg + hb;
                 }
             }
         }
@@ -365,12 +448,12 @@ __device__ __forceinline__ f32x4 fold_extra(f32x4 v, const fg_view& g, int fp, i
 // fp32 accumulation order per thread as in_bwd_stats_kernel: results are bit-identical).  NTG: the gradient and gadd
 // are read non-temporally -- with gsum the apply pass reads the gathered sum instead of them, so they are dead after
 // this pass, and src + gsum (268 MB at the resblock shape) can stay in the 256-MB Infinity Cache for the apply pass
-template <bool NTG>
+template <bool NTG, bool HEAD = false>
 __global__ void __launch_bounds__(NT) in_bwd_stats_u_kernel(fg_view g, int fp, fg_view gadd, fg_view src,
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ rstd, int act, int chunks,
                                                             double* __restrict__ work, fg_view gsum,
-                                                            float* __restrict__ gmax_part) {
+                                                            float* __restrict__ gmax_part, HeadArgs hd = HeadArgs{}) {
     const int C = src.c_alloc, L = C / 4, PG = NT / L;
     unsigned gm = 0;
     const int n = blockIdx.y, chunk = blockIdx.x;
@@ -383,10 +466,13 @@ __global__ void __launch_bounds__(NT) in_bwd_stats_u_kernel(fg_view g, int fp, f
     if (gi < PG) {
         const f32x4 m = ld4(mean + (size_t)n * C + 4 * c4);
         const f32x4 r = ld4(rstd + (size_t)n * C + 4 * c4);
+        f32x4 wr[HEAD ? HEAD_NB : 1];
+        if constexpr (HEAD) head_weights(hd, c4, wr);
         int y = (p0 + gi) / w, x = (p0 + gi) - ((p0 + gi) / w) * w;
         for (int p = p0 + gi; p < p1; p += kRowU * PG) {
             int ys[kRowU], xs[kRowU];
             f32x4 sv[kRowU], gv[kRowU], av[kRowU];
+            HeadG hg[HEAD ? kRowU : 1];
 #pragma unroll
             for (int k = 0; k < kRowU; ++k) {
                 ys[k] = y;
@@ -394,7 +480,10 @@ __global__ void __launch_bounds__(NT) in_bwd_stats_u_kernel(fg_view g, int fp, f
                 const bool ok = p + k * PG < p1;
                 sv[k] = ok ? ld4(src.ptr + fg::vidx(src, n, y, x) + 4 * c4) : f32x4{0.f, 0.f, 0.f, 0.f};
                 const float* gp = g.ptr + fg::vidx(g, n, y + fp, x + fp) + 4 * c4;
-                gv[k] = ok ? (NTG ? ld4_nt(gp) : ld4(gp)) : f32x4{0.f, 0.f, 0.f, 0.f};
+                if constexpr (HEAD)
+                    hg[k] = head_load(hd.y, n, ok ? y : 0, ok ? x : 0);
+                else
+                    gv[k] = ok ? (NTG ? ld4_nt(gp) : ld4(gp)) : f32x4{0.f, 0.f, 0.f, 0.f};
                 const float* ap = gadd.ptr + fg::vidx(gadd, n, y, x) + 4 * c4;
                 av[k] = (ok && gadd.ptr) ? (NTG ? ld4_nt(ap) : ld4(ap)) : f32x4{0.f, 0.f, 0.f, 0.f};
                 x += PG;
@@ -406,6 +495,7 @@ __global__ void __launch_bounds__(NT) in_bwd_stats_u_kernel(fg_view g, int fp, f
 #pragma unroll
             for (int k = 0; k < kRowU; ++k) {
                 if (p + k * PG >= p1) break;
+                if constexpr (HEAD) gv[k] = head_grad(hg[k], wr, hd.n_out);
                 f32x4 gk = gv[k];
                 if (fold_border(ys[k], xs[k], h, w, fp)) gk = fold_extra(gk, g, fp, n, ys[k], xs[k], h, w, c4);
                 gk += av[k];
@@ -639,7 +729,7 @@ __global__ void in_bwd_apply_kernel(fg_view g, int fp, fg_view gadd, fg_view src
 }
 
 // row form of the backward apply (C/4 | 256): block = one padded output row, kRowU pixels' loads in flight
-template <bool NTL>
+template <bool NTL, bool HEAD = false>
 __global__ void __launch_bounds__(NT) in_bwd_apply_rows_kernel(fg_view g, int fp, fg_view gadd, fg_view src,
                                                                const float* __restrict__ mean,
                                                                const float* __restrict__ rstd,
@@ -647,7 +737,8 @@ __global__ void __launch_bounds__(NT) in_bwd_apply_rows_kernel(fg_view g, int fp
                                                                unsigned* __restrict__ amax,
                                                                const double* __restrict__ bpart,
                                                                float* __restrict__ bias_grad, int bias_accumulate,
-                                                               int lshift, const float* __restrict__ split_slot) {
+                                                               int lshift, const float* __restrict__ split_slot,
+                                                               HeadArgs hd = HeadArgs{}) {
     // pre-split output: the scale of the bound the finalize published (the consumer derives the same one)
     const float ss = split_slot ? fgc::pow2_scale(split_slot) : 0.f;
     if (bias_grad && blockIdx.x == 0) {
@@ -674,18 +765,24 @@ __global__ void __launch_bounds__(NT) in_bwd_apply_rows_kernel(fg_view g, int fp
         const f32x4 m = ld4(mean + nc), r = ld4(rstd + nc);
         const f32x4 k01 = ld4(coef + nc * 2), k23 = ld4(coef + nc * 2 + 4);
         const f32x4 c1 = {k01[0], k01[2], k23[0], k23[2]}, c2 = {k01[1], k01[3], k23[1], k23[3]};
+        f32x4 wr[HEAD ? HEAD_NB : 1];
+        if constexpr (HEAD) head_weights(hd, c4, wr);
         const float* srow = src.ptr + fg::vidx(src, n, y, 0) + 4 * c4;
-        const float* grow = g.ptr + fg::vidx(g, n, y + fp, fp) + 4 * c4;
+        const float* grow = HEAD ? nullptr : g.ptr + fg::vidx(g, n, y + fp, fp) + 4 * c4;
         const float* arow = gadd.ptr ? gadd.ptr + fg::vidx(gadd, n, y, 0) + 4 * c4 : nullptr;
         for (int xp0 = gi; xp0 < wp; xp0 += kRowU * PG) {
             f32x4 sv[kRowU], gv[kRowU], av[kRowU];
+            HeadG hg[HEAD ? kRowU : 1];
             bool ok[kRowU];
 #pragma unroll
             for (int k = 0; k < kRowU; ++k) {
                 const int x = xp0 + k * PG - pad;
                 ok[k] = x >= 0 && x < w;
                 sv[k] = ok[k] ? ldx<NTL>(srow + (size_t)x * C) : z;
-                gv[k] = ok[k] ? ldx<NTL>(grow + (size_t)x * C) : z;
+                if constexpr (HEAD)
+                    hg[k] = head_load(hd.y, n, y, ok[k] ? x : 0);
+                else
+                    gv[k] = ok[k] ? ldx<NTL>(grow + (size_t)x * C) : z;
                 av[k] = (ok[k] && arow) ? ldx<NTL>(arow + (size_t)x * C) : z;
             }
 #pragma unroll
@@ -695,6 +792,7 @@ __global__ void __launch_bounds__(NT) in_bwd_apply_rows_kernel(fg_view g, int fp
                 f32x4 out = z;
                 if (ok[k]) {
                     const int x = xp - pad;
+                    if constexpr (HEAD) gv[k] = head_grad(hg[k], wr, hd.n_out);
                     f32x4 gk = gv[k];
                     if (fold_border(y, x, h, w, fp)) gk = fold_extra(gk, g, fp, n, y, x, h, w, c4);
                     gk += av[k];
@@ -989,10 +1087,16 @@ FG_API int fg_in_stats(fg_view src, float eps, float* mean, float* rstd, double*
 namespace {
 int in_apply_impl(fg_view src, const float* mean, const float* rstd, int act, fg_view residual, fg_view dst,
                   int pad_mode, float* absmax, float* split_slot, hipStream_t stream, float* ps_ptr = nullptr,
-                  float* ps_slot = nullptr, const float* res_amax = nullptr, int splitpix = 0);
+                  float* ps_slot = nullptr, const float* res_amax = nullptr, int splitpix = 0,
+                  const HeadArgs* head = nullptr);
 int in_bwd_impl(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, const float* mean, const float* rstd, int act,
                 fg_view dst, float* bias_grad, int bias_accumulate, fg_view gsum, double* work, float* absmax,
-                float* split_slot, hipStream_t stream);
+                float* split_slot, hipStream_t stream, const HeadArgs* head = nullptr);
+bool head_ok(const HeadArgs& h, const fg_view& v) {
+    return h.w && h.n_out >= 1 && h.n_out <= HEAD_NB && v.c_alloc == HEAD_CI && h.y.ptr && h.y.c_alloc >= h.n_out &&
+           h.y.c_alloc <= HEAD_NO && h.y.c_alloc % 4 == 0 && h.y.n == v.n && h.y.h == v.h && h.y.w == v.w &&
+           ((uintptr_t)h.y.ptr & 15) == 0 && ((uintptr_t)h.w & 15) == 0;
+}
 }  // namespace
 
 FG_API int fg_in_apply(fg_view src, const float* mean, const float* rstd, int act, fg_view residual, fg_view dst,
@@ -1020,6 +1124,33 @@ FG_API int fg_in_apply_presplit(fg_view src, const float* mean, const float* rst
                          stream);
 }
 
+FG_API int fg_in_apply_head(fg_view src, const float* mean, const float* rstd, int act, fg_view dst, int pad_mode,
+                             float* absmax, const float* w, const float* b, int n_out, fg_view y, hipStream_t stream) {
+    const HeadArgs h{w, b, n_out, y};
+    if (!head_ok(h, dst) || dst.pad != 0 || y.pad != 0)
+        return fg::fail(FG_ERR_INVALID, "fg_in_apply_head: needs C 64, an unpadded dst, n_out <= 16 logits in a 16-B "
+                                        "aligned unpadded view of the same grid (C=%d, pad %d, n_out %d, y.c_alloc %d)",
+                        dst.c_alloc, dst.pad, n_out, y.c_alloc);
+    return in_apply_impl(src, mean, rstd, act, fg_view{nullptr, 0, 0, 0, 0, 0}, dst, pad_mode, absmax, nullptr, stream,
+                         nullptr, nullptr, nullptr, 0, &h);
+}
+
+FG_API int fg_in_bwd_head(fg_view gy, const float* w, int n_out, fg_view src, const float* mean, const float* rstd,
+                          int act, fg_view dst, float* bias_grad, int bias_accumulate, double* work, float* absmax,
+                          float* scale_slot, hipStream_t stream) {
+    const HeadArgs h{w, nullptr, n_out, gy};
+    if (!head_ok(h, src) || gy.pad != 0 || gy.c_alloc < HEAD_NB ||
+        (scale_slot && (dst.c_alloc % 8 || ((uintptr_t)dst.ptr & 31))))
+        return fg::fail(FG_ERR_INVALID, "fg_in_bwd_head: needs C 64, n_out <= 16 logit gradients in a 16-B aligned "
+                                        "unpadded view of the same grid (C=%d, n_out %d, gy.c_alloc %d)", src.c_alloc,
+                        n_out, gy.c_alloc);
+    // gsrc stands in for the 64-channel gradient the head replaces (its geometry is what the checks read)
+    fg_view gs = src;
+    gs.pad = 0;
+    return in_bwd_impl(gs, 0, fg_view{nullptr, 0, 0, 0, 0, 0}, src, mean, rstd, act, dst, bias_grad, bias_accumulate,
+                       fg_view{nullptr, 0, 0, 0, 0, 0}, work, scale_slot ? nullptr : absmax, scale_slot, stream, &h);
+}
+
 FG_API int fg_in_apply_splitpix(fg_view src, const float* mean, const float* rstd, int act, fg_view dst, int pad_mode,
                                  float* scale_slot, hipStream_t stream) {
     if (!scale_slot || (dst.c_alloc != 32 && dst.c_alloc != 64) || ((uintptr_t)dst.ptr & 31))
@@ -1032,7 +1163,7 @@ FG_API int fg_in_apply_splitpix(fg_view src, const float* mean, const float* rst
 namespace {
 int in_apply_impl(fg_view src, const float* mean, const float* rstd, int act, fg_view residual, fg_view dst,
                   int pad_mode, float* absmax, float* split_slot, hipStream_t stream, float* ps_ptr, float* ps_slot,
-                  const float* res_amax, int splitpix) {
+                  const float* res_amax, int splitpix, const HeadArgs* head) {
     if (!ok_view(src) || !ok_view(dst) || !mean || !rstd || src.c_alloc % 4 || dst.c_alloc != src.c_alloc ||
         dst.h != src.h || dst.w != src.w || dst.n != src.n)
         return fg::fail(FG_ERR_INVALID, "fg_in_apply: bad args");
@@ -1041,11 +1172,18 @@ int in_apply_impl(fg_view src, const float* mean, const float* rstd, int act, fg
     if (pad_mode == FG_PAD_REFLECT && (dst.pad >= dst.h || dst.pad >= dst.w))
         return fg::fail(FG_ERR_INVALID, "fg_in_apply: reflect pad too large");
     const int C4 = dst.c_alloc / 4;
+    if (head) {
+        auto kern = in_nt2_on() ? in_apply_rows_kernel<true, true> : in_apply_rows_kernel<false, true>;
+        hipLaunchKernelGGL(kern, dim3(dst.n * (dst.h + 2 * dst.pad)), dim3(NT), 0, stream, src, mean, rstd, act,
+                           residual, dst, pad_mode, ilog2(C4), reinterpret_cast<unsigned*>(absmax), split_slot, ps_ptr,
+                           ps_slot, res_amax, splitpix, *head);
+        return fg::launched("in_apply_rows_head");
+    }
     if ((g_in_rows || split_slot || ps_ptr) && NT % C4 == 0) {
         auto kern = in_nt2_on() ? in_apply_rows_kernel<true> : in_apply_rows_kernel<false>;
         hipLaunchKernelGGL(kern, dim3(dst.n * (dst.h + 2 * dst.pad)), dim3(NT), 0, stream, src, mean,
                            rstd, act, residual, dst, pad_mode, ilog2(C4), reinterpret_cast<unsigned*>(absmax),
-                           split_slot, ps_ptr, ps_slot, res_amax, splitpix);
+                           split_slot, ps_ptr, ps_slot, res_amax, splitpix, HeadArgs{});
         return fg::launched("in_apply_rows");
     }
     const long long total = (long long)dst.n * (dst.h + 2 * dst.pad) * (dst.w + 2 * dst.pad) * (dst.c_alloc / 4);
@@ -1075,7 +1213,7 @@ FG_API int fg_in_bwd_presplit(fg_view gsrc, int fold_pad, fg_view gadd, fg_view 
 namespace {
 int in_bwd_impl(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, const float* mean, const float* rstd, int act,
                 fg_view dst, float* bias_grad, int bias_accumulate, fg_view gsum, double* work, float* absmax,
-                float* split_slot, hipStream_t stream) {
+                float* split_slot, hipStream_t stream, const HeadArgs* head) {
     if (!ok_view(gsrc) || !ok_view(src) || !ok_view(dst) || !mean || !rstd || !work || src.c_alloc % 4 ||
         (NT % (src.c_alloc / 4)) != 0 || gsrc.c_alloc != src.c_alloc || dst.c_alloc != src.c_alloc ||
         dst.h != src.h || dst.w != src.w || dst.n != src.n)
@@ -1098,12 +1236,15 @@ int in_bwd_impl(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, const flo
     static const bool nt_env = [] { const char* e = getenv("FLOODGAN_IN_NT"); return !e || atoi(e) != 0; }();
     const char* nte = getenv("FLOODGAN_IN_NT_AB");          // A/B hook read per call (scripts/ab_step.py in_nt)
     const bool ntg = gsum.ptr && (nte ? atoi(nte) != 0 : nt_env);
-    if ((g_in_rows || split_slot) && ntg)
+    if (head)
+        hipLaunchKernelGGL((in_bwd_stats_u_kernel<false, true>), dim3(chunks, src.n), dim3(NT), 0, stream, gsrc, 0, gadd,
+                           src, mean, rstd, act, chunks, work, gsum, gmax_part, *head);
+    else if ((g_in_rows || split_slot) && ntg)
         hipLaunchKernelGGL(in_bwd_stats_u_kernel<true>, dim3(chunks, src.n), dim3(NT), 0, stream, gsrc, fold_pad, gadd,
-                           src, mean, rstd, act, chunks, work, gsum, gmax_part);
+                           src, mean, rstd, act, chunks, work, gsum, gmax_part, HeadArgs{});
     else if (g_in_rows || split_slot)
         hipLaunchKernelGGL(in_bwd_stats_u_kernel<false>, dim3(chunks, src.n), dim3(NT), 0, stream, gsrc, fold_pad, gadd,
-                           src, mean, rstd, act, chunks, work, gsum, gmax_part);
+                           src, mean, rstd, act, chunks, work, gsum, gmax_part, HeadArgs{});
     else
         hipLaunchKernelGGL(in_bwd_stats_kernel, dim3(chunks, src.n), dim3(NT), 0, stream, gsrc, fold_pad, gadd, src,
                            mean, rstd, act, chunks, work, gsum);
@@ -1116,12 +1257,19 @@ int in_bwd_impl(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, const flo
     const long long total = (long long)dst.n * (dst.h + 2 * dst.pad) * (dst.w + 2 * dst.pad) * (C / 4);
     // with gsum the apply pass reads the gathered gradient the statistics pass wrote (one read, no fold)
     const fg_view none = {nullptr, 0, 0, 0, 0, 0};
+    if (head) {
+        auto kern = in_nt2_on() ? in_bwd_apply_rows_kernel<true, true> : in_bwd_apply_rows_kernel<false, true>;
+        hipLaunchKernelGGL(kern, dim3(dst.n * (dst.h + 2 * dst.pad)), dim3(NT), 0, stream, gsrc, 0, none, src, mean,
+                           rstd, coef, act, dst, reinterpret_cast<unsigned*>(absmax), bpart, bias_grad,
+                           bias_accumulate, ilog2(C / 4), split_slot, *head);
+        return fg::launched("in_bwd_apply_rows_head");
+    }
     if (g_in_rows || split_slot) {
         auto kern = in_nt2_on() ? in_bwd_apply_rows_kernel<true> : in_bwd_apply_rows_kernel<false>;
         hipLaunchKernelGGL(kern, dim3(dst.n * (dst.h + 2 * dst.pad)), dim3(NT), 0, stream,
                            gsum.ptr ? gsum : gsrc, gsum.ptr ? 0 : fold_pad, gsum.ptr ? none : gadd, src, mean, rstd,
                            coef, act, dst, reinterpret_cast<unsigned*>(absmax), bpart, bias_grad, bias_accumulate,
-                           ilog2(C / 4), split_slot);
+                           ilog2(C / 4), split_slot, HeadArgs{});
         return fg::launched("in_bwd_apply_rows");
     }
     hipLaunchKernelGGL(in_bwd_apply_kernel, dim3(fg::blocks_for(total, 256, 4096)), dim3(256), 0, stream,

@@ -23,6 +23,11 @@ N_ATT = 10           # attention logits (deconv3_attention's output channels)
 # the attention head's 1x1 conv and its gradients as fp32 FMA kernels (csrc/head1x1.hip); FLOODGAN_HEAD_1X1=0:
 # the implicit-GEMM engine
 HEAD_1X1 = os.environ.get("FLOODGAN_HEAD_1X1", "1") != "0"
+# round 5: the attention head's 1x1 conv fused into the norm passes of its input (fg_in_apply_head / fg_in_bwd_head:
+# the forward's logits formed by the apply pass, the backward's 64-channel input gradient formed in registers from the
+# logits gradient by the statistics and apply passes) -- no conv1x1 forward / input-gradient launches and no re-read
+# or materialisation of a 537-MB 64-channel tensor; bit-identical.  Off by default until it measures faster (FLOODGAN_FUSED_HEAD=1 turns it on)
+FUSED_HEAD = os.environ.get("FLOODGAN_FUSED_HEAD", "0") == "1"
 ATT_ALLOC = 16       # 10 attention channels
 
 
@@ -183,7 +188,15 @@ def gen_forward(P, x, save=True, x_extra=None):
         # layout directly (no fp32 copy, no fg_split_pixels pass)
         # (when the window kernels take the head: output rows of >= 256 px, a multiple of 32; ops.win_eligible)
         spx = tag == "content" and ps and SPLITPIX and ops.USE_WIN and W >= 256 and W % 32 == 0
-        md2, rd2, ad2 = _norm(d2, FG_ACT_RELU, pad2, mode2, stats=st, splitpix=spx)
+        if tag == "attention" and HEAD_1X1 and FUSED_HEAD:
+            # relu(IN(d2)) and the 1x1 head's logits in one pass (fg_in_apply_head)
+            md2, rd2 = st if st is not None else ops.in_stats(d2)
+            ad2 = Buf.empty(N, H, W, 64, 0, dev)
+            al = Buf.empty(N, H, W, ATT_ALLOC, 0, dev)
+            ops.in_apply_head(d2, md2, rd2, FG_ACT_RELU, ad2, FG_PAD_ZERO, P["deconv3_attention.weight"],
+                              P["deconv3_attention.bias"], N_ATT, al)
+        else:
+            md2, rd2, ad2 = _norm(d2, FG_ACT_RELU, pad2, mode2, stats=st, splitpix=spx)
         heads[tag] = dict(d1=d1, md1=md1, rd1=rd1, ad1=ad1, d2=d2, md2=md2, rd2=rd2, ad2=ad2)
     cl = Buf.empty(N, H, W, CONTENT_ALLOC, 0, dev)
     _conv_fwd(P, "deconv3_content", heads["content"]["ad2"], 3, 7, 1, cl)
@@ -192,12 +205,15 @@ def gen_forward(P, x, save=True, x_extra=None):
         ops.tanh_head_fwd(cl, 3, out)
         S.update(heads=heads, cl=cl)
         return out, None, (S if save else None)
-    al = Buf.empty(N, H, W, ATT_ALLOC, 0, dev)
-    if HEAD_1X1:
+    if HEAD_1X1 and FUSED_HEAD:
+        pass                                          # al: written by the attention head's norm pass above
+    elif HEAD_1X1:
+        al = Buf.empty(N, H, W, ATT_ALLOC, 0, dev)
         # 1x1 64 -> 10: a per-pixel matrix-vector product, fp32 FMA over LDS-staged tiles (csrc/head1x1.hip)
         ops.conv1x1_fwd(heads["attention"]["ad2"], P["deconv3_attention.weight"], P["deconv3_attention.bias"],
                         N_ATT, al)
     else:
+        al = Buf.empty(N, H, W, ATT_ALLOC, 0, dev)
         _conv_fwd(P, "deconv3_attention", heads["attention"]["ad2"], 0, 1, 1, al)
     mask = torch.empty(N, H, W, dtype=torch.float32, device=dev)
     ops.tail_fwd(cl, al, x, out, mask)
@@ -385,12 +401,13 @@ def gen_backward(P, S, g_out, grads_into=None, ready=None, input_grad=None, accu
     heads = [("content", hc, g_ad2c, 3)]
     if attention:
         # ---- deconv3_attention: 1x1
-        g_ad2a = Buf.empty(N, H, W, 64, 0, dev)
+        g_ad2a = None if HEAD_1X1 and FUSED_HEAD else Buf.empty(N, H, W, 64, 0, dev)
         if HEAD_1X1:
             names = ("deconv3_attention.weight", "deconv3_attention.bias")
             G.off_path(lambda: ops.conv1x1_wgrad(gal, ha["ad2"], N_ATT, G.get(names[0]), G.get(names[1]), G.acc),
                        (gal, ha["ad2"]), names)
-            ops.conv1x1_dgrad(gal, P["deconv3_attention.weight"], N_ATT, g_ad2a)
+            if g_ad2a is not None:
+                ops.conv1x1_dgrad(gal, P["deconv3_attention.weight"], N_ATT, g_ad2a)
         else:
             _wgrad_conv(P, G, "deconv3_attention", gal, ha["ad2"], 0, 1, 1)
             ops.channel_sum(gal, 10, G.get("deconv3_attention.bias"), G.acc)
@@ -401,8 +418,12 @@ def gen_backward(P, S, g_out, grads_into=None, ready=None, input_grad=None, accu
     ps = ops.presplit_on()     # conv-output gradients read only by pipelined convs / weight gradients
     for idx, (tag, hd, g_ad2, fold) in enumerate(heads):
         g_d2 = Buf.empty(N, H, W, 64, 1, dev)
-        ops.in_bwd(g_ad2, fold, None, hd["d2"], hd["md2"], hd["rd2"], FG_ACT_RELU, g_d2,
-                   G.get(f"deconv2_{tag}.bias"), G.acc, presplit=ps)
+        if g_ad2 is None:        # the fused head: the input gradient w^T gal formed inside the norm passes
+            ops.in_bwd_head(gal, P["deconv3_attention.weight"], N_ATT, hd["d2"], hd["md2"], hd["rd2"], FG_ACT_RELU,
+                            g_d2, G.get(f"deconv2_{tag}.bias"), G.acc, presplit=ps)
+        else:
+            ops.in_bwd(g_ad2, fold, None, hd["d2"], hd["md2"], hd["rd2"], FG_ACT_RELU, g_d2,
+                       G.get(f"deconv2_{tag}.bias"), G.acc, presplit=ps)
         name = f"deconv2_{tag}"
         w = P[name + ".weight"]
         G.wgrad(PL.wgrad_convT(hd["ad1"], g_d2, 3, 1, w.shape[0]), PL.wmap_wgrad(w.shape, True, g_d2.c, 3),

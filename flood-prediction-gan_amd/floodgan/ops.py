@@ -792,6 +792,33 @@ def in_bwd(gsrc, fold_pad, gadd, src, mean, rstd, act, dst, bias_grad=None, bias
                              L.ptr(_amax_out(dst)), L.stream_handle()), "in_bwd")
 
 
+def in_apply_head(src, mean, rstd, act, dst, pad_mode, w, b, n_out, Y):
+    """fg_in_apply_head: dst = act(IN(src)) (fp32, unpadded; absmax slot raised) AND the attention head's 1x1 logits
+    Y[..., :n_out] = w dst + b (Y's other channels 0), bit-identical to in_apply + conv1x1_fwd"""
+    _wrote(dst, Y)
+    L.check(_lib().fg_in_apply_head(view(src), L.ptr(mean), L.ptr(rstd), act, view(dst), pad_mode,
+                                    L.ptr(_amax_out(dst)), L.ptr(w.contiguous()), L.ptr(b), n_out, view(Y),
+                                    L.stream_handle()), "in_apply_head")
+
+
+def in_bwd_head(GY, w, n_out, src, mean, rstd, act, dst, bias_grad=None, bias_accumulate=False, presplit=False):
+    """fg_in_bwd_head: the norm backward of the attention head's input with the incoming gradient w^T GY formed from
+    the logits gradient GY in registers (bit-identical to conv1x1_dgrad + in_bwd; no 64-channel gradient buffer)"""
+    work = _work(src.n, src.c, src.t.device)
+    if presplit and presplit_fits(dst):
+        assert L.fwd_f16x3()
+        slot = _amax_out(dst)
+        L.check(_lib().fg_in_bwd_head(view(GY), L.ptr(w.contiguous()), n_out, view(src), L.ptr(mean), L.ptr(rstd), act,
+                                      view(dst), L.ptr(bias_grad), int(bias_accumulate), L.ptr(work), None, L.ptr(slot),
+                                      L.stream_handle()), "in_bwd_head")
+        _mark_presplit(dst)
+        return
+    _wrote(dst)
+    L.check(_lib().fg_in_bwd_head(view(GY), L.ptr(w.contiguous()), n_out, view(src), L.ptr(mean), L.ptr(rstd), act,
+                                  view(dst), L.ptr(bias_grad), int(bias_accumulate), L.ptr(work),
+                                  L.ptr(_amax_out(dst)), None, L.stream_handle()), "in_bwd_head")
+
+
 def act_bwd(g, y, act, border_zero=False):
     # in place g *= act'(y) with act' in {0, 0.2, 1}: |g| cannot grow, so a cached absmax slot still
     # bounds it and is kept; a cached pre-split copy no longer matches the contents and is dropped.  Without a

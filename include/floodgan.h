@@ -403,6 +403,20 @@ int fg_in_bwd_presplit(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, co
                        const float* rstd, int act, fg_view dst, float* bias_grad, int bias_accumulate, fg_view gsum,
                        double* work, float* scale_slot, hipStream_t stream);
 
+/* The attention head Conv2d(64, n_out <= 16, 1) (models/model_architectures.py:334, :369) fused into the norm
+ * passes of its input (the replaced interfaces: fg_in_apply + fg_conv1x1_fwd, fg_conv1x1_dgrad + fg_in_bwd).
+ * fg_in_apply_head: fg_in_apply (no residual; C = 64, dst unpadded) that also writes the logits
+ * y[p][o] = b[o] + sum_c w[o][c] dst[p][c] (w [n_out][64], y: a 16-B aligned unpadded view of the same grid,
+ * n_out <= c_alloc <= 16; channels n_out.. get 0) -- bit-identical to fg_conv1x1_fwd's.
+ * fg_in_bwd_head: fg_in_bwd of the head's input whose incoming gradient is w^T gy, formed from the logits
+ * gradient gy (unpadded, n_out <= c_alloc <= 16) in fg_conv1x1_dgrad's fma order (bit-identical to running
+ * it first); scale_slot non-NULL: dst in the FG_PRESPLIT format as fg_in_bwd_presplit (absmax ignored). */
+int fg_in_apply_head(fg_view src, const float* mean, const float* rstd, int act, fg_view dst, int pad_mode,
+                     float* absmax, const float* w, const float* b, int n_out, fg_view y, hipStream_t stream);
+int fg_in_bwd_head(fg_view gy, const float* w, int n_out, fg_view src, const float* mean, const float* rstd,
+                   int act, fg_view dst, float* bias_grad, int bias_accumulate, double* work, float* absmax,
+                   float* scale_slot, hipStream_t stream);
+
 
 /* g *= act'(y) in place over the interior (y = saved activation output).  absmax (optional absmax slot,
  * initialised by the caller) is raised to max |g| over the interior -- a bound for the whole buffer when its

@@ -618,6 +618,32 @@ def test_f16x3_dynamic_range(case, report):
         assert a < max(KTOL, 4 * b), res
 
 
+def test_fused_attention_head_bit_identical(report):
+    """The attention head's 1x1 conv fused into its input's norm passes (fg_in_apply_head: the logits formed by the
+    apply pass; fg_in_bwd_head: the 64-channel input gradient w^T g_logits formed inside the norm backward) against the
+    separate conv1x1 forward / input-gradient kernels: two training iterations of the fused step (64x64, batch 2) give
+    bit-identical losses, G / D parameters and attention masks."""
+    from floodgan import executor as X
+    x, y = _inputs(2, res=64, seed=11)
+    out = []
+    prev = X.FUSED_HEAD
+    try:
+        for fused in (False, True):
+            X.FUSED_HEAD = fused
+            m = _model()
+            ls = [m.step_fn(x.to(DEV), y.to(DEV)).cpu() for _ in range(2)]
+            torch.cuda.synchronize()
+            out.append((torch.stack(ls), [p.detach().cpu().clone() for p in m.generator.parameters()],
+                        [p.detach().cpu().clone() for p in m.discriminator.parameters()],
+                        m.step_fn.last_mask.detach().cpu().clone()))
+    finally:
+        X.FUSED_HEAD = prev
+    assert torch.equal(out[0][0], out[1][0]), (out[0][0], out[1][0])
+    assert all(torch.equal(a, b) for a, b in zip(out[0][1], out[1][1]))
+    assert all(torch.equal(a, b) for a, b in zip(out[0][2], out[1][2]))
+    assert torch.equal(out[0][3], out[1][3])
+
+
 def test_fused_step_deterministic():
     """Run-to-run determinism of the fused step (every reduction in a fixed order, no atomics in the sums):
     two fresh models trained two iterations on the same batches give bit-identical losses and parameters."""
