@@ -343,9 +343,10 @@ def main():
     ap.add_argument("--data", choices=["resident", "tiles"], default="resident",
                     help="tiles: feed the step through the staged tile pipeline (floodgan.data.TileLoader) from "
                          "synthetic TIFF tiles on disk, --res = Resize size, --crop quadrants (BASELINE configs[4])")
-    ap.add_argument("--dropout-rng", choices=["device", "host"], default="device",
-                    help="pix2pix: Dropout(0.5) masks decided on the device (default) or drawn on the host exactly as the "
-                         "reference's CPU path draws them (the RNG-parity mode)")
+    ap.add_argument("--dropout-rng", choices=["device", "host"], default="host",
+                    help="pix2pix: Dropout(0.5) masks = torch's CPU stream, exactly as the reference's CPU path draws "
+                         "them, regenerated on the device (host: the default, RNG parity) or hashed on the device "
+                         "(device: no RNG parity)")
     ap.add_argument("--crop", type=int, default=None)
     ap.add_argument("--tile", type=int, default=1024, help="raw tile edge for --data tiles (xBD tiles are 1024)")
     ap.add_argument("--tiles", type=int, default=8, help="distinct synthetic tiles for --data tiles")
@@ -483,7 +484,7 @@ def main():
                                     f"(9-ch G input, 12-ch D input), batch {B}/GPU" if not (cycle or p2p) else
                                     f"Pix2Pix paired train step (U-Net-256 G with BatchNorm + Dropout, BatchNorm "
                                     f"PatchGAN), {R}x{R}, topography=all, batch {B}/GPU, dropout masks "
-                                    f"{'drawn on the host as the reference draws them (RNG parity)' if args.dropout_rng == 'host' else 'decided on the device (no RNG parity)'}"
+                                    f"{'= torch CPU-generator stream as the reference draws them, generated on the device (RNG parity)' if args.dropout_rng == 'host' else 'hashed on the device (no RNG parity)'}"
                                     if p2p else
                                     f"{m.model} train_cycle step (2 G + 2 D, recreated images, Adam x2), {R}x{R}, "
                                     f"topography=all (9-ch G and D inputs), batch {B}/GPU"),

@@ -18,10 +18,10 @@ its bias and feeds the tanh head.  BatchNorm (training mode: batch statistics, r
 updated in place on the module buffers; eval mode: running statistics) is one statistics pass and
 one apply pass that also writes the activated copies.  Dropout(0.5) of levels 5-7 is fused into the
 BatchNorm apply / backward passes, its keep decisions either
-  "device" (default): a counter-based hash of (seed, element) evaluated in the apply pass and
+  "device":  a counter-based hash of (seed, element) evaluated in the apply pass and
              recomputed in the backward -- no mask is drawn, stored or copied; one 62-bit seed per
              generator call comes from torch's CPU generator, so torch.manual_seed fixes the masks; or
-  "host":    the 0/1 masks torch's CPU generator gives the reference's CPU path (F.dropout:
+  "host" (default since round 5): the 0/1 masks torch's CPU generator gives the reference's CPU path (F.dropout:
              empty_like(x).bernoulli_(0.5), innermost level first: 7, 6, 5), bit for bit -- a seeded run then
              reproduces the reference's CPU run (the parity mode).  Round 5: the masks are no longer drawn on
              the host; the device regenerates torch's MT19937 stream from the generator's state with chunked
@@ -122,7 +122,7 @@ def dropout_shapes(n, h, w):
     return {k: (n, 512, h >> (k - 1), w >> (k - 1)) for k in DROPOUT_LEVELS}
 
 
-def draw_dropout(n, h, w, mode="device", device="cuda"):
+def draw_dropout(n, h, w, mode="host", device="cuda"):
     """One generator call's Dropout decisions: {level: device 0/1 mask} ("host": torch's CPU stream, regenerated
     on the device; the generator advanced before returning) or {level: seed} ("device")"""
     if mode == "host":
