@@ -26,7 +26,8 @@ HEAD_1X1 = os.environ.get("FLOODGAN_HEAD_1X1", "1") != "0"
 # round 5: the attention head's 1x1 conv fused into the norm passes of its input (fg_in_apply_head / fg_in_bwd_head:
 # the forward's logits formed by the apply pass, the backward's 64-channel input gradient formed in registers from the
 # logits gradient by the statistics and apply passes) -- no conv1x1 forward / input-gradient launches and no re-read
-# or materialisation of a 537-MB 64-channel tensor; bit-identical; interleaved A/B 45.95 -> 45.60 ms per step (profiles/round5/r5f_ab_fused_head.log).  FLOODGAN_FUSED_HEAD=0: the separate kernels
+# or materialisation of a 537-MB 64-channel tensor; bit-identical; interleaved A/B 45.95 -> 45.60 ms per step
+# (profiles/round5/r5f_ab_fused_head.log).  FLOODGAN_FUSED_HEAD=0: the separate kernels
 FUSED_HEAD = os.environ.get("FLOODGAN_FUSED_HEAD", "1") != "0"
 ATT_ALLOC = 16       # 10 attention channels
 

@@ -409,8 +409,9 @@ int fg_in_bwd_presplit(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, co
  * y[p][o] = b[o] + sum_c w[o][c] dst[p][c] (w [n_out][64], y: a 16-B aligned unpadded view of the same grid,
  * n_out <= c_alloc <= 16; channels n_out.. get 0) -- bit-identical to fg_conv1x1_fwd's.
  * fg_in_bwd_head: fg_in_bwd of the head's input whose incoming gradient is w^T gy, formed from the logits
- * gradient gy (unpadded, n_out <= c_alloc <= 16) in fg_conv1x1_dgrad's fma order (bit-identical to running
- * it first); scale_slot non-NULL: dst in the FG_PRESPLIT format as fg_in_bwd_presplit (absmax ignored). */
+ * gradient gy (unpadded, n_out <= 12, 12 <= c_alloc <= 16: three 16-B quads are read per pixel) in
+ * fg_conv1x1_dgrad's fma order (bit-identical to running it first); scale_slot non-NULL: dst in the FG_PRESPLIT
+ * format as fg_in_bwd_presplit (absmax ignored). */
 int fg_in_apply_head(fg_view src, const float* mean, const float* rstd, int act, fg_view dst, int pad_mode,
                      float* absmax, const float* w, const float* b, int n_out, fg_view y, hipStream_t stream);
 int fg_in_bwd_head(fg_view gy, const float* w, int n_out, fg_view src, const float* mean, const float* rstd,
