@@ -215,7 +215,8 @@ __global__ void __launch_bounds__(512, 1) stem_wgrad_kernel(const fg_wgrad_probl
 // The forward's ring: copies 1-3 of each piece start 8 B past their 1280-B slot, so that the 32 lanes of a fragment
 // read (16 pixels x 2 k groups, each lane on the copy of its pixel's alignment) hit 64 distinct banks -- with the
 // copies 320 dwords (0 mod 64) apart the reads were 3-way conflicted (half of the kernel's LDS cycles were
-// SQ_LDS_BANK_CONFLICT, profiles/round4/r4_pmc_stem_fwd.json)
+// SQ_LDS_BANK_CONFLICT in round 4; after the offsets: profiles/round4/r4l_pmc_stem_fwd.json, round 5 in-step:
+// profiles/round5/r5_pmc_stem_fwd.json)
 constexpr int SF_PIECE = 4 * ST_COPYB + 16;
 constexpr int SF_XROW = 2 * SF_PIECE;
 __device__ __forceinline__ int sf_copy(int t) { return t * ST_COPYB + (t ? 8 : 0); }

@@ -10,11 +10,10 @@
 // The strip comes from a pre-split copy of the input (fg_split_pixels: per pixel the fp16 pieces
 // h[C] and l[C] of the scaled fp32 values, 16-B chunks XOR-swizzled by the pixel's column so the
 // shifted fragment reads are bank-conflict free) and the kernel row's KW taps of weights from the
-// fg_pack_weight_f16 layout; both sit in LDS together, single-buffered, and the next row's strip and
-// weights are loaded into registers while the current row's KW taps run: one barrier pair per kernel
-// row, 168 MFMAs per wave between them (round 4: the earlier LDS-DMA form with one barrier per tap and
-// 24 MFMAs between barriers ran 1.35 / 1.33 ms forward / input gradient against 1.21 / 1.13 ms here,
-// profiles/round4/r4c_ab_win.log).
+// fg_pack_weight_f16 layout; both sit in LDS together.  Each kind runs on two 4-wave workgroups per
+// CU that walk a kernel row per phase (conv_win2_kernel / conv_win2_dgrad_kernel below); round 4's
+// one-workgroup-per-CU 8-wave form (1.21 / 1.13 ms forward / input gradient, profiles/round4/r4c_ab_win.log)
+// was replaced by them (1.08 / 0.95 ms) and removed in round 5.
 #include "conv_common.hpp"
 
 namespace {
@@ -59,179 +58,6 @@ struct WinArgs {
     int tiles_per_img;
 };
 
-// One kernel row per barrier pair: the whole row's weights (KW taps, [s][pc][NR][C]) and its input strip sit in LDS
-// together (68.6 + 57.3 KB at C 64); the next row's strip and weights are loaded into registers (16-B buffer loads)
-// while the KW taps of the current row run, and written over the current ones after a barrier.
-//
-// BM = 512 (C = 32, the input gradient): 64-row waves over all 64 output columns, 8 A + 8 B fragments per 48 MFMAs
-// (341 LDS bytes per MFMA instead of 512); the 32-channel strip of 524 pixels (67 KB) and the row's weights (57 KB)
-// still fit in LDS.  Needs output rows of >= BM pixels (a tile spans at most two row segments): 1141 -> 1071 us at
-// bs 8 (profiles/round4/r4j_bench_win.log).  The forward's analogue (64-row waves paired over the two 32-channel
-// halves, 683 -> 512 LDS bytes per MFMA) ran 1.5 % slower and was dropped.
-template <int C, int KW, int TN, int NW, int BM = 256>
-__global__ void __launch_bounds__(NW * 64, 1) conv_win_kernel(const WinArgs args) {
-    constexpr int NT = NW * 64;
-    constexpr int WM = BM / NW, TM = WM / 16;
-    constexpr int PB = 4 * C;                                   // strip bytes per pixel (h | l)
-    constexpr int NR = TN * 16;                                 // weight rows staged
-    constexpr int STRIP_BYTES = (BM + 2 * (KW - 1)) * PB;
-    constexpr int SCH = (STRIP_BYTES / 16 + NT - 1) / NT;       // strip 16-B chunks per thread
-    constexpr int W_TAP = 2 * NR * C * 2;                       // [pc][NR][C] fp16 per tap
-    constexpr int TAP_CH = W_TAP / 16;
-    constexpr int WCH = KW * TAP_CH / NT;                       // weight 16-B chunks per thread per kernel row
-    static_assert((KW * TAP_CH) % NT == 0, "weight row is not a whole number of chunks per thread");
-    constexpr int W_OFF = (STRIP_BYTES + 1023) / 1024 * 1024;
-    __shared__ __attribute__((aligned(1024))) char smem[W_OFF + KW * W_TAP];
-
-    const fg_conv_problem& P = args.P;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wid = fg::xcd_remap(blockIdx.x, gridDim.x);
-    const int img = wid / args.tiles_per_img;
-    const int p0 = (wid - img * args.tiles_per_img) * BM;
-    const int mab = P.m_a * P.m_b;
-    const int a0 = p0 / P.m_b, b0 = p0 - (p0 / P.m_b) * P.m_b;
-    const int len0 = min(BM, min(P.m_b - b0, mab - p0));
-    const int len1 = (a0 + 1 < P.m_a) ? min(BM - len0, P.m_b) : 0;
-    const int s0pix = len0 + KW - 1;
-    const int strip_bytes = (len0 + len1 + 2 * (KW - 1)) * PB;
-    const int wp = args.wp;
-    constexpr int kOOB = 0x7fffffff;
-
-    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)args.xs, 0, 0x7fffffff, 0x00020000);
-    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)P.w, 0, 0x7fffffff, 0x00020000);
-
-    // strip chunk o = (tid + i NT) * 16 of the LDS strip <- its source byte (row offset r * wp * PB added per row)
-    const int seg0_pix = img * (int)(P.sxn / C) + a0 * wp + b0;
-    const int seg1_pix = img * (int)(P.sxn / C) + (a0 + 1) * wp;
-    int s_src[SCH];
-#pragma unroll
-    for (int i = 0; i < SCH; ++i) {
-        const int o = (tid + i * NT) * 16;
-        s_src[i] = o >= strip_bytes ? -1 : o < s0pix * PB ? seg0_pix * PB + o : seg1_pix * PB + (o - s0pix * PB);
-    }
-    // weight chunk F = tid + i NT of the row image [s][pc][NR][C]: tap s = F / TAP_CH, in-tap chunk f
-    int w_src[WCH];
-#pragma unroll
-    for (int i = 0; i < WCH; ++i) {
-        const int F = tid + i * NT, s = F / TAP_CH, f = F - s * TAP_CH;
-        const int pc = f / (NR * C / 8);
-        const int rem = f - pc * (NR * C / 8);
-        const int n = rem / (C / 8);
-        const int ch = (rem - n * (C / 8)) ^ swz_wrow<C>(n);
-        w_src[i] = (min(n, P.n_out - 1) * (P.ldw / 8) + ch) * 32 + pc * 16 + ((s * C) / 8) * 32;
-    }
-    f32x4 rs[SCH], rw[WCH];
-    auto load = [&](int r) {
-        const int soff = r * wp * PB, woff = ((r * P.jp) / 8) * 32;
-#pragma unroll
-        for (int i = 0; i < SCH; ++i)
-            rs[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, s_src[i] >= 0 ? s_src[i] + soff : kOOB, 0, 0));
-#pragma unroll
-        for (int i = 0; i < WCH; ++i)
-            rw[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(wr, w_src[i] + woff, 0, 0));
-    };
-    auto store = [&]() {
-#pragma unroll
-        for (int i = 0; i < SCH; ++i)
-            if (s_src[i] >= 0) *reinterpret_cast<f32x4*>(smem + (tid + i * NT) * 16) = rs[i];
-#pragma unroll
-        for (int i = 0; i < WCH; ++i) *reinterpret_cast<f32x4*>(smem + W_OFF + (tid + i * NT) * 16) = rw[i];
-    };
-
-    const float sa = fgc::pow2_scale(P.x_absmax);
-    const float sb = fgc::pow2_scale(P.w_absmax);
-    const float out_scale = 1.f / (sa * sb);
-
-    const int fr = lane & 15, g = lane >> 4;
-    int q0[TM], x0[TM];
-#pragma unroll
-    for (int tm = 0; tm < TM; ++tm) {
-        const int i = wave * WM + tm * 16 + fr;
-        q0[tm] = i < len0 ? i : i + KW - 1;
-        x0[tm] = i < len0 ? b0 + i : i - len0;
-    }
-    f32x4 acc[TM][TN];
-#pragma unroll
-    for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-        for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    constexpr int CC = C / 32;
-    auto tap = [&](int s) {
-        f16x8 ah[CC][TM], al[CC][TM];
-#pragma unroll
-        for (int cc = 0; cc < CC; ++cc)
-#pragma unroll
-            for (int tm = 0; tm < TM; ++tm) {
-                const char* px = smem + (q0[tm] + s) * PB;
-                const int sw = swz_strip<C>(x0[tm] + s);
-                ah[cc][tm] = *reinterpret_cast<const f16x8*>(px + ((cc * 4 + g) ^ sw) * 16);
-                al[cc][tm] = *reinterpret_cast<const f16x8*>(px + ((C / 8 + cc * 4 + g) ^ sw) * 16);
-            }
-        const char* wb = smem + W_OFF + s * W_TAP;
-#pragma unroll
-        for (int cc = 0; cc < CC; ++cc) {
-            f16x8 bh[TN], bl[TN];
-#pragma unroll
-            for (int tn = 0; tn < TN; ++tn) {
-                const int n = tn * 16 + fr;
-                const char* row = wb + n * (2 * C) + ((cc * 4 + g) ^ swz_wrow<C>(n)) * 16;
-                bh[tn] = *reinterpret_cast<const f16x8*>(row);
-                bl[tn] = *reinterpret_cast<const f16x8*>(row + NR * 2 * C);
-            }
-#pragma unroll
-            for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-                for (int tn = 0; tn < TN; ++tn) {
-                    acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[cc][tm], bh[tn], acc[tm][tn], 0, 0, 0);
-                    acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[cc][tm], bl[tn], acc[tm][tn], 0, 0, 0);
-                    acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[cc][tm], bh[tn], acc[tm][tn], 0, 0, 0);
-                }
-        }
-    };
-
-    const int KH = P.kh;
-    load(0);
-    store();
-    __syncthreads();
-    for (int r = 0; r < KH; ++r) {
-        if (r + 1 < KH) load(r + 1);
-#pragma unroll
-        for (int s = 0; s < KW; ++s) tap(s);
-        if (r + 1 < KH) {
-            __syncthreads();
-            store();
-            __syncthreads();
-        }
-    }
-
-    // ---- epilogue
-    const int act = P.act;
-    const bool accum = P.accumulate != 0;
-    float bias_v[TN];
-#pragma unroll
-    for (int tn = 0; tn < TN; ++tn) bias_v[tn] = P.bias ? P.bias[min(tn * 16 + fr, P.n_out - 1)] : 0.f;
-#pragma unroll
-    for (int tm = 0; tm < TM; ++tm) {
-#pragma unroll
-        for (int reg = 0; reg < 4; ++reg) {
-            const int i = wave * WM + tm * 16 + 4 * g + reg;
-            if (i >= len0 + len1) continue;
-            const int a = i < len0 ? a0 : a0 + 1, b = i < len0 ? b0 + i : i - len0;
-            float* yrow = P.y + img * P.syn + a * P.sya + b * P.syb;
-#pragma unroll
-            for (int tn = 0; tn < TN; ++tn) {
-                const int n = tn * 16 + fr;
-                if (n >= P.n_out) continue;
-                float v = fg::act_fwd(acc[tm][tn][reg] * out_scale + bias_v[tn], act);
-                float* dst = yrow + n * P.syc;
-                if (accum) v += *dst;
-                *dst = v;
-            }
-        }
-    }
-}
-
 typedef __attribute__((address_space(3))) void lds_void;
 
 // nothing is scheduled across it
@@ -245,8 +71,8 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, int v
 // C = 64 forward, two workgroups per CU: a workgroup of 4 waves x 64 rows walks 14 "phases" -- one kernel row's
 // 32-channel half each: the strip's half pixels (268 px x 128 B, in the 32-channel chunk swizzle) and that half of
 // the row's 7 taps of weights (28 KB), 63 KB of LDS -- so two workgroups share a CU and one's copy / barriers run
-// under the other's MFMAs (the 8-wave kernel above holds 123 KB: one workgroup per CU, every wave idle during each
-// row's copy).  A phase's operands arrive by LDS-DMA (16-B buffer loads straight into LDS; the other workgroup's
+// under the other's MFMAs (round 4's 8-wave kernel held 123 KB: one workgroup per CU, every wave idle during each
+// row's copy; removed in round 5).  A phase's operands arrive by LDS-DMA (16-B buffer loads straight into LDS; the other workgroup's
 // MFMAs cover the latency), and the registers that frees hold the next tap's fragments, read ahead of the current
 // tap's MFMAs (sched_barrier keeps that order).  Per tap and wave: 8 A + 4 B fragment reads for 24 MFMAs (512 LDS
 // bytes per MFMA, was 683).  Register-staged copies instead of DMA, without the read-ahead: 1.5-2.5 % slower
@@ -401,7 +227,7 @@ __global__ void __launch_bounds__(256, 2) conv_win2_kernel(const WinArgs args) {
         }
     }
 
-    // ---- epilogue (as conv_win_kernel)
+    // ---- epilogue: scale, bias, activation, optional accumulate
     const int act = P.act;
     const bool accum = P.accumulate != 0;
     float bias_v[TN];
@@ -558,7 +384,7 @@ __global__ void __launch_bounds__(256, 2) conv_win2_dgrad_kernel(const WinArgs a
         for (int s = G0; s < KW; ++s) tap(s, s - G0);
     }
 
-    // ---- epilogue (as conv_win_kernel)
+    // ---- epilogue: scale, bias, activation, optional accumulate
     const int act = P.act;
     const bool accum = P.accumulate != 0;
     float bias_v[TN];
@@ -585,38 +411,18 @@ __global__ void __launch_bounds__(256, 2) conv_win2_dgrad_kernel(const WinArgs a
     }
 }
 
-// 8 waves (two per SIMD, 32 rows each: a partner wave's MFMAs cover each wave's fragment-read latency; 4 waves of 64
-// rows ran 1.31 ms on both geometries, profiles/round4/r4c_ab_win.log)
-template <int C, int KW, int TN>
+// the forward (C 64) and the input gradient (C 32) each on two 4-wave workgroups per CU: forward 1201 -> 1078 us
+// (profiles/round4/r4z_bench_win.log), input gradient 1071 -> 952 us (r4zb_bench_win.log) against round 4's 8-wave
+// kernels, which were removed in round 5 with their FLOODGAN_WIN_2WG / FLOODGAN_WIN_BM switches
+template <int C, int KW>
 int launch_win(const WinArgs& a, int tiles, hipStream_t stream) {
     if constexpr (C == 32) {
-        // the input gradient on two 4-wave workgroups per CU (1071 -> 952 us, profiles/round4/r4zb_bench_win.log;
-        // A/B: FLOODGAN_WIN_2WG=0 runs the 8-wave kernels, 512-row tiles unless FLOODGAN_WIN_BM=256)
-        const char* e2 = getenv("FLOODGAN_WIN_2WG");
-        if (!(e2 && atoi(e2) == 0)) {
-            hipLaunchKernelGGL((conv_win2_dgrad_kernel<KW>), dim3(tiles), dim3(256), 0, stream, a);
-            return fg::launched("conv_win2_dgrad");
-        }
-        const char* e = getenv("FLOODGAN_WIN_BM");      // A/B: 256 = 32-row waves
-        if (a.P.m_b >= 512 && !(e && atoi(e) == 256)) {
-            WinArgs b = a;
-            b.tiles_per_img = (a.P.m_a * a.P.m_b + 511) / 512;
-            hipLaunchKernelGGL((conv_win_kernel<C, KW, TN, 8, 512>), dim3(b.tiles_per_img * a.P.m_img), dim3(512), 0,
-                               stream, b);
-            return fg::launched("conv_win");
-        }
+        hipLaunchKernelGGL((conv_win2_dgrad_kernel<KW>), dim3(tiles), dim3(256), 0, stream, a);
+        return fg::launched("conv_win2_dgrad");
+    } else {
+        hipLaunchKernelGGL((conv_win2_kernel<KW>), dim3(tiles), dim3(256), 0, stream, a);
+        return fg::launched("conv_win2");
     }
-    if constexpr (C == 64) {
-        // the forward on two 4-wave workgroups per CU (1201 -> 1078 us, profiles/round4/r4z_bench_win.log;
-        // A/B: FLOODGAN_WIN_2WG=0 runs the 8-wave kernel)
-        const char* e = getenv("FLOODGAN_WIN_2WG");
-        if (!(e && atoi(e) == 0)) {
-            hipLaunchKernelGGL((conv_win2_kernel<KW>), dim3(tiles), dim3(256), 0, stream, a);
-            return fg::launched("conv_win2");
-        }
-    }
-    hipLaunchKernelGGL((conv_win_kernel<C, KW, TN, 8>), dim3(tiles), dim3(512), 0, stream, a);
-    return fg::launched("conv_win");
 }
 
 }  // namespace
@@ -662,6 +468,6 @@ FG_API int fg_conv_win(const fg_conv_problem* prob, const void* x_split, long lo
     a.wp = (int)wp;
     a.tiles_per_img = (p.m_a * p.m_b + 255) / 256;
     const int tiles = a.tiles_per_img * p.m_img;
-    if (C == 64) return launch_win<64, 7, 2>(a, tiles, stream);
-    return launch_win<32, 7, 4>(a, tiles, stream);
+    if (C == 64) return launch_win<64, 7>(a, tiles, stream);
+    return launch_win<32, 7>(a, tiles, stream);
 }

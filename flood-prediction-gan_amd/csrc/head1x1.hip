@@ -5,7 +5,6 @@
 // bs 8, 512^2).  Each kernel here stages a 64-pixel tile of its pixel-major operands into LDS with
 // coalesced 16-B loads (a thread owning a whole pixel would make every wave-wide load touch 64 lines), then
 // works from LDS:
-//   forward:        thread = (pixel, group of 4 outputs), writes its float4 of the 16-channel logits row;
 //   input gradient: thread = (pixel, group of 16 input channels), writes 4 float4 of the 64-channel row;
 //   weight + bias:  thread = (output o, channel quad), sums over the block's pixels; per-block partials are
 //                   reduced over blocks in fp64 in a fixed order (deterministic).
@@ -37,67 +36,6 @@ __device__ __forceinline__ void stage(const fg_view& v, int q4, int p0, int P, f
         const int px = i / q4, q = i - px * q4, p = p0 + px;
         const f32x4 val = p < P ? ld4(v.ptr + pix_off(v, p) + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
         st4(lds + px * stride + 4 * q, val);
-    }
-}
-
-__global__ void __launch_bounds__(256) conv1x1_fwd_kernel(fg_view x, const float* __restrict__ w,
-                                                          const float* __restrict__ b, int n_out, fg_view y) {
-    __shared__ __attribute__((aligned(16))) float xs[2][TP * XS];
-    __shared__ __attribute__((aligned(16))) float ws[NO * XS];
-    const int P = x.n * x.h * x.w, ntiles = (P + TP - 1) / TP;
-    // persistent: the weights are staged once per block, the block walks tiles blockIdx.x, + gridDim.x, ...
-    // with the next tile's loads in flight (registers) while the current one is computed
-    for (int i = threadIdx.x; i < NO * CI; i += 256) {
-        const int o = i / CI, c = i - o * CI;
-        ws[o * XS + c] = o < n_out ? w[i] : 0.f;
-    }
-    const int px = threadIdx.x >> 2, og = threadIdx.x & 3;
-    float bias[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) bias[j] = (b && 4 * og + j < n_out) ? b[4 * og + j] : 0.f;
-    // staging: thread t loads quads t, t + 256, t + 512, t + 768 of the tile (pixel i / 16, quad i % 16)
-    f32x4 rv[4];
-    auto load = [&](int t) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int i = threadIdx.x + 256 * k, pp = i >> 4, q = i & 15, p = t * TP + pp;
-            rv[k] = (t < ntiles && p < P) ? ld4(x.ptr + pix_off(x, p) + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-    };
-    auto store = [&](float* dst) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int i = threadIdx.x + 256 * k;
-            st4(dst + (i >> 4) * XS + 4 * (i & 15), rv[k]);
-        }
-    };
-    int t = blockIdx.x, buf = 0;
-    load(t);
-    store(xs[0]);
-    load(t + gridDim.x);
-    __syncthreads();
-    for (; t < ntiles; t += gridDim.x, buf ^= 1) {
-        if (t + gridDim.x < ntiles) store(xs[buf ^ 1]);
-        load(t + 2 * gridDim.x);
-        const int p = t * TP + px;
-        float acc[4] = {bias[0], bias[1], bias[2], bias[3]};
-        if (4 * og < n_out) {
-            const float* xr = xs[buf] + px * XS;
-#pragma unroll
-            for (int q = 0; q < CI / 4; ++q) {
-                const f32x4 v = ld4(xr + 4 * q);
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const f32x4 wv = ld4(ws + (4 * og + j) * XS + 4 * q);
-                    acc[j] = fmaf(v[0], wv[0], acc[j]);
-                    acc[j] = fmaf(v[1], wv[1], acc[j]);
-                    acc[j] = fmaf(v[2], wv[2], acc[j]);
-                    acc[j] = fmaf(v[3], wv[3], acc[j]);
-                }
-            }
-        }
-        if (p < P && 4 * og < y.c_alloc) st4(y.ptr + pix_off(y, p) + 4 * og, f32x4{acc[0], acc[1], acc[2], acc[3]});
-        __syncthreads();
     }
 }
 
@@ -205,9 +143,6 @@ __global__ void __launch_bounds__(256) conv1x1_fwd_lanes(fg_view x, const float*
     }
 }
 
-// A/B and test hook: FLOODGAN_HEAD_LANES=0 runs the forward's LDS-tile kernel
-static bool lanes_on() { const char* e = getenv("FLOODGAN_HEAD_LANES"); return !e || atoi(e) != 0; }
-
 // block: pixels [blockIdx.x * per, +per) in tiles of TP; thread (o = t / 16, channel quad cq = t % 16)
 // accumulates 4 channels of dw[o] (+ the bias sum for cq == 0); partial slab[blk][o][CI + 1]
 __global__ void __launch_bounds__(256) conv1x1_wgrad_kernel(fg_view gy, fg_view x, int n_out, int per,
@@ -285,15 +220,9 @@ FG_API int fg_conv1x1_fwd(fg_view x, const float* w, const float* bias, int n_ou
         return fg::fail(FG_ERR_INVALID, "fg_conv1x1_fwd: bad args (c_in %d, n_out %d, y.c_alloc %d)", x.c_alloc, n_out,
                         y.c_alloc);
     const int P = x.n * x.h * x.w;
-    if (lanes_on()) {
-        const long long steps = ((long long)P + 4 * LU - 1) / (4 * LU);          // wave steps
-        hipLaunchKernelGGL(conv1x1_fwd_lanes, dim3((unsigned)std::min<long long>((steps + 3) / 4, 8 * fg::num_cus())),
-                           dim3(256), 0, stream, x, w, bias, n_out, y);
-        return fg::launched("conv1x1_fwd");
-    }
-    const int ntiles = (P + TP - 1) / TP;
-    hipLaunchKernelGGL(conv1x1_fwd_kernel, dim3(std::min(ntiles, 4 * fg::num_cus())), dim3(256), 0, stream, x, w, bias,
-                       n_out, y);
+    const long long steps = ((long long)P + 4 * LU - 1) / (4 * LU);              // wave steps
+    hipLaunchKernelGGL(conv1x1_fwd_lanes, dim3((unsigned)std::min<long long>((steps + 3) / 4, 8 * fg::num_cus())),
+                       dim3(256), 0, stream, x, w, bias, n_out, y);
     return fg::launched("conv1x1_fwd");
 }
 

@@ -63,7 +63,7 @@ __global__ void in_stats_kernel(fg_view src, int chunks, double* __restrict__ wo
     const int per = (HW + chunks - 1) / chunks;
     const int p0 = chunk * per, p1 = min(HW, p0 + per);
     const int g = threadIdx.x / L, c4 = threadIdx.x - (threadIdx.x / L) * L;
-    __shared__ double red[NT][8];
+    __shared__ float red[NT][8];     // fp32 per-thread sums (exact as floats), combined in fp64
     f32x4 s = {0.f, 0.f, 0.f, 0.f}, ss = {0.f, 0.f, 0.f, 0.f};
     if (g < PG) {
         const f32x4 K = ld4(src.ptr + fg::vidx(src, n, 0, 0) + 4 * c4);
@@ -461,7 +461,7 @@ __global__ void __launch_bounds__(NT) in_bwd_stats_u_kernel(fg_view g, int fp, f
     const int per = (HW + chunks - 1) / chunks;
     const int p0 = chunk * per, p1 = min(HW, p0 + per);
     const int gi = threadIdx.x / L, c4 = threadIdx.x - (threadIdx.x / L) * L;
-    __shared__ double red[NT][12];
+    __shared__ float red[NT][12];    // fp32 per-thread sums (exact as floats), combined in fp64: 12 KB, not 24
     f32x4 sg = {0.f, 0.f, 0.f, 0.f}, sgx = sg, sx = sg;
     if (gi < PG) {
         const f32x4 m = ld4(mean + (size_t)n * C + 4 * c4);
@@ -552,7 +552,7 @@ __global__ void in_bwd_stats_kernel(fg_view g, int fp, fg_view gadd, fg_view src
     const int per = (HW + chunks - 1) / chunks;
     const int p0 = chunk * per, p1 = min(HW, p0 + per);
     const int gi = threadIdx.x / L, c4 = threadIdx.x - (threadIdx.x / L) * L;
-    __shared__ double red[NT][12];
+    __shared__ float red[NT][12];    // fp32 per-thread sums (exact as floats), combined in fp64: 12 KB, not 24
     f32x4 sg = {0.f, 0.f, 0.f, 0.f}, sgx = sg, sx = sg;
     if (gi < PG) {
         const f32x4 m = ld4(mean + (size_t)n * C + 4 * c4);
@@ -897,7 +897,7 @@ __global__ void __launch_bounds__(256) channel_sum4_kernel(fg_view src, int chun
     const long long P = (long long)src.n * src.h * src.w;
     const long long per = (P + chunks - 1) / chunks;
     const long long p0 = blockIdx.x * per, p1 = min(P, p0 + per);
-    __shared__ double red[NT][4];
+    __shared__ float red[NT][4];     // fp32 per-thread sums, combined in fp64
     f32x4 s = {0.f, 0.f, 0.f, 0.f};
     if (gi < PG && p0 + gi < p1) {
         const long long q = p0 + gi;

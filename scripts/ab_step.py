@@ -1,7 +1,7 @@
 """A/B of engine switches on the full bs-8 512^2 training step, interleaved in ONE process (device
 clocks and boxes differ by several percent, so separate bench runs cannot resolve small gains).
   python scripts/ab_step.py f3_persistent [rounds] [steps] [values, default 0,1]
-Switches: f3_persistent, f3_sched, f3_order, f3_fill, f3_interleave, head_1x1, wgrad_f3, use_win, in_rows, presplit, ps_wide (values 4,5), ps_resid, stem_fwd, splitpix, d0_dgrad, in_nt, in_nt2, head_lanes, win_2wg, fused_head."""
+Switches: f3_persistent, f3_sched, f3_order, f3_fill, f3_interleave, head_1x1, wgrad_f3, use_win, in_rows, presplit, ps_wide (values 4,5), ps_resid, stem_fwd, splitpix, d0_dgrad, in_nt, in_nt2, fused_head."""
 import os
 import sys
 import time
@@ -44,10 +44,6 @@ def switch(name, on):
         ops.USE_WIN = bool(on)
     elif name == "stem_fwd":
         os.environ["FLOODGAN_STEM_FWD"] = str(int(on))
-    elif name == "win_2wg":
-        os.environ["FLOODGAN_WIN_2WG"] = str(int(on))
-    elif name == "head_lanes":
-        os.environ["FLOODGAN_HEAD_LANES"] = str(int(on))
     elif name == "in_nt2":
         os.environ["FLOODGAN_IN_NT2_AB"] = str(int(on))
     elif name == "in_nt":

@@ -1,7 +1,7 @@
 """Timing (GPU) of the row-strip window kernel on the content head's forward (7x7 64 -> 27 at 512^2) and input
 gradient (7x7 27(32) -> 64 over 518^2), bs 8 (round 4: its LDS-DMA form, one barrier per tap, was replaced by the
-register-staged one, profiles/round4/r4c_ab_win.log).
-  python scripts/ab_win.py"""
+register-staged one, profiles/round4/r4c_ab_win.log; round 5 keeps only the two-workgroup kernels).
+  python scripts/bench_win.py"""
 import os
 import sys
 
@@ -35,21 +35,9 @@ def main():
     dgr = PL.conv_problem(gcl, 6, 7, 1, ops.pack_weight(w, md), md, Y)
     for name, prob, out, flops in (("content fwd 7x7 64->27 @512", fwd, cl, 2.0 * N * 512 * 512 * 27 * 64 * 49),
                                    ("content dgrad 7x7 27->64 @518", dgr, Y, 2.0 * N * 518 * 518 * 64 * 27 * 49)):
-        ref = None
-        # FLOODGAN_WIN_2WG: 1 = two 4-wave workgroups per CU (the default), 0 = one 8-wave workgroup per CU
-        # (the input gradient's two-workgroup kernel uses LDS-DMA phases)
-        var = ("FLOODGAN_WIN_2WG", ("0", "1"))
-        for _ in range(2):
-            for v in var[1]:
-                os.environ[var[0]] = v
-                out.t.zero_()
-                ms = min(time_it(lambda: ops.conv_win(prob)) for _ in range(3))
-                if ref is None:
-                    ref = out.t.clone()
-                d = float((out.t - ref).norm() / ref.norm())
-                print(f"{name:32s} {var[0][9:]}={v} {ms * 1e3:8.1f} us {flops / ms / 1e9:7.1f} TFLOP/s  rel diff {d:.1e}",
-                      flush=True)
-        os.environ.pop(var[0])
+        out.t.zero_()
+        ms = min(time_it(lambda: ops.conv_win(prob)) for _ in range(5))
+        print(f"{name:32s} {ms * 1e3:8.1f} us {flops / ms / 1e9:7.1f} TFLOP/s", flush=True)
 
 
 if __name__ == "__main__":

@@ -390,18 +390,12 @@ def test_stem_fwd_strips(H, N):
         L.set_conv_math(prev)
 
 
-@pytest.mark.parametrize("case,env", [("content_fwd", {}), ("content_fwd", {"FLOODGAN_WIN_2WG": "0"}),
-                                      ("content_dgrad", {}), ("content_dgrad_512", {}),
-                                      ("content_dgrad", {"FLOODGAN_WIN_2WG": "0"}),
-                                      ("content_dgrad_512", {"FLOODGAN_WIN_2WG": "0"}),
-                                      ("content_dgrad_512", {"FLOODGAN_WIN_2WG": "0", "FLOODGAN_WIN_BM": "256"})])
+@pytest.mark.parametrize("case,env", [("content_fwd", {}), ("content_dgrad", {}), ("content_dgrad_512", {})])
 def test_conv_window(case, env, monkeypatch):
     """the row-strip window kernel (fg_conv_win) on the content-head geometries -- 7x7 over 64
     channels -> 27, and its input gradient 27(32) -> 64 over the 6-bordered gradient -- with
     output rows of 256+ px (two-segment tiles, ragged last tile) against fp64; the forward on its two-workgroup
-    channel-half kernel (the default) and the 8-wave one (FLOODGAN_WIN_2WG=0); the input gradient on its
-    two-workgroup LDS-DMA kernel (the default) and, with FLOODGAN_WIN_2WG=0, the 8-wave ones: 512-row tiles where
-    its output rows allow (>= 512 px) and 256-row ones (FLOODGAN_WIN_BM=256)"""
+    channel-half kernel, the input gradient on its two-workgroup LDS-DMA kernel"""
     from floodgan import _lib as L, ops, plans as PL
     from floodgan.plans import Buf
     for k, v in env.items():
@@ -488,14 +482,12 @@ def test_d0_input_grad(ctot, c0, cn, H, W, acc):
 
 
 @pytest.mark.parametrize("N,H,W,n_out,xpad", [(2, 20, 37, 10, 0), (3, 9, 64, 10, 1), (1, 5, 7, 16, 0), (2, 96, 96, 3, 0)])
-@pytest.mark.parametrize("lanes", ["1", "0"])
-def test_conv1x1_head(N, H, W, n_out, xpad, lanes, monkeypatch):
+def test_conv1x1_head(N, H, W, n_out, xpad):
     """the attention head's 1x1 conv in fp32 FMA (fg_conv1x1_*): forward (pad channels written as 0), input
     gradient (the gradient's padding channels NaN: never read), weight + bias gradients (written and accumulated)
-    against fp64, ragged last tiles; the forward's lane form (FLOODGAN_HEAD_LANES=1, the default) and its LDS-tile form"""
+    against fp64, ragged last tiles; the forward in lane form"""
     from floodgan import _lib as L, ops
     from floodgan.plans import Buf
-    monkeypatch.setenv("FLOODGAN_HEAD_LANES", lanes)
     torch.manual_seed(21)
     x = torch.randn(N, 64, H, W, dtype=torch.float64)
     w = (torch.randn(n_out, 64, 1, 1, dtype=torch.float64) * 0.1).requires_grad_(True)
