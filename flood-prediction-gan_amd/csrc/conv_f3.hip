@@ -65,6 +65,13 @@ __device__ __forceinline__ void dma_stage(char* sb, int wave, __amdgpu_buffer_rs
                                                  soff_b, 0, 0);
 }
 
+// QUAD: the output offset of column group q (wave-uniform per column block; a select chain, not an indexed
+// kernel-argument load)
+__device__ __forceinline__ int quad_yoff(const fg_conv_problem& P, int q) {
+    const int y0 = (int)P.q_yoff[0], y1 = (int)P.q_yoff[1], y2 = (int)P.q_yoff[2], y3 = (int)P.q_yoff[3];
+    return q == 0 ? y0 : q == 1 ? y1 : q == 2 ? y2 : y3;
+}
+
 // output buffer resource: byte offsets below kYRecords are stored, kYOOB is dropped (the host keeps every output
 // extent below kYRecords, f3_takes)
 constexpr int kYRecords = 0x7fffff00, kYOOB = 0x7ffffff0;
@@ -89,7 +96,11 @@ __device__ __forceinline__ void wait_vmcnt() {
 // next stage's LDS-DMA pieces spread between the column groups instead of one burst.
 // PS: the A operand is in the FG_PRESPLIT format (include/floodgan.h: per 8 channels h[8] | l[8], written
 // by the norm pass that produced it) -- the two 16-B chunks a lane reads ARE its h and l fragments.
-template <int BM, int BN, int WM, int WN, int NS, int SCH, bool STATS = false, bool PS = false>
+// QUAD: the merged sub-pixel phases of a stride-2 transposed conv (fg_conv_problem.q_n): every stage's k
+// segment (r, pixel) is recorded beside its ring slot, and a wave runs the products of a column group (one
+// phase, TG*16 = q_n columns) only where q_mask says the group reads that segment; the epilogue scatters the
+// groups to their output pixels.
+template <int BM, int BN, int WM, int WN, int NS, int SCH, bool STATS = false, bool PS = false, bool QUAD = false>
 __global__ void __launch_bounds__((BM / WM) * (BN / WN) * 64, 1)
 conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
     constexpr int NWN = BN / WN;
@@ -153,10 +164,17 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
     // usable jc (channels per pixel) the run is walked as kw = jp/32 pseudo-taps of 32 (r outer).
     int it = first, ikt = 0, ic = 0, ir = 0, is = 0;
     int i_kh = 1, i_jp = 32, i_sxr = 0, i_c = 32, i_kw = 1, i_nc = 1;   // per issue tile (no kernarg reloads)
+    int i_qkw = 1, i_qsh = 5;        // QUAD: pixels per kernel row, log2(jc)
+    unsigned seg_ring = 0;           // QUAD: k segment of the stage in ring slot b at bits 4b..4b+3
     bool irev = false;
     Geo ig;
     __amdgpu_buffer_rsrc_t xr, wr;
     int a_off[A_GL], b_off[B_GL];
+    // QUAD: column group of each B piece, the groups live per k segment (bit seg*4 + q), a buffer resource with no
+    // records: a dead group's B pieces go through it (dropped by the range check: no traffic, its LDS bytes unused)
+    int b_grp[QUAD ? B_GL : 1];
+    unsigned i_segmask = 0;
+    __amdgpu_buffer_rsrc_t wr0;
     auto setup_issue = [&]() {
         ig = geo(it);
         const fg_conv_problem& P = batch.p[ig.pi];
@@ -178,6 +196,7 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
             const int row = (q - pc * (BN / 16)) * 16 + (lane >> 2);
             const int cl = (lane & 3) ^ swz_b(row);
             b_off[i] = min(ig.n0 + row, P.n_out - 1) * (P.ldw / 8) * 32 + cl * 32 + pc * 16;
+            if constexpr (QUAD) b_grp[i] = (ig.n0 + (q - pc * (BN / 16)) * 16) / P.q_n;
         }
         // alt_order: odd M tiles walk the kernel rows backwards, so neighbouring tiles (output rows
         // 2t, 2t+1 and 2t+2, 2t+3 at 128-px rows) gather the same input rows at the same time
@@ -188,7 +207,22 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
         i_c = ((alt_order & 2) && P.jc > 0 && P.jc % 32 == 0 && P.jp % P.jc == 0) ? P.jc : 32;
         i_kw = P.jp / i_c;
         i_nc = i_c / 32;
+        if constexpr (QUAD) {
+            i_qkw = P.jp / P.jc;
+            i_qsh = __builtin_ctz(P.jc);
+            i_segmask = 0;
+            for (int sg = 0; sg < 4; ++sg)
+                for (int q = 0; q < 4; ++q)
+                    if ((P.q_mask >> (q * 4 + sg)) & 1) i_segmask |= 1u << (sg * 4 + q);
+            wr0 = __builtin_amdgcn_make_buffer_rsrc((void*)P.w, 0, 0, 0x00020000);
+        }
         ikt = ic = ir = is = 0;
+    };
+    auto record_seg = [&](int buf, int r, int jb) {
+        if constexpr (QUAD) {
+            const unsigned seg = (unsigned)(r * i_qkw + (jb >> i_qsh));
+            seg_ring = (seg_ring & ~(0xFu << (4 * buf))) | (seg << (4 * buf));
+        }
     };
     // stage the next k-stage of the stream into ring buffer `buf`; false once the stream is done
     auto issue_next = [&](int buf) {
@@ -197,6 +231,7 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
         const int jb = is * i_c + ic * 32;
         const int koff = (r * i_sxr + jb) * 4;
         const int ks = r * (i_jp / 32) + jb / 32;        // packed-weight stage of this (r, jb)
+        record_seg(buf, r, jb);
 #ifdef FG_F3_DIAG
         if (!((alt_order >> 4) & 1) || ikt < NS)         // diag bit 0: no DMA after the first stages
 #endif
@@ -217,6 +252,7 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
     // ~60 issue cycles among MFMAs but 100-185 in a burst beside the fragment reads)
     int p_koff = 0, p_soffb = 0, p_buf = 0;   // p_buf: byte offset of the target stage in smem
     bool p_on = false;
+    unsigned p_live = 0xF;                     // QUAD: the column groups the staged segment feeds
     auto issue_prep = [&](int buf) {
         p_on = it < total_tiles;
         if (!p_on) return;
@@ -225,6 +261,9 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
         p_koff = __builtin_amdgcn_readfirstlane((r * i_sxr + jb) * 4);        // scalar offsets: wave-uniform
         p_soffb = __builtin_amdgcn_readfirstlane((r * (i_jp / 32) + jb / 32) * 128);
         p_buf = buf * STAGE;
+        record_seg(buf, r, jb);
+        if constexpr (QUAD)
+            p_live = __builtin_amdgcn_readfirstlane((i_segmask >> (4 * (r * i_qkw + (jb >> i_qsh)))) & 0xFu);
 #ifdef FG_F3_DIAG
         if (((alt_order >> 4) & 1) && ikt >= NS) p_on = false;
 #endif
@@ -234,7 +273,11 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
         // the LDS destination is wave-uniform (M0): say so, or the compiler emits a waterfall loop
         if (i < A_GL)
             dma_piece(smem + __builtin_amdgcn_readfirstlane(p_buf + (wave * A_GL + i) * 1024), xr, a_off[i], p_koff);
-        else
+        else if constexpr (QUAD) {
+            const bool live = __builtin_amdgcn_readfirstlane((p_live >> b_grp[i - A_GL]) & 1u) != 0;
+            dma_piece(smem + __builtin_amdgcn_readfirstlane(p_buf + A_BYTES + (wave * B_GL + (i - A_GL)) * 1024),
+                      live ? wr : wr0, b_off[i - A_GL], p_soffb);
+        } else
             dma_piece(smem + __builtin_amdgcn_readfirstlane(p_buf + A_BYTES + (wave * B_GL + (i - A_GL)) * 1024), wr,
                       b_off[i - A_GL], p_soffb);
     };
@@ -255,11 +298,25 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
     int ct = first, ckt = 0;
     Geo cg = geo(ct);
     float sa = 1.f, out_scale = 1.f;
+    // QUAD: bit seg * NLG + lg: the wave's local column group lg (TG blocks) reads k segment seg
+    constexpr int NLG = TN / (TN < 4 ? TN : 4);
+    unsigned c_live = ~0u;
     auto setup_compute = [&]() {
         cg = geo(ct);
         sa = fgc::pow2_scale(batch.p[cg.pi].x_absmax);
         out_scale = 1.f / (sa * fgc::pow2_scale(batch.p[cg.pi].w_absmax));
         ckt = 0;
+        if constexpr (QUAD) {
+            const fg_conv_problem& P = batch.p[cg.pi];
+            const int q0 = (cg.n0 + wn * WN) / P.q_n;
+            unsigned lv = 0;
+#pragma unroll
+            for (int sg = 0; sg < 4; ++sg)
+#pragma unroll
+                for (int lg = 0; lg < NLG; ++lg)
+                    if (q0 + lg < 4 && ((P.q_mask >> ((q0 + lg) * 4 + sg)) & 1)) lv |= 1u << (sg * NLG + lg);
+            c_live = __builtin_amdgcn_readfirstlane(lv);
+        }
     };
 
     f32x4 acc[TM][TN];
@@ -289,6 +346,8 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
     };
     auto compute = [&](int buf, const f32x4 (&va)[TM][2]) {
         const char* sbuf = smem + buf * STAGE;
+        // QUAD: the live column groups of this stage (all of them otherwise)
+        const unsigned lv = QUAD ? (c_live >> (((seg_ring >> (4 * buf)) & 0xFu) * NLG)) : ~0u;
         f16x8 ah[TM], al[TM];
         if constexpr (PS) {
 #pragma unroll
@@ -314,12 +373,15 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
         }
 #pragma unroll
         for (int t0 = 0; t0 < TN; t0 += TG) {
+            const bool live = !QUAD || ((lv >> (t0 / TG)) & 1u);
             f16x8 bh[TG], bl[TG];
+            if (live) {
 #pragma unroll
-            for (int t = 0; t < TG; ++t) {
-                const char* rowp = sbuf + A_BYTES + (wn * WN + (t0 + t) * 16 + fr) * 64 + b_c;
-                bh[t] = *reinterpret_cast<const f16x8*>(rowp);
-                bl[t] = *reinterpret_cast<const f16x8*>(rowp + BN * 64);
+                for (int t = 0; t < TG; ++t) {
+                    const char* rowp = sbuf + A_BYTES + (wn * WN + (t0 + t) * 16 + fr) * 64 + b_c;
+                    bh[t] = *reinterpret_cast<const f16x8*>(rowp);
+                    bl[t] = *reinterpret_cast<const f16x8*>(rowp + BN * 64);
+                }
             }
             if constexpr (SCH >= 3) {
                 // SCH 3: pieces spread over all column groups; 4: over the first half; 5: all in the
@@ -329,6 +391,7 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
 #pragma unroll
                 for (int i = (t0 / TG) * PPG; i < (t0 / TG + 1) * PPG && i < NP; ++i) issue_piece(i);
             }
+            if (!live) continue;
             if constexpr (SCH == 0) {
 #pragma unroll
                 for (int tm = 0; tm < TM; ++tm)
@@ -434,10 +497,20 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
         const bool accum = P.accumulate != 0;
         float bias_v[TN];
         int ncol[TN];
+        // QUAD: column n = q * q_n + o is channel o of the pixel at q_yoff[q]; its statistics partials sit in group
+        // q's region ([rb][q_n][2] at q * q_soff)
+        int ych[TN], yq[TN];
 #pragma unroll
         for (int tn = 0; tn < TN; ++tn) {
             ncol[tn] = cg.n0 + wn * WN + tn * 16 + fr;
-            bias_v[tn] = P.bias ? P.bias[min(ncol[tn], P.n_out - 1)] : 0.f;
+            if constexpr (QUAD) {
+                yq[tn] = ncol[tn] / P.q_n;
+                ych[tn] = ncol[tn] - yq[tn] * P.q_n;
+            } else {
+                yq[tn] = 0;
+                ych[tn] = ncol[tn];
+            }
+            bias_v[tn] = P.bias ? P.bias[min(ych[tn], P.n_out - 1)] : 0.f;
         }
         const bool full_n = cg.n0 + BN <= P.n_out;
         if (STATS && P.in_stats) {
@@ -453,7 +526,7 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
             if (rb0 < M) {
                 constexpr int SG = TN < 4 ? TN : 4;
                 const float sc = out_scale;
-                float* const dst0 = P.in_stats + (size_t)(rb0 / 32) * P.n_out * 2;
+                float* const dst0 = P.in_stats + (size_t)(rb0 / 32) * (QUAD ? P.q_n : P.n_out) * 2;
 #pragma unroll
                 for (int t0 = 0; t0 < TN; t0 += SG) {
                     float sm[SG], sq[SG];
@@ -489,7 +562,8 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
 #pragma unroll
                         for (int u = 0; u < SG; ++u)
                             if (ncol[t0 + u] < P.n_out)
-                                *reinterpret_cast<f32x2*>(dst0 + ncol[t0 + u] * 2) =
+                                *reinterpret_cast<f32x2*>(dst0 + (QUAD ? yq[t0 + u] * P.q_soff : 0) +
+                                                          ych[t0 + u] * 2) =
                                     f32x2{sm[u] * sc + bias_v[t0 + u], sq[u] * (sc * sc)};
                     }
                 }
@@ -502,7 +576,7 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
         const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc((void*)P.y, 0, kYRecords, 0x00020000);
         int coff[TN];
 #pragma unroll
-        for (int tn = 0; tn < TN; ++tn) coff[tn] = ncol[tn] * (int)P.syc;
+        for (int tn = 0; tn < TN; ++tn) coff[tn] = ych[tn] * (int)P.syc + (QUAD ? quad_yoff(P, yq[tn]) : 0);
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm) {
             // the lane's 4 consecutive rows: one decomposition, then (b, a, img) advanced with wrap-around
@@ -658,6 +732,19 @@ int launch_cfg(const ConvBatch& in, int nprob, hipStream_t stream) {
     for (int i = 0; i < nprob; ++i) stats |= b.p[i].in_stats != nullptr;
     // pre-split A operands (every problem of the batch, checked by the caller): their own instantiations
     // (WM = 32 configs, default order)
+    if (b.p[0].q_n) {
+        // the quad form (fg_conv_problem.q_n): pre-split operands on the 256 x 256 tile of 64 x 128 waves only
+        if constexpr (BM == 256 && BN == 256 && WM == 64 && WN == 128) {
+            if (stats)
+                hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 3, true, true, true>), dim3(grid), dim3(NT),
+                                   0, stream, b, total, g_f3_alt);
+            else
+                hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 3, false, true, true>), dim3(grid),
+                                   dim3(NT), 0, stream, b, total, g_f3_alt);
+            return fg::launched("conv_fwd_f3_quad");
+        }
+        return fg::fail(FG_ERR_INVALID, "conv_fwd_f3: the quad form runs on the 256 x 256 pre-split tile only");
+    }
     if (b.p[0].x_presplit) {
         if (stats) {
             hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 3, true, true>), dim3(grid), dim3(NT), 0,
@@ -743,6 +830,7 @@ static bool narrow_on() {
 int auto_cfg(const fg_conv_problem* p, int nprob, int max_n) {
     int cfg = f3_config(max_n);
     if (g_f3_tile >= 0 || cfg < 0) return cfg;
+    if (p[0].q_n) return 5;      // the quad form's one tile (launch_cfg)
     if (narrow_on() && (cfg == 6 || cfg == 7)) {
         const int alt = cfg == 7 ? 10 : 11;
         const int bm = alt == 10 ? 512 : 256, bn = alt == 10 ? 64 : 128;
@@ -771,8 +859,22 @@ bool f3_takes(const fg_conv_problem* probs, int nprob, int max_n) {
         const fg_conv_problem& p = probs[i];
         if ((p.x_presplit != 0) != (probs[0].x_presplit != 0) || (p.x_presplit && !presplit_ok(p))) return false;
         // the epilogue's buffer stores address the output with 31-bit byte offsets
+        long long qext = 0;
+        if (p.q_n) {
+            // the quad form: one pre-split problem, 256 columns in 4 groups of 64 (the 64 x 128 waves hold two
+            // groups each), k segments = kh * (jp / jc) <= 4 pixels of a power-of-two jc
+            if (nprob != 1 || !p.x_presplit || p.q_n != 64 || p.n_out != 256 || p.jc < 32 || (p.jc & (p.jc - 1)) ||
+                p.jp % p.jc || p.kh * (p.jp / p.jc) > 4 || p.q_soff < 0 || p.q_soff > (1LL << 28))
+                return false;
+            for (int q = 0; q < 4; ++q) {
+                if (p.q_yoff[q] < 0) return false;
+                qext = std::max(qext, p.q_yoff[q]);
+            }
+        }
+        // the epilogue's buffer stores address the output with 31-bit byte offsets
         const long long yext = 4 * ((long long)(p.m_img - 1) * p.syn + (long long)(p.m_a - 1) * p.sya +
-                                    (long long)(p.m_b - 1) * p.syb + (long long)(p.n_out - 1) * p.syc + 1);
+                                    (long long)(p.m_b - 1) * p.syb +
+                                    (long long)((p.q_n ? p.q_n : p.n_out) - 1) * p.syc + qext + 1);
         if (p.syn < 0 || p.sya < 0 || p.syb < 0 || p.syc < 0 || yext >= kYRecords) return false;
         // no K padding (every staged k is a real tap: padded j would gather past the row run); ldw may exceed
         // kh * jp (a kernel-row range of a larger pack: the resblock input gradient's row strips)

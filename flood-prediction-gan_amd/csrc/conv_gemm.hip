@@ -1084,7 +1084,18 @@ __device__ __forceinline__ float packed_w(const float* __restrict__ w, const fg_
     if (j >= map.kw * map.c) return 0.f;
     const int ks = j / map.c, ch = j - (j / map.c) * map.c;
     if (ch >= map.c_valid) return 0.f;
-    const int r = map.rtab[kr], s = map.stab[ks], nn = n + map.n_base;
+    int r, s;
+    if (map.q_n > 0) {            // quad form: group q's taps (a negative index: a zero segment)
+        const int q = n / map.q_n;
+        n -= q * map.q_n;
+        r = map.rtab[q * map.kh + kr];
+        s = map.stab[q * map.kw + ks];
+        if (r < 0 || s < 0) return 0.f;
+    } else {
+        r = map.rtab[kr];
+        s = map.stab[ks];
+    }
+    const int nn = n + map.n_base;
     const size_t src = map.dim0_is_n ? (((size_t)nn * map.d1 + ch) * map.KH + r) * map.KW + s
                                      : (((size_t)ch * map.d1 + nn) * map.KH + r) * map.KW + s;
     return w[src];
@@ -1329,6 +1340,8 @@ FG_API int fg_conv_fwd(const fg_conv_problem* probs, int nprob, hipStream_t stre
             return fg::fail(FG_ERR_INVALID, "fg_conv_fwd: the f16x3 math needs x_absmax and w_absmax (problem %d)", i);
         if (!aligned16(p.x) || (p.sxn | p.sxa | p.sxb | p.sxr) % 4 || p.j_valid % 4) vec = false;
         if (p.n_out > max_n) max_n = p.n_out;
+        if (p.q_n && (nprob != 1 || !p.x_presplit || !(g_conv_math & FG_MATH_FWD_F16X3)))
+            return fg::fail(FG_ERR_INVALID, "fg_conv_fwd: the quad form (q_n) is one pre-split f16x3 problem");
         b.p[i] = p;
     }
     const bool f16 = (g_conv_math & FG_MATH_FWD_F16X3) != 0;
@@ -1484,8 +1497,8 @@ FG_API int fg_conv_wgrad(const fg_wgrad_problem* prob, hipStream_t stream) {
 FG_API int fg_wgrad_reduce(const float* slabs, int splits, const fg_weight_map* map, float* dw, int accumulate,
                            hipStream_t stream) {
     if (!slabs || !map || !dw || splits < 1) return fg::fail(FG_ERR_INVALID, "fg_wgrad_reduce: bad args");
-    if (map->kh > 8 || map->kw > 8 || map->c < 1 || map->n_out < 1)
-        return fg::fail(FG_ERR_INVALID, "fg_wgrad_reduce: bad map");
+    if (map->kh > 8 || map->kw > 8 || map->c < 1 || map->n_out < 1 || map->q_n != 0)
+        return fg::fail(FG_ERR_INVALID, "fg_wgrad_reduce: bad map (the quad form packs weights only)");
     const long long total = (long long)map->n_out * map->kh * map->kw * map->c;
     if (total <= 256 * 1024 && splits >= 32 && total * 4 < (long long)splits * 1024) {
         // few elements, many slabs: parallel over the splits too
@@ -1498,9 +1511,14 @@ FG_API int fg_wgrad_reduce(const float* slabs, int splits, const fg_weight_map* 
     return fg::launched("wgrad_reduce");
 }
 
+// the quad form (fg_weight_map.q_n): 1-2 taps per axis and group, at most 4 groups of whole rows
+static bool bad_quad(const fg_weight_map& m) {
+    return m.q_n < 0 || (m.q_n > 0 && (m.kh > 2 || m.kw > 2 || m.n_out % m.q_n || m.n_out / m.q_n > 4));
+}
+
 FG_API int fg_pack_weight(const float* w, const fg_weight_map* map, float* wp, hipStream_t stream) {
     if (!w || !map || !wp) return fg::fail(FG_ERR_INVALID, "fg_pack_weight: null");
-    if (map->kh > 8 || map->kw > 8 || map->jp % BK || map->jp < map->kw * map->c || map->c < 1)
+    if (map->kh > 8 || map->kw > 8 || map->jp % BK || map->jp < map->kw * map->c || map->c < 1 || bad_quad(*map))
         return fg::fail(FG_ERR_INVALID, "fg_pack_weight: bad map kh=%d kw=%d c=%d jp=%d", map->kh, map->kw, map->c,
                         map->jp);
     const long long total = (long long)map->n_out * map->kh * map->jp;
@@ -1511,7 +1529,7 @@ FG_API int fg_pack_weight(const float* w, const fg_weight_map* map, float* wp, h
 
 FG_API int fg_pack_weight_split(const float* w, const fg_weight_map* map, void* wps, hipStream_t stream) {
     if (!w || !map || !wps || !aligned16(wps)) return fg::fail(FG_ERR_INVALID, "fg_pack_weight_split: null/unaligned");
-    if (map->kh > 8 || map->kw > 8 || map->jp % BK || map->jp < map->kw * map->c || map->c < 1)
+    if (map->kh > 8 || map->kw > 8 || map->jp % BK || map->jp < map->kw * map->c || map->c < 1 || bad_quad(*map))
         return fg::fail(FG_ERR_INVALID, "fg_pack_weight_split: bad map kh=%d kw=%d c=%d jp=%d", map->kh, map->kw,
                         map->c, map->jp);
     const long long total = (long long)map->n_out * map->kh * map->jp / 8;
@@ -1524,7 +1542,7 @@ FG_API int fg_pack_weight_f16(const float* w, const fg_weight_map* map, const fl
                               hipStream_t stream) {
     if (!w || !map || !wps || !w_absmax || !aligned16(wps))
         return fg::fail(FG_ERR_INVALID, "fg_pack_weight_f16: null/unaligned");
-    if (map->kh > 8 || map->kw > 8 || map->jp % BK || map->jp < map->kw * map->c || map->c < 1)
+    if (map->kh > 8 || map->kw > 8 || map->jp % BK || map->jp < map->kw * map->c || map->c < 1 || bad_quad(*map))
         return fg::fail(FG_ERR_INVALID, "fg_pack_weight_f16: bad map kh=%d kw=%d c=%d jp=%d", map->kh, map->kw,
                         map->c, map->jp);
     const long long total = (long long)map->n_out * map->kh * map->jp / 8;
@@ -1545,7 +1563,7 @@ FG_API int fg_pack_weight_f16_batch(const fg_pack_job* jobs, int njobs, hipStrea
         const fg_weight_map& m = J.map;
         if (!J.w || !J.dst || !J.w_absmax || !aligned16(J.dst))
             return fg::fail(FG_ERR_INVALID, "fg_pack_weight_f16_batch: job %d null/unaligned", j);
-        if (m.kh > 8 || m.kw > 8 || m.jp % BK || m.jp < m.kw * m.c || m.c < 1 || m.n_out < 1)
+        if (m.kh > 8 || m.kw > 8 || m.jp % BK || m.jp < m.kw * m.c || m.c < 1 || m.n_out < 1 || bad_quad(m))
             return fg::fail(FG_ERR_INVALID, "fg_pack_weight_f16_batch: job %d bad map kh=%d kw=%d c=%d jp=%d", j,
                             m.kh, m.kw, m.c, m.jp);
         b.job[j] = J;

@@ -41,7 +41,8 @@ class fg_conv_problem(C.Structure):
                 ("kh", C.c_int), ("j_valid", C.c_int), ("jp", C.c_int),
                 ("n_out", C.c_int), ("ldw", C.c_int), ("act", C.c_int), ("accumulate", C.c_int),
                 ("w_split", C.c_int), ("x_absmax", C.c_void_p), ("w_absmax", C.c_void_p), ("jc", C.c_int),
-                ("in_stats", C.c_void_p), ("x_presplit", C.c_int)]
+                ("in_stats", C.c_void_p), ("x_presplit", C.c_int),
+                ("q_n", C.c_int), ("q_mask", C.c_int), ("q_yoff", C.c_longlong * 4), ("q_soff", C.c_longlong)]
 
 
 class fg_wgrad_problem(C.Structure):
@@ -58,7 +59,7 @@ class fg_weight_map(C.Structure):
     _fields_ = [("n_out", C.c_int), ("kh", C.c_int), ("kw", C.c_int), ("c", C.c_int),
                 ("c_valid", C.c_int), ("jp", C.c_int), ("dim0_is_n", C.c_int),
                 ("d0", C.c_int), ("d1", C.c_int), ("KH", C.c_int), ("KW", C.c_int),
-                ("n_base", C.c_int), ("rtab", C.c_int * 8), ("stab", C.c_int * 8)]
+                ("n_base", C.c_int), ("rtab", C.c_int * 8), ("stab", C.c_int * 8), ("q_n", C.c_int)]
 
 
 class fg_pack_job(C.Structure):

@@ -12,6 +12,7 @@ import os
 
 import torch
 
+from . import _lib as L
 from . import ops
 from . import plans as PL
 from ._lib import FG_ACT_LRELU, FG_ACT_NONE, FG_ACT_RELU, FG_PAD_REFLECT, FG_PAD_ZERO, require_device
@@ -107,8 +108,27 @@ def _conv_fwd(P, name, X, pad, k, stride, Y, act=FG_ACT_NONE, tag=None, in_stats
                                      act=act)], tag=tag, in_stats=in_stats)
 
 
+# round 5: the four output phases of a stride-2, 3-tap transposed op with 64 output channels as ONE problem (the quad
+# form, plans.quad_map): each input pixel gathered once for all phases, zero segments skipped in the kernel
+QUAD = os.environ.get("FLOODGAN_QUAD", "1") != "0"
+
+
+def _quad_ok(X, shape, k, Y):
+    return (QUAD and k == 3 and shape[1] == 64 and isinstance(Y, Buf) and Y.c == 64 and ops.is_presplit(X)
+            and L.fwd_f16x3() and (Y.h, Y.w, Y.n) == (2 * X.h, 2 * X.w, X.n) and X.pad >= 1 and X.c % 32 == 0
+            and X.c & (X.c - 1) == 0)
+
+
+def _quad(P, name, X, Y, bias=None, in_stats=False):
+    w = P[name + ".weight"]
+    m, d0, mask = PL.quad_map(w.shape, 3, 1, X.c)
+    return ops.conv([PL.quad_problem(X, m, d0, mask, ops.pack_weight(w, m), Y, bias=bias)], in_stats=in_stats)
+
+
 def _convT_fwd(P, name, X, Y):
     w = P[name + ".weight"]
+    if _quad_ok(X, w.shape, 3, Y):
+        return _quad(P, name, X, Y, bias=P[name + ".bias"], in_stats=True)
     maps = PL.phase_maps(w.shape, 3, 1, X.c)
     wps = [ops.pack_weight(w, m) for m, _, _ in maps]
     return ops.conv(PL.phase_problems(X, w.shape, 3, 1, Y, wps, maps, bias=P[name + ".bias"]), in_stats=True)
@@ -341,6 +361,9 @@ def _dgrad_s1(P, name, gyp, pad_used, k, Y):
 
 def _dgrad_s2(P, name, gy, k, Y=None, y_nchw=None, n_base=0, n_out=None, accumulate=0):
     w = P[name + ".weight"]
+    if y_nchw is None and not n_base and n_out is None and not accumulate and _quad_ok(gy, w.shape, k, Y):
+        _quad(P, name, gy, Y)
+        return
     maps = PL.phase_maps(w.shape, k, 1, gy.c, n_base=n_base, n_out=n_out)
     wps = [ops.pack_weight(w, m) for m, _, _ in maps]
     ops.conv(PL.phase_problems(gy, w.shape, k, 1, Y, wps, maps, y_nchw=y_nchw, accumulate=accumulate))

@@ -52,6 +52,7 @@ def wmap_struct(m):
     for i in range(8):
         s.rtab[i] = int(m["rtab"][i]) if i < len(m["rtab"]) else 0
         s.stab[i] = int(m["stab"][i]) if i < len(m["stab"]) else 0
+    s.q_n = int(m.get("q_n", 0))
     return s
 
 
@@ -387,7 +388,7 @@ def conv(probs, tag=None, in_stats=False):
     if USE_WIN and len(probs) == 1 and win_eligible(probs[0]):
         return conv_win(probs[0], tag)
     stats = _conv(probs, in_stats, tag)
-    return None if stats is None else _merge_stats(len(probs), *stats)
+    return None if stats is None else _merge_stats(*stats)
 
 
 def _conv(probs, in_stats=False, tag=None):
@@ -404,6 +405,10 @@ def _conv(probs, in_stats=False, tag=None):
             setattr(s, k, int(p[k]))
         s.jc = getattr(p["x"][0], "c", 0)
         s.x_presplit = int(is_presplit(p["x"][0]))
+        if p.get("q_n"):
+            s.q_n, s.q_mask = int(p["q_n"]), int(p["q_mask"])
+            for q in range(4):
+                s.q_yoff[q] = int(p["q_yoff"][q])
         if f16:
             xb = p["x"][0]
             if id(xb) not in keep:
@@ -442,10 +447,20 @@ def _merge_stats(nprob, buf, n_img, rb, c):
 
 def _stats_partials(probs, arr):
     """attach epilogue-statistics buffers to the problem structs when the pipelined kernel takes them:
-    (buffer, images, 32-row blocks per image and problem, channels) or None"""
+    (regions, buffer, images, 32-row blocks per image and region, channels) or None -- one region per problem, or
+    per column group of a quad-form problem"""
     Y = probs[0]["y"][0]
     if not isinstance(Y, Buf) or any(p["y"][0] is not Y for p in probs):
         return None
+    if probs[0].get("q_n"):           # the quad form: one region per column group (= phase), merged like 4 problems
+        p, ng, c = probs[0], probs[0]["n_out"] // probs[0]["q_n"], probs[0]["q_n"]
+        if c != Y.c or (p["m_a"] * p["m_b"]) % 32 or not _lib().fg_conv_stats_ok(arr, 1):
+            return None
+        rb = p["m_a"] * p["m_b"] // 32
+        buf = torch.empty(ng * Y.n * rb * c * 2, dtype=torch.float32, device=Y.t.device)
+        arr[0].in_stats = buf.data_ptr()
+        arr[0].q_soff = Y.n * rb * c * 2
+        return ng, buf, Y.n, rb, c
     rows = {p["m_a"] * p["m_b"] for p in probs}
     c = probs[0]["n_out"]
     if len(rows) != 1 or c != Y.c or any(p["n_out"] != c or p["m_img"] != Y.n for p in probs):
@@ -457,7 +472,7 @@ def _stats_partials(probs, arr):
     buf = torch.empty(len(probs) * Y.n * rb * c * 2, dtype=torch.float32, device=Y.t.device)
     for i in range(len(probs)):
         arr[i].in_stats = buf.data_ptr() + 4 * i * Y.n * rb * c * 2
-    return buf, Y.n, rb, c
+    return len(probs), buf, Y.n, rb, c
 
 
 def split_pixels(X):

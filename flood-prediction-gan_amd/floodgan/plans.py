@@ -265,6 +265,52 @@ def phase_problems(S, shape, k, p, Y, wp_list, maps, bias=None, act=0, accumulat
     return probs
 
 
+# column groups of the quad form in the order (py, px) = (0,0), (1,1), (0,1), (1,0): the 64 x 128 waves of its tile
+# hold two groups each, and this pairing gives them 5 and 4 of the 9 live (group, segment) products of a 3-tap
+# kernel instead of 3 and 6 (conv_f3.hip QUAD)
+QUAD_PHASES = ((0, 0), (1, 1), (0, 1), (1, 0))
+
+
+def quad_map(shape, k, p, c_alloc, n_out=None):
+    """The four phases of a stride-2 transposed op with a 3-tap kernel as ONE pack (the quad form,
+    fg_weight_map.q_n): packed row q*n_out + o is output channel o of phase QUAD_PHASES[q]; k runs over the
+    2 x 2 input neighbourhood (a + R, b + S), R, S in {0, 1}, of the output block (2a.., 2b..).  Returns
+    (map, d0, q_mask): d0 the neighbourhood's offset, q_mask bit q*4 + R*2 + S set where phase q has a tap."""
+    n_out = shape[1] if n_out is None else n_out
+    taps = {ph: phase_taps(k, p, ph) for ph in (0, 1)}
+    d0 = min(d for d, _ in taps.values())
+    assert all(d - d0 + len(r) <= 2 for d, r in taps.values()), "the quad form needs <= 2 taps per phase"
+
+    def tab(ph):
+        d, r = taps[ph]
+        return [r[i - (d - d0)] if 0 <= i - (d - d0) < len(r) else -1 for i in range(2)]
+
+    rtab, stab, mask = [], [], 0
+    for q, (py, px) in enumerate(QUAD_PHASES):
+        rt, st = tab(py), tab(px)
+        rtab += rt
+        stab += st
+        for R in range(2):
+            for S in range(2):
+                if rt[R] >= 0 and st[S] >= 0:
+                    mask |= 1 << (q * 4 + R * 2 + S)
+    m = dict(n_out=4 * n_out, kh=2, kw=2, c=c_alloc, c_valid=shape[0], jp=rup(2 * c_alloc), dim0_is_n=0,
+             d0=shape[0], d1=shape[1], KH=shape[2], KW=shape[3], n_base=0, rtab=rtab, stab=stab, q_n=n_out)
+    return m, d0, mask
+
+
+def quad_problem(S, m, d0, mask, wp, Y, bias=None):
+    """The quad-form problem over S (zero border >= 1) into Y (NHWC Buf, 2x S's extent) -- see quad_map"""
+    assert S.pad >= 1 and -S.pad <= d0 and d0 + 1 + S.h - 1 <= S.h - 1 + S.pad and isinstance(Y, Buf)
+    assert (Y.h, Y.w, Y.n) == (2 * S.h, 2 * S.w, S.n) and Y.c == m["q_n"]
+    prob = dict(x=(S, S.off(d0, d0)), w=(wp, 0), bias=bias, sxn=S.s_img, sxa=S.s_row, sxb=S.c, sxr=S.s_row,
+                m_img=S.n, m_a=S.h, m_b=S.w, kh=2, j_valid=2 * S.c, jp=m["jp"], n_out=m["n_out"], ldw=2 * m["jp"],
+                act=0, accumulate=0, y=(Y, Y.off(0, 0)), syn=Y.s_img, sya=2 * Y.s_row, syb=2 * Y.c, syc=1,
+                q_n=m["q_n"], q_mask=mask,
+                q_yoff=[Y.off(py, px) - Y.off(0, 0) for py, px in QUAD_PHASES])
+    return prob
+
+
 def phase_maps(shape, k, p, c_alloc, n_base=0, n_out=None):
     return [wmap_phase(shape, True, k, p, py, px, c_alloc, n_base, n_out)
             for py, px in ((0, 0), (0, 1), (1, 0), (1, 1))]

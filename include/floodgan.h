@@ -105,6 +105,20 @@ typedef struct fg_conv_problem {
                              fg_in_apply_presplit / fg_in_bwd_presplit, whose scale is the pow2 scale
                              of x_absmax; the pipelined kernel reads its fragments as they stand (no
                              split).  Only the pipelined f16x3 kernel takes such problems.          */
+    /* Merged sub-pixel phases ("quad" form, round 5) of a stride-2 transposed conv / stride-2 input gradient with
+     * a 3-tap kernel (models/model_architectures.py:184, :190 ConvTranspose2d(128, 64, 3, 2, 1, 1) and the
+     * input gradient of :172 Conv2d(64, 128, 3, 2, 1)): ONE problem whose rows m = (img, a, b) are the input
+     * pixels and whose k runs over their 2 x 2 neighbourhood (kh = 2, j = 2 pixels x jc), so each input pixel
+     * is gathered once for all four output phases.  q_n > 0: the columns come in n_out / q_n <= 4 groups of
+     * q_n; column n = q*q_n + o is channel o of output pixel row_y(m) + q_yoff[q] (bias[o]); bit q*4 + seg of
+     * q_mask says whether group q reads k segment seg = r * (jp / jc) + j / jc (the packed weights of a
+     * segment a group does not read are zero, and the kernel skips their MFMAs).  in_stats: group q's partials
+     * at in_stats + q * q_soff, laid out [rb][q_n][2] (fg_in_stats_partials with nprob = n_out / q_n).
+     * Only the pipelined f16x3 kernel on pre-split operands takes such problems (q_n = 64, n_out = 256). */
+    int q_n;
+    int q_mask;
+    long long q_yoff[4];
+    long long q_soff;
 } fg_conv_problem;
 
 /*
@@ -146,6 +160,9 @@ typedef struct fg_weight_map {
     int n_base;           /* packed row n reads PyTorch index n + n_base                    */
     int rtab[8];          /* kernel-row index per packed r                                  */
     int stab[8];          /* kernel-col index per packed s                                  */
+    int q_n;              /* 0, or: packed row n is channel n % q_n (+ n_base) of group q = n / q_n, whose
+                             taps are rtab[q*kh + r] / stab[q*kw + s] (kh, kw <= 2); a negative tap index
+                             packs zeros (the quad form of fg_conv_problem)                           */
 } fg_weight_map;
 
 /* ---------------------------------------------------------------------------------------- */

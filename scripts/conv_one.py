@@ -1,5 +1,5 @@
 """Run one conv-engine launch shape repeatedly (for rocprofv3 counter passes).
-  python scripts/conv_one.py [fwd|fwd_stats|fwd_stats_ps|wgrad|dgrad_ps|wgrad_ps|stem_fwd|stem_wgrad|win_fwd] [reps]
+  python scripts/conv_one.py [fwd|fwd_stats|fwd_stats_ps|wgrad|dgrad_ps|wgrad_ps|stem_fwd|stem_wgrad|win_fwd|quad_stats|convT4_stats] [reps]
   -- resblock 3x3 256->256 @128, bs 8 (stem_*: the generator stem 7x7 9->64 @512, bs 8, on its strip kernels)
   (fwd_stats: with the InstanceNorm statistics epilogue, as the step's conv1 runs; fwd_stats_ps: on a FG_PRESPLIT
   operand written by the norm pass, as the step's conv2 runs; dgrad_ps: the input-gradient interior launch of
@@ -53,13 +53,31 @@ def win_fwd(dev):
     return lambda: ops.conv_win(prob)
 
 
+def deconv2(kind, dev):
+    """deconv2 (ConvTranspose2d(128, 64, 3, 2, 1, 1), bs 8, 256^2 -> 512^2) on a pre-split relu(IN(.)) operand with
+    the statistics epilogue: quad_stats = the quad form, convT4_stats = the four phase problems"""
+    from floodgan import executor as X
+    L.set_conv_math("f16x3")
+    N, H = 8, 256
+    c = Buf.empty(N, H, H, 128, 0, dev)
+    c.t.normal_()
+    mean, rstd = ops.in_stats(c)
+    S = Buf.empty(N, H, H, 128, 1, dev)
+    ops.in_apply(c, mean, rstd, 1, None, S, 0, presplit=True)
+    P = {"t.weight": torch.randn(128, 64, 3, 3, device=dev) * 0.05, "t.bias": torch.zeros(64, device=dev)}
+    Y = Buf.empty(N, 2 * H, 2 * H, 64, 0, dev)
+    X.QUAD = kind == "quad_stats"
+    return lambda: X._convT_fwd(P, "t", S, Y)
+
+
 def main():
     kind = sys.argv[1] if len(sys.argv) > 1 else "fwd"
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
     L.load()
     dev = "cuda"
-    if kind.startswith("stem_") or kind == "win_fwd":
-        fn = stem(kind, dev) if kind != "win_fwd" else win_fwd(dev)
+    if kind.startswith("stem_") or kind in ("win_fwd", "quad_stats", "convT4_stats"):
+        fn = (stem(kind, dev) if kind.startswith("stem_") else win_fwd(dev) if kind == "win_fwd" else
+              deconv2(kind, dev))
         for _ in range(reps):
             fn()
         torch.cuda.synchronize()

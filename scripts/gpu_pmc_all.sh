@@ -13,6 +13,8 @@ for k in $KINDS; do
     stem_wgrad) key=stem_wgrad_kernel; ktag="stem_wgrad_kernel"; name=stem_wgrad;;
     stem_fwd) key=stem_fwd_kernel; ktag="stem_fwd_kernel"; name=stem_fwd;;
     win_fwd) key=conv_win2_kernel; ktag="conv_win2_kernel<7>"; name=win_fwd;;
+    quad_stats) key="true, true, true>"; ktag="conv_fwd_f3_kernel<256,256,...,STATS,PS,QUAD> (deconv2)"; name=deconv2_quad;;
+    convT4_stats) key="512, 64, 64, 64, 2, 3, true, true, false>"; ktag="conv_fwd_f3_kernel<512,64,...> (deconv2 4 phases)"; name=deconv2_4phase;;
     *) echo "unknown kind $k"; exit 1;;
   esac
   KIND=$k scripts/gpu_pmc.sh "${TAG}_$k" || { echo "pmc $k failed"; exit 1; }

@@ -873,6 +873,57 @@ def test_presplit_f3_tiles_and_stats(case, cfg, persistent):
         lib.fg_set_f3_persistent(1)
 
 
+@pytest.mark.parametrize("persistent", [1, 3])
+@pytest.mark.parametrize("N,cin,H,W", [(2, 128, 16, 16), (1, 128, 9, 7), (2, 256, 12, 10), (8, 128, 64, 64)])
+def test_quad_convT(N, cin, H, W, persistent):
+    """The quad form (one problem for the 4 output phases of a stride-2 3-tap transposed op, zero segments
+    skipped: plans.quad_map / conv_f3.hip QUAD) on a FG_PRESPLIT operand: ConvTranspose2d(cin, 64, 3, 2, 1, 1)
+    with bias, and the input gradient of Conv2d(64, cin, 3, 2, 1), vs fp64; the forward's epilogue statistics vs
+    fg_in_stats of its output; bit-identical outputs with and without the statistics; ragged tiles (9 x 7),
+    the tile-crossing stream (persistent 3) -- and the executor routing deconv2 / conv2's input gradient to it"""
+    from floodgan import _lib as L, executor as X, ops, plans as PL
+    from floodgan.plans import Buf
+    lib = L.load()
+    try:
+        lib.fg_set_f3_persistent(persistent)
+        torch.manual_seed(17)
+        c = torch.randn(N, cin, H, W, dtype=torch.float64) * 1.2 + 0.1
+        cb = buf_from(c, 0, "constant")
+        mean, rstd = ops.in_stats(cb)
+        S = Buf.empty(N, H, W, cin, 1, DEV)
+        ops.in_apply(cb, mean, rstd, 1, None, S, 0, presplit=True)        # relu(IN(c)), zero border, pre-split
+        x64 = F.relu(F.instance_norm(c, eps=1e-5))
+        w = torch.randn(cin, 64, 3, 3, dtype=torch.float64) * 0.05
+        b = torch.randn(64, dtype=torch.float64) * 0.1
+        y64 = F.conv_transpose2d(x64, w, b, stride=2, padding=1, output_padding=1)
+        inp = torch.zeros(N, 64, 2 * H, 2 * W, dtype=torch.float64, requires_grad=True)
+        g64, = torch.autograd.grad(F.conv2d(inp, w, stride=2, padding=1), inp, x64)
+        P = {"t.weight": w.float().to(DEV), "t.bias": b.float().to(DEV)}
+        assert X._quad_ok(S, w.shape, 3, Buf.empty(N, 2 * H, 2 * W, 64, 0, DEV))
+        outs = []
+        for stats in (False, True):
+            Y = Buf.empty(N, 2 * H, 2 * W, 64, 0, DEV)
+            st = X._quad(P, "t", S, Y, bias=P["t.bias"], in_stats=stats)
+            assert ops.LAST_CONV_KERNEL == "conv_fwd_f3_quad"
+            outs.append((Y, st))
+        G = Buf.empty(N, 2 * H, 2 * W, 64, 0, DEV)
+        X._dgrad_s2(P, "t", S, 3, Y=G)
+        assert ops.LAST_CONV_KERNEL == "conv_fwd_f3_quad"
+        Yr = Buf.empty(N, 2 * H, 2 * W, 64, 0, DEV)
+        st_r = X._convT_fwd(P, "t", S, Yr)
+        torch.cuda.synchronize()
+        (Y0, _), (Y1, st) = outs
+        assert nrel(nchw(Y0), y64) < KTOL, nrel(nchw(Y0), y64)
+        assert torch.equal(Y0.interior(), Y1.interior()) and torch.equal(Yr.interior(), Y0.interior())
+        assert nrel(nchw(G), g64) < KTOL, nrel(nchw(G), g64)
+        if (H * W) % 32 == 0:
+            assert st is not None and st_r is not None
+            mean_ref, rstd_ref = ops.in_stats(Y1)
+            assert nrel(st[0], mean_ref) < KTOL and nrel(st[1], rstd_ref) < KTOL
+    finally:
+        lib.fg_set_f3_persistent(1)
+
+
 def test_fused_in_stats_declined():
     """a conv the epilogue statistics cannot cover (output rows per image not a multiple of 32, e.g. the
     discriminator's 4x4 stride-1 conv) returns None and the caller computes the statistics itself"""

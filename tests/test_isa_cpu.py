@@ -65,7 +65,7 @@ def test_conv_f3_epilogue_store_count(tmp_path):
     names = _demangle([n for n, _ in funcs])
     checked = 0
     for name, (_, body) in zip(names, funcs):
-        m = re.search(r"conv_fwd_f3_kernel<(\d+), (\d+), (\d+), (\d+), (\d+), (\d+), (true|false), (true|false)>", name)
+        m = re.search(r"conv_fwd_f3_kernel<(\d+), (\d+), (\d+), (\d+), (\d+), (\d+), (true|false), (true|false)(?:, (?:true|false))?>", name)
         assert m, name
         wm, wn = int(m.group(3)), int(m.group(4))
         nst = (wm // 16) * 4 * (wn // 16)

@@ -266,3 +266,52 @@ def test_phase_partial_channels():
     for prob in PL.phase_problems(G, w.shape, 4, 1, None, wps, maps, y_nchw=(out.view(-1), 3, 8, 8)):
         emu_conv(prob)
     assert close(out, ref[:, 9:12])
+
+
+def test_quad_map_and_problem():
+    """the quad form (plans.quad_map / quad_problem) emulated in fp64 on the CPU: the 4 phases of
+    ConvTranspose2d(ci, 64, 3, 2, 1, 1) as one GEMM over the 2 x 2 input neighbourhood, scattered by q_yoff,
+    equal torch's conv_transpose2d; the packed weights are zero exactly where q_mask is clear; each wave of the
+    64 x 128 tiling (column groups {0, 1} and {2, 3}) has 5 resp. 4 live (group, segment) products"""
+    import numpy as np
+    from floodgan import plans as PL
+    from floodgan.plans import Buf
+    torch.manual_seed(0)
+    N, H, W, ci = 2, 3, 4, 32
+    x = torch.randn(N, ci, H, W, dtype=torch.float64)
+    w = torch.randn(ci, 64, 3, 3, dtype=torch.float64)
+    ref = torch.nn.functional.conv_transpose2d(x, w, stride=2, padding=1, output_padding=1)
+    S = Buf(torch.zeros(N * (H + 2) * (W + 2) * ci, dtype=torch.float64), N, H, W, ci, 1)
+    S.interior().copy_(x.permute(0, 2, 3, 1))
+    Y = Buf(torch.zeros(N * (2 * H + 2) * (2 * W + 2) * 64, dtype=torch.float64), N, 2 * H, 2 * W, 64, 1)
+    m, d0, mask = PL.quad_map(w.shape, 3, 1, ci)
+    assert (m["n_out"], m["q_n"], d0) == (256, 64, 0)
+    Wp = np.zeros((256, 2 * m["jp"]))
+    for n in range(256):
+        q, o = divmod(n, 64)
+        for kr in range(2):
+            for ks in range(2):
+                r, s = m["rtab"][q * 2 + kr], m["stab"][q * 2 + ks]
+                if r >= 0 and s >= 0:
+                    Wp[n, kr * m["jp"] + ks * ci: kr * m["jp"] + (ks + 1) * ci] = w[:, o, r, s].numpy()
+    for q in range(4):
+        for seg in range(4):
+            R, Sg = divmod(seg, 2)
+            blk = Wp[q * 64:(q + 1) * 64, R * m["jp"] + Sg * ci: R * m["jp"] + (Sg + 1) * ci]
+            assert bool(np.abs(blk).sum() > 0) == bool((mask >> (q * 4 + seg)) & 1)
+    live = [sum((mask >> (q * 4 + sg)) & 1 for q in g for sg in range(4)) for g in ((0, 1), (2, 3))]
+    assert live == [5, 4]
+    p = PL.quad_problem(S, m, d0, mask, None, Y)
+    xs, yv = S.t.numpy().ravel(), Y.t.numpy().ravel()
+    for img in range(N):
+        for a in range(H):
+            for b in range(W):
+                row = p["x"][1] + img * p["sxn"] + a * p["sxa"] + b * p["sxb"]
+                A = np.concatenate([xs[row + r * p["sxr"]: row + r * p["sxr"] + p["jp"]] for r in range(2)])
+                out = Wp @ A
+                base = p["y"][1] + img * p["syn"] + a * p["sya"] + b * p["syb"]
+                for n in range(256):
+                    q, o = divmod(n, 64)
+                    yv[base + o + p["q_yoff"][q]] = out[n]
+    got = Y.interior().permute(0, 3, 1, 2)
+    assert float((got - ref).abs().max()) < 1e-10
