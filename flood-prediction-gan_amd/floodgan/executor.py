@@ -549,6 +549,18 @@ def disc_pack(pairs, c_in_total):
     return buf
 
 
+def disc_prefix(buf, n):
+    """The first n images of a disc_pack buffer as a Buf of their own (a view: the G step's D input (x, fake) is the
+    D step's first half, so it is not packed again), with the buffer's absmax slot -- it bounds the whole buffer, so
+    it bounds the prefix"""
+    img = buf.t.numel() // buf.n
+    v = Buf(buf.t[:n * img], n, buf.h, buf.w, buf.c, buf.pad)
+    slot = getattr(buf.t, "_fg_amax", None)
+    if slot is not None and getattr(buf.t, "_fg_amax_ver", None) == buf.t._version:
+        v.t._fg_amax, v.t._fg_amax_ver = slot, v.t._version
+    return v
+
+
 def disc_forward(P, inp, save=True):
     """inp: Buf from disc_pack (zero border 1).  Returns (pred [N,1,ho,wo], saved)."""
     N, H, W = inp.n, inp.h, inp.w

@@ -77,7 +77,7 @@ class PairedStep:
         self.dflat.begin(self.group)
         X.disc_backward(self.dp, dS, g_pred, param_grads=True, grads_into=self._grads(self.dp),
                         ready=self.dflat.ready)
-        del dS, dinp
+        del dS
         self.dflat.finish()
         self.opt_d.step()
         if self.d_after is not None:
@@ -86,7 +86,7 @@ class PairedStep:
                 for k, p in self.D.named_parameters():
                     p.copy_(self.d_after[k])
         # ---- generator step against the updated discriminator                 (:636-646)
-        dinp = X.disc_pack([(x, fake)], C + 3)
+        dinp = X.disc_prefix(dinp, N)          # (x, fake): the D step's first half, unchanged since
         pred, dS = X.disc_forward(self.dp, dinp, save=True)
         g_pred = torch.empty_like(pred)
         ops.mse_const(pred, 1.0, inv, losses[2:3], g_pred)
@@ -162,10 +162,10 @@ class Pix2PixStep(PairedStep):
         self.dflat.begin(self.group)
         P2P.disc_backward(self.dp, dS, g_pred, param_grads=True, grads_into=self._grads(self.dp),
                           ready=self.dflat.ready)
-        del dS, dinp
+        del dS
         self.dflat.finish()
         self.opt_d.step()
-        dinp = X.disc_pack([(x, fake)], C + 3)
+        dinp = X.disc_prefix(dinp, N)          # (x, fake): the D step's first half, unchanged since
         pred, dS = P2P.disc_forward(self.dp, self.db, dinp, groups=1, training=True, save=True)
         g_pred = torch.empty_like(pred)
         ops.mse_const(pred, 1.0, inv, losses[2:3], g_pred)
@@ -175,6 +175,7 @@ class Pix2PixStep(PairedStep):
                           input_grad_accumulate=True)
         if rec is not None:
             rec["D"].append(P2P.disc_act_decisions(dS))
+            rec["L1"] = [{"l1": torch.sign(fake.detach() - y)}]   # the L1 term's sign decisions (-1 / 0 / +1)
             self.decisions = rec
         del dS, dinp
         self.gflat.begin(self.group)

@@ -286,6 +286,11 @@ class PairedStepOracle:
         l_d.backward()
         if record is not None:
             record["d_grads"] = OrderedDict((k, v.grad.detach().clone()) for k, v in self.D.items())
+            # dl_d/d(model.11.bias) = mean(pred_fake) + mean(pred_real - 1): a sum whose terms can cancel, so its
+            # attainable relative accuracy is u * (mean|pred_fake| + mean|pred_real - 1|) / |sum| (checked against
+            # that mass, tests/test_gpu_northstar.py u_compare)
+            record["d_sum_mass"] = {"model.11.bias": float(pred_fake.detach().abs().mean() +
+                                                          (pred_real.detach() - 1).abs().mean())}
         self.opt_d.step()
         if record is not None:
             record["d_after_own"] = OrderedDict((k, v.detach().clone()) for k, v in self.D.items())

@@ -296,8 +296,12 @@ def u_compare(st, rec, P0, P_hip, g_hip):
     iteration and the gradients its optimiser steps used.  Returns (rows, bad): per parameter (net, name,
     gradient error, direction agreement of the decided elements, decided-update error, decided fraction,
     whole-tensor error); bad = rows past the bounds (gradient 1e-4, agreement 1.0, decided update 1e-3).
-    IN-cancelled biases are skipped (their gradients are rounding noise)."""
+    IN-cancelled biases are skipped (their gradients are rounding noise).  D's last bias gradient
+    is a plain sum of the prediction residuals whose terms cancel (mean(pred_fake) + mean(pred_real - 1)): its error
+    is measured against the sum's mass (mean |pred_fake| + mean |pred_real - 1|, rec["d_sum_mass"]) when that
+    exceeds the sum -- the forward-error bound of a sum -- not against the cancelled result."""
     skip_g, skip_d = O.cancelled_biases()
+    mass = rec.get("d_sum_mass", {})
     rows, bad = [], []
     for net, grads, skip, opt_ref, params_ref, order in (
             ("G", rec["g_grads"], skip_g, st.opt_g, st.G, list(st.G)),
@@ -306,6 +310,10 @@ def u_compare(st, rec, P0, P_hip, g_hip):
             if k in skip:
                 continue
             ge = nrel(g_hip[net][k], grads[k])
+            if net == "D" and k in mass:
+                ref = grads[k].detach().double().cpu()
+                den = max(float(ref.norm()), mass[k] * ref.numel() ** 0.5, 1e-30)
+                ge = float((g_hip[net][k].detach().double().cpu() - ref).norm()) / den
             m_ref = opt_ref.state[opt_ref.param_groups[0]["params"][order.index(k)]]["exp_avg"]
             agree, uerr, frac, perr = _update_agreement(P0[net][k], P_hip[net][k], params_ref[k], g_hip[net][k],
                                                         grads[k], m_ref)
