@@ -33,6 +33,7 @@ __device__ __forceinline__ int swz_a(int row) { return ((row >> 1) & 1) ^ (((row
 __device__ __forceinline__ int swz_b(int row) { return ((row >> 3) & 1) << 1; }                        // 4 chunks
 
 typedef __attribute__((address_space(3))) void lds_void;
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 // f16x3 split with scalar f32 arithmetic (packed-f32 VALU beside MFMAs costs extra issue
 // cycles): v*s = h + l, h = fp16(v*s), l = fp16(v*s - h), the residual exact in fp32
@@ -65,6 +66,15 @@ __device__ __forceinline__ void dma_stage(char* sb, int wave, __amdgpu_buffer_rs
                                                  soff_b, 0, 0);
 }
 
+// the conv's MFMA with the operands exchanged: D^T = B^T A^T, so that a lane's 4 accumulator registers are 4
+// CONSECUTIVE output columns (channels) of one output row (pixel): lane l holds row (l & 15) and columns
+// 4 (l >> 4) .. +3 of its 16 x 16 block.  The NHWC epilogue then stores 16 B per lane (one dwordx4 per block)
+// instead of four scattered dwords: a quarter of the store instructions, which bounded the epilogue
+// (round 5: the no-epilogue diagnostic ran deconv2 in 0.67 of its time, the resblock conv in 0.92)
+__device__ __forceinline__ f32x4 mma_t(f16x8 a, f16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(b, a, c, 0, 0, 0);
+}
+
 // QUAD: the output offset of column group q (wave-uniform per column block; a select chain, not an indexed
 // kernel-argument load)
 __device__ __forceinline__ int quad_yoff(const fg_conv_problem& P, int q) {
@@ -80,6 +90,8 @@ constexpr int kYRecords = 0x7fffff00, kYOOB = 0x7ffffff0;
 __device__ __forceinline__ void dma_piece(char* dst, __amdgpu_buffer_rsrc_t r, int voff, int soff) {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)dst, 16, voff, soff, 0, 0);
 }
+
+constexpr int cap63(int n) { return n < 63 ? n : 63; }
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
@@ -397,30 +409,30 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
                 for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
                     for (int t = 0; t < TG; ++t)
-                        acc[tm][t0 + t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[tm], bh[t], acc[tm][t0 + t], 0, 0, 0);
+                        acc[tm][t0 + t] = mma_t(al[tm], bh[t], acc[tm][t0 + t]);
 #pragma unroll
                 for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
                     for (int t = 0; t < TG; ++t)
-                        acc[tm][t0 + t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[tm], bl[t], acc[tm][t0 + t], 0, 0, 0);
+                        acc[tm][t0 + t] = mma_t(ah[tm], bl[t], acc[tm][t0 + t]);
 #pragma unroll
                 for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
                     for (int t = 0; t < TG; ++t)
-                        acc[tm][t0 + t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[tm], bh[t], acc[tm][t0 + t], 0, 0, 0);
+                        acc[tm][t0 + t] = mma_t(ah[tm], bh[t], acc[tm][t0 + t]);
             } else {
 #pragma unroll
                 for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
                     for (int t = 0; t < TG; ++t) {
-                        acc[tm][t0 + t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[tm], bh[t], acc[tm][t0 + t], 0, 0, 0);
-                        acc[tm][t0 + t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[tm], bl[t], acc[tm][t0 + t], 0, 0, 0);
+                        acc[tm][t0 + t] = mma_t(ah[tm], bh[t], acc[tm][t0 + t]);
+                        acc[tm][t0 + t] = mma_t(ah[tm], bl[t], acc[tm][t0 + t]);
                     }
 #pragma unroll
                 for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
                     for (int t = 0; t < TG; ++t)
-                        acc[tm][t0 + t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[tm], bh[t], acc[tm][t0 + t], 0, 0, 0);
+                        acc[tm][t0 + t] = mma_t(al[tm], bh[t], acc[tm][t0 + t]);
             }
         }
     };
@@ -475,134 +487,125 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
 #pragma unroll
                 for (int t = 0; t < TG2; ++t) {
                     f32x4& c = acc[tm][gi * TG2 + t];
-                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[tm], bh[sl][t], c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[tm], bl[sl][t], c, 0, 0, 0);
+                    c = mma_t(ah[tm], bh[sl][t], c);
+                    c = mma_t(ah[tm], bl[sl][t], c);
                 }
 #pragma unroll
             for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
                 for (int t = 0; t < TG2; ++t) {
                     f32x4& c = acc[tm][gi * TG2 + t];
-                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[tm], bh[sl][t], c, 0, 0, 0);
+                    c = mma_t(al[tm], bh[sl][t], c);
                 }
         }
     };
 
-    // ---- epilogue of the compute tile: scale, bias, activation, strided store (or accumulate)
-    int issued = 0, done = 0, epi_issued = 0;
+    // ---- epilogue of the compute tile: scale, bias, activation, strided store (or accumulate).  Accumulator
+    // layout (mma_t): acc[tm][tn][r] is row m0 + tm*16 + fr, column n0 + tn*16 + 4g + r.
+    constexpr int NSTV = TM * TN, NSTS = TM * TN * 4;   // stores per epilogue: dwordx4 (NHWC) / dword (strided)
+    int issued = 0, done = 0, epi_issued = 0, epi_nst = NSTS;
     auto epilogue = [&]() {
         const fg_conv_problem& P = batch.p[cg.pi];
         const int mab = P.m_a * P.m_b, M = P.m_img * mab;
         const int act = P.act;
         const bool accum = P.accumulate != 0;
-        float bias_v[TN];
-        int ncol[TN];
-        // QUAD: column n = q * q_n + o is channel o of the pixel at q_yoff[q]; its statistics partials sit in group
-        // q's region ([rb][q_n][2] at q * q_soff)
-        int ych[TN], yq[TN];
+        // a lane's 4 columns are contiguous and 16-B aligned in y: one dwordx4 store per block
+        bool vec = P.syc == 1 && P.n_out % 4 == 0 && ((uintptr_t)P.y & 15) == 0 &&
+                   ((P.syn | P.sya | P.syb) & 3) == 0;
+        if constexpr (QUAD) vec = vec && ((P.q_yoff[0] | P.q_yoff[1] | P.q_yoff[2] | P.q_yoff[3]) & 3) == 0;
+        // QUAD: column n = q * q_n + o is channel o of the pixel at q_yoff[q] (q uniform per 16-column block); its
+        // statistics partials sit in group q's region ([rb][q_n][2] at q * q_soff)
+        int nc0[TN], ych[TN], yq[TN];
+        f32x4 bias4[TN];
 #pragma unroll
         for (int tn = 0; tn < TN; ++tn) {
-            ncol[tn] = cg.n0 + wn * WN + tn * 16 + fr;
+            nc0[tn] = cg.n0 + wn * WN + tn * 16 + 4 * g;
             if constexpr (QUAD) {
-                yq[tn] = ncol[tn] / P.q_n;
-                ych[tn] = ncol[tn] - yq[tn] * P.q_n;
+                yq[tn] = nc0[tn] / P.q_n;
+                ych[tn] = nc0[tn] - yq[tn] * P.q_n;
             } else {
                 yq[tn] = 0;
-                ych[tn] = ncol[tn];
+                ych[tn] = nc0[tn];
             }
-            bias_v[tn] = P.bias ? P.bias[min(ych[tn], P.n_out - 1)] : 0.f;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) bias4[tn][r] = P.bias ? P.bias[min(ych[tn] + r, P.n_out - 1)] : 0.f;
         }
         const bool full_n = cg.n0 + BN <= P.n_out;
         if (STATS && P.in_stats) {
-            // InstanceNorm partials of each 32-row block of this wave's rows (WM / 32 of them: tm blocks
-            // hb*TB .. hb*TB+TB-1, x g x reg), per column: two passes (mean, then M2) over the raw accumulators, each
-            // reduced over the 4 lanes of the column (g); out_scale (a power of 2) and the bias are applied to the
-            // results.  Columns go in groups of SG so that a group's cross-lane exchanges are in flight together
+            // InstanceNorm partials of each 32-row block of this wave's rows (WM / 32 of them: tm blocks hb*TB ..
+            // hb*TB+1, 16 rows each across the lanes of a DPP row), per column: two passes (mean, then M2) over the raw
+            // accumulators -- the two rows of a lane summed in registers, then over the 16 lanes of the row
+            // (fg::row_sum16); out_scale (a power of 2) and the bias are applied to the results
             constexpr int NB = WM / 32, TB = TM / NB;
             static_assert(WM % 32 == 0 && TB * 16 == 32, "32-row statistics blocks");
 #pragma unroll
             for (int hb = 0; hb < NB; ++hb) {
             const int rb0 = cg.m0 + wm * WM + hb * 32;
             if (rb0 < M) {
-                constexpr int SG = TN < 4 ? TN : 4;
                 const float sc = out_scale;
                 float* const dst0 = P.in_stats + (size_t)(rb0 / 32) * (QUAD ? P.q_n : P.n_out) * 2;
 #pragma unroll
-                for (int t0 = 0; t0 < TN; t0 += SG) {
-                    float sm[SG], sq[SG];
+                for (int tn = 0; tn < TN; ++tn) {
+                    f32x4 sm, sq;
 #pragma unroll
-                    for (int u = 0; u < SG; ++u) {
-                        f32x2 s2 = f32x2{acc[hb * TB][t0 + u][0], acc[hb * TB][t0 + u][1]} +
-                                   f32x2{acc[hb * TB][t0 + u][2], acc[hb * TB][t0 + u][3]};
+                    for (int r = 0; r < 4; ++r) sm[r] = fg::row_sum16(acc[hb * TB][tn][r] + acc[hb * TB + 1][tn][r]);
 #pragma unroll
-                        for (int tm = hb * TB + 1; tm < hb * TB + TB; ++tm)
-                            s2 += f32x2{acc[tm][t0 + u][0], acc[tm][t0 + u][1]} +
-                                  f32x2{acc[tm][t0 + u][2], acc[tm][t0 + u][3]};
-                        sm[u] = s2[0] + s2[1];
+                    for (int r = 0; r < 4; ++r) {
+                        const float mu = sm[r] * (1.f / 32);
+                        sm[r] = mu;
+                        const float d0 = acc[hb * TB][tn][r] - mu, d1 = acc[hb * TB + 1][tn][r] - mu;
+                        sq[r] = fg::row_sum16(d0 * d0 + d1 * d1);
                     }
+                    if (fr == 0) {
+                        float* const dst = dst0 + (QUAD ? yq[tn] * P.q_soff : 0) + ych[tn] * 2;
 #pragma unroll
-                    for (int u = 0; u < SG; ++u) sm[u] = fg::rows_sum4(sm[u]);     // lanes l, l^16, l^32, l^48
-#pragma unroll
-                    for (int u = 0; u < SG; ++u) {
-                        const float mu = sm[u] * (1.f / 32);
-                        sm[u] = mu;
-                        const f32x2 m2 = {mu, mu};
-                        f32x2 q2;
-#pragma unroll
-                        for (int tm = hb * TB; tm < hb * TB + TB; ++tm) {
-                            const f32x2 d0 = f32x2{acc[tm][t0 + u][0], acc[tm][t0 + u][1]} - m2;
-                            const f32x2 d1 = f32x2{acc[tm][t0 + u][2], acc[tm][t0 + u][3]} - m2;
-                            q2 = tm > hb * TB ? q2 + d0 * d0 + d1 * d1 : d0 * d0 + d1 * d1;
-                        }
-                        sq[u] = q2[0] + q2[1];
-                    }
-#pragma unroll
-                    for (int u = 0; u < SG; ++u) sq[u] = fg::rows_sum4(sq[u]);     // lanes l, l^16, l^32, l^48
-                    if (g == 0) {
-#pragma unroll
-                        for (int u = 0; u < SG; ++u)
-                            if (ncol[t0 + u] < P.n_out)
-                                *reinterpret_cast<f32x2*>(dst0 + (QUAD ? yq[t0 + u] * P.q_soff : 0) +
-                                                          ych[t0 + u] * 2) =
-                                    f32x2{sm[u] * sc + bias_v[t0 + u], sq[u] * (sc * sc)};
+                        for (int r = 0; r < 4; ++r)
+                            if (nc0[tn] + r < P.n_out)
+                                *reinterpret_cast<f32x2*>(dst + 2 * r) =
+                                    f32x2{sm[r] * sc + bias4[tn][r], sq[r] * (sc * sc)};
                     }
                 }
             }
             }
         }
-        // the stores: TM x 4 x TN buffer stores per lane, ALWAYS issued (rows past M / columns past n_out get an
-        // out-of-range offset, which the hardware drops), so the stage waits after this epilogue can leave
-        // exactly that many younger VMEM operations in flight (see wait_stage) instead of draining them
+        // the stores: TM x TN dwordx4 (vec) or TM x TN x 4 dword buffer stores per lane, ALWAYS issued (rows past M /
+        // columns past n_out get an out-of-range offset, which the hardware drops), so the stage waits after this
+        // epilogue can leave exactly that many younger VMEM operations in flight (see wait_stage)
         const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc((void*)P.y, 0, kYRecords, 0x00020000);
         int coff[TN];
 #pragma unroll
         for (int tn = 0; tn < TN; ++tn) coff[tn] = ych[tn] * (int)P.syc + (QUAD ? quad_yoff(P, yq[tn]) : 0);
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm) {
-            // the lane's 4 consecutive rows: one decomposition, then (b, a, img) advanced with wrap-around
-            const int m0 = cg.m0 + wm * WM + tm * 16 + 4 * g;
+            const int m = cg.m0 + wm * WM + tm * 16 + fr;
             int img, a, b;
-            fgc::decomp(min(m0, M - 1), P.m_b, mab, img, a, b);
+            fgc::decomp(min(m, M - 1), P.m_b, mab, img, a, b);
+            const bool row_ok = m < M;
+            const int roff = img * (int)P.syn + a * (int)P.sya + b * (int)P.syb;
 #pragma unroll
-            for (int reg = 0; reg < 4; ++reg) {
-                if (reg) {
-                    if (++b == P.m_b) {
-                        b = 0;
-                        if (++a == P.m_a) { a = 0; ++img; }
+            for (int tn = 0; tn < TN; ++tn) {
+                f32x4 v;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = fg::act_fwd(acc[tm][tn][r] * out_scale + bias4[tn][r], act);
+                if (vec) {
+                    const bool ok = row_ok && (full_n || nc0[tn] < P.n_out);
+                    if (accum && ok) v += *reinterpret_cast<const f32x4*>(P.y + roff + coff[tn]);
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), yr,
+                                                           ok ? (roff + coff[tn]) * 4 : kYOOB, 0, 0);
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const bool ok = row_ok && (full_n || nc0[tn] + r < P.n_out);
+                        const int off = roff + coff[tn] + r * (int)P.syc;
+                        float w = v[r];
+                        if (accum && ok) w += P.y[off];
+                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(w), yr, ok ? off * 4 : kYOOB, 0, 0);
                     }
-                }
-                const bool row_ok = m0 + reg < M;
-                const int roff = img * (int)P.syn + a * (int)P.sya + b * (int)P.syb;
-#pragma unroll
-                for (int tn = 0; tn < TN; ++tn) {
-                    const bool ok = row_ok && (full_n || ncol[tn] < P.n_out);
-                    float v = fg::act_fwd(acc[tm][tn][reg] * out_scale + bias_v[tn], act);
-                    if (accum && ok) v += P.y[roff + coff[tn]];
-                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), yr, ok ? (roff + coff[tn]) * 4 : kYOOB, 0, 0);
                 }
             }
         }
         epi_issued = issued;
+        epi_nst = vec ? NSTV : NSTS;
     };
 
     // ---- NS-deep ring over the stage stream: stage s+NS-1 is issued right after the barrier that
@@ -617,18 +620,22 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
         if (issue_next(s0)) ++issued;
     int cur = 0, nxt = NS - 1;
     // wait for stage `done`'s own DMAs: the VMEM operations younger than them are the stages issued after it
-    // and, when stage `done` was issued before the last epilogue, that epilogue's NST stores (vmcnt counts
-    // loads, LDS-DMA and stores together, in issue order).  Any smaller count is safe (it waits for more).
-    // NST is the trip count of the epilogue's store loop (tm < TM, reg < 4, tn < TN: one raw_buffer_store_b32
-    // each, never predicated off); tests/test_isa_cpu.py checks every instantiation's code object issues exactly
-    // that many single-dword buffer stores and no merged wider ones.
-    constexpr int D = A_GL + B_GL, NST = TM * 4 * TN;
-    constexpr int W1 = D < 63 ? D : 63, WS = NST < 63 ? NST : 63, WSD = NST + D < 63 ? NST + D : 63;
+    // and, when stage `done` was issued before the last epilogue, that epilogue's epi_nst stores (vmcnt counts
+    // loads, LDS-DMA and stores together, in issue order).  Any smaller count is safe (it waits for more): each
+    // branch waits for min(c, 63) with c <= younger.  The store counts are the trip counts of the epilogue's two
+    // store loops (never predicated off); tests/test_isa_cpu.py checks every instantiation's code object issues
+    // exactly NSTV dwordx4 and NSTS dword buffer stores and no other widths.
+    constexpr int D = A_GL + B_GL;
     auto wait_stage = [&]() {
-        const int younger = (issued - done - 1) * D + (done < epi_issued ? NST : 0);
-        if (younger >= NST + D) wait_vmcnt<WSD>();
-        else if (younger >= NST) wait_vmcnt<WS>();
-        else if (younger >= D) wait_vmcnt<W1>();
+        const int younger = (issued - done - 1) * D + (done < epi_issued ? epi_nst : 0);
+        if (NS == 3 && younger >= NSTS + 2 * D) wait_vmcnt<cap63(NSTS + 2 * D)>();
+        else if (younger >= NSTS + D) wait_vmcnt<cap63(NSTS + D)>();
+        else if (younger >= NSTS) wait_vmcnt<cap63(NSTS)>();
+        else if (NS == 3 && younger >= NSTV + 2 * D) wait_vmcnt<cap63(NSTV + 2 * D)>();
+        else if (younger >= NSTV + D) wait_vmcnt<cap63(NSTV + D)>();
+        else if (younger >= NSTV) wait_vmcnt<cap63(NSTV)>();
+        else if (NS == 3 && younger >= 2 * D) wait_vmcnt<cap63(2 * D)>();
+        else if (younger >= D) wait_vmcnt<cap63(D)>();
         else wait_vmcnt<0>();
     };
     while (true) {

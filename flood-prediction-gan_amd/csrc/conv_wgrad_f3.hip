@@ -214,17 +214,17 @@ conv_wgrad_f3_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
             for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
                 for (int t = 0; t < TG; ++t)
-                    acc[tm][t0 + t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[tm], bh[t], acc[tm][t0 + t], 0, 0, 0);
+                    acc[tm][t0 + t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[t], al[tm], acc[tm][t0 + t], 0, 0, 0);
 #pragma unroll
             for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
                 for (int t = 0; t < TG; ++t)
-                    acc[tm][t0 + t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[tm], bl[t], acc[tm][t0 + t], 0, 0, 0);
+                    acc[tm][t0 + t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bl[t], ah[tm], acc[tm][t0 + t], 0, 0, 0);
 #pragma unroll
             for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
                 for (int t = 0; t < TG; ++t)
-                    acc[tm][t0 + t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[tm], bh[t], acc[tm][t0 + t], 0, 0, 0);
+                    acc[tm][t0 + t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[t], ah[tm], acc[tm][t0 + t], 0, 0, 0);
         }
     };
 
@@ -246,22 +246,22 @@ conv_wgrad_f3_kernel(const fg_wgrad_problem P, int tiles_a, int tiles_k) {
         __syncthreads();
     }
 
-    // ---- epilogue: scaled fp32 slab rows a, columns k
+    // ---- epilogue: scaled fp32 slab rows a, columns k.  The MFMAs take their operands exchanged (D^T = B^T A^T), so a
+    // lane's 4 accumulator registers are 4 consecutive columns k of one row a: one 16-B store per 16 x 16 block
+    // instead of four scattered dwords (K % 4 == 0, launch_wgrad_f3)
     float* out = P.out + (size_t)split * P.n_a * K;
     const float osc = 1.f / (sp * sx);
     const int fr = lane & 15;
 #pragma unroll
-    for (int tm = 0; tm < TM; ++tm)
+    for (int tm = 0; tm < TM; ++tm) {
+        const int a = a0 + wa * 64 + tm * 16 + fr;
+        if (a >= P.n_a) continue;
 #pragma unroll
-        for (int reg = 0; reg < 4; ++reg) {
-            const int a = a0 + wa * 64 + tm * 16 + 4 * g + reg;
-            if (a >= P.n_a) continue;
-#pragma unroll
-            for (int tn = 0; tn < TN; ++tn) {
-                const int k = k0 + wk * WK + tn * 16 + fr;
-                if (k < K) out[(size_t)a * K + k] = acc[tm][tn][reg] * osc;
-            }
+        for (int tn = 0; tn < TN; ++tn) {
+            const int k = k0 + wk * WK + tn * 16 + 4 * g;
+            if (k < K) *reinterpret_cast<f32x4*>(out + (size_t)a * K + k) = acc[tm][tn] * osc;
         }
+    }
 }
 
 }  // namespace

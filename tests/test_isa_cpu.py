@@ -1,10 +1,11 @@
 """Static checks on the gfx950 code object inside the built libfloodgan.so (no GPU needed).
 
-conv_f3.hip's stage wait (wait_stage) counts the VMEM operations a wave may leave in flight after an epilogue as
-NST = TM * 4 * TN buffer stores -- one per (row group, row, column tile), issued unconditionally.  If the compiler
-ever merged those stores into wider ones, or dropped some, the count would be too loose and a stage's LDS could be
-read before its DMA landed, with no error anywhere.  This test disassembles every conv_fwd_f3_kernel instantiation
-and checks that it issues exactly NST single-dword buffer stores and no wider ones."""
+conv_f3.hip's stage wait (wait_stage) counts the VMEM operations a wave may leave in flight after an epilogue as the
+epilogue's store count: NSTV = TM * TN dwordx4 stores on NHWC outputs (one per 16 x 16 block, a lane's 4 consecutive
+channels), NSTS = TM * TN * 4 dword stores on strided outputs -- issued unconditionally.  If the compiler ever merged
+or split those stores, or dropped some, the count would be too loose and a stage's LDS could be read before its DMA
+landed, with no error anywhere.  This test disassembles every conv_fwd_f3_kernel instantiation and checks that it
+issues exactly NSTV dwordx4 and NSTS dword buffer stores and no other widths."""
 import os
 import re
 import shutil
@@ -68,10 +69,12 @@ def test_conv_f3_epilogue_store_count(tmp_path):
         m = re.search(r"conv_fwd_f3_kernel<(\d+), (\d+), (\d+), (\d+), (\d+), (\d+), (true|false), (true|false)(?:, (?:true|false))?>", name)
         assert m, name
         wm, wn = int(m.group(3)), int(m.group(4))
-        nst = (wm // 16) * 4 * (wn // 16)
+        nstv = (wm // 16) * (wn // 16)
         stores = len(re.findall(r"\bbuffer_store_dword\b", body))
-        wide = len(re.findall(r"\bbuffer_store_dwordx\d", body))
-        assert wide == 0, f"{name}: {wide} merged buffer stores"
-        assert stores == nst, f"{name}: {stores} buffer stores, wait_stage assumes NST = {nst}"
+        x4 = len(re.findall(r"\bbuffer_store_dwordx4\b", body))
+        other = len(re.findall(r"\bbuffer_store_dwordx[23]\b", body))
+        assert other == 0, f"{name}: {other} dwordx2/x3 buffer stores"
+        assert x4 == nstv, f"{name}: {x4} dwordx4 buffer stores, wait_stage assumes NSTV = {nstv}"
+        assert stores == 4 * nstv, f"{name}: {stores} dword buffer stores, wait_stage assumes NSTS = {4 * nstv}"
         checked += 1
     assert checked >= 12
