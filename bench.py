@@ -77,12 +77,12 @@ def resblock_wgrad_bytes(batch, res):
 # with the InstanceNorm statistics epilogue; dgrad = the input-gradient interior; wgrad = the weight gradient
 RESBLOCK_KINDS = {
     "resblock_conv_fwd": dict(kernel="conv_fwd_f3_kernel<256,256,...,STATS>", bytes=resblock_conv_bytes,
-                              pmc=[os.path.join(ROOT, "profiles", "round4", "r4_pmc_resblock_fwd_stats_ps.json")]),
+                              pmc=[os.path.join(ROOT, "profiles", "round5", "r5_pmc_resblock_fwd_stats_ps.json")]),
     "resblock_conv_dgrad": dict(kernel="conv_fwd_f3_kernel<256,256,...> (input-gradient interior)",
                                 bytes=resblock_dgrad_bytes,
-                                pmc=[os.path.join(ROOT, "profiles", "round4", "r4_pmc_resblock_dgrad_ps.json")]),
+                                pmc=[os.path.join(ROOT, "profiles", "round5", "r5_pmc_resblock_dgrad_ps.json")]),
     "resblock_conv_wgrad": dict(kernel="conv_wgrad_f3_kernel<256,0,3>", bytes=resblock_wgrad_bytes,
-                                pmc=[os.path.join(ROOT, "profiles", "round4", "r4_pmc_resblock_wgrad_ps.json")]),
+                                pmc=[os.path.join(ROOT, "profiles", "round5", "r5_pmc_resblock_wgrad_ps.json")]),
 }
 
 

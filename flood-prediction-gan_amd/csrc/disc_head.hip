@@ -3,8 +3,8 @@
 // matrix-core work.  The implicit-GEMM engine ran it as a 32-column tile with 31 idle columns,
 // re-gathering each input pixel 16 times (~0.25 ms per call at batch 16).  Here, in plain fp32
 // FMA (the reference's arithmetic):
-//   forward: one wave per 4 consecutive output pixels, lanes over channels (8 each), the 16 taps'
-//            weights held in registers, a wave reduction per pixel;
+//   forward: one wave per 4 x 4 output block, lanes over channels (8 each), the 16 taps'
+//            weights held in registers, the block's 7 x 7 input window read once, a wave reduction per pixel;
 //   weight gradient: input-pixel-centric -- each thread owns 2 channels x 16 taps of dW and adds
 //            g[y-r][x-s] * a[y][x][c] for the 16 output pixels that read input pixel (y, x), so
 //            every input pixel is read once; per-block partial sums go to fg_wgrad_reduce slabs.
@@ -16,16 +16,20 @@ namespace {
 
 constexpr int C = 512, KT = 16;   // channels, 4x4 taps
 
-// x: padded input (pad 1) of image n at (row, col) -> x + ((n*hp + row)*wp + col)*C
+// x: padded input (pad 1) of image n at (row, col) -> x + ((n*hp + row)*wp + col)*C.  One wave per 4 x 4 block of
+// output pixels (round 5; was 1 x 4): it reads the block's 7 x 7 input window once -- 49 pixels for 16 outputs, 3.1
+// reads per output pixel instead of 7 -- and adds each input pixel's 8 channels of this lane into every output of
+// the block that reads it (up to 16 taps); a wave reduction per output pixel at the end.
 __global__ void __launch_bounds__(256) n1_fwd_kernel(const float* __restrict__ x, int hp, int wp,
                                                      const float* __restrict__ w, const float* __restrict__ bias,
                                                      float* __restrict__ y, int nimg, int ho, int wo) {
     const int lane = threadIdx.x & 63;
-    const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);            // global wave: 4 pixels of one row
-    const int qpr = (wo + 3) / 4;                                   // quads per output row
-    const int row = gw / qpr;                                       // n*ho + oy
-    if (row >= nimg * ho) return;
-    const int n = row / ho, oy = row - n * ho, ox0 = (gw - row * qpr) * 4;
+    const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);            // global wave: a 4 x 4 output block
+    const int bpr = (wo + 3) / 4, bpi = ((ho + 3) / 4) * bpr;      // blocks per block-row, per image
+    const int n = gw / bpi;
+    if (n >= nimg) return;
+    const int rem = gw - n * bpi, by = rem / bpr;
+    const int oy0 = by * 4, ox0 = (rem - by * bpr) * 4;
     // weights of this lane's 8 channels, 16 taps: w[0][c][r][s] = w[c*16 + r*4 + s]
     float wr[8][KT];
 #pragma unroll
@@ -38,32 +42,45 @@ __global__ void __launch_bounds__(256) n1_fwd_kernel(const float* __restrict__ x
             wr[e][t4 * 4 + 2] = v[2];
             wr[e][t4 * 4 + 3] = v[3];
         }
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    float acc[4][4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const float* xrow = x + ((size_t)(n * hp + oy + r) * wp + ox0) * C + lane * 8;
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 7; ++j) {                               // input columns ox0 .. ox0+6
-            if (ox0 + j >= wp) break;
-            const f32x4 a = *reinterpret_cast<const f32x4*>(xrow + j * C);
-            const f32x4 b = *reinterpret_cast<const f32x4*>(xrow + j * C + 4);
+        for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
+#pragma unroll
+    for (int iy = 0; iy < 7; ++iy) {                               // input rows oy0 .. oy0+6
+        if (oy0 + iy >= hp) break;
+        const float* xrow = x + ((size_t)(n * hp + oy0 + iy) * wp + ox0) * C + lane * 8;
+#pragma unroll
+        for (int ix = 0; ix < 7; ++ix) {                           // input columns ox0 .. ox0+6
+            if (ox0 + ix >= wp) break;
+            const f32x4 a = *reinterpret_cast<const f32x4*>(xrow + ix * C);
+            const f32x4 b = *reinterpret_cast<const f32x4*>(xrow + ix * C + 4);
             const float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
 #pragma unroll
-            for (int p = 0; p < 4; ++p) {                           // output ox0+p uses tap s = j - p
-                const int s = j - p;
-                if (s < 0 || s > 3) continue;
+            for (int i = 0; i < 4; ++i) {                          // output row oy0+i uses tap r = iy - i
+                const int r = iy - i;
+                if (r < 0 || r > 3) continue;
 #pragma unroll
-                for (int e = 0; e < 8; ++e) acc[p] = fmaf(v[e], wr[e][r * 4 + s], acc[p]);
+                for (int j = 0; j < 4; ++j) {                      // output column ox0+j uses tap s = ix - j
+                    const int s = ix - j;
+                    if (s < 0 || s > 3) continue;
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) acc[i][j] = fmaf(v[e], wr[e][r * 4 + s], acc[i][j]);
+                }
             }
         }
     }
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
-        float v = acc[p];
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-        if (lane == 0 && ox0 + p < wo) y[(size_t)row * wo + ox0 + p] = v + (bias ? bias[0] : 0.f);
-    }
+        for (int j = 0; j < 4; ++j) {
+            float v = acc[i][j];
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+            if (lane == 0 && oy0 + i < ho && ox0 + j < wo)
+                y[((size_t)n * ho + oy0 + i) * wo + ox0 + j] = v + (bias ? bias[0] : 0.f);
+        }
 }
 
 // gp: output gradient with a zero border of 3 (so g[y-r][x-s] never leaves the buffer) of image
@@ -216,7 +233,7 @@ FG_API int fg_conv_n1_fwd(const float* x, int nimg, int hp, int wp, int c, const
         ((uintptr_t)x & 15) || ((uintptr_t)w & 15))
         return fg::fail(FG_ERR_INVALID, "fg_conv_n1_fwd: needs a 512-channel input padded by 1, a 4x4 kernel, "
                                         "stride 1 (ho = hp - 3)");
-    const long long waves = (long long)nimg * ho * ((wo + 3) / 4);
+    const long long waves = (long long)nimg * ((ho + 3) / 4) * ((wo + 3) / 4);
     hipLaunchKernelGGL(n1_fwd_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, stream, x, hp, wp, w, bias, y,
                        nimg, ho, wo);
     return fg::launched("conv_n1_fwd");

@@ -81,6 +81,10 @@ __device__ __forceinline__ float rows_sum4(float v) {
     return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
+// head1x1.hip: the 1x1 head's weight-gradient slab reduction ([block][n_out][65] -> dw [n_out][64], db [n_out])
+int conv1x1_wgrad_reduce_launch(const float* slab, int blocks, int n_out, float* dw, float* db, int accumulate,
+                                hipStream_t stream);
+
 inline int blocks_for(long long work, int per_block, int cap = 1 << 20) {
     long long b = (work + per_block - 1) / per_block;
     if (b < 1) b = 1;

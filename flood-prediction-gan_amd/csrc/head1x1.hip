@@ -239,6 +239,17 @@ FG_API int fg_conv1x1_dgrad(fg_view gy, const float* w, int n_out, fg_view gx, h
 
 FG_API long long fg_conv1x1_wgrad_workspace_floats(int n_out) { return (long long)WG_BLOCKS * n_out * (CI + 1); }
 
+namespace fg {
+// the slab reduction of fg_conv1x1_wgrad, for the fused attention-head backward (fg_in_bwd_head) too
+int conv1x1_wgrad_reduce_launch(const float* slab, int blocks, int n_out, float* dw, float* db, int accumulate,
+                                hipStream_t stream) {
+    const int total = n_out * (CI + 1);
+    hipLaunchKernelGGL(conv1x1_wgrad_reduce, dim3((total + 63) / 64), dim3(1024), 0, stream, slab, blocks, n_out, dw, db,
+                       accumulate);
+    return fg::launched("conv1x1_wgrad_reduce");
+}
+}  // namespace fg
+
 FG_API int fg_conv1x1_wgrad(fg_view gy, fg_view x, int n_out, float* dw, float* db, int accumulate, float* work,
                             hipStream_t stream) {
     if (!ok(gy, (n_out + 3) / 4 * 4, 1 << 20) || !ok(x, CI, CI) || !dw || !work || n_out < 1 || n_out > NO ||

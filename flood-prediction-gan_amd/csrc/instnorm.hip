@@ -248,6 +248,8 @@ struct HeadArgs {
     const float* b;     // forward: [n_out] or null
     int n_out;
     fg_view y;          // forward: the logits (16-ch allocation, pad 0); backward: the logits gradient (16 ch)
+    float* wslab = nullptr;   // backward (round 5): per-block partials of the 1x1 weight / bias gradient,
+                              // [block][n_out][65] (conv1x1_wgrad's slab layout), or null
 };
 
 template <int CTRL>
@@ -388,7 +390,7 @@ __global__ void __launch_bounds__(NT) in_apply_rows_kernel(fg_view src, const fl
                     else store_splitpix<32>(pxb, o, ss, c4, xp);
                 } else if (split_slot) {
                     store_presplit(drow + (size_t)xp * C, o, ss, c4 & 1);
-                } else {
+                } else if (!HEAD || dst.ptr) {      // the fused head may skip its activation (dst null)
                     am = max(am, absbits4(o));
                     *reinterpret_cast<f32x4*>(drow + (size_t)xp * C) = o;
                     if (psrow) store_presplit(psrow + (size_t)xp * C, o, ss, c4 & 1);
@@ -463,18 +465,32 @@ __global__ void __launch_bounds__(NT) in_bwd_stats_u_kernel(fg_view g, int fp, f
     const int gi = threadIdx.x / L, c4 = threadIdx.x - (threadIdx.x / L) * L;
     __shared__ float red[NT][12];    // fp32 per-thread sums (exact as floats), combined in fp64: 12 KB, not 24
     f32x4 sg = {0.f, 0.f, 0.f, 0.f}, sgx = sg, sx = sg;
+    // HEAD with wslab: the 1x1 head's weight / bias gradient, sum_p g_logits[p][o] * act(xhat[p][c]) and
+    // sum_p g_logits[p][o], from the operands this pass holds anyway (the activation is recomputed from src, so the
+    // forward need not write it)
+    const bool wg = HEAD && hd.wslab;
+    f32x4 wacc[HEAD ? HEAD_NB : 1];
+    float bacc[HEAD ? HEAD_NB : 1];
+#pragma unroll
+    for (int o = 0; o < (HEAD ? HEAD_NB : 1); ++o) {
+        wacc[o] = f32x4{0.f, 0.f, 0.f, 0.f};
+        bacc[o] = 0.f;
+    }
+    // (the head variant keeps 2 pixels in flight per thread, not kRowU: its logits-gradient quads, weights and
+    // weight-gradient accumulators would otherwise push it past 256 VGPRs, one wave per SIMD)
+    constexpr int RU = HEAD ? 2 : kRowU;
     if (gi < PG) {
         const f32x4 m = ld4(mean + (size_t)n * C + 4 * c4);
         const f32x4 r = ld4(rstd + (size_t)n * C + 4 * c4);
         f32x4 wr[HEAD ? HEAD_NB : 1];
         if constexpr (HEAD) head_weights(hd, c4, wr);
         int y = (p0 + gi) / w, x = (p0 + gi) - ((p0 + gi) / w) * w;
-        for (int p = p0 + gi; p < p1; p += kRowU * PG) {
-            int ys[kRowU], xs[kRowU];
-            f32x4 sv[kRowU], gv[kRowU], av[kRowU];
-            HeadG hg[HEAD ? kRowU : 1];
+        for (int p = p0 + gi; p < p1; p += RU * PG) {
+            int ys[RU], xs[RU];
+            f32x4 sv[RU], gv[RU], av[RU];
+            HeadG hg[HEAD ? RU : 1];
 #pragma unroll
-            for (int k = 0; k < kRowU; ++k) {
+            for (int k = 0; k < RU; ++k) {
                 ys[k] = y;
                 xs[k] = x;
                 const bool ok = p + k * PG < p1;
@@ -493,7 +509,7 @@ __global__ void __launch_bounds__(NT) in_bwd_stats_u_kernel(fg_view g, int fp, f
                 }
             }
 #pragma unroll
-            for (int k = 0; k < kRowU; ++k) {
+            for (int k = 0; k < RU; ++k) {
                 if (p + k * PG >= p1) break;
                 if constexpr (HEAD) gv[k] = head_grad(hg[k], wr, hd.n_out);
                 f32x4 gk = gv[k];
@@ -501,6 +517,21 @@ __global__ void __launch_bounds__(NT) in_bwd_stats_u_kernel(fg_view g, int fp, f
                 gk += av[k];
                 if (gsum.ptr) *reinterpret_cast<f32x4*>(gsum.ptr + fg::vidx(gsum, n, ys[k], xs[k]) + 4 * c4) = gk;
                 const f32x4 xh = (sv[k] - m) * r;
+                if constexpr (HEAD) {
+                    if (wg) {
+                        f32x4 a;
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) a[e] = fg::act_fwd(xh[e], act);
+#pragma unroll
+                        for (int o = 0; o < HEAD_NB; ++o)
+                            if (o < hd.n_out) {
+                                const float go = hg[k].q[o / 4][o % 4];
+#pragma unroll
+                                for (int e = 0; e < 4; ++e) wacc[o][e] = fmaf(go, a[e], wacc[o][e]);
+                                bacc[o] += go;
+                            }
+                    }
+                }
 #pragma unroll
                 for (int e = 0; e < 4; ++e) gk[e] *= fg::act_grad(xh[e], act);
                 gm = max(gm, absbits4(gk));
@@ -539,6 +570,51 @@ __global__ void __launch_bounds__(NT) in_bwd_stats_u_kernel(fg_view g, int fp, f
             wk[3 * e] = a[e];
             wk[3 * e + 1] = a[4 + e];
             wk[3 * e + 2] = a[8 + e];
+        }
+    }
+    if constexpr (HEAD) {
+        if (wg) {
+            // the block's partial: over the 4 pixel groups of a wave (lanes l, l^16, l^32, l^48: same c4), then over
+            // the 4 waves in LDS; slab row o of block (n, chunk): 64 weight columns, then the bias
+            constexpr int NV = HEAD_NB * 5;          // 48 weight + 12 bias values per c4
+            __shared__ float wred[NT / 64][16][NV];
+            const int wave = threadIdx.x >> 6;
+#pragma unroll
+            for (int o = 0; o < HEAD_NB; ++o) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    float v = wacc[o][e];
+                    v += __shfl_xor(v, 16);
+                    v += __shfl_xor(v, 32);
+                    wacc[o][e] = v;
+                }
+                float bv = bacc[o];
+                bv += __shfl_xor(bv, 16);
+                bv += __shfl_xor(bv, 32);
+                bacc[o] = bv;
+            }
+            if ((threadIdx.x & 63) < 16) {
+#pragma unroll
+                for (int o = 0; o < HEAD_NB; ++o) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) wred[wave][c4][o * 4 + e] = wacc[o][e];
+                    wred[wave][c4][HEAD_NB * 4 + o] = bacc[o];
+                }
+            }
+            __syncthreads();
+            float* slab = hd.wslab + (size_t)(n * chunks + chunk) * hd.n_out * (HEAD_CI + 1);
+            for (int i = threadIdx.x; i < 16 * NV; i += NT) {
+                const int q = i / NV, j = i - q * NV;
+                float v = 0.f;
+#pragma unroll
+                for (int wv = 0; wv < NT / 64; ++wv) v += wred[wv][q][j];
+                if (j < HEAD_NB * 4) {
+                    const int o = j >> 2;
+                    if (o < hd.n_out) slab[o * (HEAD_CI + 1) + 4 * q + (j & 3)] = v;
+                } else if (q == 0 && j - HEAD_NB * 4 < hd.n_out) {
+                    slab[(j - HEAD_NB * 4) * (HEAD_CI + 1) + HEAD_CI] = v;
+                }
+            }
         }
     }
 }
@@ -1131,24 +1207,34 @@ FG_API int fg_in_apply_head(fg_view src, const float* mean, const float* rstd, i
         return fg::fail(FG_ERR_INVALID, "fg_in_apply_head: needs C 64, an unpadded dst, n_out <= 16 logits in a 16-B "
                                         "aligned unpadded view of the same grid (C=%d, pad %d, n_out %d, y.c_alloc %d)",
                         dst.c_alloc, dst.pad, n_out, y.c_alloc);
-    return in_apply_impl(src, mean, rstd, act, fg_view{nullptr, 0, 0, 0, 0, 0}, dst, pad_mode, absmax, nullptr, stream,
-                         nullptr, nullptr, nullptr, 0, &h);
+    return in_apply_impl(src, mean, rstd, act, fg_view{nullptr, 0, 0, 0, 0, 0}, dst, pad_mode, dst.ptr ? absmax : nullptr,
+                         nullptr, stream, nullptr, nullptr, nullptr, 0, &h);
+}
+
+FG_API int fg_in_head_wgrad_workspace_floats(int n, int h, int w, int n_out) {
+    return choose_chunks(n, (long long)h * w) * n * n_out * (HEAD_CI + 1);
 }
 
 FG_API int fg_in_bwd_head(fg_view gy, const float* w, int n_out, fg_view src, const float* mean, const float* rstd,
                           int act, fg_view dst, float* bias_grad, int bias_accumulate, double* work, float* absmax,
-                          float* scale_slot, hipStream_t stream) {
-    const HeadArgs h{w, nullptr, n_out, gy};
+                          float* scale_slot, float* dw, float* db, int wg_accumulate, float* wg_work,
+                          hipStream_t stream) {
+    HeadArgs h{w, nullptr, n_out, gy};
     if (!head_ok(h, src) || gy.pad != 0 || gy.c_alloc < HEAD_NB ||
-        (scale_slot && (dst.c_alloc % 8 || ((uintptr_t)dst.ptr & 31))))
+        (scale_slot && (dst.c_alloc % 8 || ((uintptr_t)dst.ptr & 31))) || (dw && !wg_work))
         return fg::fail(FG_ERR_INVALID, "fg_in_bwd_head: needs C 64, n_out <= 16 logit gradients in a 16-B aligned "
-                                        "unpadded view of the same grid (C=%d, n_out %d, gy.c_alloc %d)", src.c_alloc,
-                        n_out, gy.c_alloc);
+                                        "unpadded view of the same grid, and a workspace with dw (C=%d, n_out %d, "
+                                        "gy.c_alloc %d)", src.c_alloc, n_out, gy.c_alloc);
+    if (dw) h.wslab = wg_work;
     // gsrc stands in for the 64-channel gradient the head replaces (its geometry is what the checks read)
     fg_view gs = src;
     gs.pad = 0;
-    return in_bwd_impl(gs, 0, fg_view{nullptr, 0, 0, 0, 0, 0}, src, mean, rstd, act, dst, bias_grad, bias_accumulate,
-                       fg_view{nullptr, 0, 0, 0, 0, 0}, work, scale_slot ? nullptr : absmax, scale_slot, stream, &h);
+    const int rc = in_bwd_impl(gs, 0, fg_view{nullptr, 0, 0, 0, 0, 0}, src, mean, rstd, act, dst, bias_grad,
+                               bias_accumulate, fg_view{nullptr, 0, 0, 0, 0, 0}, work, scale_slot ? nullptr : absmax,
+                               scale_slot, stream, &h);
+    if (rc || !dw) return rc;
+    return fg::conv1x1_wgrad_reduce_launch(wg_work, choose_chunks(src.n, (long long)src.h * src.w) * src.n, n_out, dw,
+                                           db, wg_accumulate, stream);
 }
 
 FG_API int fg_in_apply_splitpix(fg_view src, const float* mean, const float* rstd, int act, fg_view dst, int pad_mode,
@@ -1164,7 +1250,8 @@ namespace {
 int in_apply_impl(fg_view src, const float* mean, const float* rstd, int act, fg_view residual, fg_view dst,
                   int pad_mode, float* absmax, float* split_slot, hipStream_t stream, float* ps_ptr, float* ps_slot,
                   const float* res_amax, int splitpix, const HeadArgs* head) {
-    if (!ok_view(src) || !ok_view(dst) || !mean || !rstd || src.c_alloc % 4 || dst.c_alloc != src.c_alloc ||
+    const bool dst_ok = ok_view(dst) || (head && !dst.ptr && dst.n > 0 && dst.h > 0 && dst.w > 0 && dst.pad == 0);
+    if (!ok_view(src) || !dst_ok || !mean || !rstd || src.c_alloc % 4 || dst.c_alloc != src.c_alloc ||
         dst.h != src.h || dst.w != src.w || dst.n != src.n)
         return fg::fail(FG_ERR_INVALID, "fg_in_apply: bad args");
     if (residual.ptr && (residual.c_alloc != src.c_alloc || residual.h != src.h || residual.w != src.w))

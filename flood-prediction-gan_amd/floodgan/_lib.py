@@ -149,7 +149,9 @@ SIGNATURES = {
     "fg_in_apply_head": [fg_view, C.c_void_p, C.c_void_p, C.c_int, fg_view, C.c_int, C.c_void_p, C.c_void_p,
                          C.c_void_p, C.c_int, fg_view, C.c_void_p],
     "fg_in_bwd_head": [fg_view, C.c_void_p, C.c_int, fg_view, C.c_void_p, C.c_void_p, C.c_int, fg_view, C.c_void_p,
-                       C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p],
+                       C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p,
+                       C.c_void_p],
+    "fg_in_head_wgrad_workspace_floats": [C.c_int, C.c_int, C.c_int, C.c_int],
     "fg_in_bwd_presplit": [fg_view, C.c_int, fg_view, fg_view, C.c_void_p, C.c_void_p, C.c_int, fg_view, C.c_void_p,
                            C.c_int, fg_view, C.c_void_p, C.c_void_p, C.c_void_p],
     "fg_act_bwd": [fg_view, fg_view, C.c_int, C.c_void_p, C.c_void_p],

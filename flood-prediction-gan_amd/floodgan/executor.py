@@ -210,11 +210,12 @@ def gen_forward(P, x, save=True, x_extra=None):
         # (when the window kernels take the head: output rows of >= 256 px, a multiple of 32; ops.win_eligible)
         spx = tag == "content" and ps and SPLITPIX and ops.USE_WIN and W >= 256 and W % 32 == 0
         if tag == "attention" and HEAD_1X1 and FUSED_HEAD:
-            # relu(IN(d2)) and the 1x1 head's logits in one pass (fg_in_apply_head)
+            # the 1x1 head's logits from relu(IN(d2)) in the norm pass (fg_in_apply_head); the activation itself is
+            # not written: the head's backward recomputes it from d2 for the weight gradient (round 5)
             md2, rd2 = st if st is not None else ops.in_stats(d2)
-            ad2 = Buf.empty(N, H, W, 64, 0, dev)
+            ad2 = None
             al = Buf.empty(N, H, W, ATT_ALLOC, 0, dev)
-            ops.in_apply_head(d2, md2, rd2, FG_ACT_RELU, ad2, FG_PAD_ZERO, P["deconv3_attention.weight"],
+            ops.in_apply_head(d2, md2, rd2, FG_ACT_RELU, None, FG_PAD_ZERO, P["deconv3_attention.weight"],
                               P["deconv3_attention.bias"], N_ATT, al)
         else:
             md2, rd2, ad2 = _norm(d2, FG_ACT_RELU, pad2, mode2, stats=st, splitpix=spx)
@@ -426,12 +427,13 @@ def gen_backward(P, S, g_out, grads_into=None, ready=None, input_grad=None, accu
     if attention:
         # ---- deconv3_attention: 1x1
         g_ad2a = None if HEAD_1X1 and FUSED_HEAD else Buf.empty(N, H, W, 64, 0, dev)
-        if HEAD_1X1:
+        if HEAD_1X1 and g_ad2a is not None:
             names = ("deconv3_attention.weight", "deconv3_attention.bias")
             G.off_path(lambda: ops.conv1x1_wgrad(gal, ha["ad2"], N_ATT, G.get(names[0]), G.get(names[1]), G.acc),
                        (gal, ha["ad2"]), names)
-            if g_ad2a is not None:
-                ops.conv1x1_dgrad(gal, P["deconv3_attention.weight"], N_ATT, g_ad2a)
+            ops.conv1x1_dgrad(gal, P["deconv3_attention.weight"], N_ATT, g_ad2a)
+        elif HEAD_1X1:
+            pass                   # the fused head: weight, bias and input gradients in its norm backward below
         else:
             _wgrad_conv(P, G, "deconv3_attention", gal, ha["ad2"], 0, 1, 1)
             ops.channel_sum(gal, 10, G.get("deconv3_attention.bias"), G.acc)
@@ -442,9 +444,11 @@ def gen_backward(P, S, g_out, grads_into=None, ready=None, input_grad=None, accu
     ps = ops.presplit_on()     # conv-output gradients read only by pipelined convs / weight gradients
     for idx, (tag, hd, g_ad2, fold) in enumerate(heads):
         g_d2 = Buf.empty(N, H, W, 64, 1, dev)
-        if g_ad2 is None:        # the fused head: the input gradient w^T gal formed inside the norm passes
+        if g_ad2 is None:        # the fused head: the input gradient w^T gal formed inside the norm passes, the head's
+            # weight / bias gradients from the activation recomputed in the statistics pass
             ops.in_bwd_head(gal, P["deconv3_attention.weight"], N_ATT, hd["d2"], hd["md2"], hd["rd2"], FG_ACT_RELU,
-                            g_d2, G.get(f"deconv2_{tag}.bias"), G.acc, presplit=ps)
+                            g_d2, G.get(f"deconv2_{tag}.bias"), G.acc, presplit=ps,
+                            wgrad=(G.get("deconv3_attention.weight"), G.get("deconv3_attention.bias"), G.acc))
         else:
             ops.in_bwd(g_ad2, fold, None, hd["d2"], hd["md2"], hd["rd2"], FG_ACT_RELU, g_d2,
                        G.get(f"deconv2_{tag}.bias"), G.acc, presplit=ps)
@@ -503,7 +507,7 @@ def _decided(B, lo=0, hi=None, pre=None, mean=None):
     LeakyReLU): NCHW bool on the host.  A pre-split output (FG_PRESPLIT) is decided from the norm's input
     `pre` and `mean` instead: act((c - mean) * rstd) > 0 <=> c > mean (rstd > 0; fp32 subtraction keeps the
     sign)."""
-    if ops.is_presplit(B) or ops.is_splitpix(B):
+    if B is None or ops.is_presplit(B) or ops.is_splitpix(B):     # (None: the fused head's unwritten activation)
         d = pre.interior() > mean.view(pre.n, 1, 1, pre.c)
         return d[lo:hi].permute(0, 3, 1, 2).contiguous().cpu()
     return (B.interior()[lo:hi] > 0).permute(0, 3, 1, 2).contiguous().cpu()

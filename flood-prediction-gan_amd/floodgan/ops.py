@@ -809,29 +809,46 @@ def in_bwd(gsrc, fold_pad, gadd, src, mean, rstd, act, dst, bias_grad=None, bias
 
 def in_apply_head(src, mean, rstd, act, dst, pad_mode, w, b, n_out, Y):
     """fg_in_apply_head: dst = act(IN(src)) (fp32, unpadded; absmax slot raised) AND the attention head's 1x1 logits
-    Y[..., :n_out] = w dst + b (Y's other channels 0), bit-identical to in_apply + conv1x1_fwd"""
-    _wrote(dst, Y)
-    L.check(_lib().fg_in_apply_head(view(src), L.ptr(mean), L.ptr(rstd), act, view(dst), pad_mode,
-                                    L.ptr(_amax_out(dst)), L.ptr(w.contiguous()), L.ptr(b), n_out, view(Y),
-                                    L.stream_handle()), "in_apply_head")
+    Y[..., :n_out] = w dst + b (Y's other channels 0), bit-identical to in_apply + conv1x1_fwd.  dst None: only the
+    logits (the fused backward, in_bwd_head with wgrad, recomputes the activation)"""
+    if dst is None:
+        _wrote(Y)
+        dv = L.fg_view(None, src.n, src.h, src.w, src.c, 0)
+        amax = None
+    else:
+        _wrote(dst, Y)
+        dv, amax = view(dst), L.ptr(_amax_out(dst))
+    L.check(_lib().fg_in_apply_head(view(src), L.ptr(mean), L.ptr(rstd), act, dv, pad_mode, amax,
+                                    L.ptr(w.contiguous()), L.ptr(b), n_out, view(Y), L.stream_handle()),
+            "in_apply_head")
 
 
-def in_bwd_head(GY, w, n_out, src, mean, rstd, act, dst, bias_grad=None, bias_accumulate=False, presplit=False):
+def in_bwd_head(GY, w, n_out, src, mean, rstd, act, dst, bias_grad=None, bias_accumulate=False, presplit=False,
+                wgrad=None):
     """fg_in_bwd_head: the norm backward of the attention head's input with the incoming gradient w^T GY formed from
-    the logits gradient GY in registers (bit-identical to conv1x1_dgrad + in_bwd; no 64-channel gradient buffer)"""
+    the logits gradient GY in registers (bit-identical to conv1x1_dgrad + in_bwd; no 64-channel gradient buffer).
+    wgrad = (dw, db, accumulate): also the head's weight / bias gradients (the replaced conv1x1_wgrad), from the
+    activation recomputed inside the statistics pass"""
     work = _work(src.n, src.c, src.t.device)
+    dw = db = wg_work = None
+    acc = 0
+    if wgrad is not None:
+        dw, db, acc = wgrad
+        nf = int(_lib().fg_in_head_wgrad_workspace_floats(src.n, src.h, src.w, n_out))
+        wg_work = torch.empty(nf, dtype=torch.float32, device=src.t.device)
+    tail = (L.ptr(dw), L.ptr(db), int(acc), L.ptr(wg_work), L.stream_handle())
     if presplit and presplit_fits(dst):
         assert L.fwd_f16x3()
         slot = _amax_out(dst)
         L.check(_lib().fg_in_bwd_head(view(GY), L.ptr(w.contiguous()), n_out, view(src), L.ptr(mean), L.ptr(rstd), act,
                                       view(dst), L.ptr(bias_grad), int(bias_accumulate), L.ptr(work), None, L.ptr(slot),
-                                      L.stream_handle()), "in_bwd_head")
+                                      *tail), "in_bwd_head")
         _mark_presplit(dst)
         return
     _wrote(dst)
     L.check(_lib().fg_in_bwd_head(view(GY), L.ptr(w.contiguous()), n_out, view(src), L.ptr(mean), L.ptr(rstd), act,
                                   view(dst), L.ptr(bias_grad), int(bias_accumulate), L.ptr(work),
-                                  L.ptr(_amax_out(dst)), None, L.stream_handle()), "in_bwd_head")
+                                  L.ptr(_amax_out(dst)), None, *tail), "in_bwd_head")
 
 
 def act_bwd(g, y, act, border_zero=False):

@@ -428,12 +428,17 @@ int fg_in_bwd_presplit(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, co
  * fg_in_bwd_head: fg_in_bwd of the head's input whose incoming gradient is w^T gy, formed from the logits
  * gradient gy (unpadded, n_out <= 12, 12 <= c_alloc <= 16: three 16-B quads are read per pixel) in
  * fg_conv1x1_dgrad's fma order (bit-identical to running it first); scale_slot non-NULL: dst in the FG_PRESPLIT
- * format as fg_in_bwd_presplit (absmax ignored). */
+ * format as fg_in_bwd_presplit (absmax ignored).
+ * Round 5: fg_in_apply_head takes a dst with a NULL ptr (its geometry only): the activation is then not written,
+ * only the logits.  fg_in_bwd_head with dw non-NULL also forms the head's weight gradient dw[o][c] (+)= sum_p
+ * gy[p][o] act(xhat[p][c]) and db[o] (+)= sum_p gy[p][o] (the replaced fg_conv1x1_wgrad; wg_accumulate adds),
+ * recomputing the activation from src; wg_work holds fg_in_head_wgrad_workspace_floats(n, h, w, n_out) floats. */
 int fg_in_apply_head(fg_view src, const float* mean, const float* rstd, int act, fg_view dst, int pad_mode,
                      float* absmax, const float* w, const float* b, int n_out, fg_view y, hipStream_t stream);
+int fg_in_head_wgrad_workspace_floats(int n, int h, int w, int n_out);
 int fg_in_bwd_head(fg_view gy, const float* w, int n_out, fg_view src, const float* mean, const float* rstd,
                    int act, fg_view dst, float* bias_grad, int bias_accumulate, double* work, float* absmax,
-                   float* scale_slot, hipStream_t stream);
+                   float* scale_slot, float* dw, float* db, int wg_accumulate, float* wg_work, hipStream_t stream);
 
 
 /* g *= act'(y) in place over the interior (y = saved activation output).  absmax (optional absmax slot,

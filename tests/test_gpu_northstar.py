@@ -626,11 +626,13 @@ def test_f16x3_dynamic_range(case, report):
         assert a < max(KTOL, 4 * b), res
 
 
-def test_fused_attention_head_bit_identical(report):
+def test_fused_attention_head(report):
     """The attention head's 1x1 conv fused into its input's norm passes (fg_in_apply_head: the logits formed by the
-    apply pass; fg_in_bwd_head: the 64-channel input gradient w^T g_logits formed inside the norm backward) against the
-    separate conv1x1 forward / input-gradient kernels: two training iterations of the fused step (64x64, batch 2) give
-    bit-identical losses, G / D parameters and attention masks."""
+    apply pass, the activation not written; fg_in_bwd_head: the 64-channel input gradient w^T g_logits formed inside
+    the norm backward, and the head's weight / bias gradients from the activation recomputed in its statistics pass)
+    against the separate conv1x1 forward / input-gradient / weight-gradient kernels, one iteration of the fused step
+    (64x64, batch 2) from the same weights: bit-identical losses, attention mask and every gradient except the head's
+    own weight and bias (a different summation order: within 1e-6)."""
     from floodgan import executor as X
     x, y = _inputs(2, res=64, seed=11)
     out = []
@@ -639,17 +641,21 @@ def test_fused_attention_head_bit_identical(report):
         for fused in (False, True):
             X.FUSED_HEAD = fused
             m = _model()
-            ls = [m.step_fn(x.to(DEV), y.to(DEV)).cpu() for _ in range(2)]
+            ls = m.step_fn(x.to(DEV), y.to(DEV)).cpu()
             torch.cuda.synchronize()
-            out.append((torch.stack(ls), [p.detach().cpu().clone() for p in m.generator.parameters()],
-                        [p.detach().cpu().clone() for p in m.discriminator.parameters()],
+            out.append((ls, {k: p.grad.detach().cpu().clone() for k, p in m.generator.named_parameters()},
+                        {k: p.grad.detach().cpu().clone() for k, p in m.discriminator.named_parameters()},
                         m.step_fn.last_mask.detach().cpu().clone()))
     finally:
         X.FUSED_HEAD = prev
+    head = {"deconv3_attention.weight", "deconv3_attention.bias"}
     assert torch.equal(out[0][0], out[1][0]), (out[0][0], out[1][0])
-    assert all(torch.equal(a, b) for a, b in zip(out[0][1], out[1][1]))
-    assert all(torch.equal(a, b) for a, b in zip(out[0][2], out[1][2]))
     assert torch.equal(out[0][3], out[1][3])
+    assert all(torch.equal(out[0][1][k], out[1][1][k]) for k in out[0][1] if k not in head)
+    assert all(torch.equal(out[0][2][k], out[1][2][k]) for k in out[0][2])
+    errs = {k: nrel(out[1][1][k], out[0][1][k]) for k in head}
+    report("fused_attention_head", head_grad_rel=errs)
+    assert max(errs.values()) < 1e-6, errs
 
 
 def test_fused_step_deterministic():
