@@ -38,6 +38,9 @@ int choose_chunks(int n, long long hw, int target = 2048) {
     if (c < 1) c = 1;
     return (int)c;
 }
+// the fused attention head's statistics pass (2 waves per SIMD at its register count): 512 workgroups are one
+// resident round, and its weight-gradient slab (one row per workgroup) stays 4x smaller for the reduction
+int head_chunks(int n, long long hw) { return choose_chunks(n, hw, 512); }
 
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 // non-temporal (streaming) load: for bytes read for the last time, so they do not displace reused ones from the
@@ -476,9 +479,9 @@ __global__ void __launch_bounds__(NT) in_bwd_stats_u_kernel(fg_view g, int fp, f
         wacc[o] = f32x4{0.f, 0.f, 0.f, 0.f};
         bacc[o] = 0.f;
     }
-    // (the head variant keeps 2 pixels in flight per thread, not kRowU: its logits-gradient quads, weights and
+    // (the head variant keeps 3 pixels in flight per thread, not kRowU: its logits-gradient quads, weights and
     // weight-gradient accumulators would otherwise push it past 256 VGPRs, one wave per SIMD)
-    constexpr int RU = HEAD ? 2 : kRowU;
+    constexpr int RU = HEAD ? 3 : kRowU;
     if (gi < PG) {
         const f32x4 m = ld4(mean + (size_t)n * C + 4 * c4);
         const f32x4 r = ld4(rstd + (size_t)n * C + 4 * c4);
@@ -1212,7 +1215,7 @@ FG_API int fg_in_apply_head(fg_view src, const float* mean, const float* rstd, i
 }
 
 FG_API int fg_in_head_wgrad_workspace_floats(int n, int h, int w, int n_out) {
-    return choose_chunks(n, (long long)h * w) * n * n_out * (HEAD_CI + 1);
+    return head_chunks(n, (long long)h * w) * n * n_out * (HEAD_CI + 1);
 }
 
 FG_API int fg_in_bwd_head(fg_view gy, const float* w, int n_out, fg_view src, const float* mean, const float* rstd,
@@ -1233,7 +1236,7 @@ FG_API int fg_in_bwd_head(fg_view gy, const float* w, int n_out, fg_view src, co
                                bias_accumulate, fg_view{nullptr, 0, 0, 0, 0, 0}, work, scale_slot ? nullptr : absmax,
                                scale_slot, stream, &h);
     if (rc || !dw) return rc;
-    return fg::conv1x1_wgrad_reduce_launch(wg_work, choose_chunks(src.n, (long long)src.h * src.w) * src.n, n_out, dw,
+    return fg::conv1x1_wgrad_reduce_launch(wg_work, head_chunks(src.n, (long long)src.h * src.w) * src.n, n_out, dw,
                                            db, wg_accumulate, stream);
 }
 
@@ -1315,7 +1318,7 @@ int in_bwd_impl(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, const flo
         return fg::fail(FG_ERR_INVALID, "fg_in_bwd: gsum shape");
     // ~2048 workgroups (measured against 1024 / 512 / 256 / 128 at bs 8: 512 within noise, fewer slower,
     // profiles/round3/r3ai_bwd_wg.log)
-    const int chunks = choose_chunks(src.n, (long long)src.h * src.w);
+    const int chunks = head ? head_chunks(src.n, (long long)src.h * src.w) : choose_chunks(src.n, (long long)src.h * src.w);
     const int C = src.c_alloc;
     float* coef = reinterpret_cast<float*>(work + (size_t)src.n * C * MAX_CHUNKS * 3);
     double* bpart = work + (size_t)src.n * C * MAX_CHUNKS * 3 + (size_t)src.n * C;
