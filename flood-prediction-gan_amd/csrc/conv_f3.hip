@@ -99,6 +99,77 @@ __device__ __forceinline__ void wait_vmcnt() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// vmcnt(min(n, 63)) for a run-time n (the deep rings of NS > 3: a jump table, a few scalar instructions per stage)
+__device__ __forceinline__ void wait_vmcnt_rt(int n) {
+    switch (n < 63 ? n : 63) {
+        case 0: wait_vmcnt<0>(); break;
+        case 1: wait_vmcnt<1>(); break;
+        case 2: wait_vmcnt<2>(); break;
+        case 3: wait_vmcnt<3>(); break;
+        case 4: wait_vmcnt<4>(); break;
+        case 5: wait_vmcnt<5>(); break;
+        case 6: wait_vmcnt<6>(); break;
+        case 7: wait_vmcnt<7>(); break;
+        case 8: wait_vmcnt<8>(); break;
+        case 9: wait_vmcnt<9>(); break;
+        case 10: wait_vmcnt<10>(); break;
+        case 11: wait_vmcnt<11>(); break;
+        case 12: wait_vmcnt<12>(); break;
+        case 13: wait_vmcnt<13>(); break;
+        case 14: wait_vmcnt<14>(); break;
+        case 15: wait_vmcnt<15>(); break;
+        case 16: wait_vmcnt<16>(); break;
+        case 17: wait_vmcnt<17>(); break;
+        case 18: wait_vmcnt<18>(); break;
+        case 19: wait_vmcnt<19>(); break;
+        case 20: wait_vmcnt<20>(); break;
+        case 21: wait_vmcnt<21>(); break;
+        case 22: wait_vmcnt<22>(); break;
+        case 23: wait_vmcnt<23>(); break;
+        case 24: wait_vmcnt<24>(); break;
+        case 25: wait_vmcnt<25>(); break;
+        case 26: wait_vmcnt<26>(); break;
+        case 27: wait_vmcnt<27>(); break;
+        case 28: wait_vmcnt<28>(); break;
+        case 29: wait_vmcnt<29>(); break;
+        case 30: wait_vmcnt<30>(); break;
+        case 31: wait_vmcnt<31>(); break;
+        case 32: wait_vmcnt<32>(); break;
+        case 33: wait_vmcnt<33>(); break;
+        case 34: wait_vmcnt<34>(); break;
+        case 35: wait_vmcnt<35>(); break;
+        case 36: wait_vmcnt<36>(); break;
+        case 37: wait_vmcnt<37>(); break;
+        case 38: wait_vmcnt<38>(); break;
+        case 39: wait_vmcnt<39>(); break;
+        case 40: wait_vmcnt<40>(); break;
+        case 41: wait_vmcnt<41>(); break;
+        case 42: wait_vmcnt<42>(); break;
+        case 43: wait_vmcnt<43>(); break;
+        case 44: wait_vmcnt<44>(); break;
+        case 45: wait_vmcnt<45>(); break;
+        case 46: wait_vmcnt<46>(); break;
+        case 47: wait_vmcnt<47>(); break;
+        case 48: wait_vmcnt<48>(); break;
+        case 49: wait_vmcnt<49>(); break;
+        case 50: wait_vmcnt<50>(); break;
+        case 51: wait_vmcnt<51>(); break;
+        case 52: wait_vmcnt<52>(); break;
+        case 53: wait_vmcnt<53>(); break;
+        case 54: wait_vmcnt<54>(); break;
+        case 55: wait_vmcnt<55>(); break;
+        case 56: wait_vmcnt<56>(); break;
+        case 57: wait_vmcnt<57>(); break;
+        case 58: wait_vmcnt<58>(); break;
+        case 59: wait_vmcnt<59>(); break;
+        case 60: wait_vmcnt<60>(); break;
+        case 61: wait_vmcnt<61>(); break;
+        case 62: wait_vmcnt<62>(); break;
+        case 63: wait_vmcnt<63>(); break;
+        default: wait_vmcnt<63>(); break;
+    }
+}
+
 // SCH selects the per-stage instruction order: 0 = read+split all of A, then the three products
 // per column group smallest first; 1 = the A reads are issued before the next stage's DMA (their
 // LDS latency hides behind the DMA issue) and each column group's products run hh, hl, lh, so the
@@ -611,7 +682,7 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
     // ---- NS-deep ring over the stage stream: stage s+NS-1 is issued right after the barrier that
     // retires stage s-1's reads; before it, this wave waits for its own DMAs of stage s (counted
     // vmcnt: the younger NS-2 stages stay in flight) and the barrier makes everyone's visible
-    static_assert(NS == 2 || NS == 3, "ring depth");
+    static_assert(NS >= 2 && NS <= 6, "ring depth");
     if (first >= total_tiles) return;
     setup_issue();
     setup_compute();
@@ -628,6 +699,10 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
     constexpr int D = A_GL + B_GL;
     auto wait_stage = [&]() {
         const int younger = (issued - done - 1) * D + (done < epi_issued ? epi_nst : 0);
+        if constexpr (NS > 3) {            // the latency-bound small launches' deep ring: the exact count
+            wait_vmcnt_rt(younger);
+            return;
+        }
         if (NS == 3 && younger >= NSTS + 2 * D) wait_vmcnt<cap63(NSTS + 2 * D)>();
         else if (younger >= NSTS + D) wait_vmcnt<cap63(NSTS + D)>();
         else if (younger >= NSTS) wait_vmcnt<cap63(NSTS)>();
@@ -923,7 +998,7 @@ int launch_fwd_f3(const ConvBatch& b, int nprob, int max_n, hipStream_t stream, 
         case 6: *rc = launch_cfg<256, 128, 32, 128, 2>(b, nprob, stream); return 1;
         case 7: *rc = launch_cfg<256, 64, 32, 64, 3>(b, nprob, stream); return 1;
         case 8: *rc = launch_cfg<256, 64, 64, 64, 3>(b, nprob, stream); return 1;
-        case 9: *rc = launch_cfg<128, 64, 32, 64, 3>(b, nprob, stream); return 1;
+        case 9: *rc = launch_cfg<128, 64, 32, 64, 6>(b, nprob, stream); return 1;
         case 10: *rc = launch_cfg<512, 64, 64, 64, 2>(b, nprob, stream); return 1;
         case 11: *rc = launch_cfg<256, 128, 64, 64, 3>(b, nprob, stream); return 1;
         default: return 0;
