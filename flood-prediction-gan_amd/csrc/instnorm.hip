@@ -1110,6 +1110,47 @@ __global__ void in_partials_finalize(const double* __restrict__ work, int nprob,
     }
 }
 
+// one launch for short partial lists (K = nprob * rb_per_img <= kPartialsDirectK: the resblock convs' 512 blocks
+// per image): block = (image, 16 channels), thread = (channel, one of 16 slices of the 32-row blocks), the slices
+// summed in LDS and finalized in the same block -- the two launches above cost ~13 us where this one streams its
+// 64 KB per block
+constexpr int kPartialsDirectK = 2048;
+__global__ void in_partials_direct(const float* __restrict__ part, int nprob, int n_img, int rb_per_img, int c,
+                                   float eps, float* __restrict__ mean, float* __restrict__ rstd) {
+    const int img = blockIdx.x, cl = threadIdx.x & 15, sl = threadIdx.x >> 4;
+    const int ch = blockIdx.y * 16 + cl;
+    const size_t prob_stride = (size_t)n_img * rb_per_img * c * 2;
+    double s1 = 0, s2 = 0;
+    if (ch < c) {
+        for (int pr = 0; pr < nprob; ++pr) {
+            const float* base = part + pr * prob_stride + ((size_t)img * rb_per_img * c + ch) * 2;
+#pragma unroll 8
+            for (int rb = sl; rb < rb_per_img; rb += 16) {
+                const f32x2 q = *reinterpret_cast<const f32x2*>(base + (size_t)rb * c * 2);
+                const double m = q[0];
+                s1 += 32.0 * m;
+                s2 += (double)q[1] + 32.0 * m * m;
+            }
+        }
+    }
+    __shared__ double red[256][2];
+    red[threadIdx.x][0] = s1;
+    red[threadIdx.x][1] = s2;
+    __syncthreads();
+    if (sl == 0 && ch < c) {
+        for (int q = 1; q < 16; ++q) {
+            s1 += red[q * 16 + cl][0];
+            s2 += red[q * 16 + cl][1];
+        }
+        const double n = 32.0 * nprob * rb_per_img;
+        const double mu = s1 / n;
+        double var = s2 / n - mu * mu;
+        if (var < 0) var = 0;
+        mean[img * c + ch] = (float)mu;
+        rstd[img * c + ch] = (float)(1.0 / sqrt(var + (double)eps));
+    }
+}
+
 }  // namespace
 
 FG_API long long fg_in_partials_workspace_doubles(int n_img, int c) {
@@ -1121,6 +1162,11 @@ FG_API int fg_in_stats_partials(const float* partials, int nprob, int n_img, int
     if (!partials || !mean || !rstd || !work || nprob < 1 || nprob > 4 || n_img < 1 || rb_per_img < 1 || c < 1)
         return fg::fail(FG_ERR_INVALID, "fg_in_stats_partials: bad args");
     const int cg = (c + 63) / 64, K = nprob * rb_per_img;
+    if (K <= kPartialsDirectK) {
+        hipLaunchKernelGGL(in_partials_direct, dim3(n_img, (c + 15) / 16), dim3(256), 0, stream, partials, nprob, n_img,
+                           rb_per_img, c, eps, mean, rstd);
+        return fg::launched("in_stats_partials");
+    }
     // ~1024 blocks over the chip, each thread at least ~4 of the image's 32-row blocks
     const int splits = std::max(1, std::min({kPartialSplitsMax, (1024 + n_img * cg - 1) / (n_img * cg), K / 16}));
     hipLaunchKernelGGL(in_partials_reduce, dim3(n_img, cg, splits), dim3(256), 0, stream, partials, nprob, n_img,
