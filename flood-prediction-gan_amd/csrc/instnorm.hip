@@ -42,6 +42,7 @@ int choose_chunks(int n, long long hw, int target = 2048) {
 // resident round, and its weight-gradient slab (one row per workgroup) stays 4x smaller for the reduction
 int head_chunks(int n, long long hw) { return choose_chunks(n, hw, 512); }
 
+
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 // non-temporal (streaming) load: for bytes read for the last time, so they do not displace reused ones from the
 // Infinity Cache
@@ -1363,7 +1364,8 @@ int in_bwd_impl(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, const flo
     if (gsum.ptr && (gsum.c_alloc != src.c_alloc || gsum.h != src.h || gsum.w != src.w || gsum.n != src.n))
         return fg::fail(FG_ERR_INVALID, "fg_in_bwd: gsum shape");
     // ~2048 workgroups (measured against 1024 / 512 / 256 / 128 at bs 8: 512 within noise, fewer slower,
-    // profiles/round3/r3ai_bwd_wg.log)
+    // profiles/round3/r3ai_bwd_wg.log; round 5, interleaved in one process: 512 for a 4x smaller finalize read is
+    // 0.12 ms slower per step, profiles/round5/r5n_ab_in_bwd_wg_not_kept.log)
     const int chunks = head ? head_chunks(src.n, (long long)src.h * src.w) : choose_chunks(src.n, (long long)src.h * src.w);
     const int C = src.c_alloc;
     float* coef = reinterpret_cast<float*>(work + (size_t)src.n * C * MAX_CHUNKS * 3);
