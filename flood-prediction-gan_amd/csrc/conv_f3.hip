@@ -713,6 +713,12 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
         else if (younger >= D) wait_vmcnt<cap63(D)>();
         else wait_vmcnt<0>();
     };
+    // order bit 3 (SCH >= 3): at a tile boundary the ring slot just computed is refilled BEFORE the epilogue's
+    // stores (after a barrier: every wave is done reading it), and the next stage issues nothing.  vmcnt retires
+    // in issue order, so the stage waits then reach the stores one stage later: they drain under two stages of
+    // MFMAs instead of one (every CU finishes its tile at the same time and the write burst queues).
+    const bool pre_epi = SCH >= 3 && (alt_order & 8);
+    bool pre_issued = false;
     while (true) {
         wait_stage();
 #ifdef FG_F3_DIAG
@@ -736,9 +742,11 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
             compute(cur, va);
         } else if constexpr (SCH >= 3) {
             load_a(cur, va);
-            issue_prep(nxt);
+            if (pre_issued) p_on = false;
+            else issue_prep(nxt);
             compute(cur, va);
-            if (issue_advance()) ++issued;
+            if (!pre_issued && issue_advance()) ++issued;
+            pre_issued = false;
         } else {
             f16x8 bh[2][TG2], bl[2][TG2];
             load_a(cur, va);
@@ -750,6 +758,20 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
         cur = cur == NS - 1 ? 0 : cur + 1;
         nxt = nxt == NS - 1 ? 0 : nxt + 1;
         if (++ckt == cg.nkt) {
+            if constexpr (SCH >= 3) {
+                bool pre = pre_epi && it < total_tiles;
+#ifdef FG_F3_DIAG
+                pre = pre && !((alt_order >> 5) & 1);
+#endif
+                if (pre) {
+                    __builtin_amdgcn_s_barrier();
+                    issue_prep(nxt);
+#pragma unroll
+                    for (int i = 0; i < A_GL + B_GL; ++i) issue_piece(i);
+                    if (issue_advance()) ++issued;
+                    pre_issued = true;
+                }
+            }
 #ifdef FG_F3_DIAG
             if (!((alt_order >> 8) & 1))                 // diag bit 4: no epilogue (timing only)
 #endif
@@ -765,9 +787,10 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
     }
 }
 
-int g_f3_alt = 7;     // fg_set_f3_order: bit 0 alternates the kernel-row order of odd M tiles,
+int g_f3_alt = 15;    // fg_set_f3_order: bit 0 alternates the kernel-row order of odd M tiles,
                       // bit 1 walks k chunk-outer (taps of one channel chunk back to back),
-                      // bit 2 raises the priority of the second half of the waves
+                      // bit 2 raises the priority of the second half of the waves,
+                      // bit 3 refills the freed ring slot before a tile's epilogue stores
 int g_f3_persist = 1; // fg_set_f3_persistent: 1 resident workgroups loop over tiles, 0 one workgroup per
                       // tile, n >= 2 at most n workgroups (test hook: forces the tile-crossing stream
                       // -- setup_issue() mid-stream, next tile's stages in flight over an epilogue --
@@ -1026,7 +1049,7 @@ FG_API int fg_set_f3_sched(int sched) {
 }
 
 FG_API int fg_set_f3_order(int alt) {
-    if (alt < 0 || alt > 7) return fg::fail(FG_ERR_INVALID, "fg_set_f3_order: %d", alt);
+    if (alt < 0 || alt > 15) return fg::fail(FG_ERR_INVALID, "fg_set_f3_order: %d", alt);
     g_f3_alt = alt;
     return 0;
 }

@@ -196,12 +196,14 @@ int fg_set_fwd_tile(int cfg);
 /* Same for the split-math weight-gradient kernels (0..5). */
 int fg_set_wgrad_tile(int cfg);
 /* Tuning hook of the LDS-DMA pipelined f16x3 forward kernel (conv_f3.hip, used for N > 64 when
- * the operands allow): -1 automatic (default), -2 never use it, 0..9 force a tile config. */
+ * the operands allow): -1 automatic (default), -2 never use it, 0..11 force a tile config. */
 int fg_set_f3_tile(int cfg);
 /* Tuning hook, k-walk order of the pipelined forward kernel: bit 0 = odd M tiles walk the kernel
  * rows backwards (L2 sharing between neighbouring tiles); bit 1 = channel-chunk-outer walk (the
  * taps of one 32-channel chunk back to back, needs fg_conv_problem.jc); bit 2 = static priority
- * for the second half of the waves.  Default 7. */
+ * for the second half of the waves; bit 3 = at a tile boundary the freed LDS ring slot is refilled
+ * before the epilogue's stores (stage schedules 3-5), so the stores drain under two stages.
+ * Default 15. */
 int fg_set_f3_order(int alt);
 /* Tuning hook: per-stage instruction order of the pipelined forward kernel: 0 = split all of A,
  * then the products; 1 = A reads ahead of the DMA issue, h-half products first; 2 = as 1 with

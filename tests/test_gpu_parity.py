@@ -165,7 +165,8 @@ def test_convT(cin, cout, H, conv_math):
 
 
 @pytest.mark.parametrize("persistent,sched,order", [(0, 2, 3), (1, 2, 3), (1, 1, 3), (1, 0, 3), (1, 1, 2),
-                                                    (1, 1, 1), (1, 1, 0), (1, 1, 7), (1, 3, 7), (0, 3, 7)])
+                                                    (1, 1, 1), (1, 1, 0), (1, 1, 7), (1, 3, 7), (0, 3, 7),
+                                                    (1, 3, 15), (3, 3, 15)])
 @pytest.mark.parametrize("cfg", [-2, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11])
 @pytest.mark.parametrize("case", [(256, 256, 3, 1, 1, "reflect", 20), (128, 256, 4, 2, 1, "constant", 22),
                                   (64, 128, 3, 2, 1, "constant", 30), (256, 512, 4, 1, 1, "constant", 11),
@@ -203,7 +204,7 @@ def test_conv_f3_tiles(case, cfg, persistent, sched, order):
         L.set_f3_tile(-1)
         L.load().fg_set_f3_persistent(1)
         L.load().fg_set_f3_sched(-1)
-        L.load().fg_set_f3_order(7)
+        L.load().fg_set_f3_order(L.F3_ORDER_DEFAULT)
         L.set_conv_math(prev)
 
 
@@ -231,20 +232,26 @@ def test_conv_f3_persistent_bit_exact(case, cfg):
         m = PL.wmap_conv_fwd(wd.shape, X.c)
         Ho = PL.out_size(H, k, s, p)
         out = {}
-        for persistent in (0, 2, 3, 7):
-            L.load().fg_set_f3_persistent(persistent)
-            Y = Buf.empty(3, Ho, Ho, cout, 0, DEV)
-            Y.t.fill_(float("nan"))
-            ops.conv([PL.conv_problem(X, p, k, s, ops.pack_weight(wd, m), m, Y, bias=torch.ones(cout, device=DEV))])
-            assert ops.LAST_CONV_KERNEL == "conv_fwd_f3", ops.LAST_CONV_KERNEL
-            out[persistent] = Y.t.clone()
+        # order bit 3: the freed ring slot refilled before each tile's epilogue stores (the stage waits then count
+        # those stores one stage later)
+        for order in (7, 15):
+            L.load().fg_set_f3_order(order)
+            for persistent in (0, 2, 3, 7):
+                L.load().fg_set_f3_persistent(persistent)
+                Y = Buf.empty(3, Ho, Ho, cout, 0, DEV)
+                Y.t.fill_(float("nan"))
+                ops.conv([PL.conv_problem(X, p, k, s, ops.pack_weight(wd, m), m, Y,
+                                          bias=torch.ones(cout, device=DEV))])
+                assert ops.LAST_CONV_KERNEL == "conv_fwd_f3", ops.LAST_CONV_KERNEL
+                out[order, persistent] = Y.t.clone()
         torch.cuda.synchronize()
-        assert not torch.isnan(out[0]).any()
-        for persistent in (2, 3, 7):
-            assert torch.equal(out[persistent], out[0]), persistent
+        assert not torch.isnan(out[7, 0]).any()
+        for key in out:
+            assert torch.equal(out[key], out[7, 0]), key
     finally:
         L.set_f3_tile(-1)
         L.load().fg_set_f3_persistent(1)
+        L.load().fg_set_f3_order(L.F3_ORDER_DEFAULT)
         L.set_conv_math(prev)
 
 
