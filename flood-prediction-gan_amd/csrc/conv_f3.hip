@@ -932,10 +932,16 @@ static bool narrow_on() {
     return on;
 }
 
+// N = 65..128 on pre-split operands: cfg 12 = 512 x 128 as 8 waves of 64 x 128 -- the resblock tile's wave shape
+// (96 MFMAs per wave between two barriers, 24 fragment reads), where the 64 x 64 waves of cfg 11 run 48 per barrier;
+// its two 80 KB stages are the whole 160 KB of LDS.  Taken whenever the launch still fills half the CUs.
+int g_f3_ps_tall = 1;  // fg_set_f3_ps_tall (A/B hook): 0 keeps cfg 11 / 6
+
 int auto_cfg(const fg_conv_problem* p, int nprob, int max_n) {
     int cfg = f3_config(max_n);
     if (g_f3_tile >= 0 || cfg < 0) return cfg;
     if (p[0].q_n) return 5;      // the quad form's one tile (launch_cfg)
+    if (cfg == 6 && g_f3_ps_tall && p[0].x_presplit && 2 * batch_tiles(p, nprob, 512, 128) > fg::num_cus()) return 12;
     if (narrow_on() && (cfg == 6 || cfg == 7)) {
         const int alt = cfg == 7 ? 10 : 11;
         const int bm = alt == 10 ? 512 : 256, bn = alt == 10 ? 64 : 128;
@@ -1024,6 +1030,7 @@ int launch_fwd_f3(const ConvBatch& b, int nprob, int max_n, hipStream_t stream, 
         case 9: *rc = launch_cfg<128, 64, 32, 64, 6>(b, nprob, stream); return 1;
         case 10: *rc = launch_cfg<512, 64, 64, 64, 2>(b, nprob, stream); return 1;
         case 11: *rc = launch_cfg<256, 128, 64, 64, 3>(b, nprob, stream); return 1;
+        case 12: *rc = launch_cfg<512, 128, 64, 128, 2>(b, nprob, stream); return 1;
         default: return 0;
     }
 }
@@ -1031,7 +1038,7 @@ int launch_fwd_f3(const ConvBatch& b, int nprob, int max_n, hipStream_t stream, 
 }  // namespace fgc
 
 FG_API int fg_set_f3_tile(int cfg) {
-    if (cfg < -2 || cfg > 11) return fg::fail(FG_ERR_INVALID, "fg_set_f3_tile: %d", cfg);
+    if (cfg < -2 || cfg > 12) return fg::fail(FG_ERR_INVALID, "fg_set_f3_tile: %d", cfg);
     g_f3_tile = cfg;
     return 0;
 }
@@ -1063,6 +1070,12 @@ FG_API int fg_set_f3_interleave(int on) {
 FG_API int fg_set_f3_ps_wide(int cfg) {
     if (cfg != 4 && cfg != 5) return fg::fail(FG_ERR_INVALID, "fg_set_f3_ps_wide: %d", cfg);
     fgc::g_f3_ps_wide = cfg;
+    return 0;
+}
+
+FG_API int fg_set_f3_ps_tall(int on) {
+    if (on < 0 || on > 1) return fg::fail(FG_ERR_INVALID, "fg_set_f3_ps_tall: %d", on);
+    fgc::g_f3_ps_tall = on;
     return 0;
 }
 

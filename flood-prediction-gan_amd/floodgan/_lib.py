@@ -111,6 +111,7 @@ SIGNATURES = {
     "fg_set_wgrad_f3": [C.c_int],
     "fg_set_in_rows": [C.c_int],
     "fg_set_f3_ps_wide": [C.c_int],
+    "fg_set_f3_ps_tall": [C.c_int],
     "fg_conv_wgrad": [C.POINTER(fg_wgrad_problem), C.c_void_p],
     "fg_wgrad_reduce": [C.c_void_p, C.c_int, C.POINTER(fg_weight_map), C.c_void_p, C.c_int, C.c_void_p],
     "fg_pack_weight": [C.c_void_p, C.POINTER(fg_weight_map), C.c_void_p, C.c_void_p],
@@ -258,7 +259,7 @@ def set_wgrad_tile(cfg):
 
 
 def set_f3_tile(cfg):
-    """Tuning hook of the pipelined f16x3 forward kernel: -1 automatic, -2 off, 0..3 forced."""
+    """Tuning hook of the pipelined f16x3 forward kernel: -1 automatic, -2 off, 0..12 forced."""
     check(load().fg_set_f3_tile(int(cfg)), "set_f3_tile")
 
 

@@ -196,7 +196,7 @@ int fg_set_fwd_tile(int cfg);
 /* Same for the split-math weight-gradient kernels (0..5). */
 int fg_set_wgrad_tile(int cfg);
 /* Tuning hook of the LDS-DMA pipelined f16x3 forward kernel (conv_f3.hip, used for N > 64 when
- * the operands allow): -1 automatic (default), -2 never use it, 0..11 force a tile config. */
+ * the operands allow): -1 automatic (default), -2 never use it, 0..12 force a tile config. */
 int fg_set_f3_tile(int cfg);
 /* Tuning hook, k-walk order of the pipelined forward kernel: bit 0 = odd M tiles walk the kernel
  * rows backwards (L2 sharing between neighbouring tiles); bit 1 = channel-chunk-outer walk (the
@@ -221,6 +221,9 @@ int fg_set_f3_fill(int on);
 /* A/B hook: the tile of the pipelined kernel for pre-split (FG_PRESPLIT) operands with N > 128 that fill the
  * chip: 4 = 256x256 as 8 waves of 32x256, 5 (default) = 8 waves of 64x128. */
 int fg_set_f3_ps_wide(int cfg);
+/* A/B hook: 1 (default) = pre-split operands with 64 < N <= 128 that fill the chip run on the 512x128 tile of
+ * 8 waves of 64x128 (config 12); 0 = the 256x128 tiles (configs 11 / 6). */
+int fg_set_f3_ps_tall(int on);
 /* A/B hook: 1 (default) = a pipelined-kernel launch of problems with equal tile counts (the four phases of a
  * transposed conv or of a stride-2 input gradient) interleaves their tiles (tile t -> problem t % count), so
  * the phases read each input row at the same time; 0 = problem after problem. */

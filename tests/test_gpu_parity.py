@@ -167,7 +167,7 @@ def test_convT(cin, cout, H, conv_math):
 @pytest.mark.parametrize("persistent,sched,order", [(0, 2, 3), (1, 2, 3), (1, 1, 3), (1, 0, 3), (1, 1, 2),
                                                     (1, 1, 1), (1, 1, 0), (1, 1, 7), (1, 3, 7), (0, 3, 7),
                                                     (1, 3, 15), (3, 3, 15)])
-@pytest.mark.parametrize("cfg", [-2, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11])
+@pytest.mark.parametrize("cfg", [-2, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12])
 @pytest.mark.parametrize("case", [(256, 256, 3, 1, 1, "reflect", 20), (128, 256, 4, 2, 1, "constant", 22),
                                   (64, 128, 3, 2, 1, "constant", 30), (256, 512, 4, 1, 1, "constant", 11),
                                   (128, 64, 3, 1, 1, "constant", 21)])
@@ -208,7 +208,7 @@ def test_conv_f3_tiles(case, cfg, persistent, sched, order):
         L.set_conv_math(prev)
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12])
 @pytest.mark.parametrize("case", [(32, 128, 1, 1, 0, "constant", 40),    # K = 32: one k chunk per tile (nkt < NS)
                                   (64, 64, 1, 1, 0, "constant", 37),     # K = 64: two chunks, ragged M
                                   (32, 256, 3, 1, 1, "reflect", 24)])    # K = 288: several chunks per tile
@@ -833,7 +833,7 @@ def test_presplit_resblock_convs(N, H):
 
 
 @pytest.mark.parametrize("persistent", [1, 3])
-@pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11])
+@pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12])
 @pytest.mark.parametrize("case", [(256, 256, 3, 1, 1, 20), (128, 64, 3, 2, 1, 24), (64, 128, 3, 1, 1, 17)])
 def test_presplit_f3_tiles_and_stats(case, cfg, persistent):
     """every pipelined tile config (and the automatic choice, -1) on a FG_PRESPLIT operand, with and without the
