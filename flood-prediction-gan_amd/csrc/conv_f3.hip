@@ -283,7 +283,10 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
         }
         // alt_order: odd M tiles walk the kernel rows backwards, so neighbouring tiles (output rows
         // 2t, 2t+1 and 2t+2, 2t+3 at 128-px rows) gather the same input rows at the same time
-        irev = (alt_order & 1) && (ig.mt & 1);
+        // bit 4: the same by 512-row blocks of output rows (m0 / 512 odd) instead of by tile: every tile height up
+        // to 512 then gives a row the same k order, so a sample's values do not depend on the tile config its
+        // batch size selects
+        irev = (alt_order & 1) && (((alt_order & 16) ? (ig.m0 >> 9) : ig.mt) & 1);
         i_kh = P.kh;
         i_jp = P.jp;
         i_sxr = (int)P.sxr;
@@ -316,7 +319,7 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
         const int ks = r * (i_jp / 32) + jb / 32;        // packed-weight stage of this (r, jb)
         record_seg(buf, r, jb);
 #ifdef FG_F3_DIAG
-        if (!((alt_order >> 4) & 1) || ikt < NS)         // diag bit 0: no DMA after the first stages
+        if (!((alt_order >> 5) & 1) || ikt < NS)         // diag bit 0: no DMA after the first stages
 #endif
         dma_stage<A_GL, B_GL, A_BYTES>(smem + buf * STAGE, wave, xr, wr, a_off, b_off, koff, ks * 128);
         if (++is == i_kw) {
@@ -348,7 +351,7 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
         if constexpr (QUAD)
             p_live = __builtin_amdgcn_readfirstlane((i_segmask >> (4 * (r * i_qkw + (jb >> i_qsh)))) & 0xFu);
 #ifdef FG_F3_DIAG
-        if (((alt_order >> 4) & 1) && ikt >= NS) p_on = false;
+        if (((alt_order >> 5) & 1) && ikt >= NS) p_on = false;
 #endif
     };
     auto issue_piece = [&](int i) {
@@ -440,7 +443,7 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
             }
         } else
 #ifdef FG_F3_DIAG
-        if ((alt_order >> 6) & 1) {                      // diag bit 2: no split (A bits reinterpreted)
+        if ((alt_order >> 7) & 1) {                      // diag bit 2: no split (A bits reinterpreted)
 #pragma unroll
             for (int tm = 0; tm < TM; ++tm) {
                 ah[tm] = __builtin_bit_cast(f16x8, va[tm][0]);
@@ -722,13 +725,13 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
     while (true) {
         wait_stage();
 #ifdef FG_F3_DIAG
-        if (!((alt_order >> 7) & 1))                     // diag bit 3: no barrier (timing only)
+        if (!((alt_order >> 8) & 1))                     // diag bit 3: no barrier (timing only)
 #endif
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
         f32x4 va[TM][2];
 #ifdef FG_F3_DIAG
-        if ((alt_order >> 5) & 1) {                      // diag bit 1: DMA and barriers only
+        if ((alt_order >> 6) & 1) {                      // diag bit 1: DMA and barriers only
             if (issue_next(nxt)) ++issued;
         } else
 #endif
@@ -761,7 +764,7 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
             if constexpr (SCH >= 3) {
                 bool pre = pre_epi && it < total_tiles;
 #ifdef FG_F3_DIAG
-                pre = pre && !((alt_order >> 5) & 1);
+                pre = pre && !((alt_order >> 6) & 1);
 #endif
                 if (pre) {
                     __builtin_amdgcn_s_barrier();
@@ -773,7 +776,7 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
                 }
             }
 #ifdef FG_F3_DIAG
-            if (!((alt_order >> 8) & 1))                 // diag bit 4: no epilogue (timing only)
+            if (!((alt_order >> 9) & 1))                 // diag bit 4: no epilogue (timing only)
 #endif
             epilogue();
 #pragma unroll
@@ -787,10 +790,11 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
     }
 }
 
-int g_f3_alt = 15;    // fg_set_f3_order: bit 0 alternates the kernel-row order of odd M tiles,
+int g_f3_alt = 31;    // fg_set_f3_order: bit 0 alternates the kernel-row order of odd M tiles,
                       // bit 1 walks k chunk-outer (taps of one channel chunk back to back),
                       // bit 2 raises the priority of the second half of the waves,
-                      // bit 3 refills the freed ring slot before a tile's epilogue stores
+                      // bit 3 refills the freed ring slot before a tile's epilogue stores,
+                      // bit 4 takes bit 0's parity from 512-row blocks instead of tiles
 int g_f3_persist = 1; // fg_set_f3_persistent: 1 resident workgroups loop over tiles, 0 one workgroup per
                       // tile, n >= 2 at most n workgroups (test hook: forces the tile-crossing stream
                       // -- setup_issue() mid-stream, next tile's stages in flight over an epilogue --
@@ -831,7 +835,7 @@ int launch_cfg(const ConvBatch& in, int nprob, hipStream_t stream) {
     // timing-only diagnostic build (outputs are wrong): FG_F3_DIAG=1 compute without data movement,
     // 2 data movement without compute
     const char* dg = getenv("FG_F3_DIAG");
-    const int g_f3_alt = ::g_f3_alt | ((dg ? atoi(dg) : 0) << 4);
+    const int g_f3_alt = ::g_f3_alt | ((dg ? atoi(dg) : 0) << 5);
 #endif
     bool stats = false;
     for (int i = 0; i < nprob; ++i) stats |= b.p[i].in_stats != nullptr;
@@ -1056,7 +1060,7 @@ FG_API int fg_set_f3_sched(int sched) {
 }
 
 FG_API int fg_set_f3_order(int alt) {
-    if (alt < 0 || alt > 15) return fg::fail(FG_ERR_INVALID, "fg_set_f3_order: %d", alt);
+    if (alt < 0 || alt > 31) return fg::fail(FG_ERR_INVALID, "fg_set_f3_order: %d", alt);
     g_f3_alt = alt;
     return 0;
 }

@@ -77,7 +77,7 @@ class fg_adam_tensor(C.Structure):
 FG_TILE_MAX_CH = 16
 
 # fg_set_f3_order's default (csrc/conv_f3.hip g_f3_alt): tests restore it after sweeping the bits
-F3_ORDER_DEFAULT = 15
+F3_ORDER_DEFAULT = 31
 
 
 class fg_tile_batch(C.Structure):

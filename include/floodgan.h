@@ -202,8 +202,9 @@ int fg_set_f3_tile(int cfg);
  * rows backwards (L2 sharing between neighbouring tiles); bit 1 = channel-chunk-outer walk (the
  * taps of one 32-channel chunk back to back, needs fg_conv_problem.jc); bit 2 = static priority
  * for the second half of the waves; bit 3 = at a tile boundary the freed LDS ring slot is refilled
- * before the epilogue's stores (stage schedules 3-5), so the stores drain under two stages.
- * Default 15. */
+ * before the epilogue's stores (stage schedules 3-5), so the stores drain under two stages; bit 4 = bit 0's
+ * parity taken from 512-row blocks of output rows instead of from tiles (a row's k order then does not depend
+ * on the tile height, so a sample's values do not depend on its batch size).  Default 31. */
 int fg_set_f3_order(int alt);
 /* Tuning hook: per-stage instruction order of the pipelined forward kernel: 0 = split all of A,
  * then the products; 1 = A reads ahead of the DMA issue, h-half products first; 2 = as 1 with

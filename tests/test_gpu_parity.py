@@ -166,7 +166,7 @@ def test_convT(cin, cout, H, conv_math):
 
 @pytest.mark.parametrize("persistent,sched,order", [(0, 2, 3), (1, 2, 3), (1, 1, 3), (1, 0, 3), (1, 1, 2),
                                                     (1, 1, 1), (1, 1, 0), (1, 1, 7), (1, 3, 7), (0, 3, 7),
-                                                    (1, 3, 15), (3, 3, 15)])
+                                                    (1, 3, 15), (3, 3, 15), (1, 3, 31), (3, 3, 31)])
 @pytest.mark.parametrize("cfg", [-2, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12])
 @pytest.mark.parametrize("case", [(256, 256, 3, 1, 1, "reflect", 20), (128, 256, 4, 2, 1, "constant", 22),
                                   (64, 128, 3, 2, 1, "constant", 30), (256, 512, 4, 1, 1, "constant", 11),
@@ -234,7 +234,7 @@ def test_conv_f3_persistent_bit_exact(case, cfg):
         out = {}
         # order bit 3: the freed ring slot refilled before each tile's epilogue stores (the stage waits then count
         # those stores one stage later)
-        for order in (7, 15):
+        for order in (7, 15, 31):
             L.load().fg_set_f3_order(order)
             for persistent in (0, 2, 3, 7):
                 L.load().fg_set_f3_persistent(persistent)
@@ -247,11 +247,52 @@ def test_conv_f3_persistent_bit_exact(case, cfg):
         torch.cuda.synchronize()
         assert not torch.isnan(out[7, 0]).any()
         for key in out:
-            assert torch.equal(out[key], out[7, 0]), key
+            assert torch.equal(out[key], out[key[0], 0]), key
+        assert torch.equal(out[15, 0], out[7, 0])   # bit 3 moves no arithmetic (bit 4 moves the reversed rows)
     finally:
         L.set_f3_tile(-1)
         L.load().fg_set_f3_persistent(1)
         L.load().fg_set_f3_order(L.F3_ORDER_DEFAULT)
+        L.set_conv_math(prev)
+
+
+@pytest.mark.parametrize("presplit", [False, True])
+def test_conv_f3_tile_height_invariant(presplit):
+    """order bit 4 (default): odd 512-row blocks of output rows walk the kernel rows backwards whatever the tile
+    height, so every tile config gives a row the same k order -- the outputs of 128-, 256- and 512-row tiles are
+    bit-identical, and a sample's values do not depend on the tile config its batch size selects (the batch-8 vs
+    batch-1 check of test_bs8_generator_backward_equals_sum_of_bs1_512)"""
+    from floodgan import _lib as L, ops, plans as PL
+    from floodgan.plans import Buf
+    prev = L.get_conv_math()
+    L.set_conv_math("f16x3")
+    lib = L.load()
+    try:
+        torch.manual_seed(29)
+        cin, cout, H = 64, 128, 40
+        c = torch.randn(3, cin, H, H, dtype=torch.float64)
+        if presplit:
+            cb = buf_from(c, 0, "constant")
+            mean, rstd = ops.in_stats(cb)
+            X = Buf.empty(3, H, H, cin, 1, DEV)
+            ops.in_apply(cb, mean, rstd, 1, None, X, 1, presplit=True)
+        else:
+            X = buf_from(c, 1, "reflect")
+        wd = (torch.randn(cout, cin, 3, 3, dtype=torch.float64) * 0.05).float().to(DEV)
+        m = PL.wmap_conv_fwd(wd.shape, cin)
+        wp = ops.pack_weight(wd, m)
+        out = {}
+        for cfg in (3, 6, 9, 10, 11, 12):
+            L.set_f3_tile(cfg)
+            Y = Buf.empty(3, H, H, cout, 0, DEV)
+            ops.conv([PL.conv_problem(X, 1, 3, 1, wp, m, Y)])
+            out[cfg] = Y.t.clone()
+        torch.cuda.synchronize()
+        for cfg in out:
+            assert torch.equal(out[cfg], out[3]), cfg
+    finally:
+        L.set_f3_tile(-1)
+        lib.fg_set_f3_order(L.F3_ORDER_DEFAULT)
         L.set_conv_math(prev)
 
 
