@@ -357,8 +357,16 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
     auto issue_piece = [&](int i) {
         if (!p_on) return;
         // the LDS destination is wave-uniform (M0): say so, or the compiler emits a waterfall loop
-        if (i < A_GL)
+        if (i < A_GL) {
+#ifdef FG_F3_DIAG
+            if ((alt_order >> 10) & 1) {      // diag bit 5: every A piece from a fixed, L2-resident 1 KB of its own
+                dma_piece(smem + __builtin_amdgcn_readfirstlane(p_buf + (wave * A_GL + i) * 1024), xr,
+                          (((int)blockIdx.x * (BM / WM) * (BN / WN) + wave) * A_GL + i) * 1024 + lane * 16, 0);
+                return;
+            }
+#endif
             dma_piece(smem + __builtin_amdgcn_readfirstlane(p_buf + (wave * A_GL + i) * 1024), xr, a_off[i], p_koff);
+        }
         else if constexpr (QUAD) {
             const bool live = __builtin_amdgcn_readfirstlane((p_live >> b_grp[i - A_GL]) & 1u) != 0;
             dma_piece(smem + __builtin_amdgcn_readfirstlane(p_buf + A_BYTES + (wave * B_GL + (i - A_GL)) * 1024),

@@ -2,7 +2,7 @@
 scripts/gpu_diag.sh; the outputs of modes 1/2 are garbage): per geometry, the time of the full
 kernel (mode 0), of its compute alone (mode 1: no data movement after the first stages) and of
 its data movement alone (mode 2: DMA + barriers, no MFMA work); 4/5 without the A split, 9/13 as 1/5
-without the per-stage barrier.
+without the per-stage barrier; 32 with every A piece read from a fixed L2-resident window.
   python scripts/diag_f3.py [modes, default 0,1,2,4,5]"""
 import os
 import sys
@@ -17,7 +17,7 @@ from bench_conv import make, time_it  # noqa: E402
 
 
 TAGS = {0: "full", 1: "compute only", 2: "data movement only", 4: "no A split", 5: "compute only, no A split",
-        9: "compute only, no barrier", 13: "compute, no split, no barrier"}
+        9: "compute only, no barrier", 13: "compute, no split, no barrier", 32: "A from a fixed L2 window"}
 MODES = [int(v) for v in sys.argv[1].split(",")] if len(sys.argv) > 1 else [0, 1, 2, 4, 5]
 
 
