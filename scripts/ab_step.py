@@ -1,7 +1,7 @@
 """A/B of engine switches on the full bs-8 512^2 training step, interleaved in ONE process (device
 clocks and boxes differ by several percent, so separate bench runs cannot resolve small gains).
   python scripts/ab_step.py f3_persistent [rounds] [steps] [values, default 0,1]
-Switches: f3_persistent, f3_sched, f3_order, f3_fill, f3_interleave, head_1x1, wgrad_f3, use_win, in_rows, presplit, ps_wide (values 4,5), ps_tall, ps_resid, stem_fwd, splitpix, d0_dgrad, in_nt, in_nt2, fused_head, quad."""
+Switches: f3_persistent, f3_sched, f3_order, f3_fill, f3_interleave, head_1x1, wgrad_f3, use_win, in_rows, presplit, ps_wide (values 4,5), ps_tall, ps_resid, stem_fwd, splitpix, d0_dgrad, in_nt, in_nt2, fused_head, quad, n1_rows (values: rows per block)."""
 import os
 import sys
 import time
@@ -59,6 +59,8 @@ def switch(name, on):
     elif name == "splitpix":
         from floodgan import executor
         executor.SPLITPIX = bool(on)
+    elif name == "n1_rows":
+        ops.N1_ROWS = int(on)
     elif name == "quad":
         from floodgan import executor
         executor.QUAD = bool(on)
