@@ -256,6 +256,82 @@ def fp32_math_arm(B, R, dev, x, y, steps=5, warmup=1):
             "note": "same step, batch and seed on a fresh model; every conv on the exact-fp32 MFMA (157.3 TFLOP/s peak)"}
 
 
+def _rccl_version():
+    try:
+        v = torch.cuda.nccl.version()
+        return ".".join(map(str, v)) if isinstance(v, tuple) else str(v)
+    except Exception as e:          # noqa: BLE001 - reported, not fatal
+        return f"unknown ({type(e).__name__})"
+
+
+def rccl_world1(args):
+    """`--rccl-world1`: execute the RCCL path on a one-GPU box.  A one-rank ProcessGroupNCCL is initialised and
+    the step's bucketed asynchronous SUM all-reduces (parallel.FlatGrads: D's before Adam(D), G's overlapping the
+    generator backward -- models/model.py:632-633, :645-646) are forced through it although world == 1, where they
+    are identities.  Two seed-47 models step on the same batch, one with the collectives forced (arm "rccl") and
+    one without ("none"), alternating step by step; the line reports each arm's median step time, the number of
+    collectives per step and whether the two arms' losses and final parameters are bit-identical."""
+    import statistics
+
+    os.environ.update(RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=os.environ.get("MASTER_PORT") or str(_free_port()))
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", device_id=dev)
+    from floodgan import parallel
+    from floodgan.model import Model
+    B, R = args.batch, args.res
+    g = torch.Generator().manual_seed(1234)
+    x = (torch.rand((B, 9, R, R), generator=g) * 2 - 1).to(dev)
+    y = (torch.rand((B, 3, R, R), generator=g) * 2 - 1).to(dev)
+    arms = {a: Model(model="PairedAttention", num_epochs=2, topography="all", device=dev) for a in ("none", "rccl")}
+    calls = {"n": 0}
+    real_all_reduce = dist.all_reduce
+
+    def counting_all_reduce(*a, **k):
+        calls["n"] += 1
+        return real_all_reduce(*a, **k)
+    dist.all_reduce = counting_all_reduce
+    times = {a: [] for a in arms}
+    losses = {a: [] for a in arms}
+    try:
+        for i in range(args.warmup + args.steps):
+            for a, m in arms.items():
+                prev = parallel.set_force_collectives(a == "rccl")
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                v = m.step_fn(x, y).cpu()
+                torch.cuda.synchronize()
+                parallel.set_force_collectives(prev)
+                if i >= args.warmup:
+                    times[a].append(time.perf_counter() - t0)
+                losses[a].append(v)
+    finally:
+        dist.all_reduce = real_all_reduce
+    n_steps = args.warmup + args.steps
+    same_losses = all(torch.equal(p, q) for p, q in zip(losses["none"], losses["rccl"]))
+    pa = [p for net in (arms["none"].generator, arms["none"].discriminator) for p in net.parameters()]
+    pb = [p for net in (arms["rccl"].generator, arms["rccl"].discriminator) for p in net.parameters()]
+    same_params = all(torch.equal(p, q) for p, q in zip(pa, pb))
+    step = arms["rccl"].step_fn
+    med = {a: statistics.median(t) * 1e3 for a, t in times.items()}
+    out = {"metric": "rccl_world1", "backend": dist.get_backend(), "world_size": dist.get_world_size(),
+           "rccl_version": _rccl_version(),
+           "steps": args.steps, "warmup": args.warmup,
+           "config": {"workload": f"PairedAttention paired train step, {R}x{R}, topography=all, batch {B}"},
+           "collectives_per_step": calls["n"] / n_steps,
+           "buckets_per_step": len(step.gflat.buckets) + len(step.dflat.buckets),
+           "bytes_per_step": 4 * (step.gflat.flat.numel() + step.dflat.flat.numel()),
+           "ms_per_step_none": round(med["none"], 3), "ms_per_step_rccl": round(med["rccl"], 3),
+           "overhead_ms": round(med["rccl"] - med["none"], 3),
+           "losses_bit_identical": same_losses, "params_bit_identical": same_params,
+           "losses_last_step": [round(float(v), 5) for v in losses["rccl"][-1]]}
+    print(json.dumps(out), flush=True)
+    dist.destroy_process_group()
+    return 0 if (same_losses and same_params and calls["n"] == n_steps * out["buckets_per_step"]) else 1
+
+
 def rank_envs(n, port, base=None, backend="nccl"):
     """The environments of the N ranks `launch_ranks` starts: what torch.distributed.run would set
     (RANK, LOCAL_RANK, WORLD_SIZE, LOCAL_WORLD_SIZE, MASTER_ADDR / MASTER_PORT on 127.0.0.1) plus the
@@ -350,7 +426,15 @@ def main():
     ap.add_argument("--crop", type=int, default=None)
     ap.add_argument("--tile", type=int, default=1024, help="raw tile edge for --data tiles (xBD tiles are 1024)")
     ap.add_argument("--tiles", type=int, default=8, help="distinct synthetic tiles for --data tiles")
+    ap.add_argument("--rccl-world1", action="store_true",
+                    help="execute the step's bucketed RCCL all-reduces in a one-rank process group (identities) "
+                         "beside the same step without them: overhead and bit-identity (one-GPU evidence of the "
+                         "RCCL path; not a scaling measurement)")
     args = ap.parse_args()
+    if args.rccl_world1:
+        if args.gpus != 1 or "WORLD_SIZE" in os.environ and os.environ["WORLD_SIZE"] != "1":
+            sys.exit("bench.py --rccl-world1 runs one rank")
+        sys.exit(rccl_world1(args))
 
     backend = args.dist_backend or os.environ.get("FLOODGAN_DIST_BACKEND", "nccl")
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:

@@ -283,10 +283,19 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
         }
         // alt_order: odd M tiles walk the kernel rows backwards, so neighbouring tiles (output rows
         // 2t, 2t+1 and 2t+2, 2t+3 at 128-px rows) gather the same input rows at the same time
-        // bit 4: the same by 512-row blocks of output rows (m0 / 512 odd) instead of by tile: every tile height up
-        // to 512 then gives a row the same k order, so a sample's values do not depend on the tile config its
-        // batch size selects
-        irev = (alt_order & 1) && (((alt_order & 16) ? (ig.m0 >> 9) : ig.mt) & 1);
+        // bit 4: the same by 512-row blocks of output rows instead of by tile: every tile height up to 512 then gives
+        // a row the same k order, so a sample's values do not depend on the tile config its batch size selects.  The
+        // blocks are counted from the tile's image when an image holds a whole number of them (mab % 512 == 0: no
+        // tile of <= 512 rows straddles two images), so a sample's k order does not depend on its position in the
+        // batch either; otherwise (tiles straddle images) from the batch's first row -- tile-height invariant, but a
+        // sample's values can then depend on the batch it sits in
+        int lrow = ig.m0;
+        if ((mab & 511) == 0) {
+            int i0, a0, b0;
+            fgc::decomp(ig.m0, P.m_b, mab, i0, a0, b0);
+            lrow = ig.m0 - i0 * mab;
+        }
+        irev = (alt_order & 1) && (((alt_order & 16) ? (lrow >> 9) : ig.mt) & 1);
         i_kh = P.kh;
         i_jp = P.jp;
         i_sxr = (int)P.sxr;
@@ -318,9 +327,6 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
         const int koff = (r * i_sxr + jb) * 4;
         const int ks = r * (i_jp / 32) + jb / 32;        // packed-weight stage of this (r, jb)
         record_seg(buf, r, jb);
-#ifdef FG_F3_DIAG
-        if (!((alt_order >> 5) & 1) || ikt < NS)         // diag bit 0: no DMA after the first stages
-#endif
         dma_stage<A_GL, B_GL, A_BYTES>(smem + buf * STAGE, wave, xr, wr, a_off, b_off, koff, ks * 128);
         if (++is == i_kw) {
             is = 0;
@@ -350,21 +356,11 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
         record_seg(buf, r, jb);
         if constexpr (QUAD)
             p_live = __builtin_amdgcn_readfirstlane((i_segmask >> (4 * (r * i_qkw + (jb >> i_qsh)))) & 0xFu);
-#ifdef FG_F3_DIAG
-        if (((alt_order >> 5) & 1) && ikt >= NS) p_on = false;
-#endif
     };
     auto issue_piece = [&](int i) {
         if (!p_on) return;
         // the LDS destination is wave-uniform (M0): say so, or the compiler emits a waterfall loop
         if (i < A_GL) {
-#ifdef FG_F3_DIAG
-            if ((alt_order >> 10) & 1) {      // diag bit 5: every A piece from a fixed, L2-resident 1 KB of its own
-                dma_piece(smem + __builtin_amdgcn_readfirstlane(p_buf + (wave * A_GL + i) * 1024), xr,
-                          (((int)blockIdx.x * (BM / WM) * (BN / WN) + wave) * A_GL + i) * 1024 + lane * 16, 0);
-                return;
-            }
-#endif
             dma_piece(smem + __builtin_amdgcn_readfirstlane(p_buf + (wave * A_GL + i) * 1024), xr, a_off[i], p_koff);
         }
         else if constexpr (QUAD) {
@@ -450,15 +446,6 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
                 al[tm] = __builtin_bit_cast(f16x8, va[tm][1]);
             }
         } else
-#ifdef FG_F3_DIAG
-        if ((alt_order >> 7) & 1) {                      // diag bit 2: no split (A bits reinterpreted)
-#pragma unroll
-            for (int tm = 0; tm < TM; ++tm) {
-                ah[tm] = __builtin_bit_cast(f16x8, va[tm][0]);
-                al[tm] = __builtin_bit_cast(f16x8, va[tm][1]);
-            }
-        } else
-#endif
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm) {
             const float v[8] = {va[tm][0][0], va[tm][0][1], va[tm][0][2], va[tm][0][3],
@@ -732,17 +719,9 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
     bool pre_issued = false;
     while (true) {
         wait_stage();
-#ifdef FG_F3_DIAG
-        if (!((alt_order >> 8) & 1))                     // diag bit 3: no barrier (timing only)
-#endif
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
         f32x4 va[TM][2];
-#ifdef FG_F3_DIAG
-        if ((alt_order >> 6) & 1) {                      // diag bit 1: DMA and barriers only
-            if (issue_next(nxt)) ++issued;
-        } else
-#endif
         if constexpr (SCH == 0) {
             if (issue_next(nxt)) ++issued;
             load_a(cur, va);
@@ -771,9 +750,6 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
         if (++ckt == cg.nkt) {
             if constexpr (SCH >= 3) {
                 bool pre = pre_epi && it < total_tiles;
-#ifdef FG_F3_DIAG
-                pre = pre && !((alt_order >> 6) & 1);
-#endif
                 if (pre) {
                     __builtin_amdgcn_s_barrier();
                     issue_prep(nxt);
@@ -783,9 +759,6 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
                     pre_issued = true;
                 }
             }
-#ifdef FG_F3_DIAG
-            if (!((alt_order >> 9) & 1))                 // diag bit 4: no epilogue (timing only)
-#endif
             epilogue();
 #pragma unroll
             for (int tm = 0; tm < TM; ++tm)
@@ -839,12 +812,6 @@ int launch_cfg(const ConvBatch& in, int nprob, hipStream_t stream) {
         b.interleave = eq ? 1 : 0;
     }
     const int sched = g_f3_sched >= 0 ? g_f3_sched : 3;
-#ifdef FG_F3_DIAG
-    // timing-only diagnostic build (outputs are wrong): FG_F3_DIAG=1 compute without data movement,
-    // 2 data movement without compute
-    const char* dg = getenv("FG_F3_DIAG");
-    const int g_f3_alt = ::g_f3_alt | ((dg ? atoi(dg) : 0) << 5);
-#endif
     bool stats = false;
     for (int i = 0; i < nprob; ++i) stats |= b.p[i].in_stats != nullptr;
     // pre-split A operands (every problem of the batch, checked by the caller): their own instantiations
@@ -951,8 +918,9 @@ int g_f3_ps_tall = 1;  // fg_set_f3_ps_tall (A/B hook): 0 keeps cfg 11 / 6
 
 int auto_cfg(const fg_conv_problem* p, int nprob, int max_n) {
     int cfg = f3_config(max_n);
-    if (g_f3_tile >= 0 || cfg < 0) return cfg;
-    if (p[0].q_n) return 5;      // the quad form's one tile (launch_cfg)
+    if (cfg < 0) return cfg;
+    if (p[0].q_n) return 5;      // the quad form's one tile (launch_cfg), whatever tile fg_set_f3_tile forces
+    if (g_f3_tile >= 0) return cfg;
     if (cfg == 6 && g_f3_ps_tall && p[0].x_presplit && 2 * batch_tiles(p, nprob, 512, 128) > fg::num_cus()) return 12;
     if (narrow_on() && (cfg == 6 || cfg == 7)) {
         const int alt = cfg == 7 ? 10 : 11;

@@ -53,11 +53,10 @@ template <bool NTL>
 __device__ __forceinline__ f32x4 ldx(const float* p) { return NTL ? ld4_nt(p) : ld4(p); }
 // the apply passes' last reads of their inputs (the conv output, the residual / gradient) are non-temporal: the
 // Infinity Cache then keeps the output the next conv reads instead of bytes never read again -- step 46.08 -> 45.60
-// ms (profiles/round4/r4q_ab_in_nt2.log); FLOODGAN_IN_NT2=0 turns it off, FLOODGAN_IN_NT2_AB is read per call (A/B)
+// ms (profiles/round4/r4q_ab_in_nt2.log); FLOODGAN_IN_NT2=0 turns it off (read once per process)
 bool in_nt2_on() {
     static const bool env = [] { const char* e = getenv("FLOODGAN_IN_NT2"); return !e || atoi(e) != 0; }();
-    const char* ab = getenv("FLOODGAN_IN_NT2_AB");
-    return ab ? atoi(ab) != 0 : env;
+    return env;
 }
 
 __global__ void in_stats_kernel(fg_view src, int chunks, double* __restrict__ work) {
@@ -1372,8 +1371,7 @@ int in_bwd_impl(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, const flo
     double* bpart = work + (size_t)src.n * C * MAX_CHUNKS * 3 + (size_t)src.n * C;
     float* gmax_part = split_slot ? reinterpret_cast<float*>(bpart + (size_t)src.n * C) : nullptr;
     static const bool nt_env = [] { const char* e = getenv("FLOODGAN_IN_NT"); return !e || atoi(e) != 0; }();
-    const char* nte = getenv("FLOODGAN_IN_NT_AB");          // A/B hook read per call (scripts/ab_step.py in_nt)
-    const bool ntg = gsum.ptr && (nte ? atoi(nte) != 0 : nt_env);
+    const bool ntg = gsum.ptr && nt_env;
     if (head)
         hipLaunchKernelGGL((in_bwd_stats_u_kernel<false, true>), dim3(chunks, src.n), dim3(NT), 0, stream, gsrc, 0, gadd,
                            src, mean, rstd, act, chunks, work, gsum, gmax_part, *head);

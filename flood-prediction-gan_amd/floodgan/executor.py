@@ -21,14 +21,13 @@ from .plans import Buf
 N_BLOCKS = 9
 CONTENT_ALLOC = 32   # 27 content channels, padded for aligned NHWC rows
 N_ATT = 10           # attention logits (deconv3_attention's output channels)
-# the attention head's 1x1 conv and its gradients as fp32 FMA kernels (csrc/head1x1.hip); FLOODGAN_HEAD_1X1=0:
-# the implicit-GEMM engine
-HEAD_1X1 = os.environ.get("FLOODGAN_HEAD_1X1", "1") != "0"
-# round 5: the attention head's 1x1 conv fused into the norm passes of its input (fg_in_apply_head / fg_in_bwd_head:
+# the attention head's 1x1 conv and its gradients run as exact-fp32 FMA work (csrc/head1x1.hip; the implicit-GEMM
+# engine path lost -0.13 ms per step, profiles/round2/r2ag_ab_head_1x1.log, and was retired in round 6).  Round 5: the attention head's 1x1 conv fused into the norm passes of its input (fg_in_apply_head / fg_in_bwd_head:
 # the forward's logits formed by the apply pass, the backward's 64-channel input gradient formed in registers from the
 # logits gradient by the statistics and apply passes) -- no conv1x1 forward / input-gradient launches and no re-read
 # or materialisation of a 537-MB 64-channel tensor; bit-identical; interleaved A/B 45.95 -> 45.60 ms per step
-# (profiles/round5/r5f_ab_fused_head.log).  FLOODGAN_FUSED_HEAD=0: the separate kernels
+# (profiles/round5/r5f_ab_fused_head.log).  FLOODGAN_FUSED_HEAD=0: the separate head1x1 kernels (the reference the
+# fused passes are tested against, tests/test_gpu_northstar.py::test_fused_attention_head)
 FUSED_HEAD = os.environ.get("FLOODGAN_FUSED_HEAD", "1") != "0"
 ATT_ALLOC = 16       # 10 attention channels
 
@@ -109,12 +108,11 @@ def _conv_fwd(P, name, X, pad, k, stride, Y, act=FG_ACT_NONE, tag=None, in_stats
 
 
 # round 5: the four output phases of a stride-2, 3-tap transposed op with 64 output channels as ONE problem (the quad
-# form, plans.quad_map): each input pixel gathered once for all phases, zero segments skipped in the kernel
-QUAD = os.environ.get("FLOODGAN_QUAD", "1") != "0"
-
-
+# form, plans.quad_map): each input pixel gathered once for all phases, zero segments skipped in the kernel.  The
+# FLOODGAN_QUAD=0 switch was retired in round 6: the four-phase problems remain for every other shape, and
+# tests/test_gpu_parity.py::test_quad_convT checks the quad form against fp64.
 def _quad_ok(X, shape, k, Y):
-    return (QUAD and k == 3 and shape[1] == 64 and isinstance(Y, Buf) and Y.c == 64 and ops.is_presplit(X)
+    return (k == 3 and shape[1] == 64 and isinstance(Y, Buf) and Y.c == 64 and ops.is_presplit(X)
             and L.fwd_f16x3() and (Y.h, Y.w, Y.n) == (2 * X.h, 2 * X.w, X.n) and X.pad >= 1 and X.c % 32 == 0
             and X.c & (X.c - 1) == 0)
 
@@ -148,9 +146,8 @@ def _norm(c, act, pad, mode, residual=None, stats=None, presplit=False, ps_copy=
     return (mean, rstd, out, ps) if ps_copy else (mean, rstd, out)
 
 
-# the content head's input written in the window kernels' split layout by its norm pass (step 46.39 -> 46.19 ms,
-# profiles/round4/r4e_ab_splitpix.log; FLOODGAN_SPLITPIX=0: fp32 + a fg_split_pixels pass)
-SPLITPIX = os.environ.get("FLOODGAN_SPLITPIX", "1") != "0"
+# the content head's input is written in the window kernels' split layout by its norm pass (step 46.39 -> 46.19 ms,
+# profiles/round4/r4e_ab_splitpix.log; the fp32 + fg_split_pixels alternative was retired in round 6)
 
 
 def has_attention(P):
@@ -208,8 +205,8 @@ def gen_forward(P, x, save=True, x_extra=None):
         # the content head's ad2 is read only by the window conv and its weight gradient: written in their split
         # layout directly (no fp32 copy, no fg_split_pixels pass)
         # (when the window kernels take the head: output rows of >= 256 px, a multiple of 32; ops.win_eligible)
-        spx = tag == "content" and ps and SPLITPIX and ops.USE_WIN and W >= 256 and W % 32 == 0
-        if tag == "attention" and HEAD_1X1 and FUSED_HEAD:
+        spx = tag == "content" and ps and ops.USE_WIN and W >= 256 and W % 32 == 0
+        if tag == "attention" and FUSED_HEAD:
             # the 1x1 head's logits from relu(IN(d2)) in the norm pass (fg_in_apply_head); the activation itself is
             # not written: the head's backward recomputes it from d2 for the weight gradient (round 5)
             md2, rd2 = st if st is not None else ops.in_stats(d2)
@@ -227,16 +224,12 @@ def gen_forward(P, x, save=True, x_extra=None):
         ops.tanh_head_fwd(cl, 3, out)
         S.update(heads=heads, cl=cl)
         return out, None, (S if save else None)
-    if HEAD_1X1 and FUSED_HEAD:
-        pass                                          # al: written by the attention head's norm pass above
-    elif HEAD_1X1:
+    if not FUSED_HEAD:
         al = Buf.empty(N, H, W, ATT_ALLOC, 0, dev)
         # 1x1 64 -> 10: a per-pixel matrix-vector product, fp32 FMA over LDS-staged tiles (csrc/head1x1.hip)
         ops.conv1x1_fwd(heads["attention"]["ad2"], P["deconv3_attention.weight"], P["deconv3_attention.bias"],
                         N_ATT, al)
-    else:
-        al = Buf.empty(N, H, W, ATT_ALLOC, 0, dev)
-        _conv_fwd(P, "deconv3_attention", heads["attention"]["ad2"], 0, 1, 1, al)
+    # (FUSED_HEAD: al was written by the attention head's norm pass above)
     mask = torch.empty(N, H, W, dtype=torch.float32, device=dev)
     ops.tail_fwd(cl, al, x, out, mask)
     S.update(heads=heads, cl=cl, al=al)
@@ -426,18 +419,13 @@ def gen_backward(P, S, g_out, grads_into=None, ready=None, input_grad=None, accu
     heads = [("content", hc, g_ad2c, 3)]
     if attention:
         # ---- deconv3_attention: 1x1
-        g_ad2a = None if HEAD_1X1 and FUSED_HEAD else Buf.empty(N, H, W, 64, 0, dev)
-        if HEAD_1X1 and g_ad2a is not None:
+        # the fused head: weight, bias and input gradients in its norm backward below (g_ad2a None)
+        g_ad2a = None if FUSED_HEAD else Buf.empty(N, H, W, 64, 0, dev)
+        if g_ad2a is not None:
             names = ("deconv3_attention.weight", "deconv3_attention.bias")
             G.off_path(lambda: ops.conv1x1_wgrad(gal, ha["ad2"], N_ATT, G.get(names[0]), G.get(names[1]), G.acc),
                        (gal, ha["ad2"]), names)
             ops.conv1x1_dgrad(gal, P["deconv3_attention.weight"], N_ATT, g_ad2a)
-        elif HEAD_1X1:
-            pass                   # the fused head: weight, bias and input gradients in its norm backward below
-        else:
-            _wgrad_conv(P, G, "deconv3_attention", gal, ha["ad2"], 0, 1, 1)
-            ops.channel_sum(gal, 10, G.get("deconv3_attention.bias"), G.acc)
-            _dgrad_s1(P, "deconv3_attention", gal, 0, 1, g_ad2a)
         heads.append(("attention", ha, g_ad2a, 0))
     # ---- deconv2 / deconv1 of both heads
     g_h = Buf.empty(N, H // 4, W // 4, 256, 0, dev)

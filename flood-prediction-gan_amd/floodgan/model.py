@@ -135,6 +135,24 @@ class Pix2PixStep(PairedStep):
         self.last_masks = None
 
     def __call__(self, x, y):
+        N, C, H, W = x.shape
+        commit = None
+        if self.masks is not None:
+            masks = self.masks
+        elif self.G.dropout_rng == "host":
+            masks, commit = P2P.draw_dropout_deferred(N, H, W, x.device)
+        else:
+            masks = P2P.draw_dropout(N, H, W, self.G.dropout_rng, x.device)
+        self.last_masks = masks
+        try:
+            return self._iterate(x, y, masks)
+        finally:
+            # torch's CPU generator advanced past this iteration's Dropout draws -- also when the iteration raised
+            # (its masks were drawn: a retry must not reuse them); commit() raises if anything drew in between
+            if commit is not None:
+                commit()
+
+    def _iterate(self, x, y, masks):
         ws, _ = world()
         inv = 1.0 / ws
         N, C, H, W = x.shape
@@ -142,14 +160,6 @@ class Pix2PixStep(PairedStep):
         losses = torch.empty(4, dtype=torch.float32, device=dev)
         self.gflat.attach()
         self.dflat.attach()
-        commit = None
-        if self.masks is not None:
-            masks = self.masks
-        elif self.G.dropout_rng == "host":
-            masks, commit = P2P.draw_dropout_deferred(N, H, W, dev)
-        else:
-            masks = P2P.draw_dropout(N, H, W, self.G.dropout_rng, dev)
-        self.last_masks = masks
         fake, gS = P2P.gen_forward(self.gp, self.gb, x, masks=masks, training=True, save=True)
         dinp = X.disc_pack([(x, fake), (x, y)], C + 3)
         pred, dS = P2P.disc_forward(self.dp, self.db, dinp, groups=2, training=True, save=True)
@@ -184,8 +194,6 @@ class Pix2PixStep(PairedStep):
         self.gflat.finish()
         self.opt_g.step()
         self.last_output = fake
-        if commit is not None:             # torch's CPU generator advanced past this iteration's Dropout draws
-            commit()
         return losses
 
 

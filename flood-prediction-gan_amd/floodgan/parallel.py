@@ -21,6 +21,25 @@ def world():
     return 1, 0
 
 
+_force = False
+
+
+def set_force_collectives(on):
+    """Issue the gradient all-reduces even in a one-rank process group (they are then identities).  The
+    only way to execute the RCCL path -- ProcessGroupNCCL's stream beside the backward kernels, the
+    bucket hand-offs, the waits before Adam -- on a box with one GPU (`bench.py --rccl-world1`,
+    tests/test_gpu_rccl.py).  Returns the previous setting."""
+    global _force
+    prev, _force = _force, bool(on)
+    return prev
+
+
+def collectives_on():
+    """True when the step's gradient exchanges run: more than one rank, or a forced one-rank group."""
+    ws, _ = world()
+    return ws > 1 or (_force and dist.is_available() and dist.is_initialized())
+
+
 class FlatGrads:
     """Allocates one contiguous gradient buffer for `params` and points every p.grad at its
     slice (views stay valid as long as nobody sets p.grad = None).
@@ -71,8 +90,7 @@ class FlatGrads:
 
     def allreduce_sum(self, group=None):
         """In-place SUM across ranks (callers pre-scale by 1/world)."""
-        ws, _ = world()
-        if ws > 1:
+        if collectives_on():
             dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
 
     # ---- bucketed, overlapped SUM all-reduce
@@ -88,8 +106,7 @@ class FlatGrads:
         if i not in self._pending:
             return
         self._pending.remove(i)
-        ws, _ = world()
-        if ws > 1:
+        if collectives_on():
             self._handles.append(dist.all_reduce(self.buckets[i], op=dist.ReduceOp.SUM, group=self._group,
                                                  async_op=True))
 

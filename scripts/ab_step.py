@@ -1,7 +1,7 @@
 """A/B of engine switches on the full bs-8 512^2 training step, interleaved in ONE process (device
 clocks and boxes differ by several percent, so separate bench runs cannot resolve small gains).
   python scripts/ab_step.py f3_persistent [rounds] [steps] [values, default 0,1]
-Switches: f3_persistent, f3_sched, f3_order, f3_fill, f3_interleave, head_1x1, wgrad_f3, use_win, in_rows, presplit, ps_wide (values 4,5), ps_tall, ps_resid, stem_fwd, splitpix, d0_dgrad, in_nt, in_nt2, fused_head, quad, n1_rows (values: rows per block)."""
+Switches: f3_persistent, f3_sched, f3_order, f3_fill, f3_interleave, wgrad_f3, use_win, in_rows, presplit, ps_wide (values 4,5), ps_tall, ps_resid, stem_fwd, d0_dgrad, fused_head, n1_rows (values: rows per block)."""
 import os
 import sys
 import time
@@ -39,32 +39,18 @@ def switch(name, on):
         lib.fg_set_in_rows(int(on))
     elif name == "f3_interleave":
         lib.fg_set_f3_interleave(int(on))
-    elif name == "head_1x1":
-        from floodgan import executor
-        executor.HEAD_1X1 = bool(on)
     elif name == "use_win":
         ops.USE_WIN = bool(on)
     elif name == "stem_fwd":
         os.environ["FLOODGAN_STEM_FWD"] = str(int(on))
-    elif name == "in_nt2":
-        os.environ["FLOODGAN_IN_NT2_AB"] = str(int(on))
-    elif name == "in_nt":
-        os.environ["FLOODGAN_IN_NT_AB"] = str(int(on))
     elif name == "d0_dgrad":
         from floodgan import executor
         executor.D0_DGRAD = bool(on)
     elif name == "fused_head":
         from floodgan import executor
         executor.FUSED_HEAD = bool(on)
-    elif name == "splitpix":
-        from floodgan import executor
-        executor.SPLITPIX = bool(on)
     elif name == "n1_rows":
         ops.N1_ROWS = int(on)
-    elif name == "quad":
-        from floodgan import executor
-        executor.QUAD = bool(on)
-
     else:
         raise SystemExit(f"unknown switch {name}")
 

@@ -66,8 +66,13 @@ def deconv2(kind, dev):
     ops.in_apply(c, mean, rstd, 1, None, S, 0, presplit=True)
     P = {"t.weight": torch.randn(128, 64, 3, 3, device=dev) * 0.05, "t.bias": torch.zeros(64, device=dev)}
     Y = Buf.empty(N, 2 * H, 2 * H, 64, 0, dev)
-    X.QUAD = kind == "quad_stats"
-    return lambda: X._convT_fwd(P, "t", S, Y)
+    if kind == "quad_stats":
+        return lambda: X._convT_fwd(P, "t", S, Y)
+    from floodgan import plans as PL
+    maps = PL.phase_maps(P["t.weight"].shape, 3, 1, S.c)
+    wps = [ops.pack_weight(P["t.weight"], m) for m, _, _ in maps]
+    return lambda: ops.conv(PL.phase_problems(S, P["t.weight"].shape, 3, 1, Y, wps, maps, bias=P["t.bias"]),
+                            in_stats=True)
 
 
 def main():

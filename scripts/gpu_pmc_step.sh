@@ -2,18 +2,11 @@
 # Counter passes (rocprofv3 --pmc, kernel trace only) over ONE bench step (bs 8, 512^2) after one warm-up,
 # so that every kernel of the step gets its counters from the binary the bench runs.  Summarise with
 #   python scripts/pmc_step_summary.py gpurun_out/pmcstep_<tag> > profiles/.../<tag>_pmc_step.json
-# DIAG=1: the passes run scripts/diag_f3_one.py against the -DFG_F3_DIAG library instead (the
-# compute-only / no-split variants of the resblock forward; FG_F3_DIAG selects the mode).
 REPO="$(cd "$(dirname "$0")/.." && pwd)"
 OUT="$REPO/gpurun_out/pmcstep_${1:-run}"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-if [ -n "$DIAG" ]; then
-  CMD=(python3 "$REPO/scripts/diag_f3_one.py")
-  export FLOODGAN_LIB="$REPO/flood-prediction-gan_amd/build/diag/libfloodgan.so"
-else
-  CMD=(python3 "$REPO/bench.py" --workload "${WORKLOAD:-paired}" --steps 1 --warmup 1 --no-cpu-baseline)
-fi
+CMD=(python3 "$REPO/bench.py" --workload "${WORKLOAD:-paired}" --steps 1 --warmup 1 --no-cpu-baseline --no-fp32-math)
 [ -f "$OUT/avail.txt" ] || timeout -k 10 120 rocprofv3 -L > "$OUT/avail.txt" 2>&1
 i=0
 while read -r pass; do

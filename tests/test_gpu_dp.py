@@ -88,6 +88,47 @@ def _count_diff(a, b):
     return int((a.cpu() != b.cpu()).sum())
 
 
+def _flip_positions(a, b):
+    """{(network, D pass or None): [forward positions of the layers whose decisions differ]} of a paired step's
+    decision records (PairedStep.decisions): G's ReLU layers, D's LeakyReLU layers per pass (0 fake / 1 real of the
+    D step, 2 the G step), the L1 signs"""
+    pos_g = {"conv1": 0, "conv2": 1, "conv3": 2, **{f"block{i}": 3 + i for i in range(9)}}
+    out = {}
+    for net, passes in a.items():
+        for pi, (da, db) in enumerate(zip(passes, b[net])):
+            for k in da:
+                if _count_diff(da[k], db[k]):
+                    pos = (pos_g.get(k, 12 if k.startswith("deconv1") else 13) if net == "G" else
+                           {"model.0": 0, "model.2": 1, "model.5": 2, "model.8": 3}.get(k, 0))
+                    out.setdefault((net, pi if net == "D" else None), []).append(pos)
+    return out
+
+
+def _param_position(net, k):
+    """forward position of a parameter's layer in the numbering of _flip_positions (a conv that consumes a decided
+    activation sits half a step after it: its weight gradient reads the activation)"""
+    layer = k.rsplit(".", 1)[0]
+    if net == "discriminator":
+        return {"model.0": 0, "model.2": 1, "model.5": 2, "model.8": 3, "model.11": 4}[layer]
+    if layer.startswith("resnet_blocks."):
+        i, conv = layer.split(".")[1:3]
+        return 3 + int(i) - 0.5 + (0.5 if conv == "conv1" else 1.0)
+    return {"conv1": 0, "conv2": 1, "conv3": 2}.get(layer, 12 + (layer[7] == "2") + 2 * (layer[7] == "3") - 0.5)
+
+
+def _flip_reach(flips, net, k):
+    """True when a differing decision lies downstream of parameter k: its gradient then legitimately carries the
+    flip (one unit of backward flow passed or blocked, ~1/sqrt(elements) of the gradient: the 1e-3 envelope);
+    every other tensor keeps the 1e-5 bound.  A flip in D's G-step pass or in the L1 signs reaches all of G; a flip in
+    a D-step pass reaches D's layers up to the one that reads the activation."""
+    q = _param_position(net, k)
+    if net == "generator":
+        if flips.get(("D", 2)) or flips.get(("L1", None)):
+            return True
+        return any(q <= d + 0.5 for d in flips.get(("G", None), []))
+    return any(q <= d + 1 for pi in (0, 1) for d in flips.get(("D", pi), []))
+
+
 def _post_state(ranks, it):
     """the two-rank state after iteration `it`"""
     its = ranks[0]["iters"]
@@ -101,7 +142,8 @@ def test_two_rank_step_equals_single_rank(kind, n, res, tmp_path, report):
     runs the same iteration on the whole batch; in the paired step it also continues its G half on the two-rank
     discriminator after Adam(D) (PairedStep.d_after), as the oracle comparisons do.  Asserted per iteration:
       * the all-reduced gradients equal the single-process gradients: 1e-5 norm-relative (IN-cancelled biases
-        excluded, SURVEY.md §7.3) when both evaluations take the same activation / L1-sign decisions (counted);
+        excluded), widened to 1e-3 only for the tensors a differing activation / L1-sign decision
+        lies downstream of (counted and positioned; every tensor above 1e-5 is reported);
       * the losses: the two ranks' mean equals the single process's to 1e-5;
       * the update (U criterion, tests/test_gpu_northstar.py): every element whose first moment is decided --
         |m| above 10x the gradient's disagreement -- moves the same way (fraction 1.0) and the decided updates
@@ -131,13 +173,15 @@ def test_two_rank_step_equals_single_rank(kind, n, res, tmp_path, report):
             if kind == "paired":
                 step.d_after = {k: post[f"discriminator/{k}"].to(DEV) for k, _ in m.discriminator.named_parameters()}
             single = W.run(m, kind, x, y, 1)[0].double()
-            flips = _count_diff(_merge(rec["decisions"], ranks[1]["iters"][it]["decisions"]), step.decisions)
+            merged = _merge(rec["decisions"], ranks[1]["iters"][it]["decisions"])
+            flips = _count_diff(merged, step.decisions)
+            reach = _flip_positions(merged, step.decisions) if kind == "paired" else None
             mean = (ranks[0]["losses"][it].double() + ranks[1]["losses"][it].double()) / 2
             lrel = float(((mean - single).abs() / single.abs()).max())
             opt_state = {}
             for o in (m.optimizer_generator, m.optimizer_discriminator):
                 opt_state.update(o.state)
-            rows, bad = [], []
+            rows, bad, over = [], [], []
             for net, mod in W.nets(m, kind).items():
                 skip = skip_g if "generator" in net else skip_d
                 for k, p in mod.named_parameters():
@@ -150,10 +194,16 @@ def test_two_rank_step_equals_single_rank(kind, n, res, tmp_path, report):
                     agree, uerr, frac, perr = _update_agreement(rec["pre"]["state"][key], post[key], p_single,
                                                                 rec["grads"][key], p.grad, opt_state[p]["exp_avg"])
                     rows.append((net, k, ge, agree, uerr, frac, perr))
-                    if ge > (1e-5 if flips == 0 else 1e-3) or agree < 1.0 or uerr > NTOL:
+                    # 1e-5 unless a differing decision downstream of this tensor explains more (paired: by layer;
+                    # the cycle step's records are not positioned, so any flip there widens its networks' bounds)
+                    reached = flips > 0 and (reach is None or _flip_reach(reach, net, k))
+                    if ge > 1e-5:
+                        over.append((net, k, ge, reached))
+                    if ge > (1e-3 if reached else 1e-5) or agree < 1.0 or uerr > NTOL:
                         bad.append(rows[-1])
             report("dp_two_rank_vs_single_continuation", kind=kind, n=n, res=res, it=it, decisions_differing=flips,
-                   loss_rel=lrel, **u_summary(rows), bad=bad)
+                   loss_rel=lrel, **u_summary(rows), bad=bad, over_1e5=over,
+                   flip_layers={f"{a}{'' if b is None else b}": v for (a, b), v in (reach or {}).items()})
             assert flips <= 8, (it, flips)
             assert not bad, (it, bad)
             assert lrel < 1e-5, (it, mean, single)

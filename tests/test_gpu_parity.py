@@ -296,6 +296,62 @@ def test_conv_f3_tile_height_invariant(presplit):
         L.set_conv_math(prev)
 
 
+@pytest.mark.parametrize("cfg", [3, 10, 12])
+def test_conv_f3_batch_position_invariant(cfg):
+    """order bit 4 counts its 512-row blocks from the tile's image when an image holds a whole number of them, so a
+    sample's output does not depend on its position in the batch: 32 x 48 images are 1536 rows = 3 x 512,
+    so blocks counted from the batch's first row would flip the k order of every second image.  Each image of a
+    batch of 3 must equal its own batch-1 launch bit for bit, on 128- and 512-row tiles."""
+    from floodgan import _lib as L, ops, plans as PL
+    from floodgan.plans import Buf
+    prev = L.get_conv_math()
+    L.set_conv_math("f16x3")
+    try:
+        torch.manual_seed(31)
+        cin, cout, Hh, Ww = 64, 128, 32, 48
+        c = torch.randn(3, cin, Hh, Ww, dtype=torch.float64)
+        cb = buf_from(c, 0, "constant")
+        mean, rstd = ops.in_stats(cb)
+        X = Buf.empty(3, Hh, Ww, cin, 1, DEV)
+        ops.in_apply(cb, mean, rstd, 1, None, X, 1, presplit=True)
+        wd = (torch.randn(cout, cin, 3, 3, dtype=torch.float64) * 0.05).float().to(DEV)
+        m = PL.wmap_conv_fwd(wd.shape, cin)
+        wp = ops.pack_weight(wd, m)
+        L.set_f3_tile(cfg)
+        Y = Buf.empty(3, Hh, Ww, cout, 0, DEV)
+        ops.conv([PL.conv_problem(X, 1, 3, 1, wp, m, Y)])
+        img = X.t.numel() // 3
+        for i in range(3):
+            Xi = Buf(X.t[i * img:(i + 1) * img], 1, Hh, Ww, cin, 1)
+            Xi.t._fg_amax, Xi.t._fg_amax_ver = X.t._fg_amax, Xi.t._version     # the batch's scale slot
+            Xi.t._fg_presplit, Xi.t._fg_presplit_ver = True, Xi.t._version     # the producer's FG_PRESPLIT image
+            Yi = Buf.empty(1, Hh, Ww, cout, 0, DEV)
+            ops.conv([PL.conv_problem(Xi, 1, 3, 1, wp, m, Yi)])
+            assert torch.equal(Yi.t.view(-1), Y.t.view(3, -1)[i]), (cfg, i)
+    finally:
+        L.set_f3_tile(-1)
+        L.set_conv_math(prev)
+
+
+def test_paired_step_under_forced_tile():
+    """a whole paired step with a forced tile config (fg_set_f3_tile, a tuning hook): the quad-form launches
+    (deconv2, conv2's input gradient) keep their one tile instead of failing, and the pre-update losses
+    equal the default dispatch's to rounding"""
+    from floodgan import _lib as L
+    torch.manual_seed(3)
+    x = (torch.rand(2, 9, 64, 64) * 2 - 1).to(DEV)
+    y = (torch.rand(2, 3, 64, 64) * 2 - 1).to(DEV)
+    ref = _make_model().step_fn(x, y).cpu()
+    try:
+        for cfg in (4, 11):
+            L.set_f3_tile(cfg)
+            got = _make_model().step_fn(x, y).cpu()
+            assert torch.isfinite(got).all()
+            assert (got - ref).abs().max() <= 1e-5 * ref.abs().max(), (cfg, got, ref)
+    finally:
+        L.set_f3_tile(-1)
+
+
 @pytest.mark.parametrize("on", [0, 1, 2, 3])
 @pytest.mark.parametrize("case", [(256, 256, 3, 1, 1, "reflect", 40), (128, 256, 4, 2, 1, "constant", 34),
                                   (256, 512, 4, 1, 1, "constant", 17), (64, 128, 3, 2, 1, "constant", 36),
