@@ -21,7 +21,6 @@
 // (ds_read_b128: lane l reads row l&15, k-chunk l>>4) are bank-conflict free.
 // MFMA: v_mfma_f32_16x16x32_f16, three products per fragment pair (lh, hl, hh).
 #include <algorithm>
-#include <type_traits>
 
 #include "conv_common.hpp"
 
@@ -86,7 +85,7 @@ __device__ __forceinline__ int quad_yoff(const fg_conv_problem& P, int q) {
 // output buffer resource: byte offsets below kYRecords are stored, kYOOB is dropped (the host keeps every output
 // extent below kYRecords, f3_takes)
 constexpr int kYRecords = 0x7fffff00, kYOOB = 0x7ffffff0;
-// cache policy of the NHWC epilogue stores (aux operand: 2 = nt, streaming)
+// cache policy of the NHWC epilogue stores (aux operand: 2 = nt, streaming; FG_EPI_NT: a measurement build)
 #ifdef FG_EPI_NT
 constexpr int kEpiStorePolicy = 2;
 #else
@@ -190,11 +189,7 @@ __device__ __forceinline__ void wait_vmcnt_rt(int n) {
 // segment (r, pixel) is recorded beside its ring slot, and a wave runs the products of a column group (one
 // phase, TG*16 = q_n columns) only where q_mask says the group reads that segment; the epilogue scatters the
 // groups to their output pixels.
-// BST (with STATS): the epilogue statistics are the BACKWARD InstanceNorm sums of fg_conv_problem.bn_src (sum g',
-// sum g' xhat per 32-row block and column, max |g| per block) instead of (mean, M2) -- the statistics pass of the norm
-// backward that reads this output next is not needed (round 6)
-template <int BM, int BN, int WM, int WN, int NS, int SCH, bool STATS = false, bool PS = false, bool QUAD = false,
-          bool BST = false>
+template <int BM, int BN, int WM, int WN, int NS, int SCH, bool STATS = false, bool PS = false, bool QUAD = false>
 __global__ void __launch_bounds__((BM / WM) * (BN / WN) * 64, 1)
 conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
     constexpr int NWN = BN / WN;
@@ -584,7 +579,7 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
     // layout (mma_t): acc[tm][tn][r] is row m0 + tm*16 + fr, column n0 + tn*16 + 4g + r.
     constexpr int NSTV = TM * TN, NSTS = TM * TN * 4;   // stores per epilogue: dwordx4 (NHWC) / dword (strided)
     int issued = 0, done = 0, epi_issued = 0, epi_nst = NSTS;
-    auto epilogue = [&]() __attribute__((always_inline)) {
+    auto epilogue = [&]() {
         const fg_conv_problem& P = batch.p[cg.pi];
         const int mab = P.m_a * P.m_b, M = P.m_img * mab;
         const int act = P.act;
@@ -608,82 +603,10 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
                 ych[tn] = nc0[tn];
             }
 #pragma unroll
-            for (int r = 0; r < 4; ++r) bias4[tn][r] = (!BST && P.bias) ? P.bias[min(ych[tn] + r, P.n_out - 1)] : 0.f;
+            for (int r = 0; r < 4; ++r) bias4[tn][r] = P.bias ? P.bias[min(ych[tn] + r, P.n_out - 1)] : 0.f;
         }
         const bool full_n = cg.n0 + BN <= P.n_out;
-        if constexpr (BST) {
-            // the backward InstanceNorm sums of each 32-row block of this wave's rows (one image: mab % 32 == 0), per
-            // column: g = the stored value (no bias, no activation: f3_stats_ok), xhat from the saved pre-norm input
-            // bn_src (16-B loads at the store's (pixel, 4 channels)), g' = g act'(xhat); the block's two rows per lane
-            // summed in registers, then over the 16 lanes of a DPP row (fg::row_sum16).  Loads go out TH column
-            // blocks at a time (src of both rows, mean, rstd) with the accumulators still live.
-            constexpr int NB = WM / 32, TB = TM / NB, TH = TN < 2 ? TN : 2;
-            static_assert(WM % 32 == 0 && TB * 16 == 32 && TN % TH == 0, "32-row statistics blocks");
-#pragma unroll
-            for (int hb = 0; hb < NB; ++hb) {
-                const int rb0 = cg.m0 + wm * WM + hb * 32;
-                if (rb0 < M) {
-                    int bimg, ba, bb;
-                    fgc::decomp(rb0, P.m_b, mab, bimg, ba, bb);
-                    int soff[TB];
-#pragma unroll
-                    for (int tb = 0; tb < TB; ++tb) {
-                        int i2, a2, b2;
-                        fgc::decomp(min(rb0 + tb * 16 + fr, M - 1), P.m_b, mab, i2, a2, b2);
-                        soff[tb] = (int)(i2 * P.bn_sn + a2 * P.bn_sa + b2 * P.bn_sb);
-                    }
-                    const float* const mrow = P.bn_mean + (size_t)bimg * P.n_out;
-                    const float* const rrow = P.bn_rstd + (size_t)bimg * P.n_out;
-                    float* const dst0 = P.in_stats + (size_t)(rb0 / 32) * P.n_out * 2;
-                    float gmx = 0.f;
-#pragma unroll
-                    for (int t0 = 0; t0 < TN; t0 += TH) {
-                        f32x4 sv[TB][TH], mu[TH], rs[TH];
-#pragma unroll
-                        for (int t = 0; t < TH; ++t) {
-                            const int c = min(nc0[t0 + t], P.n_out - 4);     // (n_out % 4 == 0; past n_out: not stored)
-                            mu[t] = *reinterpret_cast<const f32x4*>(mrow + c);
-                            rs[t] = *reinterpret_cast<const f32x4*>(rrow + c);
-#pragma unroll
-                            for (int tb = 0; tb < TB; ++tb)
-                                sv[tb][t] = *reinterpret_cast<const f32x4*>(P.bn_src + soff[tb] + c);
-                        }
-#pragma unroll
-                        for (int t = 0; t < TH; ++t) {
-                            const int tn = t0 + t;
-                            f32x4 s1, s2;
-#pragma unroll
-                            for (int r = 0; r < 4; ++r) {
-                                float a1 = 0.f, a2 = 0.f;
-#pragma unroll
-                                for (int tb = 0; tb < TB; ++tb) {
-                                    const float gv = acc[hb * TB + tb][tn][r] * out_scale;
-                                    const float xh = (sv[tb][t][r] - mu[t][r]) * rs[t][r];
-                                    const float gp = gv * fg::act_grad(xh, P.bn_act);
-                                    a1 += gp;
-                                    a2 = fmaf(gp, xh, a2);
-                                    gmx = fmaxf(gmx, fabsf(gv));
-                                }
-                                s1[r] = fg::row_sum16(a1);
-                                s2[r] = fg::row_sum16(a2);
-                            }
-                            if (fr == 0) {
-                                float* const dst = dst0 + nc0[tn] * 2;
-#pragma unroll
-                                for (int r = 0; r < 4; ++r)
-                                    if (nc0[tn] + r < P.n_out) *reinterpret_cast<f32x2*>(dst + 2 * r) = f32x2{s1[r], s2[r]};
-                            }
-                        }
-                        // one batch of loads live at a time (the scheduler would otherwise hoist every batch's loads)
-                        __builtin_amdgcn_sched_barrier(0);
-                    }
-                    // max |g| of the block: over the wave, one atomic per block (the pre-split output's scale bound)
-#pragma unroll
-                    for (int off = 32; off > 0; off >>= 1) gmx = fmaxf(gmx, __shfl_xor(gmx, off));
-                    if (lane == 0) atomicMax(P.bn_gmax + bimg, __float_as_uint(gmx));
-                }
-            }
-        } else if (STATS && P.in_stats) {
+        if (STATS && P.in_stats) {
             // InstanceNorm partials of each 32-row block of this wave's rows (WM / 32 of them: tm blocks hb*TB ..
             // hb*TB+1, 16 rows each across the lanes of a DPP row), per column: two passes (mean, then M2) over the raw
             // accumulators -- the two rows of a lane summed in registers, then over the 16 lanes of the row
@@ -800,156 +723,6 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
     // MFMAs instead of one (every CU finishes its tile at the same time and the write burst queues).
     const bool pre_epi = SCH >= 3 && (alt_order & 8);
     bool pre_issued = false;
-    if constexpr (SCH == 8) {
-        // SCH 8, the stagger (MI355X_MICROARCH "Two waves per SIMD", item 9): the two waves of a SIMD run the same
-        // program, so with one barrier per stage they reach the stage's fragment reads together -- after every
-        // barrier the LDS serves 8 waves' A + B reads (128 KB) while no MFMA issues.  The second half of the waves
-        // (>= NW / 2: one per SIMD) run half a stage late: after reading stage s's A and group-0 B fragments and
-        // running group 0, a late wave reads its group-1 B fragments too and keeps them, with the A fragments, in
-        // registers across the barrier; its group-1 MFMAs run at the top of the next stage, while the early partner
-        // reads.  Registers: the held A + B are the ones a wave holds during its group-1 MFMAs anyway.  Same
-        // products in the same per-accumulator order as SCH 3: bit-identical.  Tile ends: the ring refill before
-        // the epilogue (pre_epi) is always on; a late wave's epilogue waits for its held group, at the top of the
-        // next stage (after that stage's pieces, so the stage waits count its stores as the youngest operations).
-        static_assert(PS && !QUAD && TN / TG == 2, "the stagger: pre-split operands, two column groups per stage");
-        constexpr int NP = A_GL + B_GL, PPG = (NP + 1) / 2;
-        const bool late = wave >= NW / 2;      // one role per wave
-        f32x4 vh[TM][2];
-        f16x8 hbh[TG], hbl[TG];
-        bool held = false, epi_held = false;
-        auto frags = [&](const f32x4 (&v)[TM][2], f16x8 (&ah)[TM], f16x8 (&al)[TM]) {
-#pragma unroll
-            for (int tm = 0; tm < TM; ++tm) {
-                ah[tm] = __builtin_bit_cast(f16x8, v[tm][0]);
-                al[tm] = __builtin_bit_cast(f16x8, v[tm][1]);
-            }
-        };
-        auto read_b = [&](int buf, int t0, f16x8 (&bh)[TG], f16x8 (&bl)[TG]) {
-            const char* sbuf = smem + buf * STAGE;
-#pragma unroll
-            for (int t = 0; t < TG; ++t) {
-                const char* rowp = sbuf + A_BYTES + (wn * WN + (t0 + t) * 16 + fr) * 64 + b_c;
-                bh[t] = *reinterpret_cast<const f16x8*>(rowp);
-                bl[t] = *reinterpret_cast<const f16x8*>(rowp + BN * 64);
-            }
-        };
-        auto mfma_grp = [&](int t0, const f16x8 (&ah)[TM], const f16x8 (&al)[TM], const f16x8 (&bh)[TG],
-                            const f16x8 (&bl)[TG]) {
-#pragma unroll
-            for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-                for (int t = 0; t < TG; ++t) {
-                    acc[tm][t0 + t] = mma_t(ah[tm], bh[t], acc[tm][t0 + t]);
-                    acc[tm][t0 + t] = mma_t(ah[tm], bl[t], acc[tm][t0 + t]);
-                }
-#pragma unroll
-            for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-                for (int t = 0; t < TG; ++t) acc[tm][t0 + t] = mma_t(al[tm], bh[t], acc[tm][t0 + t]);
-        };
-        auto held_group = [&]() __attribute__((always_inline)) {
-            f16x8 ah[TM], al[TM];
-            frags(vh, ah, al);
-            mfma_grp(TG, ah, al, hbh, hbl);
-            held = false;
-        };
-        // the tile's epilogue, then the next tile; false when the stream is done
-        auto finish_tile = [&]() __attribute__((always_inline)) {
-            epilogue();
-#pragma unroll
-            for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-                for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
-            ct += G;
-            if (ct >= total_tiles) return false;
-            setup_compute();
-            return true;
-        };
-        // the two roles as separate loops (a role is fixed per wave): in the early waves' loop the held registers are
-        // not live across the barrier, so its allocation is that of SCH 3
-        auto run = [&](auto late_tag) __attribute__((always_inline)) {
-            constexpr bool late = decltype(late_tag)::value;
-            bool drain = false;                   // late waves: the stream is staged out; only the held group is left
-            while (true) {
-                if (!drain) {
-                    wait_stage();
-                    __builtin_amdgcn_s_barrier();
-                    __builtin_amdgcn_sched_barrier(0);
-                    if (pre_issued) p_on = false;
-                    else issue_prep(nxt);
-                } else {
-                    p_on = false;
-                }
-                const bool had = late && held;    // the first half of the pieces goes out with the held group
-                if (had) {
-#pragma unroll
-                    for (int i = 0; i < PPG; ++i) issue_piece(i);
-                    held_group();
-                    if (epi_held) {
-                        epi_held = false;
-                        if (!finish_tile()) break;
-                    }
-                    // the next stage's fragment reads stay behind the held MFMAs (their registers are reused)
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-                load_a(cur, vh);
-                {
-                    f16x8 ah[TM], al[TM];
-                    frags(vh, ah, al);
-                    f16x8 bh[TG], bl[TG];
-                    read_b(cur, 0, bh, bl);
-                    if (!had) {
-#pragma unroll
-                        for (int i = 0; i < PPG; ++i) issue_piece(i);
-                    }
-                    if constexpr (late) {
-#pragma unroll
-                        for (int i = PPG; i < NP; ++i) issue_piece(i);
-                    }
-                    mfma_grp(0, ah, al, bh, bl);
-                    if constexpr (late) {
-                        __builtin_amdgcn_sched_barrier(0);
-                        read_b(cur, TG, hbh, hbl);
-                        held = true;
-                        // the held fragments are in registers before a barrier lets the DMA refill their ring slot
-                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                    } else {
-                        read_b(cur, TG, bh, bl);
-#pragma unroll
-                        for (int i = PPG; i < NP; ++i) issue_piece(i);
-                        mfma_grp(TG, ah, al, bh, bl);
-                    }
-                }
-                if (!pre_issued && issue_advance()) ++issued;
-                pre_issued = false;
-                ++done;
-                cur = cur == NS - 1 ? 0 : cur + 1;
-                nxt = nxt == NS - 1 ? 0 : nxt + 1;
-                if (++ckt == cg.nkt) {
-                    if (it < total_tiles) {
-                        __builtin_amdgcn_s_barrier();
-                        issue_prep(nxt);
-#pragma unroll
-                        for (int i = 0; i < NP; ++i) issue_piece(i);
-                        if (issue_advance()) ++issued;
-                        pre_issued = true;
-                    }
-                    // a late wave finishes the tile after its held group, at the top of the next stage; after the
-                    // stream's last tile that is one more pass without a stage (drain).  (The ISA test counts the
-                    // epilogue sites: one per loop.)
-                    if constexpr (late) {
-                        epi_held = true;
-                        drain = ct + G >= total_tiles;
-                    } else if (!finish_tile()) {
-                        break;
-                    }
-                }
-            }
-        };
-        if (late) run(std::true_type{});
-        else run(std::false_type{});
-        return;
-    }
     while (true) {
         wait_stage();
         __builtin_amdgcn_s_barrier();
@@ -1014,16 +787,7 @@ int g_f3_persist = 1; // fg_set_f3_persistent: 1 resident workgroups loop over t
                       // -- setup_issue() mid-stream, next tile's stages in flight over an epilogue --
                       // at small sizes)
 int g_f3_interleave = 1;  // fg_set_f3_interleave: 0 = problem-major tile order (A/B hook)
-int g_f3_sched = -1;  // fg_set_f3_sched: per-stage instruction order (kernel template SCH), -1 auto; 8 = the stagger
-                      // for the pre-split launches whose wave tile has two column groups (SCH 3 elsewhere)
-int g_f3_stagger = 0; // the automatic choice (-1) takes the stagger where it applies
-
-// the tiles with a backward-statistics (BST) instantiation: cfg 5 (the bench's resblock input gradients) and the
-// narrower tiles the automatic choice takes for smaller launches of a 256-output conv (cfgs 6, 7, 9)
-constexpr bool bst_cfg(int bm, int bn, int wm, int wn) {
-    return (bm == 256 && bn == 256 && wm == 64 && wn == 128) || (bm == 256 && bn == 128 && wm == 32 && wn == 128) ||
-           (bm == 256 && bn == 64 && wm == 32 && wn == 64) || (bm == 128 && bn == 64 && wm == 32 && wn == 64);
-}
+int g_f3_sched = -1;  // fg_set_f3_sched: per-stage instruction order (kernel template SCH), -1 auto
 
 template <int BM, int BN, int WM, int WN, int NS = 3>
 int launch_cfg(const ConvBatch& in, int nprob, hipStream_t stream) {
@@ -1053,7 +817,7 @@ int launch_cfg(const ConvBatch& in, int nprob, hipStream_t stream) {
         for (int i = 1; i < nprob; ++i) eq &= b.blk_start[i + 1] - b.blk_start[i] == b.blk_start[1];
         b.interleave = eq ? 1 : 0;
     }
-    const int sched = g_f3_sched >= 0 && g_f3_sched <= 5 ? g_f3_sched : 3;
+    const int sched = g_f3_sched >= 0 ? g_f3_sched : 3;
     bool stats = false;
     for (int i = 0; i < nprob; ++i) stats |= b.p[i].in_stats != nullptr;
     // pre-split A operands (every problem of the batch, checked by the caller): their own instantiations
@@ -1072,28 +836,6 @@ int launch_cfg(const ConvBatch& in, int nprob, hipStream_t stream) {
         return fg::fail(FG_ERR_INVALID, "conv_fwd_f3: the quad form runs on the 256 x 256 pre-split tile only");
     }
     if (b.p[0].x_presplit) {
-        if (b.p[0].bn_src) {
-            // the backward-statistics epilogue (fg_conv_problem.bn_src): one pre-split problem, the tiles the
-            // automatic choice gives a 256-output conv (f3_stats_ok)
-            if constexpr (bst_cfg(BM, BN, WM, WN)) {
-                hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 3, true, true, false, true>), dim3(grid),
-                                   dim3(NT), 0, stream, b, total, g_f3_alt);
-                return fg::launched("conv_fwd_f3_bst");
-            }
-            return fg::fail(FG_ERR_INVALID, "conv_fwd_f3: no backward-statistics instantiation for this tile");
-        }
-        if constexpr (WN == 128) {
-            // the stagger (SCH 8) where the wave tile has two column groups
-            if (g_f3_sched == 8 || (g_f3_sched < 0 && g_f3_stagger)) {
-                if (stats)
-                    hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 8, true, true>), dim3(grid), dim3(NT),
-                                       0, stream, b, total, g_f3_alt);
-                else
-                    hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 8, false, true>), dim3(grid), dim3(NT),
-                                       0, stream, b, total, g_f3_alt);
-                return fg::launched("conv_fwd_f3_presplit");
-            }
-        }
         if (stats) {
             hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 3, true, true>), dim3(grid), dim3(NT), 0,
                                stream, b, total, g_f3_alt);
@@ -1251,17 +993,6 @@ bool f3_stats_ok(const fg_conv_problem* probs, int nprob, int max_n) {
         const fg_conv_problem& p = probs[i];
         if ((p.m_a * p.m_b) % 32 || p.act != 0 || p.accumulate) return false;
     }
-    // the backward-statistics epilogue: one pre-split problem without bias on a tile with its instantiation
-    if (probs[0].bn_src) {
-        const fg_conv_problem& p = probs[0];
-        if (nprob != 1 || !p.x_presplit || p.q_n || p.bias || !p.bn_mean || !p.bn_rstd || !p.bn_gmax ||
-            p.n_out % 4 || ((uintptr_t)p.bn_src & 15) || ((uintptr_t)p.bn_mean & 15) || ((uintptr_t)p.bn_rstd & 15) ||
-            (p.bn_sn | p.bn_sa | p.bn_sb) % 4 || p.bn_sn < 0 || p.bn_sa < 0 || p.bn_sb < 0 ||
-            (long long)(p.m_img - 1) * p.bn_sn + (long long)(p.m_a - 1) * p.bn_sa + (long long)(p.m_b - 1) * p.bn_sb +
-                    p.n_out >= (1LL << 31) ||
-            !(cfg == 5 || cfg == 6 || cfg == 7 || cfg == 9))
-            return false;
-    }
     return true;
 }
 
@@ -1305,7 +1036,7 @@ FG_API int fg_set_f3_persistent(int on) {
 }
 
 FG_API int fg_set_f3_sched(int sched) {
-    if (sched < -1 || (sched > 5 && sched != 8)) return fg::fail(FG_ERR_INVALID, "fg_set_f3_sched: %d", sched);
+    if (sched < -1 || sched > 5) return fg::fail(FG_ERR_INVALID, "fg_set_f3_sched: %d", sched);
     g_f3_sched = sched;
     return 0;
 }

@@ -1346,14 +1346,10 @@ FG_API int fg_conv_fwd(const fg_conv_problem* probs, int nprob, hipStream_t stre
     }
     const bool f16 = (g_conv_math & FG_MATH_FWD_F16X3) != 0;
     const bool x6 = f16 || (g_conv_math & FG_MATH_FWD_X6) != 0;   // a split-math kernel
-    bool stats = false, bst = false;
-    for (int i = 0; i < nprob; ++i) {
-        stats |= probs[i].in_stats != nullptr;
-        bst |= probs[i].bn_src != nullptr;
-    }
-    if (bst && !stats) return fg::fail(FG_ERR_INVALID, "fg_conv_fwd: bn_src needs in_stats");
+    bool stats = false;
+    for (int i = 0; i < nprob; ++i) stats |= probs[i].in_stats != nullptr;
     // the generator stem (7x7 over 9 channels -> 64): its strip kernel, epilogue statistics included (conv_stem.hip)
-    if (f16 && nprob == 1 && ws == 2 && g_fwd_tile < 0 && stem_fwd_on() && !bst) {
+    if (f16 && nprob == 1 && ws == 2 && g_fwd_tile < 0 && stem_fwd_on()) {
         int rc = 0;
         if (fgc::launch_fwd_stem(probs[0], stream, &rc)) return rc;
     }
@@ -1435,8 +1431,7 @@ FG_API int fg_conv_fwd(const fg_conv_problem* probs, int nprob, hipStream_t stre
 FG_API int fg_conv_stats_ok(const fg_conv_problem* probs, int nprob) {
     if (!probs || nprob < 1 || nprob > 4) return 0;
     if (!(g_conv_math & FG_MATH_FWD_F16X3) || g_fwd_tile >= 0) return 0;
-    if (nprob == 1 && !probs[0].bn_src && stem_fwd_on() && fgc::stem_fwd_rows(probs[0]) && probs[0].m_b % 32 == 0)
-        return 1;
+    if (nprob == 1 && stem_fwd_on() && fgc::stem_fwd_rows(probs[0]) && probs[0].m_b % 32 == 0) return 1;
     int max_n = 0;
     for (int i = 0; i < nprob; ++i) {
         const fg_conv_problem& p = probs[i];

@@ -1047,141 +1047,8 @@ bool ok_view(const fg_view& v) { return v.ptr && v.n > 0 && v.h > 0 && v.w > 0 &
 // every 32-row block, merged in fp64 (S1 = sum 32 mean_i, S2 = sum M2_i + 32 mean_i^2) in two levels:
 // in_partials_reduce -- block = 64 channels x 4 row slices over one of `splits` ranges of an image's blocks
 // (coalesced 512-B rows of f32x2), fp64 partial sums into work; in_partials_finalize -- sums the splits.
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-// ---- backward statistics from the input-gradient conv's epilogue (round 6; fg_conv_problem.bn_src).  The epilogue
-// summed g' = g act'(xhat) and g' xhat over the interior values g of the padded-domain gradient; the reflect-pad fold
-// adds the border terms of every pixel within fp + 1 of the border (fold_extra), and the sums are linear in g:
-// this kernel adds sum over those pixels of extra * act'(xhat) * (1, xhat), and max |extra| for the pre-split bound.
-// block (border slice, image); thread = (pixel group, channel quad); fp32 per thread, fp64 across the block
-constexpr int kBorderBlocks = 8;
-__global__ void __launch_bounds__(NT) in_bwd_border_kernel(fg_view g, int fp, fg_view src, const float* __restrict__ mean,
-                                                          const float* __restrict__ rstd, int act,
-                                                          double* __restrict__ bpart2, float* __restrict__ bmax) {
-    const int C = src.c_alloc, L = C / 4, PG = NT / L;
-    const int n = blockIdx.y, h = src.h, w = src.w, bw = fp + 1;
-    const int gi = threadIdx.x / L, c4 = threadIdx.x - (threadIdx.x / L) * L;
-    // the band: rows 0 .. bw-1 and h-bw .. h-1 whole, then columns 0 .. bw-1 and w-bw .. w-1 of the rows between
-    const int nrow = 2 * bw * w, nb = nrow + 2 * bw * (h - 2 * bw);
-    f32x4 s1 = {0.f, 0.f, 0.f, 0.f}, s2 = s1;
-    unsigned mx = 0;
-    if (gi < PG) {
-        const f32x4 m = ld4(mean + (size_t)n * C + 4 * c4), r = ld4(rstd + (size_t)n * C + 4 * c4);
-        for (int i = blockIdx.x * PG + gi; i < nb; i += kBorderBlocks * PG) {
-            int y, x;
-            if (i < nrow) {
-                const int q = i / w;
-                y = q < bw ? q : h - 2 * bw + q;
-                x = i - q * w;
-            } else {
-                const int k = i - nrow, q = k / (2 * bw), e = k - q * 2 * bw;
-                y = bw + q;
-                x = e < bw ? e : w - 2 * bw + e;
-            }
-            const f32x4 ex = fold_extra(f32x4{0.f, 0.f, 0.f, 0.f}, g, fp, n, y, x, h, w, c4);
-            const f32x4 xh = (ld4(src.ptr + fg::vidx(src, n, y, x) + 4 * c4) - m) * r;
-            mx = max(mx, absbits4(ex));
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const float gp = ex[e] * fg::act_grad(xh[e], act);
-                s1[e] += gp;
-                s2[e] = fmaf(gp, xh[e], s2[e]);
-            }
-        }
-    }
-    __shared__ float red[NT][8];
-    __shared__ unsigned mred[NT / 64];
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) mx = max(mx, (unsigned)__shfl_xor((int)mx, off));
-    if ((threadIdx.x & 63) == 0) mred[threadIdx.x >> 6] = mx;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        red[threadIdx.x][e] = s1[e];
-        red[threadIdx.x][4 + e] = s2[e];
-    }
-    __syncthreads();
-    if (threadIdx.x < L) {
-        double a[8] = {0};
-        for (int gg = 0; gg < PG; ++gg)
-#pragma unroll
-            for (int e = 0; e < 8; ++e) a[e] += red[gg * L + threadIdx.x][e];
-        double* wk = bpart2 + ((size_t)(n * kBorderBlocks + blockIdx.x) * C + 4 * threadIdx.x) * 2;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            wk[2 * e] = a[e];
-            wk[2 * e + 1] = a[4 + e];
-        }
-    }
-    if (threadIdx.x == 0) {
-        unsigned v = 0;
-        for (int i = 0; i < NT / 64; ++i) v = max(v, mred[i]);
-        bmax[n * kBorderBlocks + blockIdx.x] = __uint_as_float(v);
-    }
-}
-
-// the coefficients of the apply pass from the epilogue's block sums (+ the border terms): block = (image, 16
-// channels), thread = (channel, one of 16 slices of the 32-row blocks), fp64, a fixed order (deterministic).  The
-// (IN-cancelled) conv-bias gradient's per-plane part -rstd * sum(xhat) * sum(g' xhat) / HW is exactly 0 here:
-// sum(xhat) over a normalised plane is 0 (the statistics pass summed its rounding noise).
-__global__ void __launch_bounds__(256) in_bwd_partials_finalize(const float* __restrict__ part, int rb_per_img, int C,
-                                                                 int HWi, const double* __restrict__ bpart2,
-                                                                 const float* __restrict__ bmax,
-                                                                 const unsigned* __restrict__ gmax,
-                                                                 const float* __restrict__ rstd, float* __restrict__ coef,
-                                                                 double* __restrict__ bpart,
-                                                                 float* __restrict__ split_slot) {
-    const int img = blockIdx.x, cl = threadIdx.x & 15, sl = threadIdx.x >> 4;
-    const int ch = blockIdx.y * 16 + cl;
-    double s1 = 0, s2 = 0;
-    if (ch < C) {
-        const float* base = part + ((size_t)img * rb_per_img * C + ch) * 2;
-#pragma unroll 8
-        for (int rb = sl; rb < rb_per_img; rb += 16) {
-            const f32x2 q = *reinterpret_cast<const f32x2*>(base + (size_t)rb * C * 2);
-            s1 += q[0];
-            s2 += q[1];
-        }
-        if (bpart2 && sl < kBorderBlocks) {
-            const double* b = bpart2 + ((size_t)(img * kBorderBlocks + sl) * C + ch) * 2;
-            s1 += b[0];
-            s2 += b[1];
-        }
-    }
-    __shared__ double red[256][2];
-    __shared__ unsigned bmx;
-    if (threadIdx.x == 0) bmx = 0;
-    red[threadIdx.x][0] = s1;
-    red[threadIdx.x][1] = s2;
-    __syncthreads();
-    if (sl == 0 && ch < C) {
-        for (int q = 1; q < 16; ++q) {
-            s1 += red[q * 16 + cl][0];
-            s2 += red[q * 16 + cl][1];
-        }
-        const int idx = img * C + ch;
-        const float c1 = (float)(s1 / HWi), c2 = (float)(s2 / HWi);
-        coef[(size_t)idx * 2] = c1;
-        coef[(size_t)idx * 2 + 1] = c2;
-        bpart[idx] = 0.0;
-        if (split_slot) {
-            // |g'| <= |interior g| + |fold extra| (each bounded by its max over the image)
-            float gmx = __uint_as_float(gmax[img]);
-            if (bpart2) {
-                float e = 0.f;
-                for (int k = 0; k < kBorderBlocks; ++k) e = fmaxf(e, bmax[img * kBorderBlocks + k]);
-                gmx += e;
-            }
-            const float b = rstd[idx] * (gmx + fabsf(c1) + sqrtf((float)(HWi - 1)) * fabsf(c2)) * 1.001f;
-            atomicMax(&bmx, __float_as_uint(b));
-        }
-    }
-    if (split_slot) {
-        __syncthreads();
-        if (threadIdx.x == 0)
-            atomicMax(reinterpret_cast<unsigned*>(split_slot) + ((img * gridDim.y + blockIdx.y) & (FG_AMAX_SHARDS - 1)), bmx);
-    }
-}
-
 constexpr int kPartialSplitsMax = 64;
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 __global__ void in_partials_reduce(const float* __restrict__ part, int nprob, int n_img, int rb_per_img, int c,
                                    int splits, double* __restrict__ work) {
@@ -1477,43 +1344,6 @@ FG_API int fg_in_bwd_presplit(fg_view gsrc, int fold_pad, fg_view gadd, fg_view 
                                         "dst (C=%d)", dst.c_alloc);
     return in_bwd_impl(gsrc, fold_pad, gadd, src, mean, rstd, act, dst, bias_grad, bias_accumulate, gsum, work, nullptr,
                        scale_slot, stream);
-}
-
-FG_API int fg_in_bwd_partials(fg_view gsrc, int fold_pad, fg_view src, const float* mean, const float* rstd, int act,
-                              fg_view dst, float* bias_grad, int bias_accumulate, const float* partials, int rb_per_img,
-                              const unsigned* gmax, double* work, float* absmax, float* scale_slot,
-                              hipStream_t stream) {
-    if (!ok_view(gsrc) || !ok_view(src) || !ok_view(dst) || !mean || !rstd || !work || !partials || !gmax ||
-        src.c_alloc % 4 || (NT % (src.c_alloc / 4)) != 0 || gsrc.c_alloc != src.c_alloc || dst.c_alloc != src.c_alloc ||
-        dst.h != src.h || dst.w != src.w || dst.n != src.n || rb_per_img * 32 != src.h * src.w)
-        return fg::fail(FG_ERR_INVALID, "fg_in_bwd_partials: bad args");
-    if (gsrc.h != src.h + 2 * fold_pad || gsrc.w != src.w + 2 * fold_pad || fold_pad < 0 ||
-        2 * (fold_pad + 1) > src.h || 2 * (fold_pad + 1) > src.w)
-        return fg::fail(FG_ERR_INVALID, "fg_in_bwd_partials: gsrc %dx%d vs src %dx%d fold %d", gsrc.h, gsrc.w, src.h,
-                        src.w, fold_pad);
-    if (scale_slot && (dst.c_alloc % 8 || ((uintptr_t)dst.ptr & 31)))
-        return fg::fail(FG_ERR_INVALID, "fg_in_bwd_partials: a pre-split dst needs C %% 8 == 0 and 32-B alignment");
-    const int C = src.c_alloc;
-    float* coef = reinterpret_cast<float*>(work + (size_t)src.n * C * MAX_CHUNKS * 3);
-    double* bpart = work + (size_t)src.n * C * MAX_CHUNKS * 3 + (size_t)src.n * C;
-    double* bpart2 = fold_pad ? work : nullptr;                                            // [n][kBorderBlocks][C][2]
-    float* bmax = reinterpret_cast<float*>(bpart + (size_t)src.n * C);                    // [n][kBorderBlocks]
-    if (fold_pad) {
-        hipLaunchKernelGGL(in_bwd_border_kernel, dim3(kBorderBlocks, src.n), dim3(NT), 0, stream, gsrc, fold_pad, src,
-                           mean, rstd, act, bpart2, bmax);
-        const int e = fg::launched("in_bwd_border");
-        if (e) return e;
-    }
-    hipLaunchKernelGGL(in_bwd_partials_finalize, dim3(src.n, (C + 15) / 16), dim3(256), 0, stream, partials, rb_per_img,
-                       C, src.h * src.w, bpart2, bmax, gmax, rstd, coef, bpart, scale_slot);
-    int e = fg::launched("in_bwd_partials_finalize");
-    if (e) return e;
-    const fg_view none = {nullptr, 0, 0, 0, 0, 0};
-    auto kern = in_nt2_on() ? in_bwd_apply_rows_kernel<true> : in_bwd_apply_rows_kernel<false>;
-    hipLaunchKernelGGL(kern, dim3(dst.n * (dst.h + 2 * dst.pad)), dim3(NT), 0, stream, gsrc, fold_pad, none, src, mean,
-                       rstd, coef, act, dst, reinterpret_cast<unsigned*>(scale_slot ? nullptr : absmax), bpart, bias_grad,
-                       bias_accumulate, ilog2(C / 4), scale_slot, HeadArgs{});
-    return fg::launched("in_bwd_apply_rows");
 }
 
 namespace {

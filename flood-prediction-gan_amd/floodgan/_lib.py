@@ -42,9 +42,7 @@ class fg_conv_problem(C.Structure):
                 ("n_out", C.c_int), ("ldw", C.c_int), ("act", C.c_int), ("accumulate", C.c_int),
                 ("w_split", C.c_int), ("x_absmax", C.c_void_p), ("w_absmax", C.c_void_p), ("jc", C.c_int),
                 ("in_stats", C.c_void_p), ("x_presplit", C.c_int),
-                ("q_n", C.c_int), ("q_mask", C.c_int), ("q_yoff", C.c_longlong * 4), ("q_soff", C.c_longlong),
-                ("bn_src", C.c_void_p), ("bn_sn", C.c_longlong), ("bn_sa", C.c_longlong), ("bn_sb", C.c_longlong),
-                ("bn_mean", C.c_void_p), ("bn_rstd", C.c_void_p), ("bn_act", C.c_int), ("bn_gmax", C.c_void_p)]
+                ("q_n", C.c_int), ("q_mask", C.c_int), ("q_yoff", C.c_longlong * 4), ("q_soff", C.c_longlong)]
 
 
 class fg_wgrad_problem(C.Structure):
@@ -160,8 +158,6 @@ SIGNATURES = {
     "fg_in_head_wgrad_workspace_floats": [C.c_int, C.c_int, C.c_int, C.c_int],
     "fg_in_bwd_presplit": [fg_view, C.c_int, fg_view, fg_view, C.c_void_p, C.c_void_p, C.c_int, fg_view, C.c_void_p,
                            C.c_int, fg_view, C.c_void_p, C.c_void_p, C.c_void_p],
-    "fg_in_bwd_partials": [fg_view, C.c_int, fg_view, C.c_void_p, C.c_void_p, C.c_int, fg_view, C.c_void_p, C.c_int,
-                           C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p],
     "fg_act_bwd": [fg_view, fg_view, C.c_int, C.c_void_p, C.c_void_p],
     "fg_channel_sum": [fg_view, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p],
     "fg_channel_sum_workspace_doubles": [C.c_int],

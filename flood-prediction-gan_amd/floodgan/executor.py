@@ -274,29 +274,17 @@ def _block_bwd(P, pre, b, grad, G):
     ops.in_bwd(gsrc, fold, gadd, cb2, b["mb2"], b["rb2"], FG_ACT_NONE, g_cb2, G.get(pre + "conv2.bias"), G.acc,
                gsum=g_h if lazy else None, presplit=ps)
     _wgrad_conv(P, G, pre + "conv2", g_cb2, b["rb"], 1, 3, 1, tag="resblock_conv_wgrad")
-    # gradient w.r.t. the reflect-padded relu output; its interior conv's epilogue also forms the norm's backward sums
-    bn = (b["cb1"], b["mb1"], b["rb1"], FG_ACT_RELU) if BWD_STATS_EPI else None
-    g_rbp, bst = _dgrad_s1_padded(P, pre + "conv2", g_cb2, bn=bn)
+    g_rbp = _dgrad_s1_padded(P, pre + "conv2", g_cb2)  # gradient w.r.t. the reflect-padded relu output
     g_cb1 = Buf.empty(N, Hh, Ww, Cc, 2, dev)
-    if bst is not None:
-        ops.in_bwd_partials(g_rbp, 1, b["cb1"], b["mb1"], b["rb1"], FG_ACT_RELU, g_cb1, bst, G.get(pre + "conv1.bias"),
-                            G.acc, presplit=ps)
-    else:
-        ops.in_bwd(g_rbp, 1, None, b["cb1"], b["mb1"], b["rb1"], FG_ACT_RELU, g_cb1, G.get(pre + "conv1.bias"), G.acc,
-                   presplit=ps)
+    ops.in_bwd(g_rbp, 1, None, b["cb1"], b["mb1"], b["rb1"], FG_ACT_RELU, g_cb1, G.get(pre + "conv1.bias"), G.acc,
+               presplit=ps)
     _wgrad_conv(P, G, pre + "conv1", g_cb1, b["h"] if b.get("h_ps") is None else b["h_ps"], 1, 3, 1,
                 tag="resblock_conv_wgrad")
-    g_hp, _ = _dgrad_s1_padded(P, pre + "conv1", g_cb1)
+    g_hp = _dgrad_s1_padded(P, pre + "conv1", g_cb1)
     return g_hp, 1, g_h                               # reflect-pad adjoint + residual path, summed lazily
 
 
-# round 6: the backward statistics of an InstanceNorm (sum g', sum g' xhat) formed in the epilogue of the input-gradient
-# conv that produces its incoming gradient (fg_conv_problem.bn_src; the resblocks' first norms, D's model.5 norm),
-# instead of a statistics pass over the gradient and the saved input.  FLOODGAN_BWD_STATS=0: the pass
-BWD_STATS_EPI = os.environ.get("FLOODGAN_BWD_STATS", "1") != "0"
-
-
-def _dgrad_s1_padded(P, name, gy, bn=None):
+def _dgrad_s1_padded(P, name, gy):
     """Input gradient of a 3x3 stride-1 conv that read a reflect-padded (1) input: the gradient over the
     whole (H+2) x (W+2) padded domain, as an unpadded Buf of that extent (the layout in_bwd / fold_add
     fold).  Computed as the H x W interior -- an output grid of H-px rows, which the pipelined kernel's
@@ -310,9 +298,7 @@ def _dgrad_s1_padded(P, name, gy, bn=None):
     m = PL.wmap_conv_dgrad_s1(w.shape, gy.c)
     wp = ops.pack_weight(w, m)
     out = Buf.empty(N, Hh, Ww, Cc, 1, gy.t.device)     # interior = padded rows / cols 1..H
-    # bn: the interior's epilogue also emits the backward sums of the norm this gradient feeds (the edge strips'
-    # fold terms are added by fg_in_bwd_partials): returns (padded gradient, handle or None)
-    bst = ops.conv([PL.conv_problem(gy, 1, 3, 1, wp, m, out)], tag="resblock_conv_dgrad", bn=bn)
+    ops.conv([PL.conv_problem(gy, 1, 3, 1, wp, m, out)], tag="resblock_conv_dgrad")
     # padded-domain position p reads gy rows / cols p-2 .. p (relative to gy's interior; rows -2, -1 and
     # H, H+1 are zero); out's interior origin is padded position 1.  Row strips: one row of the full
     # pack (gather row r at pack row r); column strips: packs of their single kernel column.
@@ -322,7 +308,7 @@ def _dgrad_s1_padded(P, name, gy, bn=None):
         ms = PL.wmap_conv_dgrad_s1_taps(w.shape, gy.c, (0, 1, 2), (col,))
         strips.append(PL.window_problem(gy, -1, x0, Hh, 1, 3, 1, ops.pack_weight(w, ms), ms, out, 0, ox))
     ops.conv(strips)
-    return out.padded(), bst
+    return out.padded()
 
 
 def _to_nchw(B):
@@ -361,10 +347,10 @@ def _wgrad_conv(P, G, name, gy, X, pad, k, stride, tag=None):
             (gy, X), tag=tag)
 
 
-def _dgrad_s1(P, name, gyp, pad_used, k, Y, bn=None):
+def _dgrad_s1(P, name, gyp, pad_used, k, Y):
     w = P[name + ".weight"]
     m = PL.wmap_conv_dgrad_s1(w.shape, gyp.c)
-    return ops.conv([PL.conv_problem(gyp, pad_used, k, 1, ops.pack_weight(w, m), m, Y)], bn=bn)
+    ops.conv([PL.conv_problem(gyp, pad_used, k, 1, ops.pack_weight(w, m), m, Y)])
 
 
 def _dgrad_s2(P, name, gy, k, Y=None, y_nchw=None, n_base=0, n_out=None, accumulate=0):
@@ -631,16 +617,11 @@ def disc_backward(P, S, g_pred, param_grads=True, grads_into=None, input_grad=No
         _wgrad_conv(P, G, "model.8", g_e3, a2, 1, 4, 1)
         G.ready(ready, "model.8")
     g_a2 = Buf.empty(N, a2.h, a2.w, 256, 0, dev)
-    bn = (S["e2"], S["m2"], S["r2"], FG_ACT_LRELU) if BWD_STATS_EPI else None
-    bst = _dgrad_s1(P, "model.8", g_e3, 2, 4, g_a2, bn=bn)
+    _dgrad_s1(P, "model.8", g_e3, 2, 4, g_a2)
     # model.5 (k4 s2 p1)
     g_e2 = Buf.empty(N, a2.h, a2.w, 256, 1, dev)
-    if bst is not None:
-        ops.in_bwd_partials(g_a2, 0, S["e2"], S["m2"], S["r2"], FG_ACT_LRELU, g_e2, bst,
-                            G.get("model.5.bias") if param_grads else None, presplit=ps)
-    else:
-        ops.in_bwd(g_a2, 0, None, S["e2"], S["m2"], S["r2"], FG_ACT_LRELU, g_e2,
-                   G.get("model.5.bias") if param_grads else None, presplit=ps)
+    ops.in_bwd(g_a2, 0, None, S["e2"], S["m2"], S["r2"], FG_ACT_LRELU, g_e2,
+               G.get("model.5.bias") if param_grads else None, presplit=ps)
     a1 = S["a1"]
     if param_grads:
         _wgrad_conv(P, G, "model.5", g_e2, a1, 1, 4, 2)

@@ -379,24 +379,19 @@ FUSED_IN_STATS = os.environ.get("FLOODGAN_FUSED_IN_STATS", "1") != "0"
 LAST_CONV_KERNEL = None    # the kernel family the last conv() launch ran (fg_last_launch; tests)
 
 
-def conv(probs, tag=None, in_stats=False, bn=None):
+def conv(probs, tag=None, in_stats=False):
     """Launch 1-4 fg_conv_problem dicts (plans.conv_problem / phase_problems) in one kernel
     (the row-strip window kernel for a lone eligible 7x7 conv, see win_eligible).  in_stats=True:
     the problems all write one output Buf (the 4 phases of a transposed conv, or a single conv) that an
     InstanceNorm reads next; when the pipelined kernel takes them, its epilogue also emits the norm's
-    statistics partials and conv returns (mean, rstd) per (image, channel), else None.
-    bn = (src Buf, mean, rstd, act) (round 6): the output is the gradient w.r.t. act(IN(src)); when the pipelined
-    kernel takes the problem, its epilogue emits the BACKWARD statistics of that norm (fg_conv_problem.bn_src) and
-    conv returns the handle in_bwd_partials takes, else None (the caller runs in_bwd's statistics pass)."""
-    if bn is not None:
-        return _conv(probs, True, tag, bn=bn)
+    statistics partials and conv returns (mean, rstd) per (image, channel), else None."""
     if USE_WIN and len(probs) == 1 and win_eligible(probs[0]):
         return conv_win(probs[0], tag)
     stats = _conv(probs, in_stats, tag)
     return None if stats is None else _merge_stats(*stats)
 
 
-def _conv(probs, in_stats=False, tag=None, bn=None):
+def _conv(probs, in_stats=False, tag=None):
     arr = (L.fg_conv_problem * len(probs))()
     f16 = L.fwd_f16x3()
     keep = {}
@@ -431,25 +426,11 @@ def _conv(probs, in_stats=False, tag=None, bn=None):
             s.w_absmax = wa.data_ptr()
             if CHECK_SCALES and wt.dtype == torch.float32:
                 check_scale(wt, wa, "fp32 weight")
-    gmax = None
-    if bn is not None and len(probs) == 1 and f16 and FUSED_IN_STATS:
-        src, mean, rstd, act = bn
-        gmax = torch.zeros(src.n, dtype=torch.int32, device=src.t.device)
-        s = arr[0]
-        s.bn_src = src.t.data_ptr() + 4 * src.off(0, 0)
-        s.bn_sn, s.bn_sa, s.bn_sb = src.s_img, src.s_row, src.c
-        s.bn_mean, s.bn_rstd, s.bn_act, s.bn_gmax = L.ptr(mean), L.ptr(rstd), int(act), gmax.data_ptr()
-        keep["bn"] = bn
     stats = _stats_partials(probs, arr) if (in_stats and FUSED_IN_STATS) else None
-    if gmax is not None and stats is None:          # the kernel does not take it: a plain launch, the pass runs
-        arr[0].bn_src = arr[0].bn_mean = arr[0].bn_rstd = arr[0].bn_gmax = None
-        gmax = None
     _timed(tag, lambda: L.check(_lib().fg_conv_fwd(arr, len(probs), L.stream_handle()), "conv_fwd"))
     global LAST_CONV_KERNEL
     LAST_CONV_KERNEL = L.last_launch()
     _wrote(*[p["y"][0] for p in probs])
-    if bn is not None:
-        return None if gmax is None else stats + (gmax,)
     return stats
 
 
@@ -824,25 +805,6 @@ def in_bwd(gsrc, fold_pad, gadd, src, mean, rstd, act, dst, bias_grad=None, bias
     L.check(_lib().fg_in_bwd(view(gsrc), fold_pad, view(gadd), view(src), L.ptr(mean), L.ptr(rstd), act, view(dst),
                              L.ptr(bias_grad), int(bias_accumulate), view(gsum), L.ptr(work),
                              L.ptr(_amax_out(dst)), L.stream_handle()), "in_bwd")
-
-
-def in_bwd_partials(gsrc, fold_pad, src, mean, rstd, act, dst, handle, bias_grad=None, bias_accumulate=False,
-                    presplit=False):
-    """in_bwd (no residual gradient) with the statistics pass replaced by the block sums the conv that wrote gsrc's
-    interior emitted in its epilogue (handle: conv(..., bn=...)'s return value); fg_in_bwd_partials"""
-    _, buf, n_img, rb, c, gmax = handle
-    assert n_img == src.n and c == src.c and rb * 32 == src.h * src.w
-    work = _work(src.n, src.c, src.t.device)
-    tail = (view(dst), L.ptr(bias_grad), int(bias_accumulate), L.ptr(buf), rb, L.ptr(gmax), L.ptr(work))
-    if presplit and presplit_fits(dst):
-        assert L.fwd_f16x3()
-        slot = _amax_out(dst)
-        L.check(_lib().fg_in_bwd_partials(view(gsrc), fold_pad, view(src), L.ptr(mean), L.ptr(rstd), act, *tail, None,
-                                          L.ptr(slot), L.stream_handle()), "in_bwd_partials")
-        _mark_presplit(dst)
-        return
-    L.check(_lib().fg_in_bwd_partials(view(gsrc), fold_pad, view(src), L.ptr(mean), L.ptr(rstd), act, *tail,
-                                      L.ptr(_amax_out(dst)), None, L.stream_handle()), "in_bwd_partials")
 
 
 def in_apply_head(src, mean, rstd, act, dst, pad_mode, w, b, n_out, Y):

@@ -119,18 +119,6 @@ typedef struct fg_conv_problem {
     int q_mask;
     long long q_yoff[4];
     long long q_soff;
-    /* Backward InstanceNorm statistics from the epilogue (round 6; models/model_architectures.py:343-345, 412-418,
-     * whose backward needs sum g' and sum g' xhat per plane).  bn_src set (with in_stats): the stored value g of row
-     * m = (img, a, b), column n is the gradient w.r.t. act(xhat), xhat = (bn_src[img*bn_sn + a*bn_sa + b*bn_sb + n]
-     * - bn_mean[img*n_out + n]) * bn_rstd[img*n_out + n], act = bn_act; instead of (mean, M2) the epilogue writes
-     * the block sums (sum g', sum g' xhat) of g' = g act'(xhat) at in_stats[(rb * n_out + n) * 2], and raises
-     * bn_gmax[img] (float bits) to max |g|.  Only the pipelined f16x3 kernel on pre-split operands takes it. */
-    const float* bn_src;
-    long long bn_sn, bn_sa, bn_sb;
-    const float* bn_mean;
-    const float* bn_rstd;
-    int bn_act;
-    unsigned* bn_gmax;
 } fg_conv_problem;
 
 /*
@@ -437,16 +425,6 @@ int fg_in_apply_dual(fg_view src, const float* mean, const float* rstd, int act,
 int fg_in_bwd_presplit(fg_view gsrc, int fold_pad, fg_view gadd, fg_view src, const float* mean,
                        const float* rstd, int act, fg_view dst, float* bias_grad, int bias_accumulate, fg_view gsum,
                        double* work, float* scale_slot, hipStream_t stream);
-
-/* Round 6: fg_in_bwd (no gadd / gsum) whose statistics pass is replaced by the block sums the input-gradient conv
- * that wrote gsrc's interior emitted in its epilogue (fg_conv_problem.bn_src: partials [n][rb_per_img][C][2] =
- * (sum g', sum g' xhat) per 32-pixel block, gmax[n] = max |g| as float bits).  The reflect-pad fold's border terms
- * (fold_pad > 0) are added by a small kernel over the fold band; then the coefficients (the conv-bias gradient's
- * per-plane part is exactly 0: sum xhat = 0 over a normalised plane) and the apply pass.  scale_slot non-NULL: dst
- * in the FG_PRESPLIT format (absmax ignored), as fg_in_bwd_presplit.  Replaces the same interfaces as fg_in_bwd. */
-int fg_in_bwd_partials(fg_view gsrc, int fold_pad, fg_view src, const float* mean, const float* rstd, int act,
-                       fg_view dst, float* bias_grad, int bias_accumulate, const float* partials, int rb_per_img,
-                       const unsigned* gmax, double* work, float* absmax, float* scale_slot, hipStream_t stream);
 
 /* The attention head Conv2d(64, n_out <= 16, 1) (models/model_architectures.py:334, :369) fused into the norm
  * passes of its input (the replaced interfaces: fg_in_apply + fg_conv1x1_fwd, fg_conv1x1_dgrad + fg_in_bwd).

@@ -1,7 +1,7 @@
 """A/B of engine switches on the full bs-8 512^2 training step, interleaved in ONE process (device
 clocks and boxes differ by several percent, so separate bench runs cannot resolve small gains).
   python scripts/ab_step.py f3_persistent [rounds] [steps] [values, default 0,1]
-Switches: f3_persistent, f3_sched, f3_order, f3_fill, f3_interleave, wgrad_f3, use_win, in_rows, presplit, ps_wide (values 4,5), ps_tall, ps_resid, stem_fwd, d0_dgrad, fused_head, bwd_stats, n1_rows (values: rows per block)."""
+Switches: f3_persistent, f3_sched, f3_order, f3_fill, f3_interleave, wgrad_f3, use_win, in_rows, presplit, ps_wide (values 4,5), ps_tall, ps_resid, stem_fwd, d0_dgrad, fused_head, n1_rows (values: rows per block)."""
 import os
 import sys
 import time
@@ -49,9 +49,6 @@ def switch(name, on):
     elif name == "fused_head":
         from floodgan import executor
         executor.FUSED_HEAD = bool(on)
-    elif name == "bwd_stats":
-        from floodgan import executor
-        executor.BWD_STATS_EPI = bool(on)
     elif name == "n1_rows":
         ops.N1_ROWS = int(on)
     else:

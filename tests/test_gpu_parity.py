@@ -879,64 +879,6 @@ def test_in_apply_dual(act, residual, pad_mode):
     assert bool(((dec - r).abs() <= 2.0 ** -21 * r.abs() + 4 * 2.0 ** -24 / s).all())
 
 
-@pytest.mark.parametrize("presplit", [False, True])
-@pytest.mark.parametrize("N,H,fold,act", [(2, 16, 1, 1), (8, 32, 1, 1), (8, 128, 1, 1), (3, 24, 0, 2), (4, 16, 0, 2)])
-def test_bwd_stats_epilogue(N, H, fold, act, presplit, report):
-    """Round 6: the InstanceNorm backward with its statistics from the input-gradient conv's epilogue
-    (fg_conv_problem.bn_src + fg_in_bwd_partials) vs the same backward with the statistics pass (fg_in_bwd), on the
-    same conv output: the resblock form (the reflect-padded 3x3 input gradient over the interior + edge strips, the
-    fold's border terms added by the band kernel; ReLU) at 16^2 bs 2 (128-row tiles), 32^2 bs 8 and the bench's 128^2
-    bs 8 (the 256 x 256 tile, two tiles per workgroup), and D's model.5 form (a 4x4 stride-1 input gradient, no fold,
-    LeakyReLU).  The norm's output gradient within 2e-6 (the block sums merge in another order), the pre-split output
-    decoding to it and its scale bound covering it; the (IN-cancelled) conv-bias gradient is exactly 0 on this path
-    (sum xhat = 0 over a normalised plane)."""
-    from floodgan import executor as X, ops, plans as PL
-    from floodgan.plans import Buf
-    C = 256
-    torch.manual_seed(41 + H)
-    k = 3 if fold else 4
-    src64 = torch.randn(N, C, H, H, dtype=torch.float64) * 1.4 + 0.3
-    src = buf_from(src64, 0, "constant")
-    mean, rstd = ops.in_stats(src)
-    w = (torch.randn(C, C, k, k, dtype=torch.float64) * 0.03).float().to(DEV)
-    P = {"conv.weight": w}
-    # the conv-output gradient: pre-split, zero border (k - 1)
-    gy64 = torch.randn(N, C, H - (0 if fold else 1), H - (0 if fold else 1), dtype=torch.float64)   # 4x4 s1 p1: H-1
-    gsrc = buf_from(gy64, 0, "constant")
-    gmean, grstd = ops.in_stats(gsrc)
-    gy = Buf.empty(N, gsrc.h, gsrc.w, C, 2, DEV)
-    ops.in_bwd(gsrc, 0, None, gsrc, gmean, grstd, 0, gy, None, presplit=True)
-    bn = (src, mean, rstd, act)
-    if fold:
-        gpad, handle = X._dgrad_s1_padded(P, "conv", gy, bn=bn)       # (the edge strips launch last)
-    else:
-        gpad = Buf.empty(N, H, H, C, 0, DEV)
-        handle = X._dgrad_s1(P, "conv", gy, 2, 4, gpad, bn=bn)
-        assert ops.LAST_CONV_KERNEL == "conv_fwd_f3_bst", ops.LAST_CONV_KERNEL
-    assert handle is not None
-    outs, bias = {}, {}
-    for path in ("epilogue", "pass"):
-        dst = Buf.empty(N, H, H, C, 1, DEV)
-        bg = torch.full((C,), float("nan"), device=DEV)
-        if path == "epilogue":
-            ops.in_bwd_partials(gpad, fold, src, mean, rstd, act, dst, handle, bg, presplit=presplit)
-        else:
-            ops.in_bwd(gpad, fold, None, src, mean, rstd, act, dst, bg, presplit=presplit)
-        outs[path], bias[path] = dst, bg
-    torch.cuda.synchronize()
-    if presplit:
-        dec = {p: _decode_presplit(outs[p], outs[p].t._fg_amax)[0] for p in outs}
-        bound = float(outs["epilogue"].t._fg_amax.max())
-        assert float(dec["epilogue"].abs().max()) <= bound, bound
-    else:
-        dec = {p: outs[p].t.double() for p in outs}
-    e = nrel(dec["epilogue"], dec["pass"])
-    report("bwd_stats_epilogue", N=N, H=H, fold=fold, act=act, presplit=presplit, rel=e)
-    assert e < 2e-6, e
-    assert torch.equal(bias["epilogue"], torch.zeros_like(bias["epilogue"]))
-    assert torch.isfinite(bias["pass"]).all()
-
-
 @pytest.mark.parametrize("N,H", [(2, 16), (1, 24)])
 def test_presplit_resblock_convs(N, H):
     """The resblock convs on FG_PRESPLIT operands (the pipelined forward, its input-gradient interior + edge strips,
@@ -977,7 +919,7 @@ def test_presplit_resblock_convs(N, H):
         ops.wgrad(PL.wgrad_conv(gys[presplit], xs[presplit], 1, 3, 1, C), PL.wmap_wgrad(w.shape, True, C, 3), dw)
         dw_p = torch.empty(C, C, 3, 3, device=DEV)      # gradient pre-split, activation fp32
         ops.wgrad(PL.wgrad_conv(gys[presplit], xs[False], 1, 3, 1, C), PL.wmap_wgrad(w.shape, True, C, 3), dw_p)
-        gxp, _ = X._dgrad_s1_padded(P, "conv", gys[presplit])
+        gxp = X._dgrad_s1_padded(P, "conv", gys[presplit])
         torch.cuda.synchronize()
         res[presplit] = (nchw(Y), dw.cpu(), dw_p.cpu(), _fold_cpu(nchw(gxp).double(), 1))
     for presplit in (False, True):
@@ -1033,59 +975,6 @@ def test_presplit_f3_tiles_and_stats(case, cfg, persistent):
     finally:
         L.set_f3_tile(-1)
         lib.fg_set_f3_persistent(1)
-
-
-@pytest.mark.parametrize("cfg", [0, 5, 6, 12])
-@pytest.mark.parametrize("case", [(256, 256, 3, 1, 1, 20, 2), (128, 128, 3, 2, 1, 26, 3), (256, 256, 3, 1, 1, 32, 8),
-                                  (64, 256, 1, 1, 0, 24, 2)])
-def test_presplit_stagger_bit_exact(case, cfg):
-    """the stagger (SCH 8: the late half of the waves keeps its last column group's fragments in registers across
-    the barrier and runs those MFMAs at the top of the next stage; its tile epilogues move there too) computes the
-    same products in the same per-accumulator order as SCH 3: outputs and epilogue statistics bit-identical, over
-    one workgroup per tile, the tile-crossing streams of 2 / 3 / 7 resident workgroups and the automatic grid, both
-    ring-refill orders, ragged tiles, one k chunk per tile (K = 64 < the ring depth of stages) and many"""
-    from floodgan import _lib as L, ops, plans as PL
-    from floodgan.plans import Buf
-    cin, cout, k, s, p, H, N = case
-    lib = L.load()
-    try:
-        L.set_f3_tile(cfg)
-        torch.manual_seed(19)
-        c = torch.randn(N, cin, H, H, dtype=torch.float64) * 1.1 + 0.3
-        cb = buf_from(c, 0, "constant")
-        mean, rstd = ops.in_stats(cb)
-        X = Buf.empty(N, H, H, cin, p, DEV)
-        ops.in_apply(cb, mean, rstd, 1, None, X, 1 if p else 0, presplit=True)
-        w = torch.randn(cout, cin, k, k, dtype=torch.float64) * 0.05
-        wd = w.float().to(DEV)
-        m = PL.wmap_conv_fwd(wd.shape, cin)
-        wp = ops.pack_weight(wd, m)
-        Ho = PL.out_size(H, k, s, p)
-        stats = (Ho * Ho) % 32 == 0
-        out = {}
-        for sched in (3, 8):
-            lib.fg_set_f3_sched(sched)
-            for order in (31, 23):
-                lib.fg_set_f3_order(order)
-                for persistent in (0, 1, 2, 3, 7):
-                    lib.fg_set_f3_persistent(persistent)
-                    Y = Buf.empty(N, Ho, Ho, cout, 0, DEV)
-                    Y.t.fill_(float("nan"))
-                    st = ops.conv([PL.conv_problem(X, p, k, s, wp, m, Y, bias=torch.ones(cout, device=DEV))],
-                                  in_stats=stats)
-                    out[sched, order, persistent] = (Y.t.clone(), None if st is None else [t.clone() for t in st])
-        torch.cuda.synchronize()
-        ref, ref_st = out[3, 31, 0]
-        assert not torch.isnan(ref).any()
-        for key, (y, st) in out.items():
-            assert torch.equal(y, ref), key
-            if stats:
-                assert st is not None and all(torch.equal(a, b) for a, b in zip(st, ref_st)), key
-    finally:
-        L.set_f3_tile(-1)
-        lib.fg_set_f3_persistent(1)
-        lib.fg_set_f3_sched(-1)
-        lib.fg_set_f3_order(L.F3_ORDER_DEFAULT)
 
 
 @pytest.mark.parametrize("persistent", [1, 3])
