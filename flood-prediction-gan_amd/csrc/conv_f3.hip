@@ -85,12 +85,6 @@ __device__ __forceinline__ int quad_yoff(const fg_conv_problem& P, int q) {
 // output buffer resource: byte offsets below kYRecords are stored, kYOOB is dropped (the host keeps every output
 // extent below kYRecords, f3_takes)
 constexpr int kYRecords = 0x7fffff00, kYOOB = 0x7ffffff0;
-// cache policy of the NHWC epilogue stores (aux operand: 2 = nt, streaming; FG_EPI_NT: a measurement build)
-#ifdef FG_EPI_NT
-constexpr int kEpiStorePolicy = 2;
-#else
-constexpr int kEpiStorePolicy = 0;
-#endif
 
 // one 1-KiB LDS-DMA piece (per-lane byte offset, per-stage scalar offset)
 __device__ __forceinline__ void dma_piece(char* dst, __amdgpu_buffer_rsrc_t r, int voff, int soff) {
@@ -666,7 +660,7 @@ conv_fwd_f3_kernel(const ConvBatch batch, int total_tiles, int alt_order) {
                     const bool ok = row_ok && (full_n || nc0[tn] < P.n_out);
                     if (accum && ok) v += *reinterpret_cast<const f32x4*>(P.y + roff + coff[tn]);
                     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), yr,
-                                                           ok ? (roff + coff[tn]) * 4 : kYOOB, 0, kEpiStorePolicy);
+                                                           ok ? (roff + coff[tn]) * 4 : kYOOB, 0, 0);
                 } else {
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
