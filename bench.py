@@ -77,12 +77,12 @@ def resblock_wgrad_bytes(batch, res):
 # with the InstanceNorm statistics epilogue; dgrad = the input-gradient interior; wgrad = the weight gradient
 RESBLOCK_KINDS = {
     "resblock_conv_fwd": dict(kernel="conv_fwd_f3_kernel<256,256,...,STATS>", bytes=resblock_conv_bytes,
-                              pmc=[os.path.join(ROOT, "profiles", "round5", "r5_pmc_resblock_fwd_stats_ps.json")]),
+                              pmc=[os.path.join(ROOT, "profiles", "round6", "r6_pmc_resblock_fwd_stats_ps.json")]),
     "resblock_conv_dgrad": dict(kernel="conv_fwd_f3_kernel<256,256,...> (input-gradient interior)",
                                 bytes=resblock_dgrad_bytes,
-                                pmc=[os.path.join(ROOT, "profiles", "round5", "r5_pmc_resblock_dgrad_ps.json")]),
+                                pmc=[os.path.join(ROOT, "profiles", "round6", "r6_pmc_resblock_dgrad_ps.json")]),
     "resblock_conv_wgrad": dict(kernel="conv_wgrad_f3_kernel<256,0,3>", bytes=resblock_wgrad_bytes,
-                                pmc=[os.path.join(ROOT, "profiles", "round5", "r5_pmc_resblock_wgrad_ps.json")]),
+                                pmc=[os.path.join(ROOT, "profiles", "round6", "r6_pmc_resblock_wgrad_ps.json")]),
 }
 
 
@@ -426,6 +426,10 @@ def main():
     ap.add_argument("--crop", type=int, default=None)
     ap.add_argument("--tile", type=int, default=1024, help="raw tile edge for --data tiles (xBD tiles are 1024)")
     ap.add_argument("--tiles", type=int, default=8, help="distinct synthetic tiles for --data tiles")
+    ap.add_argument("--timer-events", choices=["dispatch", "none", "device", "system"], default="dispatch",
+                    help="how ops.KernelTimer times the tagged kernels: events on the kernel's own dispatch packet "
+                         "(default), or marker events around the call with no / device / system release ('system' "
+                         "is torch.cuda.Event's, ~6 us of L2 writeback per event inside the timed step)")
     ap.add_argument("--rccl-world1", action="store_true",
                     help="execute the step's bucketed RCCL all-reduces in a one-rank process group (identities) "
                          "beside the same step without them: overhead and bit-identity (one-GPU evidence of the "
@@ -509,7 +513,8 @@ def main():
     if world > 1:
         dist.barrier()
     tag = "p2p_d_model8_fwd" if p2p else "resblock_conv_fwd"
-    timer = ops.KernelTimer([tag] + ([] if p2p or cycle else ["resblock_conv_dgrad", "resblock_conv_wgrad"]))
+    timer = ops.KernelTimer([tag] + ([] if p2p or cycle else ["resblock_conv_dgrad", "resblock_conv_wgrad"]),
+                            events=args.timer_events)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     with timer:
@@ -591,6 +596,10 @@ def main():
                                      pmc_traffic("conv_fwd_f3_kernel<256,256,...,STATS>" if nprod == 3 else None,
                                                  RESBLOCK_KINDS[tag]["pmc"])),
                          "avg_launch_ms": round(avg_ms, 4), "launches": len(durs),
+                         "timing": ("HIP events on the dispatch packet of every tagged launch of the timed steps (hipExtLaunchKernel)"
+                                    if args.timer_events == "dispatch" else
+                                    f"HIP marker events around every tagged launch of the timed steps "
+                                    f"(release: {args.timer_events})"),
                          "flop_per_launch": flops},
             "step_tflops": (None if cycle else
                             round((p2p_step_gflop_per_img(R) if p2p else STEP_GFLOP_PER_IMG_512 * (R / 512) ** 2)

@@ -820,10 +820,10 @@ int launch_cfg(const ConvBatch& in, int nprob, hipStream_t stream) {
         // the quad form (fg_conv_problem.q_n): pre-split operands on the 256 x 256 tile of 64 x 128 waves only
         if constexpr (BM == 256 && BN == 256 && WM == 64 && WN == 128) {
             if (stats)
-                hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 3, true, true, true>), dim3(grid), dim3(NT),
+                FG_LAUNCH((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 3, true, true, true>), dim3(grid), dim3(NT),
                                    0, stream, b, total, g_f3_alt);
             else
-                hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 3, false, true, true>), dim3(grid),
+                FG_LAUNCH((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 3, false, true, true>), dim3(grid),
                                    dim3(NT), 0, stream, b, total, g_f3_alt);
             return fg::launched("conv_fwd_f3_quad");
         }
@@ -831,11 +831,11 @@ int launch_cfg(const ConvBatch& in, int nprob, hipStream_t stream) {
     }
     if (b.p[0].x_presplit) {
         if (stats) {
-            hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 3, true, true>), dim3(grid), dim3(NT), 0,
+            FG_LAUNCH((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 3, true, true>), dim3(grid), dim3(NT), 0,
                                stream, b, total, g_f3_alt);
             return fg::launched("conv_fwd_f3_presplit");
         }
-        hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 3, false, true>), dim3(grid), dim3(NT), 0, stream, b,
+        FG_LAUNCH((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 3, false, true>), dim3(grid), dim3(NT), 0, stream, b,
                            total, g_f3_alt);
         return fg::launched("conv_fwd_f3_presplit");
     }
@@ -843,29 +843,29 @@ int launch_cfg(const ConvBatch& in, int nprob, hipStream_t stream) {
     // the launches without statistics keep the plain epilogue's code
     if constexpr (WM == 32) {
         if (stats) {
-            hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 3, true>), dim3(grid), dim3(NT), 0, stream, b,
+            FG_LAUNCH((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 3, true>), dim3(grid), dim3(NT), 0, stream, b,
                                total, g_f3_alt);
             return fg::launched("conv_fwd_f3");
         }
     }
     if (stats) return fg::fail(FG_ERR_INVALID, "conv_fwd_f3: epilogue statistics need a WM = 32 tile");
     if (sched == 5)
-        hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 5>), dim3(grid), dim3(NT), 0, stream, b, total,
+        FG_LAUNCH((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 5>), dim3(grid), dim3(NT), 0, stream, b, total,
                            g_f3_alt);
     else if (sched == 4)
-        hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 4>), dim3(grid), dim3(NT), 0, stream, b, total,
+        FG_LAUNCH((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 4>), dim3(grid), dim3(NT), 0, stream, b, total,
                            g_f3_alt);
     else if (sched == 3)
-        hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 3>), dim3(grid), dim3(NT), 0, stream, b, total,
+        FG_LAUNCH((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 3>), dim3(grid), dim3(NT), 0, stream, b, total,
                            g_f3_alt);
     else if (sched == 2)
-        hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 2>), dim3(grid), dim3(NT), 0, stream, b, total,
+        FG_LAUNCH((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 2>), dim3(grid), dim3(NT), 0, stream, b, total,
                            g_f3_alt);
     else if (sched == 1)
-        hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 1>), dim3(grid), dim3(NT), 0, stream, b, total,
+        FG_LAUNCH((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 1>), dim3(grid), dim3(NT), 0, stream, b, total,
                            g_f3_alt);
     else
-        hipLaunchKernelGGL((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 0>), dim3(grid), dim3(NT), 0, stream, b, total,
+        FG_LAUNCH((conv_fwd_f3_kernel<BM, BN, WM, WN, NS, 0>), dim3(grid), dim3(NT), 0, stream, b, total,
                            g_f3_alt);
     return fg::launched("conv_fwd_f3");
 }

@@ -1215,13 +1215,13 @@ template <class SM, int BM, int BN, int WM, int WN, int MINW, int PF, bool SWZ =
 int launch_fwd_x6(const ConvBatch& b, int total, bool vec, bool ws, hipStream_t stream) {
     constexpr int NT = (BM / WM) * (BN / WN) * 64;
     if (vec && ws)
-        hipLaunchKernelGGL((conv_fwd_x6_kernel<SM, BM, BN, WM, WN, true, true, MINW, PF, SWZ>), dim3(total), dim3(NT), 0, stream, b);
+        FG_LAUNCH((conv_fwd_x6_kernel<SM, BM, BN, WM, WN, true, true, MINW, PF, SWZ>), dim3(total), dim3(NT), 0, stream, b);
     else if (vec)
-        hipLaunchKernelGGL((conv_fwd_x6_kernel<SM, BM, BN, WM, WN, true, false, MINW, PF, SWZ>), dim3(total), dim3(NT), 0, stream, b);
+        FG_LAUNCH((conv_fwd_x6_kernel<SM, BM, BN, WM, WN, true, false, MINW, PF, SWZ>), dim3(total), dim3(NT), 0, stream, b);
     else if (ws)
-        hipLaunchKernelGGL((conv_fwd_x6_kernel<SM, BM, BN, WM, WN, false, true, MINW, PF, SWZ>), dim3(total), dim3(NT), 0, stream, b);
+        FG_LAUNCH((conv_fwd_x6_kernel<SM, BM, BN, WM, WN, false, true, MINW, PF, SWZ>), dim3(total), dim3(NT), 0, stream, b);
     else
-        hipLaunchKernelGGL((conv_fwd_x6_kernel<SM, BM, BN, WM, WN, false, false, MINW, PF, SWZ>), dim3(total), dim3(NT), 0, stream, b);
+        FG_LAUNCH((conv_fwd_x6_kernel<SM, BM, BN, WM, WN, false, false, MINW, PF, SWZ>), dim3(total), dim3(NT), 0, stream, b);
     return fg::launched("conv_fwd_x6");
 }
 
@@ -1229,9 +1229,9 @@ template <int BM, int BN, int WM, int WN>
 int launch_fwd(const ConvBatch& b, int total, bool vec, hipStream_t stream) {
     constexpr int NT = (BM / WM) * (BN / WN) * 64;
     if (vec)
-        hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, WM, WN, true>), dim3(total), dim3(NT), 0, stream, b);
+        FG_LAUNCH((conv_fwd_kernel<BM, BN, WM, WN, true>), dim3(total), dim3(NT), 0, stream, b);
     else
-        hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, WM, WN, false>), dim3(total), dim3(NT), 0, stream, b);
+        FG_LAUNCH((conv_fwd_kernel<BM, BN, WM, WN, false>), dim3(total), dim3(NT), 0, stream, b);
     return fg::launched("conv_fwd");
 }
 
@@ -1244,13 +1244,13 @@ int launch_wgrad_x6(const fg_wgrad_problem& p, bool vx, bool vp, hipStream_t str
     const int ta = (p.n_a + BA - 1) / BA, tk = (K + BKC - 1) / BKC;
     dim3 g(ta * tk * p.splits), blk(NT);
     if (vx && vp)
-        hipLaunchKernelGGL((conv_wgrad_x6_kernel<SM, BA, BKC, WA, WK, true, true, MINW, WAB>), g, blk, 0, stream, p, ta, tk);
+        FG_LAUNCH((conv_wgrad_x6_kernel<SM, BA, BKC, WA, WK, true, true, MINW, WAB>), g, blk, 0, stream, p, ta, tk);
     else if (vx)
-        hipLaunchKernelGGL((conv_wgrad_x6_kernel<SM, BA, BKC, WA, WK, true, false, MINW, WAB>), g, blk, 0, stream, p, ta, tk);
+        FG_LAUNCH((conv_wgrad_x6_kernel<SM, BA, BKC, WA, WK, true, false, MINW, WAB>), g, blk, 0, stream, p, ta, tk);
     else if (vp)
-        hipLaunchKernelGGL((conv_wgrad_x6_kernel<SM, BA, BKC, WA, WK, false, true, MINW, WAB>), g, blk, 0, stream, p, ta, tk);
+        FG_LAUNCH((conv_wgrad_x6_kernel<SM, BA, BKC, WA, WK, false, true, MINW, WAB>), g, blk, 0, stream, p, ta, tk);
     else
-        hipLaunchKernelGGL((conv_wgrad_x6_kernel<SM, BA, BKC, WA, WK, false, false, MINW, WAB>), g, blk, 0, stream, p, ta, tk);
+        FG_LAUNCH((conv_wgrad_x6_kernel<SM, BA, BKC, WA, WK, false, false, MINW, WAB>), g, blk, 0, stream, p, ta, tk);
     return fg::launched("conv_wgrad_x6");
 }
 
@@ -1277,13 +1277,13 @@ int launch_wgrad(const fg_wgrad_problem& p, bool vx, bool vp, hipStream_t stream
     const int total = ta * tk * p.splits;
     dim3 g(total), blk(NT);
     if (vx && vp)
-        hipLaunchKernelGGL((conv_wgrad_kernel<BA, BKC, WA, WK, true, true>), g, blk, 0, stream, p, ta, tk);
+        FG_LAUNCH((conv_wgrad_kernel<BA, BKC, WA, WK, true, true>), g, blk, 0, stream, p, ta, tk);
     else if (vx)
-        hipLaunchKernelGGL((conv_wgrad_kernel<BA, BKC, WA, WK, true, false>), g, blk, 0, stream, p, ta, tk);
+        FG_LAUNCH((conv_wgrad_kernel<BA, BKC, WA, WK, true, false>), g, blk, 0, stream, p, ta, tk);
     else if (vp)
-        hipLaunchKernelGGL((conv_wgrad_kernel<BA, BKC, WA, WK, false, true>), g, blk, 0, stream, p, ta, tk);
+        FG_LAUNCH((conv_wgrad_kernel<BA, BKC, WA, WK, false, true>), g, blk, 0, stream, p, ta, tk);
     else
-        hipLaunchKernelGGL((conv_wgrad_kernel<BA, BKC, WA, WK, false, false>), g, blk, 0, stream, p, ta, tk);
+        FG_LAUNCH((conv_wgrad_kernel<BA, BKC, WA, WK, false, false>), g, blk, 0, stream, p, ta, tk);
     return fg::launched("conv_wgrad");
 }
 

@@ -436,7 +436,7 @@ int launch_fwd_stem(const fg_conv_problem& p, hipStream_t stream, int* rc) {
     const int rows = stem_fwd_rows(p);
     if (!rows) return 0;
     const int grid = p.m_img * (p.m_b / ST_PX) * (p.m_a / rows);
-    hipLaunchKernelGGL(stem_fwd_kernel, dim3(grid), dim3(512), 0, stream, p, rows);
+    FG_LAUNCH(stem_fwd_kernel, dim3(grid), dim3(512), 0, stream, p, rows);
     *rc = fg::launched("stem_fwd");
     return 1;
 }
@@ -457,7 +457,7 @@ int stem_wgrad_rows(const fg_wgrad_problem& p) {
 int launch_wgrad_stem(const fg_wgrad_problem& p, hipStream_t stream, int* rc) {
     const int rows = stem_wgrad_rows(p);
     if (!rows) return 0;
-    hipLaunchKernelGGL(stem_wgrad_kernel, dim3(p.splits), dim3(512), 0, stream, p, rows);
+    FG_LAUNCH(stem_wgrad_kernel, dim3(p.splits), dim3(512), 0, stream, p, rows);
     *rc = fg::launched("stem_wgrad");
     return 1;
 }

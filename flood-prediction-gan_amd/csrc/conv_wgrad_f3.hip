@@ -288,25 +288,25 @@ int launch_wgrad_f3(const fg_wgrad_problem& p, hipStream_t stream, int* rc) {
             return 0;
         if (TA == 64) {
             if (ps == 1)
-                hipLaunchKernelGGL((conv_wgrad_f3_kernel<64, 0, 1>), grid, dim3(512), 0, stream, p, ta, tk);
+                FG_LAUNCH((conv_wgrad_f3_kernel<64, 0, 1>), grid, dim3(512), 0, stream, p, ta, tk);
             else if (ps == 2)
-                hipLaunchKernelGGL((conv_wgrad_f3_kernel<64, 0, 2>), grid, dim3(512), 0, stream, p, ta, tk);
+                FG_LAUNCH((conv_wgrad_f3_kernel<64, 0, 2>), grid, dim3(512), 0, stream, p, ta, tk);
             else
-                hipLaunchKernelGGL((conv_wgrad_f3_kernel<64, 0, 3>), grid, dim3(512), 0, stream, p, ta, tk);
+                FG_LAUNCH((conv_wgrad_f3_kernel<64, 0, 3>), grid, dim3(512), 0, stream, p, ta, tk);
         } else if (TA == 256) {
             if (ps == 1)
-                hipLaunchKernelGGL((conv_wgrad_f3_kernel<256, 0, 1>), grid, dim3(512), 0, stream, p, ta, tk);
+                FG_LAUNCH((conv_wgrad_f3_kernel<256, 0, 1>), grid, dim3(512), 0, stream, p, ta, tk);
             else if (ps == 2)
-                hipLaunchKernelGGL((conv_wgrad_f3_kernel<256, 0, 2>), grid, dim3(512), 0, stream, p, ta, tk);
+                FG_LAUNCH((conv_wgrad_f3_kernel<256, 0, 2>), grid, dim3(512), 0, stream, p, ta, tk);
             else
-                hipLaunchKernelGGL((conv_wgrad_f3_kernel<256, 0, 3>), grid, dim3(512), 0, stream, p, ta, tk);
+                FG_LAUNCH((conv_wgrad_f3_kernel<256, 0, 3>), grid, dim3(512), 0, stream, p, ta, tk);
         } else {
             if (ps == 1)
-                hipLaunchKernelGGL((conv_wgrad_f3_kernel<128, 1, 1>), grid, dim3(512), 0, stream, p, ta, tk);
+                FG_LAUNCH((conv_wgrad_f3_kernel<128, 1, 1>), grid, dim3(512), 0, stream, p, ta, tk);
             else if (ps == 2)
-                hipLaunchKernelGGL((conv_wgrad_f3_kernel<128, 1, 2>), grid, dim3(512), 0, stream, p, ta, tk);
+                FG_LAUNCH((conv_wgrad_f3_kernel<128, 1, 2>), grid, dim3(512), 0, stream, p, ta, tk);
             else
-                hipLaunchKernelGGL((conv_wgrad_f3_kernel<128, 1, 3>), grid, dim3(512), 0, stream, p, ta, tk);
+                FG_LAUNCH((conv_wgrad_f3_kernel<128, 1, 3>), grid, dim3(512), 0, stream, p, ta, tk);
         }
         *rc = fg::launched("conv_wgrad_f3_presplit");
         return 1;
@@ -314,15 +314,15 @@ int launch_wgrad_f3(const fg_wgrad_problem& p, hipStream_t stream, int* rc) {
     // measured: the interleaved staging pays off on the 128-row tiles only
     const int sch = g_wgrad_f3 == 3 || (g_wgrad_f3 == 2 && TA == 128) ? 1 : 0;
     if (TA == 64)
-        hipLaunchKernelGGL((conv_wgrad_f3_kernel<64, 0>), grid, dim3(512), 0, stream, p, ta, tk);
+        FG_LAUNCH((conv_wgrad_f3_kernel<64, 0>), grid, dim3(512), 0, stream, p, ta, tk);
     else if (TA == 256 && sch == 1)
-        hipLaunchKernelGGL((conv_wgrad_f3_kernel<256, 1>), grid, dim3(512), 0, stream, p, ta, tk);
+        FG_LAUNCH((conv_wgrad_f3_kernel<256, 1>), grid, dim3(512), 0, stream, p, ta, tk);
     else if (TA == 256)
-        hipLaunchKernelGGL((conv_wgrad_f3_kernel<256, 0>), grid, dim3(512), 0, stream, p, ta, tk);
+        FG_LAUNCH((conv_wgrad_f3_kernel<256, 0>), grid, dim3(512), 0, stream, p, ta, tk);
     else if (sch == 1)
-        hipLaunchKernelGGL((conv_wgrad_f3_kernel<128, 1>), grid, dim3(512), 0, stream, p, ta, tk);
+        FG_LAUNCH((conv_wgrad_f3_kernel<128, 1>), grid, dim3(512), 0, stream, p, ta, tk);
     else
-        hipLaunchKernelGGL((conv_wgrad_f3_kernel<128, 0>), grid, dim3(512), 0, stream, p, ta, tk);
+        FG_LAUNCH((conv_wgrad_f3_kernel<128, 0>), grid, dim3(512), 0, stream, p, ta, tk);
     *rc = fg::launched("conv_wgrad_f3");
     return 1;
 }

@@ -96,6 +96,12 @@ SIGNATURES = {
     "fg_last_launch": [],
     "fg_version": [],
     "fg_device_ok": [],
+    "fg_timing_event_create": [C.c_int, C.POINTER(C.c_void_p)],
+    "fg_timing_event_record": [C.c_void_p, C.c_void_p],
+    "fg_timing_event_elapsed": [C.c_void_p, C.c_void_p, C.POINTER(C.c_float)],
+    "fg_timing_event_destroy": [C.c_void_p],
+    "fg_timing_arm": [C.c_void_p, C.c_void_p],
+    "fg_timing_disarm": [],
     "fg_conv_fwd": [C.POINTER(fg_conv_problem), C.c_int, C.c_void_p],
     "fg_conv_stats_ok": [C.POINTER(fg_conv_problem), C.c_int],
     "fg_set_conv_math": [C.c_int],

@@ -331,12 +331,23 @@ _CONV_FIELDS = ("sxn", "sxa", "sxb", "sxr", "syn", "sya", "syb", "syc", "m_img",
                 "jp", "n_out", "ldw", "act", "accumulate")
 
 
+TIMER_EVENTS = {"system": 0, "device": 1, "none": 2, "dispatch": 2}
+
+
 class KernelTimer:
     """HIP-event timing of tagged launches on the current stream (used by bench.py to time the
-    dominant kernel live inside the timed region)."""
+    dominant kernel live inside the timed region).
 
-    def __init__(self, tags):
+    events: "dispatch" (default) attaches the start / stop events to the timed kernel's own dispatch packet
+    (fg_timing_arm -> hipExtLaunchKernel: the pipelined conv / weight-gradient launch of the tagged call), so the
+    stream carries no extra packet.  "system" / "device" / "none" record marker events around the tagged call with
+    that release scope; "system" is torch.cuda.Event's: every record writes back and invalidates L2, ~6 us per
+    event at the step's kernel boundaries, which the timed step then carries (profiles/round6/r6k_*)."""
+
+    def __init__(self, tags, events="dispatch"):
         self.tags = set(tags)
+        self.dispatch = events == "dispatch"
+        self.mode = TIMER_EVENTS[events]
         self.events = {t: [] for t in tags}
 
     def __enter__(self):
@@ -348,9 +359,42 @@ class KernelTimer:
         global _TIMER
         _TIMER = self._prev
 
+    def _event(self):
+        ev = C.c_void_p()
+        L.check(_lib().fg_timing_event_create(self.mode, C.byref(ev)), "timing_event_create")
+        return ev
+
+    def record_pair(self, tag, fn):
+        s, e = self._event(), self._event()
+        if self.dispatch:
+            L.check(_lib().fg_timing_arm(s, e), "timing_arm")
+            try:
+                out = fn()
+            finally:
+                pending = _lib().fg_timing_disarm()
+            if pending:
+                raise RuntimeError(f"KernelTimer: the call tagged {tag} launched no timed kernel")
+        else:
+            st = L.stream_handle()
+            L.check(_lib().fg_timing_event_record(s, st), "timing_event_record")
+            out = fn()
+            L.check(_lib().fg_timing_event_record(e, st), "timing_event_record")
+        self.events[tag].append((s, e))
+        return out
+
     def durations_ms(self):
-        torch.cuda.synchronize()
-        return {t: [s.elapsed_time(e) for s, e in ev] for t, ev in self.events.items()}
+        """waits for the recorded launches; returns {tag: [ms per launch]} and releases the events"""
+        out = {}
+        ms = C.c_float()
+        for t, ev in self.events.items():
+            out[t] = []
+            for s, e in ev:
+                L.check(_lib().fg_timing_event_elapsed(s, e, C.byref(ms)), "timing_event_elapsed")
+                out[t].append(ms.value)
+                L.check(_lib().fg_timing_event_destroy(s), "timing_event_destroy")
+                L.check(_lib().fg_timing_event_destroy(e), "timing_event_destroy")
+        self.events = {t: [] for t in self.tags}
+        return out
 
 
 _TIMER = None
@@ -361,12 +405,7 @@ def _timed(tag, fn):
     collects `tag`"""
     if _TIMER is None or tag not in _TIMER.tags:
         return fn()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    out = fn()
-    e.record()
-    _TIMER.events[tag].append((s, e))
-    return out
+    return _TIMER.record_pair(tag, fn)
 
 
 USE_WIN = True   # route eligible single convs to the row-strip kernel (fg_conv_win)

@@ -174,6 +174,19 @@ const char* fg_last_error(void);
 const char* fg_last_launch(void);
 int fg_version(void);
 int fg_device_ok(void);   /* 0 if a gfx950 device is current, else an error code */
+/* Timing events (bench.py's live per-kernel timing).  mode 0 = hipEventDefault (system-scope release, as
+ * torch.cuda.Event), 1 = hipEventReleaseToDevice, 2 = hipEventDisableSystemFence (no L2 writeback / invalidate
+ * at the record).  fg_timing_event_elapsed waits for `end`. */
+int fg_timing_event_create(int mode, void** ev);
+int fg_timing_event_record(void* ev, hipStream_t stream);
+int fg_timing_event_elapsed(void* start, void* end, float* ms);
+int fg_timing_event_destroy(void* ev);
+/* Arm the calling thread's next convolution kernel launch (the one conv kernel an fg_conv_fwd / fg_conv_wgrad
+ * call dispatches; not the pack / absmax / reduce helpers) with start / stop events attached to the dispatch
+ * itself (hipExtLaunchKernel: no marker packet in the stream).  fg_timing_disarm clears the arm and returns 1
+ * if no launch consumed it. */
+int fg_timing_arm(void* start, void* stop);
+int fg_timing_disarm(void);
 
 /* ---------------------------------------------------------------------------------------- */
 /* convolution engine (fp32 MFMA v_mfma_f32_32x32x2_f32)                                     */

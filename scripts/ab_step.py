@@ -1,7 +1,10 @@
 """A/B of engine switches on the full bs-8 512^2 training step, interleaved in ONE process (device
 clocks and boxes differ by several percent, so separate bench runs cannot resolve small gains).
   python scripts/ab_step.py f3_persistent [rounds] [steps] [values, default 0,1]
-Switches: f3_persistent, f3_sched, f3_order, f3_fill, f3_interleave, wgrad_f3, use_win, in_rows, presplit, ps_wide (values 4,5), ps_tall, ps_resid, stem_fwd, d0_dgrad, fused_head, n1_rows (values: rows per block)."""
+Switches: timer (values 0 = no KernelTimer, 1/2/3 = bench's KernelTimer with marker events of system / device / no
+release, 4 = events on the dispatch packet),
+f3_persistent, f3_sched, f3_order, f3_fill, f3_interleave, wgrad_f3, use_win, in_rows, presplit, ps_wide (values 4,5), ps_tall, ps_resid, stem_fwd, d0_dgrad, fused_head, n1_rows (values: rows per block)."""
+import contextlib
 import os
 import sys
 import time
@@ -49,6 +52,8 @@ def switch(name, on):
     elif name == "fused_head":
         from floodgan import executor
         executor.FUSED_HEAD = bool(on)
+    elif name == "timer":
+        pass                                      # applied around the timed loop (main)
     elif name == "n1_rows":
         ops.N1_ROWS = int(on)
     else:
@@ -69,18 +74,27 @@ def main():
         switch(name, on)
         m.step_fn(x, y).cpu()
     res = {v: [] for v in vals}
+    kinds = {v: {} for v in vals}
+    tags = ["resblock_conv_fwd", "resblock_conv_dgrad", "resblock_conv_wgrad"]
     for _ in range(rounds):
         for on in vals:
             switch(name, on)
+            timer = (ops.KernelTimer(tags, events=["system", "device", "none", "dispatch"][on - 1])
+                     if name == "timer" and on > 0 else contextlib.nullcontext())
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            for _ in range(steps):
-                m.step_fn(x, y).cpu()
+            with timer:
+                for _ in range(steps):
+                    m.step_fn(x, y).cpu()
             torch.cuda.synchronize()
             res[on].append((time.perf_counter() - t0) / steps * 1e3)
+            if name == "timer" and on > 0:
+                for t, d in timer.durations_ms().items():
+                    kinds[on].setdefault(t, []).extend(d)
     for on in vals:
         v = sorted(res[on])
-        print(f"{name}={on}: ms/step min {v[0]:.2f} median {v[len(v) // 2]:.2f}  ({8e3 / v[0]:.1f} img/s best)")
+        k = "  ".join(f"{t.split('_')[-1]} {sum(d) / len(d) * 1e3:.1f} us" for t, d in kinds[on].items() if d)
+        print(f"{name}={on}: ms/step min {v[0]:.2f} median {v[len(v) // 2]:.2f}  ({8e3 / v[0]:.1f} img/s best)  {k}")
 
 
 if __name__ == "__main__":
