@@ -307,7 +307,9 @@ def _dgrad_s1_padded(P, name, gy):
     for col, x0, ox in ((2, 0, -1), (0, Ww - 1, Ww)):                                               # columns 0, W+1
         ms = PL.wmap_conv_dgrad_s1_taps(w.shape, gy.c, (0, 1, 2), (col,))
         strips.append(PL.window_problem(gy, -1, x0, Hh, 1, 3, 1, ops.pack_weight(w, ms), ms, out, 0, ox))
-    ops.conv(strips)
+    # 24 k-steps of K = 768 per tile: ~31-33 us on every tile shape (128 x 64 auto, 128 x 128, 256 x 64, ...:
+    # profiles/round6/r6m_ab_strip_tile_not_kept.log)
+    ops.conv(strips, tag="resblock_dgrad_strips")
     return out.padded()
 
 

@@ -80,7 +80,8 @@ def main():
         for on in vals:
             switch(name, on)
             timer = (ops.KernelTimer(tags, events=["system", "device", "none", "dispatch"][on - 1])
-                     if name == "timer" and on > 0 else contextlib.nullcontext())
+                     if name == "timer" and on > 0 else
+                     ops.KernelTimer(tags + ["resblock_dgrad_strips"]) if name != "timer" else contextlib.nullcontext())
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             with timer:
@@ -88,12 +89,12 @@ def main():
                     m.step_fn(x, y).cpu()
             torch.cuda.synchronize()
             res[on].append((time.perf_counter() - t0) / steps * 1e3)
-            if name == "timer" and on > 0:
+            if name != "timer" or on > 0:
                 for t, d in timer.durations_ms().items():
                     kinds[on].setdefault(t, []).extend(d)
     for on in vals:
         v = sorted(res[on])
-        k = "  ".join(f"{t.split('_')[-1]} {sum(d) / len(d) * 1e3:.1f} us" for t, d in kinds[on].items() if d)
+        k = "  ".join(f"{t.split('_')[-1]} {sum(d) / len(d) * 1e3:.1f} us" for t, d in sorted(kinds[on].items()) if d)
         print(f"{name}={on}: ms/step min {v[0]:.2f} median {v[len(v) // 2]:.2f}  ({8e3 / v[0]:.1f} img/s best)  {k}")
 
 
