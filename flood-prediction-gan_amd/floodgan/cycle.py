@@ -97,9 +97,6 @@ class CycleStep:
         # every image a generator or discriminator sees; without (C == 3) nothing is cat'ed
         cond = x[:, 3:] if C > 3 else None
         losses = torch.zeros(10, dtype=torch.float32, device=dev)
-        self.gflat.attach()
-        self.dflat.attach()
-        g1g, g2g = self._grads(self.g1), self._grads(self.g2)
 
         def ready(flat, tag):
             return lambda name: flat.ready(f"{tag}.{name}")
@@ -128,6 +125,10 @@ class CycleStep:
         # ---- generator backward: second round first; its input gradient, plus the frozen
         # discriminator's, is d/d(first-round output).  A generator's gradient buckets are complete
         # (and start their all-reduce) in its last backward of the iteration.
+        # the flat gradient views, attached once the forward is queued (the host checks overlap the GPU's work)
+        self.gflat.attach()
+        self.dflat.attach()
+        g1g, g2g = self._grads(self.g1), self._grads(self.g2)
         self.gflat.begin(self.group)
         last1 = None if self.identity else ready(self.gflat, "g1")
         last2 = None if self.identity else ready(self.gflat, "g2")

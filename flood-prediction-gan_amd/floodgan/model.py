@@ -62,8 +62,8 @@ class PairedStep:
         dev = x.device
         C = x.shape[1]
         losses = torch.empty(4, dtype=torch.float32, device=dev)
-        self.gflat.attach()
-        self.dflat.attach()
+        # (the flat gradient views are attached right before each backward: the per-parameter checks then run on
+        # the host while the GPU works through the forward instead of ahead of the step's first launch)
         # generator forward                                           (models/model.py:615)
         fake, mask, gS = X.gen_forward(self.gp, x, save=True)
         # ---- discriminator step: fake (detached) and real in one 2N batch   (:620-633)
@@ -74,6 +74,7 @@ class PairedStep:
         ops.mse_const(pred[N:], 1.0, 0.5 * inv, losses[0:1], g_pred[N:])
         rec = {"G": [X.gen_act_decisions(gS)], "D": [X.disc_act_decisions(dS, 0, N), X.disc_act_decisions(dS, N)]} \
             if self.record_decisions else None
+        self.dflat.attach()
         self.dflat.begin(self.group)
         X.disc_backward(self.dp, dS, g_pred, param_grads=True, grads_into=self._grads(self.dp),
                         ready=self.dflat.ready)
@@ -99,6 +100,7 @@ class PairedStep:
             rec["L1"] = [{"l1": torch.sign(fake.detach() - y)}]   # the L1 term's sign decisions (-1 / 0 / +1)
             self.decisions = rec
         del dS, dinp
+        self.gflat.attach()
         self.gflat.begin(self.group)
         X.gen_backward(self.gp, gS, g_fake, grads_into=self._grads(self.gp), ready=self.gflat.ready)
         del gS
@@ -158,8 +160,6 @@ class Pix2PixStep(PairedStep):
         N, C, H, W = x.shape
         dev = x.device
         losses = torch.empty(4, dtype=torch.float32, device=dev)
-        self.gflat.attach()
-        self.dflat.attach()
         fake, gS = P2P.gen_forward(self.gp, self.gb, x, masks=masks, training=True, save=True)
         dinp = X.disc_pack([(x, fake), (x, y)], C + 3)
         pred, dS = P2P.disc_forward(self.dp, self.db, dinp, groups=2, training=True, save=True)
@@ -169,6 +169,7 @@ class Pix2PixStep(PairedStep):
         rec = {"G": [P2P.gen_act_decisions(gS)], "D": [P2P.disc_act_decisions(dS, 0, N),
                                                        P2P.disc_act_decisions(dS, N)]} \
             if self.record_decisions else None
+        self.dflat.attach()
         self.dflat.begin(self.group)
         P2P.disc_backward(self.dp, dS, g_pred, param_grads=True, grads_into=self._grads(self.dp),
                           ready=self.dflat.ready)
@@ -188,6 +189,7 @@ class Pix2PixStep(PairedStep):
             rec["L1"] = [{"l1": torch.sign(fake.detach() - y)}]   # the L1 term's sign decisions (-1 / 0 / +1)
             self.decisions = rec
         del dS, dinp
+        self.gflat.attach()
         self.gflat.begin(self.group)
         P2P.gen_backward(self.gp, gS, g_fake, grads_into=self._grads(self.gp), ready=self.gflat.ready)
         del gS
