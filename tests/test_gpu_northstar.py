@@ -434,6 +434,61 @@ def test_check_scales_bench_loop_25_steps(report):
     assert counts.get("split_copy", 0) > 0, counts
 
 
+def test_f16x3_tracks_exact_fp32_30_steps_512(report):
+    """The headline's conv math (f16x3) against the exact-fp32 MFMA math over 30 consecutive training steps at
+    512x512, batch 2, from the same seed-47 initialisation and the same batches (4 distinct, cycled), with no teacher
+    forcing: the per-step losses and every parameter's total update (p_30 - p_0).  A GAN trajectory amplifies any
+    rounding difference (flipped ReLU / L1 kinks, Adam-normalised small gradients), so the yardstick is how far two
+    fp32-grade evaluations drift apart on the same trajectory: the exact-fp32 run against (a) the bf16x6 math
+    (fp32-equivalent split bf16 products) and (b) itself with the inputs perturbed by one ulp.  f16x3 must stay
+    within 3x the larger control.  (The IN-cancelled conv biases, whose updates are Adam-normalised rounding noise
+    in any evaluation, are reported apart.)"""
+    from floodgan import _lib as L
+    steps = 30
+    batches = [tuple(t.to(DEV) for t in _inputs(2, seed=900 + b)) for b in range(4)]
+    g = torch.Generator(device="cpu").manual_seed(3)
+    ulp = [tuple(t * (1 + torch.where(torch.rand(t.shape, generator=g) < 0.5, -1.0, 1.0).to(DEV) * 2.0 ** -23)
+                 for t in bt) for bt in batches]
+    skip_g, skip_d = O.cancelled_biases()
+    runs = {}
+    prev = L.get_conv_math()
+    try:
+        for arm, math, data in (("f16x3", "f16x3", batches), ("fp32", "fp32", batches), ("bf16x6", "bf16x6", batches),
+                                ("fp32_ulp", "fp32", ulp)):
+            L.set_conv_math(math)
+            m = _model()
+            nets = {"generator": m.generator, "discriminator": m.discriminator}
+            p0 = {f"{n}/{k}": p.detach().double().clone() for n, mod in nets.items() for k, p in mod.named_parameters()}
+            losses = torch.stack([m.step_fn(*data[s % 4]).cpu().double() for s in range(steps)])
+            upd = {f"{n}/{k}": p.detach().double() - p0[f"{n}/{k}"] for n, mod in nets.items()
+                   for k, p in mod.named_parameters()}
+            runs[arm] = (losses, upd)
+    finally:
+        L.set_conv_math(prev)
+    l32, u32 = runs["fp32"]
+    out = {}
+    for arm in ("f16x3", "bf16x6", "fp32_ulp"):
+        la, ua = runs[arm]
+        lrel = ((la - l32).abs() / l32.abs()).max(dim=1).values
+        rows = {}
+        for key in u32:
+            net, k = key.split("/", 1)
+            rows[key] = (nrel(ua[key], u32[key]), k in (skip_g if net == "generator" else skip_d))
+        kept = {k: v for k, (v, c) in rows.items() if not c}
+        worst_key = max(kept, key=kept.get)
+        out[arm] = dict(loss_rel_max=float(lrel.max()), loss_rel_per_step=[float(v) for v in lrel],
+                        update_rel_median=float(np.median(list(kept.values()))), update_rel_worst=kept[worst_key],
+                        worst_tensor=worst_key,
+                        cancelled_update_rel_median=float(np.median([v for v, c in rows.values() if c])))
+        print(arm, {k: v for k, v in out[arm].items() if k != "loss_rel_per_step"})
+    report("f16x3_vs_fp32_30_steps_512", steps=steps, batch=2, arms=out)
+    for arm in out:
+        assert np.isfinite(out[arm]["loss_rel_max"])
+    ctrl = {k: max(out["bf16x6"][k], out["fp32_ulp"][k]) for k in ("loss_rel_max", "update_rel_median", "update_rel_worst")}
+    for k, v in ctrl.items():
+        assert out["f16x3"][k] <= 3 * v, (k, out["f16x3"][k], v)
+
+
 # ---------------------------------------------------------------------------------------------- topography
 
 @pytest.mark.parametrize("c_in,topo", [(3, None), (4, "dem"), (6, "map")])
