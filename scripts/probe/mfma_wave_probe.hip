@@ -6,6 +6,10 @@
 //   WAVES 4: 4 waves of 128 x 128 (one per SIMD, 256 accumulators in AGPRs) -- the verdict's proposed layout,
 //            in two read schedules: all fragments of a k-step up front (SCHED 0), or A and B in halves with the
 //            next quarter's reads interleaved one per MFMA (SCHED 1, sched_group_barrier).
+// and the product layout with the pipeline's costs added one at a time: a barrier per k-step (SCHED 2), and the
+// two-stage LDS-DMA ring (SCHED 3: 64 KB per stage by buffer_load ... lds from an L2-resident source, the issuing
+// wave's vmcnt wait and the barrier before each stage's fragment reads, the next stage's DMA issued after it; SCHED 4:
+// the same with each wave's 8 DMA pieces spread one per 12 MFMAs by sched_group_barrier).
 // Prints f16 MFMA TFLOP/s (three products = one fp32-equivalent MAC: divide by 3 for the f16x3 rate) and the
 // in-kernel clock (s_memtime / s_memrealtime).
 //   hipcc -O3 --offload-arch=gfx950 -o scripts/probe/mfma_wave_probe scripts/probe/mfma_wave_probe.hip
@@ -16,6 +20,7 @@
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
 
 constexpr int TILE = 256, KS = 32;
 constexpr int IMG = TILE * KS * 2;          // bytes per [256 rows][32 halfs] piece image
@@ -33,13 +38,25 @@ template <int WAVES, int SCHED>
 __global__ void __launch_bounds__(WAVES * 64, 1) probe(const f16x8* __restrict__ src, float* __restrict__ out,
                                                         long long* __restrict__ clk, int iters) {
     constexpr int WM = WAVES == 8 ? 64 : 128, WN = 128, TM = WM / 16, TN = WN / 16;
-    __shared__ __attribute__((aligned(1024))) char smem[4 * IMG];   // A h, A l, B h, B l
+    constexpr int NBUF = SCHED >= 3 ? 2 : 1;
+    __shared__ __attribute__((aligned(1024))) char smem[NBUF * 4 * IMG];   // [buffer][A h, A l, B h, B l]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     for (int i = tid; i < 4 * IMG / 16; i += WAVES * 64)
-        reinterpret_cast<f16x8*>(smem)[i] = src[(blockIdx.x * 977 + i) % (4 * IMG / 16)];
+        reinterpret_cast<f16x8*>(smem)[i] = src[(blockIdx.x * 977 + i) % (8 * 4 * IMG / 16)];
     __syncthreads();
     const int r0 = (wave / (TILE / WN)) * WM, c0 = (wave % (TILE / WN)) * WN;
     const char *ah = smem, *al = smem + IMG, *bh = smem + 2 * IMG, *bl = smem + 3 * IMG;
+    // SCHED 3: each wave DMAs 8 of a stage's 64 1-KiB pieces; the source cycles over 8 stages (512 KB, L2-resident)
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)src, 0, 0x7fffffff, 0x00020000);
+    auto dma = [&](int stage, int buf) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(smem + buf * 4 * IMG + (wave * 8 + i) * 1024), 16,
+                                                     lane * 16, ((stage & 7) * 64 + wave * 8 + i) * 1024, 0, 0);
+    };
+    if constexpr (SCHED >= 3) {
+        dma(0, 0);
+    }
     f32x4 acc[TM][TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -48,20 +65,45 @@ __global__ void __launch_bounds__(WAVES * 64, 1) probe(const f16x8* __restrict__
     const long long t0 = __builtin_amdgcn_s_memtime(), w0 = __builtin_amdgcn_s_memrealtime();
     for (int it = 0; it < iters; ++it) {
         asm volatile("" ::: "memory");       // the fragments are re-read every k-step, as in the real loop
-        if constexpr (SCHED == 0) {
+        if constexpr (SCHED == 2) __builtin_amdgcn_s_barrier();
+        if constexpr (SCHED >= 3) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            if (SCHED == 3 && it + 1 < iters) dma(it + 1, (it + 1) & 1);
+            const int o = (it & 1) * 4 * IMG;
+            ah = smem + o;
+            al = smem + o + IMG;
+            bh = smem + o + 2 * IMG;
+            bl = smem + o + 3 * IMG;
+        }
+        if constexpr (SCHED != 1) {
             f16x8 xa[TM], ya[TM], xb[TN], yb[TN];
 #pragma unroll
             for (int i = 0; i < TM; ++i) { xa[i] = frag(ah, r0 + 16 * i, lane); ya[i] = frag(al, r0 + 16 * i, lane); }
 #pragma unroll
             for (int j = 0; j < TN; ++j) { xb[j] = frag(bh, c0 + 16 * j, lane); yb[j] = frag(bl, c0 + 16 * j, lane); }
 #pragma unroll
-            for (int i = 0; i < TM; ++i)
+            for (int i = 0; i < TM; ++i) {
 #pragma unroll
                 for (int j = 0; j < TN; ++j) {
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(yb[j], xa[i], acc[i][j], 0, 0, 0);
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xb[j], ya[i], acc[i][j], 0, 0, 0);
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xb[j], xa[i], acc[i][j], 0, 0, 0);
                 }
+                if constexpr (SCHED == 4) {
+                    // two of the wave's 8 pieces after each row block's 24 MFMAs (pinned by sched_barrier); the
+                    // last stage's pieces land in the buffer nobody reads again
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int q = 0; q < 2; ++q) {
+                        const int piece = 2 * i + q;
+                        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                            rs, (lds_void*)(smem + ((it + 1) & 1) * 4 * IMG + (wave * 8 + piece) * 1024), 16, lane * 16,
+                            ((((it + 1) & 7) * 64) + wave * 8 + piece) * 1024, 0, 0);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
         } else {
             // quarters (A half, B half): (0,0) (0,1) (1,1) (1,0); each quarter's 48 MFMAs carry the reads of the
             // next half the schedule needs (sched_group_barrier: one ds_read between consecutive MFMAs)
@@ -106,6 +148,7 @@ __global__ void __launch_bounds__(WAVES * 64, 1) probe(const f16x8* __restrict__
             quarter(1, 0);
         }
     }
+    if constexpr (SCHED >= 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const long long t1 = __builtin_amdgcn_s_memtime(), w1 = __builtin_amdgcn_s_memrealtime();
     float s = 0.f;
 #pragma unroll
@@ -150,7 +193,7 @@ int main(int argc, char** argv) {
     const int iters = argc > 1 ? atoi(argv[1]) : 2000;
     int cus = 0;
     CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
-    const size_t n = 4 * IMG / 16;
+    const size_t n = 8 * 4 * IMG / 16;      // 512 KB: the ring's 8 source stages
     std::vector<_Float16> h(n * 8);
     srand(7);
     for (auto& v : h) v = (_Float16)((rand() / (float)RAND_MAX) * 2.f - 1.f);
@@ -165,6 +208,9 @@ int main(int argc, char** argv) {
     run<8, 0>(src, out, clk, cus, iters, "8 waves 64x128 (product layout)");
     run<4, 0>(src, out, clk, cus, iters, "4 waves 128x128, reads up front");
     run<4, 1>(src, out, clk, cus, iters, "4 waves 128x128, quarter-interleaved reads");
+    run<8, 2>(src, out, clk, cus, iters, "8 waves 64x128 + barrier per k-step");
+    run<8, 3>(src, out, clk, cus, iters, "8 waves 64x128 + 2-stage LDS-DMA ring");
+    run<8, 4>(src, out, clk, cus, iters, "8 waves 64x128 + ring, DMA among the MFMAs");
     run<8, 0>(src, out, clk, cus, iters, "8 waves 64x128 (product layout, again)");
     CHECK(hipFree(src));
     CHECK(hipFree(out));
