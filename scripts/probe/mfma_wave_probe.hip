@@ -9,7 +9,8 @@
 // and the product layout with the pipeline's costs added one at a time: a barrier per k-step (SCHED 2), and the
 // two-stage LDS-DMA ring (SCHED 3: 64 KB per stage by buffer_load ... lds from an L2-resident source, the issuing
 // wave's vmcnt wait and the barrier before each stage's fragment reads, the next stage's DMA issued after it; SCHED 4:
-// the same with each wave's 8 DMA pieces spread one per 12 MFMAs by sched_group_barrier).
+// the same with each wave's 8 DMA pieces spread two per row block, pinned by sched_barrier; SCHED 5: the SCHED 3
+// ring moving half the bytes, 4 pieces per wave per stage -- the DMA volume's share of the ring's cost).
 // Prints f16 MFMA TFLOP/s (three products = one fp32-equivalent MAC: divide by 3 for the f16x3 rate) and the
 // in-kernel clock (s_memtime / s_memrealtime).
 //   hipcc -O3 --offload-arch=gfx950 -o scripts/probe/mfma_wave_probe scripts/probe/mfma_wave_probe.hip
@@ -50,7 +51,7 @@ __global__ void __launch_bounds__(WAVES * 64, 1) probe(const f16x8* __restrict__
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)src, 0, 0x7fffffff, 0x00020000);
     auto dma = [&](int stage, int buf) __attribute__((always_inline)) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
+        for (int i = 0; i < (SCHED == 5 ? 4 : 8); ++i)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(smem + buf * 4 * IMG + (wave * 8 + i) * 1024), 16,
                                                      lane * 16, ((stage & 7) * 64 + wave * 8 + i) * 1024, 0, 0);
     };
@@ -69,7 +70,7 @@ __global__ void __launch_bounds__(WAVES * 64, 1) probe(const f16x8* __restrict__
         if constexpr (SCHED >= 3) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
-            if (SCHED == 3 && it + 1 < iters) dma(it + 1, (it + 1) & 1);
+            if ((SCHED == 3 || SCHED == 5) && it + 1 < iters) dma(it + 1, (it + 1) & 1);
             const int o = (it & 1) * 4 * IMG;
             ah = smem + o;
             al = smem + o + IMG;
@@ -211,6 +212,7 @@ int main(int argc, char** argv) {
     run<8, 2>(src, out, clk, cus, iters, "8 waves 64x128 + barrier per k-step");
     run<8, 3>(src, out, clk, cus, iters, "8 waves 64x128 + 2-stage LDS-DMA ring");
     run<8, 4>(src, out, clk, cus, iters, "8 waves 64x128 + ring, DMA among the MFMAs");
+    run<8, 5>(src, out, clk, cus, iters, "8 waves 64x128 + ring moving half the bytes");
     run<8, 0>(src, out, clk, cus, iters, "8 waves 64x128 (product layout, again)");
     CHECK(hipFree(src));
     CHECK(hipFree(out));
