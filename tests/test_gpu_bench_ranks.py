@@ -18,15 +18,21 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def test_bench_two_ranks_one_line():
+@pytest.mark.parametrize("launcher", ["bench", "torchrun"])
+def test_bench_two_ranks_one_line(launcher):
+    """launcher "bench": bench.py starts its ranks itself; "torchrun": the driver's N-GPU command line
+    (torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1)"""
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     env = dict(os.environ)
-    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_PORT"):
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_PORT", "MASTER_ADDR"):
         env.pop(k, None)
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
-                        "--res", "128", "--batch", "2", "--steps", "3", "--warmup", "1", "--no-cpu-baseline",
-                        "--no-fp32-math"], env=env, capture_output=True, text=True, timeout=600)
+    args = ["--gpus", "2", "--dist-backend", "gloo", "--res", "128", "--batch", "2", "--steps", "3", "--warmup", "1",
+            "--no-cpu-baseline", "--no-fp32-math"]
+    pre = ([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+            "127.0.0.1", "--master-port", str(29500 + os.getpid() % 1000)] if launcher == "torchrun" else [sys.executable])
+    r = subprocess.run(pre + [os.path.join(ROOT, "bench.py")] + args, env=env, capture_output=True, text=True,
+                       timeout=600)
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert r.returncode == 0, f"rc {r.returncode}:\n{r.stdout[-2000:]}\n{r.stderr[-4000:]}"
     assert len(lines) == 1, r.stdout[-2000:]          # rank 0 only
